@@ -1,0 +1,137 @@
+/*
+ * hash.c -- SHA-512 (FIPS 180-4) and BLAKE2b (RFC 7693), straight from the
+ * specifications.  TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Reference roles: SHA-512 is the hash inside libsodium Ed25519 and the VRF
+ * draft-03 suite (Praos.hs:543,580); Blake2b-256 is `Blake2b_256` of
+ * cardano-crypto-class (mkInputVRF Praos/VRF.hs:55-69, hashVRF :88-99, KES
+ * vk pair hash, hashVerKeyVRF Praos.hs:541) and Blake2b-224 is `hashKey`
+ * (Praos.hs:552,595).
+ */
+#include <string.h>
+#include "oracle.h"
+
+static uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+static const uint64_t K512[80] = {
+  0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+  0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+  0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+  0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+  0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+  0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+  0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+  0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+  0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+  0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+  0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+  0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+  0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+  0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+  0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+  0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+  0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+  0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+  0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+  0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+static void sha512_block(uint64_t H[8], const uint8_t *p) {
+  uint64_t W[80];
+  for (int i = 0; i < 16; i++) {
+    uint64_t w = 0;
+    for (int j = 0; j < 8; j++) w = (w << 8) | p[8 * i + j];
+    W[i] = w;
+  }
+  for (int i = 16; i < 80; i++) {
+    uint64_t s0 = ror64(W[i - 15], 1) ^ ror64(W[i - 15], 8) ^ (W[i - 15] >> 7);
+    uint64_t s1 = ror64(W[i - 2], 19) ^ ror64(W[i - 2], 61) ^ (W[i - 2] >> 6);
+    W[i] = W[i - 16] + s0 + W[i - 7] + s1;
+  }
+  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+  for (int i = 0; i < 80; i++) {
+    uint64_t S1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
+    uint64_t ch = (e & f) ^ (~e & g);
+    uint64_t t1 = h + S1 + ch + K512[i] + W[i];
+    uint64_t S0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
+    uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint64_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+}
+
+void orc_sha512(uint8_t out[64], const uint8_t *m, size_t n) {
+  uint64_t H[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                   0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                   0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  size_t off = 0;
+  while (n - off >= 128) { sha512_block(H, m + off); off += 128; }
+  uint8_t tail[256];
+  size_t r = n - off;
+  memset(tail, 0, sizeof tail);
+  memcpy(tail, m + off, r);
+  tail[r] = 0x80;
+  size_t tl = (r + 1 + 16 <= 128) ? 128 : 256;
+  uint64_t bits = (uint64_t)n * 8;
+  for (int j = 0; j < 8; j++) tail[tl - 1 - j] = (uint8_t)(bits >> (8 * j));
+  sha512_block(H, tail);
+  if (tl == 256) sha512_block(H, tail + 128);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) out[8 * i + j] = (uint8_t)(H[i] >> (56 - 8 * j));
+}
+
+static const uint64_t B2IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                                 0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+static const uint8_t SIGMA[12][16] = {
+  {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+  {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+  {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+  {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+  {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+  {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+static void b2_compress(uint64_t h[8], const uint8_t *blk, uint64_t t, int last) {
+  uint64_t m[16], v[16];
+  for (int i = 0; i < 16; i++) {
+    uint64_t w = 0;
+    for (int j = 7; j >= 0; j--) w = (w << 8) | blk[8 * i + j];
+    m[i] = w;
+  }
+  for (int i = 0; i < 8; i++) { v[i] = h[i]; v[i + 8] = B2IV[i]; }
+  v[12] ^= t;
+  if (last) v[14] = ~v[14];
+#define G(a, b, c, d, x, y)                      \
+  do {                                           \
+    v[a] = v[a] + v[b] + x; v[d] = ror64(v[d] ^ v[a], 32); \
+    v[c] = v[c] + v[d];     v[b] = ror64(v[b] ^ v[c], 24); \
+    v[a] = v[a] + v[b] + y; v[d] = ror64(v[d] ^ v[a], 16); \
+    v[c] = v[c] + v[d];     v[b] = ror64(v[b] ^ v[c], 63); \
+  } while (0)
+  for (int r = 0; r < 12; r++) {
+    const uint8_t *s = SIGMA[r];
+    G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+    G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+    G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+    G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+    G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+    G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+    G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+    G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+  }
+#undef G
+  for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+void orc_blake2b(uint8_t *out, size_t outlen, const uint8_t *m, size_t n) {
+  uint64_t h[8];
+  for (int i = 0; i < 8; i++) h[i] = B2IV[i];
+  h[0] ^= 0x01010000ULL ^ (uint64_t)outlen;
+  size_t off = 0;
+  while (n - off > 128) { off += 128; b2_compress(h, m + off - 128, off, 0); }
+  uint8_t blk[128];
+  memset(blk, 0, 128);
+  memcpy(blk, m + off, n - off);
+  b2_compress(h, blk, n, 1);
+  for (size_t i = 0; i < outlen; i++) out[i] = (uint8_t)(h[i / 8] >> (8 * (i % 8)));
+}
