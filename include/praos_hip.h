@@ -1,0 +1,231 @@
+/*
+ * praos_hip.h -- C ABI of libpraos_hip.so, the MI355X (gfx950) batch validator
+ * for Ouroboros Praos block-header crypto.
+ *
+ * Drop-in boundary: the reference validates one header at a
+ * time in Haskell, calling C crypto per signature through cardano-crypto-class
+ * FFI (`foreign import ccall` into libsodium; result CInt 0 = ok / -1 = fail).
+ * This ABI replaces, for a contiguous batch of headers of one epoch:
+ *
+ *   praos_verify_headers  <- Praos.validateKESSignature  (Praos.hs:558-606)
+ *                            + Praos.validateVRFSignature (Praos.hs:528-556)
+ *                            as composed by updateChainDepState (Praos.hs:441-459)
+ *   praos_verify_ocert    <- DSIGN.verifySignedDSIGN vkcold (ocertToSignable oc) tau
+ *                            (Praos.hs:580; Ed25519DSIGN -> libsodium verify_detached)
+ *   praos_verify_kes      <- KES.verifySignedKES vk_hot t hvSigned hvSignature
+ *                            (Praos.hs:582; Shelley/Protocol/Praos.hs:85 for integrity)
+ *   praos_verify_vrf      <- VRF.verifyCertified vrfK (mkInputVRF slot eta0) vrfCert
+ *                            (Praos.hs:543; PraosVRF -> crypto_vrf_ietfdraft03_verify)
+ *   praos_check_leader    <- checkLeaderNatValue (vrfLeaderValue cert) sigma f
+ *                            (Praos.hs:549)
+ *   praos_apply_batch     <- the first-error-wins order of updateChainDepState plus
+ *                            the OCert counter rule (Praos.hs:584-606) and the
+ *                            reupdateChainDepState counter/nonce update (Praos.hs:468-502)
+ *
+ * Conventions (mirroring the reference FFI): plain pointers + sizes, caller-owned
+ * host buffers, nothing retained after return.  Return value 0 = ok, < 0 = system
+ * error (PRAOS_E_*).  Cryptographic failures are DATA (bits in the outputs),
+ * never return codes.  One context per host thread; calls block.
+ */
+#ifndef PRAOS_HIP_H
+#define PRAOS_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRAOS_ABI_VERSION 1
+
+/* ---- return codes ---- */
+#define PRAOS_OK 0
+#define PRAOS_E_HIP (-1)     /* HIP runtime error (see praos_last_error) */
+#define PRAOS_E_ARG (-2)     /* bad argument / inconsistent sizes */
+#define PRAOS_E_OOM (-3)     /* device allocation failed */
+#define PRAOS_E_STATE (-4)   /* praos_set_epoch not called */
+
+/* ---- per-header check bits (uint16), one per reference error constructor ---- */
+#define PRAOS_BIT_KES_BEFORE_START   0x0001u /* KESBeforeStartOCERT c0 kp */
+#define PRAOS_BIT_KES_AFTER_END      0x0002u /* KESAfterEndOCERT kp c0 maxKESEvo */
+#define PRAOS_BIT_OCERT_SIG          0x0004u /* InvalidSignatureOCERT n c0 "Verification failed" */
+#define PRAOS_BIT_KES_MERKLE         0x0008u /* InvalidKesSignatureOCERT kp c0 t "Reject" */
+#define PRAOS_BIT_KES_LEAF           0x0010u /* InvalidKesSignatureOCERT kp c0 t (Ed25519 leaf) */
+#define PRAOS_BIT_COUNTER_MISSING    0x0020u /* NoCounterForKeyHashOCERT (praos_apply_batch) */
+#define PRAOS_BIT_COUNTER_TOO_SMALL  0x0040u /* CounterTooSmallOCERT (praos_apply_batch) */
+#define PRAOS_BIT_COUNTER_OVER_INC   0x0080u /* CounterOverIncrementedOCERT (praos_apply_batch) */
+#define PRAOS_BIT_VRF_KEY_UNKNOWN    0x0100u /* VRFKeyUnknown */
+#define PRAOS_BIT_VRF_KEY_WRONG      0x0200u /* VRFKeyWrongVRFKey */
+#define PRAOS_BIT_VRF_PROOF          0x0400u /* VRFKeyBadProof: draft-03 proof rejected */
+#define PRAOS_BIT_VRF_OUTPUT         0x0800u /* VRFKeyBadProof: certified output != proof_to_hash */
+#define PRAOS_BIT_LEADER             0x1000u /* VRFLeaderValueTooBig */
+#define PRAOS_BIT_INPUT              0x8000u /* malformed batch entry (e.g. body out of range) */
+
+/* ---- verdict codes of praos_apply_batch (first failing check, Praos.hs order) ---- */
+enum praos_verdict {
+  PRAOS_V_OK = 0,
+  PRAOS_V_KES_BEFORE_START = 1,
+  PRAOS_V_KES_AFTER_END = 2,
+  PRAOS_V_OCERT_SIG = 3,
+  PRAOS_V_KES_SIG = 4,            /* detail: bit KES_MERKLE or KES_LEAF */
+  PRAOS_V_COUNTER_MISSING = 5,
+  PRAOS_V_COUNTER_TOO_SMALL = 6,
+  PRAOS_V_COUNTER_OVER_INC = 7,
+  PRAOS_V_VRF_KEY_UNKNOWN = 8,
+  PRAOS_V_VRF_KEY_WRONG = 9,
+  PRAOS_V_VRF_BAD_PROOF = 10,
+  PRAOS_V_LEADER_TOO_BIG = 11,
+  PRAOS_V_INPUT = 12
+};
+
+typedef struct praos_ctx praos_ctx;
+typedef struct praos_batch praos_batch;
+
+/* PraosParams fields used by header validation (Praos.hs:184-210) and the
+ * active slot coefficient in the form checkLeaderNatValue consumes. */
+typedef struct {
+  uint64_t slots_per_kes_period;  /* praosSlotsPerKESPeriod (must be > 0) */
+  uint64_t max_kes_evo;           /* praosMaxKESEvo */
+  int32_t f_is_one;               /* activeSlotVal f == maxBound -> leader check always true */
+  int32_t vrf_check_output;       /* 1: verifyCertified also requires certified output == beta
+                                     (cardano-crypto-class >= 2.1 semantics); 0: proof only */
+  uint8_t c_raw[16];              /* activeSlotLog f: Fixed E34 raw value, int128 LE two's complement, <= 0 */
+} praos_params;
+
+/* One entry of the stake distribution (PoolDistr, Views.hs:41-51). */
+typedef struct {
+  uint8_t hash28[28];             /* KeyHash 'StakePool = Blake2b-224(cold vk) */
+  uint8_t vrf_hash32[32];         /* individualPoolStakeVrf = Blake2b-256(vrf vk) */
+  uint8_t sigma_fp[16];           /* fromRational individualPoolStake: Fixed E34 raw, uint128 LE */
+} praos_pool;
+
+/* Headers of one batch, struct-of-arrays over caller memory (HeaderView,
+ * Views.hs:22-39).  Fixed-width fields are n records each. */
+typedef struct {
+  size_t n;
+  const uint64_t* slot;           /* hvSlotNo */
+  const uint8_t* cold_vk;         /* hvVK, n*32 */
+  const uint8_t* vrf_vk;          /* hvVrfVK, n*32 */
+  const uint8_t* vrf_out;         /* certifiedOutput of hvVrfRes, n*64 */
+  const uint8_t* vrf_proof;       /* certifiedProof, n*80 */
+  const uint8_t* hot_vk;          /* OCert ocertVkHot, n*32 */
+  const uint64_t* ocert_n;        /* ocertN */
+  const uint64_t* ocert_c0;       /* ocertKESPeriod */
+  const uint8_t* ocert_sig;       /* ocertSigma, n*64 */
+  const uint8_t* kes_sig;         /* hvSignature (Sum6KES raw), n*448 */
+  const uint64_t* body_off;       /* hvSigned: offset of the signed body bytes in body_bytes */
+  const uint32_t* body_len;       /* hvSigned length */
+  const uint8_t* body_bytes;
+  size_t body_bytes_len;
+} praos_headers;
+
+/* Outputs (any pointer may be NULL except bits). */
+typedef struct {
+  uint16_t* bits;                 /* n: PRAOS_BIT_* (crypto + range checks) */
+  int32_t* pool_idx;              /* n: index into the praos_set_epoch pool array, -1 unknown */
+  uint8_t* beta;                  /* n*64: proof_to_hash (zeros if Gamma undecodable) */
+  uint8_t* leader;                /* n*32: vrfLeaderValue, big-endian natural */
+  uint8_t* nonce;                 /* n*32: vrfNonceValue */
+} praos_out;
+
+/* ---- context ---- */
+praos_ctx* praos_open(int device);               /* NULL on failure */
+void praos_close(praos_ctx* ctx);
+const char* praos_last_error(praos_ctx* ctx);
+int praos_abi_version(void);
+
+/* Epoch-constant inputs: eta0 (NULL = NeutralNonce), pool distribution, params. */
+int praos_set_epoch(praos_ctx* ctx, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
+                    const praos_params* params);
+
+/* Blocking: H2D, all checks on the GPU, D2H. */
+int praos_verify_headers(praos_ctx* ctx, const praos_headers* h, praos_out* out);
+
+/* Device-resident pipeline (bench / streaming): upload once, run many times. */
+praos_batch* praos_batch_upload(praos_ctx* ctx, const praos_headers* h);
+int praos_batch_run(praos_ctx* ctx, praos_batch* b);          /* async on the ctx stream */
+int praos_batch_sync(praos_ctx* ctx);
+int praos_batch_download(praos_ctx* ctx, praos_batch* b, praos_out* out);
+void praos_batch_free(praos_ctx* ctx, praos_batch* b);
+/* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
+ * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run. */
+float praos_batch_kernel_ms(praos_ctx* ctx, int which);
+
+/* ---- single-primitive batches (configs C2-C4); outputs 1 = valid, 0 = invalid ---- */
+/* Ed25519 over the OCert signable hot_vk || BE64(n) || BE64(c0). */
+int praos_verify_ocert(praos_ctx* ctx, size_t n, const uint8_t* cold_vk, const uint8_t* hot_vk,
+                       const uint64_t* ocert_n, const uint64_t* ocert_c0, const uint8_t* sig, uint8_t* ok);
+/* Sum6KES: result 0 = ok, 1 = Merkle "Reject", 2 = leaf Ed25519 failure. */
+int praos_verify_kes(praos_ctx* ctx, size_t n, const uint8_t* vk, const uint32_t* period, const uint8_t* sig,
+                     const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* msg_bytes,
+                     size_t msg_bytes_len, uint8_t* result);
+/* ECVRF-ED25519-SHA512-Elligator2 draft-03 verify; alpha is 32 bytes per item. */
+int praos_verify_vrf(praos_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* proof, const uint8_t* alpha,
+                     uint8_t* ok, uint8_t* beta);
+/* checkLeaderNatValue; leader = 32-byte big-endian naturals, sigma_fp per item. */
+int praos_check_leader(praos_ctx* ctx, size_t n, const uint8_t* leader, const uint8_t* sigma_fp,
+                       const praos_params* params, uint8_t* is_leader);
+
+/* ---- host-side sequential part (Praos.hs:441-502 order and state) ----
+ * Counter map: the OCert issue numbers of praosStateOCertCounters, keyed by
+ * issuer hash (Blake2b-224 of cold vk).  Walks the batch in order: verdict =
+ * first failing check, then (as the reference does after a valid header)
+ * counters[hk] := n.  `assume_valid_prefix` semantics: every header is judged
+ * against the state left by all earlier headers of the batch as if valid.
+ * chain_stop receives the index of the first non-OK header (n if none). */
+typedef struct {
+  const uint8_t* hash28;          /* m*28, any order */
+  uint64_t* counter;              /* m: in = current counters; updated in place for existing keys */
+  size_t m;
+} praos_counters;
+
+int praos_apply_batch(praos_ctx* ctx, const praos_headers* h, const praos_out* crypto,
+                      praos_counters* counters, uint8_t* verdict, size_t* chain_stop);
+
+/* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
+ * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),
+ * VRF draft-03 proofs for alpha = mkInputVRF(slot, eta0).  Keys derive from
+ * 32-byte seeds: cold/VRF/KES seed of pool i = Blake2b-256(tag || seed || i). */
+typedef struct {
+  uint64_t n;                     /* headers */
+  uint32_t npools;
+  uint64_t first_slot;
+  uint64_t slot_stride;           /* slot of header i = first_slot + i * slot_stride */
+  uint32_t body_len;              /* synthetic signed body length (CBOR-like bytes) */
+  uint32_t corrupt_per_10000;     /* seeded corruptions (Corruption.hs model: +1 at a byte) */
+  uint8_t seed[32];
+} praos_synth_params;
+
+/* Fills caller buffers (same layout as praos_headers; body_off/body_len/body_bytes
+ * sized n, n, n*round_up(body_len, 8)+8).  Also returns the pool table
+ * (npools entries, sigma_fp left for the caller to set). */
+int praos_synthesize(praos_ctx* ctx, const praos_synth_params* sp, const praos_params* params,
+                     const uint8_t eta0[32], praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk,
+                     uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n,
+                     uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off,
+                     uint32_t* body_len, uint8_t* body_bytes, uint8_t* corrupted);
+
+/* ---- self-test entry points (unit tests of the device arithmetic) ---- */
+/* op: 0 mul, 1 sq, 2 add, 3 sub, 4 invert, 5 pow22523, 6 canon; inputs/outputs n*32 bytes LE */
+int praos_debug_fe(praos_ctx* ctx, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);
+/* SHA-512 of (64-byte prefix || msg) per item; out n*64 */
+int praos_debug_sha512(praos_ctx* ctx, size_t n, const uint8_t* prefix, const uint64_t* msg_off,
+                       const uint32_t* msg_len, const uint8_t* msg_bytes, size_t msg_bytes_len, uint8_t* out);
+/* BLAKE2b-256 of 64-byte inputs; out n*32 */
+int praos_debug_blake2b(praos_ctx* ctx, size_t n, const uint8_t* in64, uint8_t* out);
+/* x mod L for 64-byte inputs; out n*32 */
+int praos_debug_sc_reduce(praos_ctx* ctx, size_t n, const uint8_t* in64, uint8_t* out);
+/* decode point (1 = ok) and re-encode; out n*32, ok n */
+int praos_debug_decode(praos_ctx* ctx, size_t n, const uint8_t* in32, uint8_t* out, uint8_t* ok);
+/* [s]B for 32-byte scalars (< 2^255); out n*32 */
+int praos_debug_scalarmult_base(praos_ctx* ctx, size_t n, const uint8_t* s, uint8_t* out);
+/* leader check with explicit x_raw per item (4 words LE); is_leader, iters out */
+int praos_debug_leader(praos_ctx* ctx, size_t n, const uint8_t* leader, const uint8_t* x_raw16, uint8_t* is_leader,
+                       int32_t* iters);
+/* Elligator2 hash-to-curve of the VRF suite: h(pk, alpha); out n*32 */
+int praos_debug_hash_to_curve(praos_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* alpha, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -472,3 +472,18 @@ int orc_point_order_divides(const uint8_t s[32], int k) {
   init(); ge p, q; if (ge_frombytes(&p, s) != 0) return -1;
   uint8_t kk[32] = {0}; kk[0] = (uint8_t)k; ge_scalarmult(&q, kk, &p); return ge_is_identity(&q);
 }
+
+/* [s]B for a 32-byte LE scalar (no clamping); encoding out */
+void orc_scalarmult_base(uint8_t out[32], const uint8_t s[32]) {
+  init(); ge R; ge_scalarmult(&R, s, &GE_B); ge_tobytes(out, &R);
+}
+/* libsodium ge25519_frombytes then p3_tobytes; returns 1 if on curve */
+int orc_ge_reencode(uint8_t out[32], const uint8_t in[32]) {
+  init(); ge P; if (ge_frombytes(&P, in) != 0) { memset(out, 0, 32); return 0; }
+  ge_tobytes(out, &P); return 1;
+}
+/* VRF draft-03 hash_to_curve(Y, alpha) encoding; returns 0 if pk undecodable */
+int orc_vrf_hash_to_curve(uint8_t out[32], const uint8_t pk[32], const uint8_t *alpha, size_t alen) {
+  init(); ge Y; if (ge_frombytes(&Y, pk) != 0) return 0;
+  hash_to_curve(out, &Y, alpha, alen); return 1;
+}

@@ -41,6 +41,9 @@ def lib():
         L.orc_ge_decode_ok.argtypes = [c.c_char_p]
         L.orc_point_order_divides.argtypes = [c.c_char_p, c.c_int]
         L.orc_praos_header.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p]
+        L.orc_scalarmult_base.argtypes = [c.c_char_p, c.c_char_p]
+        L.orc_ge_reencode.argtypes = [c.c_char_p, c.c_char_p]
+        L.orc_vrf_hash_to_curve.argtypes = [c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t]
         _lib = L
     return _lib
 
@@ -127,6 +130,25 @@ def check_leader(leader_be: bytes, sigma_fp: int, c_raw: int, f_is_one: bool = F
 
 def has_small_order(s: bytes) -> bool:
     return bool(lib().orc_has_small_order(s))
+
+
+def scalarmult_base(s: bytes) -> bytes:
+    o = ctypes.create_string_buffer(32)
+    lib().orc_scalarmult_base(o, s)
+    return o.raw
+
+
+def reencode(s: bytes):
+    """(on_curve, canonical re-encoding) with libsodium ge25519_frombytes rules."""
+    o = ctypes.create_string_buffer(32)
+    ok = lib().orc_ge_reencode(o, s)
+    return bool(ok), o.raw
+
+
+def vrf_hash_to_curve(pk: bytes, alpha: bytes):
+    o = ctypes.create_string_buffer(32)
+    ok = lib().orc_vrf_hash_to_curve(o, pk, alpha, len(alpha))
+    return o.raw if ok else None
 
 
 def decode_ok(s: bytes) -> bool:

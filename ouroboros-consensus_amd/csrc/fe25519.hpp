@@ -1,0 +1,270 @@
+// fe25519.hpp -- GF(2^255-19) arithmetic for gfx950, one field element per lane.
+//
+// Representation: 8 x 32-bit limbs, radix 2^32, value in [0, 2^256) ("weakly
+// reduced": congruent mod p, canonicalised only for encoding / comparison).
+//
+// Why radix 2^32 (measured on MI355X, tools/microbench/intrate.hip):
+// v_mad_u64_u32 (32x32+64 -> 64 with carry-out) issues at ~5.2 cycles per
+// wave64 instruction vs ~4.3 for other VOP3 ops, so a full 32-bit MAC costs
+// barely more than an add.  The 8x8 schoolbook product is 64 MACs, each paired
+// with one v_addc_co_u32 that counts the column carry; reduction folds the
+// high 256 bits with 2^256 = 38 (mod p).  This beats radix 2^25.5 (100 MACs +
+// 64-bit carry chains) and uses 8 instead of 10 VGPRs per element.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FE_INLINE __device__ __forceinline__
+
+struct fe { uint32_t v[8]; };
+
+// acc(64) += a*b with the carry-out counted into top.  gfx950 needs two wait
+// states between a VALU write of VCC and a VALU read of it as carry-in (the
+// compiler inserts the same `s_nop 1` in its own carry chains).
+#define FE_MAC(acc, top, a, b)                                                     \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc" \
+      : "+v"(acc), "+v"(top) : "v"(a), "v"(b) : "vcc")
+
+FE_INLINE uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  return __builtin_addc(a, b, cin, cout);
+}
+FE_INLINE uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  return __builtin_subc(a, b, bin, bout);
+}
+
+FE_INLINE void fe_set(fe& r, uint32_t x) {
+  r.v[0] = x;
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = 0;
+}
+FE_INLINE void fe_const(fe& r, const uint32_t c[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c[i];
+}
+
+// r = t[0..15] mod p, t = 512-bit product
+FE_INLINE void fe_reduce512(fe& r, const uint32_t t[16]) {
+  uint64_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = (uint64_t)t[8 + i] * 38u + t[i];
+  uint32_t c = 0;
+  r.v[0] = (uint32_t)s[0];
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = addc((uint32_t)s[i], (uint32_t)(s[i - 1] >> 32), c, &c);
+  uint32_t k = (uint32_t)(s[7] >> 32) + c;           // < 40
+  uint64_t s0 = (uint64_t)k * 38u + r.v[0];
+  r.v[0] = (uint32_t)s0;
+  c = (uint32_t)(s0 >> 32);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = addc(r.v[i], 0, c, &c);
+  r.v[0] += 38u * c;                                 // cannot carry: value wrapped to < 2^11
+}
+
+FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
+  uint32_t t[16];
+  uint64_t acc = (uint64_t)a.v[0] * b.v[0];
+  t[0] = (uint32_t)acc;
+  acc >>= 32;
+#pragma unroll
+  for (int k = 1; k < 15; k++) {
+    uint32_t top = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      FE_MAC(acc, top, a.v[i], b.v[j]);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+  }
+  t[15] = (uint32_t)acc;
+  fe_reduce512(r, t);
+}
+
+FE_INLINE void fe_sq(fe& r, const fe& a) {
+  uint32_t t[16];
+  // cross products a_i a_j, i < j
+  uint64_t acc = 0;
+  t[0] = 0;
+#pragma unroll
+  for (int k = 1; k < 15; k++) {
+    uint32_t top = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j <= i || j > 7) continue;
+      FE_MAC(acc, top, a.v[i], a.v[j]);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+  }
+  t[15] = (uint32_t)acc;
+  // double (cross sum < 2^511, so no bit is lost)
+#pragma unroll
+  for (int i = 15; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
+  t[0] = 0;
+  // add diagonal squares
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)a.v[i] * a.v[i];
+    t[2 * i] = addc(t[2 * i], (uint32_t)d, c, &c);
+    t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(d >> 32), c, &c);
+  }
+  fe_reduce512(r, t);
+}
+
+FE_INLINE void fe_add(fe& r, const fe& a, const fe& b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = addc(a.v[i], b.v[i], c, &c);
+  uint32_t c2 = 0;
+  r.v[0] = addc(r.v[0], 38u * c, 0, &c2);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = addc(r.v[i], 0, c2, &c2);
+  r.v[0] += 38u * c2;
+}
+
+FE_INLINE void fe_sub(fe& r, const fe& a, const fe& b) {
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = subb(a.v[i], b.v[i], bw, &bw);
+  uint32_t b2 = 0;
+  r.v[0] = subb(r.v[0], 38u * bw, 0, &b2);
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = subb(r.v[i], 0, b2, &b2);
+  r.v[0] -= 38u * b2;
+}
+
+FE_INLINE void fe_neg(fe& r, const fe& a) {
+  fe z;
+  fe_set(z, 0);
+  fe_sub(r, z, a);
+}
+
+FE_INLINE void fe_cmov(fe& r, const fe& a, bool c) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c ? a.v[i] : r.v[i];
+}
+
+// canonical representative in [0, p)
+FE_INLINE void fe_canon(fe& r, const fe& a) {
+  // fold bit 255
+  uint32_t top = a.v[7] >> 31;
+  uint32_t c = 0;
+  r.v[0] = addc(a.v[0], 19u * top, 0, &c);
+#pragma unroll
+  for (int i = 1; i < 7; i++) r.v[i] = addc(a.v[i], 0, c, &c);
+  r.v[7] = (a.v[7] & 0x7fffffffu) + c;               // now < 2^255 + 19
+  // subtract p if r >= p  <=>  r + 19 >= 2^255
+  uint32_t u[8];
+  c = 0;
+  u[0] = addc(r.v[0], 19u, 0, &c);
+#pragma unroll
+  for (int i = 1; i < 8; i++) u[i] = addc(r.v[i], 0, c, &c);
+  const bool ge = (u[7] >> 31) != 0;
+  u[7] &= 0x7fffffffu;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = ge ? u[i] : r.v[i];
+}
+
+FE_INLINE void fe_tobytes32(uint32_t w[8], const fe& a) {   // little-endian words
+  fe c;
+  fe_canon(c, a);
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = c.v[i];
+}
+
+FE_INLINE bool fe_iszero(const fe& a) {
+  fe c;
+  fe_canon(c, a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= c.v[i];
+  return o == 0;
+}
+FE_INLINE bool fe_isnegative(const fe& a) {
+  fe c;
+  fe_canon(c, a);
+  return c.v[0] & 1;
+}
+// 255-bit load: top bit cleared, value may be >= p (arithmetic is mod p)
+FE_INLINE void fe_frombytes32(fe& r, const uint32_t w[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = w[i];
+  r.v[7] &= 0x7fffffffu;
+}
+
+FE_INLINE void fe_sqn(fe& r, const fe& a, int n) {
+  fe_sq(r, a);
+#pragma clang loop unroll(disable)
+  for (int i = 1; i < n; i++) fe_sq(r, r);
+}
+
+// z^(2^250 - 1) and helpers, shared by invert / pow22523 (standard chain)
+FE_INLINE void fe_pow2_250_1(fe& t0, fe& z11, const fe& z) {
+  fe t1, t2, t3;
+  fe_sq(t0, z);                 // 2
+  fe_sqn(t1, t0, 2);            // 8
+  fe_mul(t1, z, t1);            // 9
+  fe_mul(z11, t0, t1);          // 11
+  fe_sq(t0, z11);               // 22
+  fe_mul(t0, t1, t0);           // 2^5 - 1
+  fe_sqn(t1, t0, 5);
+  fe_mul(t0, t1, t0);           // 2^10 - 1
+  fe_sqn(t1, t0, 10);
+  fe_mul(t1, t1, t0);           // 2^20 - 1
+  fe_sqn(t2, t1, 20);
+  fe_mul(t1, t2, t1);           // 2^40 - 1
+  fe_sqn(t1, t1, 10);
+  fe_mul(t0, t1, t0);           // 2^50 - 1
+  fe_sqn(t1, t0, 50);
+  fe_mul(t1, t1, t0);           // 2^100 - 1
+  fe_sqn(t3, t1, 100);
+  fe_mul(t1, t3, t1);           // 2^200 - 1
+  fe_sqn(t1, t1, 50);
+  fe_mul(t0, t1, t0);           // 2^250 - 1
+}
+
+FE_INLINE void fe_invert_inl(fe& r, const fe& z) {      // z^(p-2)
+  fe t0, z11;
+  fe_pow2_250_1(t0, z11, z);
+  fe_sqn(t0, t0, 5);            // 2^255 - 2^5
+  fe_mul(r, t0, z11);           // 2^255 - 21
+}
+
+FE_INLINE void fe_pow22523_inl(fe& r, const fe& z) {    // z^((p-5)/8) = z^(2^252 - 3)
+  fe t0, z11;
+  fe_pow2_250_1(t0, z11, z);
+  fe_sqn(t0, t0, 2);            // 2^252 - 4
+  fe_mul(r, t0, z);             // 2^252 - 3
+}
+
+// Legendre symbol z^((p-1)/2) = z^(2^254 - 10)
+FE_INLINE void fe_chi_inl(fe& r, const fe& z) {
+  fe t0, z11;
+  fe_pow2_250_1(t0, z11, z);    // 2^250 - 1
+  fe_sqn(t0, t0, 4);            // 2^254 - 16
+  fe t1;
+  fe_sq(t1, z);                 // 2
+  fe_mul(t1, t1, z);            // 3
+  fe_sq(t1, t1);                // 6
+  fe_mul(r, t0, t1);            // 2^254 - 10
+}
+
+// Exponentiation chains (~255 squarings each) are emitted once per kernel
+// module and called by value: the call overhead is < 1% of the chain, and
+// inlining every call site multiplied compile time and code size.
+__device__ __noinline__ fe fe_invert_v(fe z) { fe r; fe_invert_inl(r, z); return r; }
+__device__ __noinline__ fe fe_pow22523_v(fe z) { fe r; fe_pow22523_inl(r, z); return r; }
+__device__ __noinline__ fe fe_chi_v(fe z) { fe r; fe_chi_inl(r, z); return r; }
+FE_INLINE void fe_invert(fe& r, const fe& z) { r = fe_invert_v(z); }
+FE_INLINE void fe_pow22523(fe& r, const fe& z) { r = fe_pow22523_v(z); }
+FE_INLINE void fe_chi(fe& r, const fe& z) { r = fe_chi_v(z); }
+
+__device__ __constant__ static const uint32_t FE_D[8] = {0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du,
+                                                          0x7779e898u, 0x8cc74079u, 0x2b6ffe73u, 0x52036ceeu};
+__device__ __constant__ static const uint32_t FE_D2[8] = {0x26b2f159u, 0xebd69b94u, 0x8283b156u, 0x00e0149au,
+                                                           0xeef3d130u, 0x198e80f2u, 0x56dffce7u, 0x2406d9dcu};
+__device__ __constant__ static const uint32_t FE_SQRTM1[8] = {0x4a0ea0b0u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u,
+                                                               0x3dfbd7a7u, 0x2b4d0099u, 0x4fc1df0bu, 0x2b832480u};

@@ -1,0 +1,94 @@
+// k_ed25519.hip -- OCert and Sum6KES kernels (Ed25519 verify per lane).
+#include "kcommon.hpp"
+
+// ------------------------------------------------------------------ OCert + KES period checks
+// bits |= KES_BEFORE_START / KES_AFTER_END / OCERT_SIG.  If ok_out != null the
+// kernel is the plain praos_verify_ocert batch (ok_out[i] = 1 when valid).
+__global__ void __launch_bounds__(NT) k_ocert(size_t n, const ge_niels* __restrict__ gbtab,
+                                              const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ hot_vk,
+                                              const uint64_t* __restrict__ ocert_n, const uint64_t* __restrict__ ocert_c0,
+                                              const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot,
+                                              uint64_t slots_per_kes_period, uint64_t max_kes_evo,
+                                              uint16_t* __restrict__ bits, uint8_t* __restrict__ ok_out) {
+  __shared__ ge_niels sbtab[8];
+  __shared__ int8_t sdig[DIG_BYTES];
+  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  DigitPlanes dp{sdig, NT, 2};
+  uint32_t pk[8], hot[8], sg[16];
+  load_words(pk, cold_vk + 32 * i, 8);
+  load_words(hot, hot_vk + 32 * i, 8);
+  load_words(sg, sig + 64 * i, 16);
+  const uint64_t nn = ocert_n[i], c0 = ocert_c0[i];
+  uint32_t hram[16];
+  ocert_hram(hram, sg, pk, hot, nn, c0);
+  const bool ok = ed25519_verify_core(pk, sg, sg + 8, hram, dp, threadIdx.x, btab);
+  if (ok_out) {
+    ok_out[i] = ok ? 1 : 0;
+    return;
+  }
+  uint16_t b = ok ? 0 : PRAOS_BIT_OCERT_SIG;
+  const uint64_t kp = slot[i] / slots_per_kes_period;        // Praos.hs:596-599
+  if (!(c0 <= kp)) b |= PRAOS_BIT_KES_BEFORE_START;          // Praos.hs:567
+  if (!(kp < c0 + max_kes_evo)) b |= PRAOS_BIT_KES_AFTER_END; // Praos.hs:568
+  bits[i] |= b;
+}
+
+// ------------------------------------------------------------------ KES
+// Header mode: t = kp >= c0 ? kp - c0 : 0 (Praos.hs:570), result to bits.
+// Plain mode (result != null): t = period[i], result 0 ok / 1 Reject / 2 leaf.
+__global__ void __launch_bounds__(NT) k_kes(size_t n, const ge_niels* __restrict__ gbtab,
+                                            const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig,
+                                            const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len,
+                                            const uint8_t* __restrict__ body, size_t body_bytes_len,
+                                            const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0,
+                                            uint64_t slots_per_kes_period, const uint32_t* __restrict__ period,
+                                            uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {
+  __shared__ ge_niels sbtab[8];
+  __shared__ int8_t sdig[DIG_BYTES];
+  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  DigitPlanes dp{sdig, NT, 2};
+  uint64_t t;
+  if (period) {
+    t = period[i];
+  } else {
+    const uint64_t kp = slot[i] / slots_per_kes_period, c0 = ocert_c0[i];
+    t = kp >= c0 ? kp - c0 : 0;
+  }
+  const uint8_t* sig = kes_sig + 448 * i;
+  uint32_t vk[8], leaf[8], sg[16];
+  load_words(vk, hot_vk + 32 * i, 8);
+  const bool merkle_ok = kes_merkle(leaf, vk, t, sig);
+  load_words(sg, sig, 16);
+  uint64_t off = body_off[i];
+  uint32_t len = body_len[i];
+  const bool in_range = (off & 7) == 0 && off <= body_bytes_len && len <= body_bytes_len - off;
+  if (!in_range) { off = 0; len = 0; }
+  uint32_t pre[16], hram[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { pre[k] = sg[k]; pre[8 + k] = leaf[k]; }
+  sha512_stream(hram, pre, 64, body + off, len);
+  const bool leaf_ok = ed25519_verify_core(leaf, sg, sg + 8, hram, dp, threadIdx.x, btab);
+  if (result) {
+    result[i] = !in_range ? 3 : (!merkle_ok ? 1 : (leaf_ok ? 0 : 2));
+    return;
+  }
+  uint16_t b = 0;
+  if (!merkle_ok) b |= PRAOS_BIT_KES_MERKLE;
+  else if (!leaf_ok) b |= PRAOS_BIT_KES_LEAF;
+  if (!in_range) b |= PRAOS_BIT_INPUT;
+  bits[i] |= b;
+}
+
+
+// ---- host launchers (kernels are only launchable from their own module)
+void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ hot_vk, const uint64_t* __restrict__ ocert_n, const uint64_t* __restrict__ ocert_c0, const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo, uint16_t* __restrict__ bits, uint8_t* __restrict__ ok_out) {
+  hipLaunchKernelGGL(k_ocert, grid, block, 0, stream, n, gbtab, cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out);
+}
+
+void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {
+  hipLaunchKernelGGL(k_kes, grid, block, 0, stream, n, gbtab, hot_vk, kes_sig, body_off, body_len, body, body_bytes_len, slot, ocert_c0, slots_per_kes_period, period, bits, result);
+}

@@ -1,0 +1,192 @@
+// k_misc.hip -- base-point table init, Fixed E34 leader check, self-test kernels.
+#include "kcommon.hpp"
+
+// ------------------------------------------------------------------ init
+// btab[k] = (k+1) B as affine niels (y+x, y-x, 2dxy); one lane per entry.
+__global__ void k_init_btab(ge_niels* btab) {
+  const int k = threadIdx.x;
+  if (k >= 8) return;
+  const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  ge_p3 B, acc;
+  ge_frombytes(B, benc, false);
+  acc = B;
+  ge_cached bc;
+  ge_p3_to_cached(bc, B);
+  for (int i = 0; i < k; i++) {
+    ge_p1p1 t;
+    ge_add(t, acc, bc);
+    ge_p1p1_to_p3(acc, t);
+  }
+  fe zi, x, y, xy, d2;
+  fe_invert(zi, acc.Z);
+  fe_mul(x, acc.X, zi);
+  fe_mul(y, acc.Y, zi);
+  fe_canon(x, x);
+  fe_canon(y, y);
+  ge_niels n;
+  fe_add(n.ypx, y, x);
+  fe_sub(n.ymx, y, x);
+  fe_mul(xy, x, y);
+  fe_const(d2, FE_D2);
+  fe_mul(n.xy2d, xy, d2);
+  btab[k] = n;
+}
+
+// ------------------------------------------------------------------ leader
+// Header mode: leader bytes from leader_in (big-endian natural), x from the
+// pool table (sorted index), bit LEADER.  Plain mode (x_item != null): x per
+// item, is_leader out.
+__global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restrict__ leader_in,
+                                               const int32_t* __restrict__ pool_sorted_idx,
+                                               const uint32_t* __restrict__ pool_x, const uint32_t* __restrict__ x_item,
+                                               int f_is_one, uint16_t* __restrict__ bits,
+                                               uint8_t* __restrict__ is_leader, int32_t* __restrict__ iters) {
+  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x[4];
+  if (x_item) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = x_item[4 * i + k];
+  } else {
+    const int32_t s = pool_sorted_idx[i];
+    if (s < 0) return;                       // VRFKeyUnknown precedes the leader check
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = pool_x[4 * s + k];
+  }
+  uint32_t raw[8], l[8];
+  load_words(raw, leader_in + 32 * i, 8);
+#pragma unroll
+  for (int k = 0; k < 8; k++) l[k] = __builtin_bswap32(raw[7 - k]);  // big-endian bytes -> LE words
+  int it = 0;
+  const bool lead = f_is_one ? true : leader_check(l, x, &it);
+  if (iters) iters[i] = it;
+  if (is_leader) { is_leader[i] = lead ? 1 : 0; return; }
+  if (!lead) bits[i] |= PRAOS_BIT_LEADER;
+}
+
+// ------------------------------------------------------------------ debug / self-test kernels
+__global__ void k_debug_fe(int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe x, y, z;
+  load_words(x.v, a + 32 * i, 8);
+  load_words(y.v, b + 32 * i, 8);
+  switch (op) {
+    case 0: fe_mul(z, x, y); break;
+    case 1: fe_sq(z, x); break;
+    case 2: fe_add(z, x, y); break;
+    case 3: fe_sub(z, x, y); break;
+    case 4: fe_invert(z, x); break;
+    case 5: fe_pow22523(z, x); break;
+    default: fe_canon(z, x); break;
+  }
+  store_words(r + 32 * i, z.v, 8);
+}
+
+__global__ void k_debug_sha512(size_t n, const uint8_t* prefix, const uint64_t* off, const uint32_t* len,
+                               const uint8_t* msg, uint8_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t pre[16], d[16];
+  load_words(pre, prefix + 64 * i, 16);
+  sha512_stream(d, pre, 64, msg + off[i], len[i]);
+  store_words(out + 64 * i, d, 16);
+}
+
+__global__ void k_debug_blake2b(size_t n, const uint8_t* in, uint8_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[16], h[8];
+  load_words(w, in + 64 * i, 16);
+  blake2b256_64(h, w);
+  store_words(out + 32 * i, h, 8);
+}
+
+__global__ void k_debug_sc_reduce(size_t n, const uint8_t* in, uint8_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[16], r[8];
+  load_words(w, in + 64 * i, 16);
+  sc_reduce512(r, w);
+  store_words(out + 32 * i, r, 8);
+}
+
+__global__ void k_debug_decode(size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8], e[8];
+  load_words(w, in + 32 * i, 8);
+  ge_p3 P;
+  ok[i] = ge_frombytes(P, w, false) ? 1 : 0;
+  ge_tobytes(e, P.X, P.Y, P.Z);
+  store_words(out + 32 * i, e, 8);
+}
+
+__global__ void __launch_bounds__(NT) k_debug_smul_base(size_t n, const ge_niels* gbtab, const uint8_t* s,
+                                                        uint8_t* out) {
+  __shared__ ge_niels sbtab[8];
+  __shared__ int8_t sdig[DIG_BYTES];
+  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  DigitPlanes dp{sdig, NT, 2};
+  uint32_t w[8], e[8];
+  load_words(w, s + 32 * i, 8);
+  store_digits(dp, 1, threadIdx.x, w);
+  ge_p3 R;
+  ge_scalarmult_base(R, dp, 1, threadIdx.x, btab);
+  ge_tobytes(e, R.X, R.Y, R.Z);
+  store_words(out + 32 * i, e, 8);
+}
+
+__global__ void k_debug_h2c(size_t n, const uint8_t* pk, const uint8_t* alpha, uint8_t* out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8], a[8], hs[8], ys[8];
+  load_words(w, pk + 32 * i, 8);
+  load_words(a, alpha + 32 * i, 8);
+  ge_p3 Y, H;
+  ge_frombytes(Y, w, false);
+  ge_enc_affine(ys, Y);
+  vrf_hash_to_curve(H, hs, ys, a);
+  store_words(out + 32 * i, hs, 8);
+}
+
+
+// ---- host launchers (kernels are only launchable from their own module)
+void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab) {
+  hipLaunchKernelGGL(k_init_btab, grid, block, 0, stream, btab);
+}
+
+void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* __restrict__ leader_in, const int32_t* __restrict__ pool_sorted_idx, const uint32_t* __restrict__ pool_x, const uint32_t* __restrict__ x_item, int f_is_one, uint16_t* __restrict__ bits, uint8_t* __restrict__ is_leader, int32_t* __restrict__ iters) {
+  hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one, bits, is_leader, iters);
+}
+
+void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r) {
+  hipLaunchKernelGGL(k_debug_fe, grid, block, 0, stream, op, n, a, b, r);
+}
+
+void launch_debug_sha512(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* prefix, const uint64_t* off, const uint32_t* len, const uint8_t* msg, uint8_t* out) {
+  hipLaunchKernelGGL(k_debug_sha512, grid, block, 0, stream, n, prefix, off, len, msg, out);
+}
+
+void launch_debug_blake2b(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* in, uint8_t* out) {
+  hipLaunchKernelGGL(k_debug_blake2b, grid, block, 0, stream, n, in, out);
+}
+
+void launch_debug_sc_reduce(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* in, uint8_t* out) {
+  hipLaunchKernelGGL(k_debug_sc_reduce, grid, block, 0, stream, n, in, out);
+}
+
+void launch_debug_decode(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok) {
+  hipLaunchKernelGGL(k_debug_decode, grid, block, 0, stream, n, in, out, ok);
+}
+
+void launch_debug_smul_base(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* s, uint8_t* out) {
+  hipLaunchKernelGGL(k_debug_smul_base, grid, block, 0, stream, n, gbtab, s, out);
+}
+
+void launch_debug_h2c(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* pk, const uint8_t* alpha, uint8_t* out) {
+  hipLaunchKernelGGL(k_debug_h2c, grid, block, 0, stream, n, pk, alpha, out);
+}

@@ -1,0 +1,256 @@
+// k_synth.hip -- synthetic chain generator kernels (db-synthesizer analogue).
+#include "kcommon.hpp"
+
+// ------------------------------------------------------------------ synthetic chain generator
+// seeds: Blake2b-256(tag || master seed(32) || BE32(i))
+__device__ __forceinline__ void derive_seed(uint32_t out[8], uint32_t tag, const uint32_t master[8], uint32_t i) {
+  uint64_t m[16];
+  // bytes: tag(1) master(32) i(4) = 37
+  uint8_t bytes[40];
+  bytes[0] = (uint8_t)tag;
+#pragma unroll
+  for (int k = 0; k < 32; k++) bytes[1 + k] = (uint8_t)(master[k / 4] >> (8 * (k % 4)));
+  bytes[33] = (uint8_t)(i >> 24); bytes[34] = (uint8_t)(i >> 16); bytes[35] = (uint8_t)(i >> 8); bytes[36] = (uint8_t)i;
+  bytes[37] = bytes[38] = bytes[39] = 0;
+#pragma unroll
+  for (int w = 0; w < 5; w++) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 7; k >= 0; k--) v = (v << 8) | bytes[8 * w + k];
+    m[w] = v;
+  }
+#pragma unroll
+  for (int w = 5; w < 16; w++) m[w] = 0;
+  uint64_t h[4];
+  blake2b_1block(h, m, 37, 32);
+#pragma unroll
+  for (int k = 0; k < 4; k++) { out[2 * k] = (uint32_t)h[k]; out[2 * k + 1] = (uint32_t)(h[k] >> 32); }
+}
+
+// KES expandSeed: r_b = Blake2b-256(b || s), b in {1, 2}
+__device__ __forceinline__ void kes_expand(uint32_t out[8], uint32_t b, const uint32_t s[8]) {
+  uint64_t m[16];
+  uint64_t prev = b & 0xff;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t w = ((uint64_t)s[2 * k + 1] << 32) | s[2 * k];
+    m[k] = prev | (w << 8);
+    prev = w >> 56;
+  }
+  m[4] = prev;
+#pragma unroll
+  for (int k = 5; k < 16; k++) m[k] = 0;
+  uint64_t h[4];
+  blake2b_1block(h, m, 33, 32);
+#pragma unroll
+  for (int k = 0; k < 4; k++) { out[2 * k] = (uint32_t)h[k]; out[2 * k + 1] = (uint32_t)(h[k] >> 32); }
+}
+
+// per pool: cold/vrf/kes seeds, cold pk, vrf pk, pool hash, vrf hash
+__global__ void __launch_bounds__(NT) k_synth_pools(uint32_t npools, const ge_niels* gbtab, const uint32_t* master,
+                                                    uint32_t* cold_seed, uint32_t* cold_pk, uint32_t* vrf_seed,
+                                                    uint32_t* vrf_pk, uint32_t* kes_seed, uint8_t* pool_hash28,
+                                                    uint8_t* pool_vrf32) {
+  __shared__ ge_niels sbtab[8];
+  __shared__ int8_t sdig[DIG_BYTES];
+  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  const uint32_t p = blockIdx.x * NT + threadIdx.x;
+  if (p >= npools) return;
+  DigitPlanes dp{sdig, NT, 2};
+  uint32_t ms[8], cs[8], vs[8], ks[8], az[16], cpk[8], vpk[8], h[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) ms[k] = master[k];
+  derive_seed(cs, 1, ms, p);
+  derive_seed(vs, 2, ms, p);
+  derive_seed(ks, 3, ms, p);
+  ed25519_expand(az, cs);
+  ed25519_pk_from_az(cpk, az, dp, threadIdx.x, btab);
+  ed25519_expand(az, vs);
+  ed25519_pk_from_az(vpk, az, dp, threadIdx.x, btab);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    cold_seed[8 * p + k] = cs[k]; cold_pk[8 * p + k] = cpk[k];
+    vrf_seed[8 * p + k] = vs[k]; vrf_pk[8 * p + k] = vpk[k]; kes_seed[8 * p + k] = ks[k];
+  }
+  blake2b_32(h, cpk, 28);
+  for (int k = 0; k < 28; k++) pool_hash28[28 * p + k] = (uint8_t)(h[k / 4] >> (8 * (k % 4)));
+  blake2b_32(h, vpk, 32);
+  for (int k = 0; k < 32; k++) pool_vrf32[32 * p + k] = (uint8_t)(h[k / 4] >> (8 * (k % 4)));
+}
+
+// per (pool, leaf): leaf seed by expandSeed down the path, leaf Ed25519 pk.
+// tree layout per pool: node[1..127] (heap order, root = 1), 8 words each;
+// leaves are nodes 64..127 (leaf j = node 64 + j).
+__global__ void __launch_bounds__(NT) k_synth_kes_leaves(uint32_t npools, const ge_niels* gbtab,
+                                                         const uint32_t* kes_seed, uint32_t* leaf_seed,
+                                                         uint32_t* tree) {
+  __shared__ ge_niels sbtab[8];
+  __shared__ int8_t sdig[DIG_BYTES];
+  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  const uint32_t g = blockIdx.x * NT + threadIdx.x;
+  if (g >= npools * 64u) return;
+  DigitPlanes dp{sdig, NT, 2};
+  const uint32_t p = g / 64, j = g % 64;
+  uint32_t s[8], r[8], az[16], pk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) s[k] = kes_seed[8 * p + k];
+  for (int d = 5; d >= 0; d--) {                 // top level first: bit 5 of j
+    kes_expand(r, ((j >> d) & 1) ? 2u : 1u, s);
+#pragma unroll
+    for (int k = 0; k < 8; k++) s[k] = r[k];
+  }
+  ed25519_expand(az, s);
+  ed25519_pk_from_az(pk, az, dp, threadIdx.x, btab);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    leaf_seed[8 * g + k] = s[k];
+    tree[(size_t)p * 128 * 8 + (64 + j) * 8 + k] = pk[k];
+  }
+}
+
+// per pool: internal nodes bottom-up, node v = Blake2b-256(node 2v || node 2v+1)
+__global__ void k_synth_kes_tree(uint32_t npools, uint32_t* tree) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npools) return;
+  uint32_t* t = tree + (size_t)p * 128 * 8;
+  for (int v = 63; v >= 1; v--) {
+    uint32_t in[16], h[8];
+    for (int k = 0; k < 8; k++) { in[k] = t[(2 * v) * 8 + k]; in[8 + k] = t[(2 * v + 1) * 8 + k]; }
+    blake2b256_64(h, in);
+    for (int k = 0; k < 8; k++) t[v * 8 + k] = h[k];
+  }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return x;
+}
+
+// per header: body bytes, OCert signature, KES signature, VRF proof/output.
+__global__ void __launch_bounds__(NT) k_synth_headers(
+    size_t n, const ge_niels* gbtab, uint32_t npools, uint64_t first_slot, uint64_t slot_stride,
+    uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral,
+    const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk,
+    const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk,
+    uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
+    uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes) {
+  __shared__ ge_niels sbtab[8];
+  __shared__ int8_t sdig[DIG_BYTES];
+  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  DigitPlanes dp{sdig, NT, 2};
+  const uint32_t p = (uint32_t)(mix64(i ^ salt) % npools);
+  const uint64_t s = first_slot + i * slot_stride;
+  const uint64_t kp = s / slots_per_kes_period;
+  const uint64_t c0 = kp - (kp % 60u);          // OCert issued at a period boundary <= kp
+  const uint64_t t = kp - c0;                   // < 60 <= maxKESEvo (62)
+  const uint64_t nn = c0 / 60u;                 // issue number grows with each new OCert
+  slot[i] = s; ocert_n[i] = nn; ocert_c0[i] = c0;
+  const uint32_t* T = tree + (size_t)p * 128 * 8;
+  uint32_t hv[8], cpk[8], vpk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { hv[k] = T[8 + k]; cpk[k] = cold_pk[8 * p + k]; vpk[k] = vrf_pk[8 * p + k]; }
+  store_words(hot_vk + 32 * i, hv, 8);
+  store_words(cold_vk + 32 * i, cpk, 8);
+  store_words(vrf_vk + 32 * i, vpk, 8);
+  // body: deterministic pseudo-random bytes (the signed HeaderBody stand-in)
+  const uint64_t boff = (uint64_t)i * (((uint64_t)blen + 7) & ~7ull);
+  body_off[i] = boff;
+  body_len[i] = blen;
+  uint64_t st = mix64(i * 0x9e3779b97f4a7c15ULL ^ salt ^ 0xb0d1);
+  for (uint32_t k = 0; k < blen; k += 8) {
+    st = mix64(st + k);
+    *(uint64_t*)(body_bytes + boff + k) = st;
+  }
+  for (uint32_t k = blen; k < ((blen + 7) & ~7u); k++) body_bytes[boff + k] = 0;
+  // OCert signature over hot_vk || BE64(n) || BE64(c0)
+  uint8_t* msg = msg_scratch + 48 * i;
+  store_words(msg, hv, 8);
+  for (int k = 0; k < 8; k++) { msg[32 + k] = (uint8_t)(nn >> (56 - 8 * k)); msg[40 + k] = (uint8_t)(c0 >> (56 - 8 * k)); }
+  uint32_t seed[8], az[16], sig[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) seed[k] = cold_seed[8 * p + k];
+  ed25519_expand(az, seed);
+  ed25519_sign_core(sig, az, cpk, msg, 48, dp, threadIdx.x, btab);
+  store_words(ocert_sig + 64 * i, sig, 16);
+  // KES: leaf t signs the body; path pairs from the tree (leaf level first)
+  const uint32_t leaf = (uint32_t)t;
+  uint32_t lpk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)p * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
+  ed25519_expand(az, seed);
+  ed25519_sign_core(sig, az, lpk, body_bytes + boff, blen, dp, threadIdx.x, btab);
+  uint8_t* ks = kes_sig + 448 * i;
+  store_words(ks, sig, 16);
+  uint32_t node = 64 + leaf;
+  for (int d = 1; d <= 6; d++) {                // level d pair = children of the ancestor at height d
+    const uint32_t parent = node >> 1;
+    store_words(ks + 64 * d, T + (2 * parent) * 8, 8);
+    store_words(ks + 64 * d + 32, T + (2 * parent + 1) * 8, 8);
+    node = parent;
+  }
+  // VRF proof for alpha = mkInputVRF(slot, eta0); output = proof_to_hash
+  uint32_t e0[8], alpha[8], proof[20];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { e0[k] = eta0[k]; seed[k] = vrf_seed[8 * p + k]; }
+  mk_input_vrf(alpha, s, e0, eta0_neutral != 0);
+  ed25519_expand(az, seed);
+  vrf_prove_core(proof, az, vpk, alpha, dp, threadIdx.x, btab);
+  store_words(vrf_proof + 80 * i, proof, 20);
+  // beta = SHA-512(0x04||0x03||enc(8 Gamma))
+  ge_p3 G, G2, G4, G8;
+  ge_frombytes(G, proof, false);
+  ge_p3_dbl_to_p3(G2, G);
+  ge_p3_dbl_to_p3(G4, G2);
+  ge_p3_dbl_to_p3(G8, G4);
+  uint32_t g8s[8], beta[16];
+  ge_tobytes(g8s, G8.X, G8.Y, G8.Z);
+  vrf_beta(beta, g8s);
+  store_words(vrf_out + 64 * i, beta, 16);
+}
+
+// Corruption model (consensus-testlib Test/Util/Corruption.hs:29-35): increment
+// the byte at offset k mod len of one chosen field.
+__global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig,
+                                uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off,
+                                const uint32_t* body_len, uint8_t* corrupted) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t r = mix64(i ^ salt ^ 0xc0ffee);
+  const bool c = (r % 10000u) < per10000;
+  corrupted[i] = c ? 1 : 0;
+  if (!c) return;
+  const uint32_t which = (uint32_t)((r >> 20) % 5u);
+  const uint32_t k = (uint32_t)(r >> 32);
+  switch (which) {
+    case 0: ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1; break;
+    case 1: kes_sig[448 * i + k % 448] += 1; corrupted[i] = 2; break;
+    case 2: vrf_proof[80 * i + k % 80] += 1; corrupted[i] = 3; break;
+    case 3: vrf_out[64 * i + k % 64] += 1; corrupted[i] = 4; break;
+    default:
+      if (body_len[i] == 0) { ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1; break; }
+      body_bytes[body_off[i] + k % body_len[i]] += 1; corrupted[i] = 5; break;
+  }
+}
+
+// ---- host launchers (kernels are only launchable from their own module)
+void launch_synth_pools(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const ge_niels* gbtab, const uint32_t* master, uint32_t* cold_seed, uint32_t* cold_pk, uint32_t* vrf_seed, uint32_t* vrf_pk, uint32_t* kes_seed, uint8_t* pool_hash28, uint8_t* pool_vrf32) {
+  hipLaunchKernelGGL(k_synth_pools, grid, block, 0, stream, npools, gbtab, master, cold_seed, cold_pk, vrf_seed, vrf_pk, kes_seed, pool_hash28, pool_vrf32);
+}
+
+void launch_synth_kes_leaves(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const ge_niels* gbtab, const uint32_t* kes_seed, uint32_t* leaf_seed, uint32_t* tree) {
+  hipLaunchKernelGGL(k_synth_kes_leaves, grid, block, 0, stream, npools, gbtab, kes_seed, leaf_seed, tree);
+}
+
+void launch_synth_kes_tree(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, uint32_t* tree) {
+  hipLaunchKernelGGL(k_synth_kes_tree, grid, block, 0, stream, npools, tree);
+}
+
+void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, uint32_t npools, uint64_t first_slot, uint64_t slot_stride, uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral, const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk, const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes) {
+  hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, first_slot, slot_stride, slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n, ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes);
+}
+
+void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted) {
+  hipLaunchKernelGGL(k_synth_corrupt, grid, block, 0, stream, n, per10000, salt, ocert_sig, kes_sig, vrf_proof, vrf_out, body_bytes, body_off, body_len, corrupted);
+}

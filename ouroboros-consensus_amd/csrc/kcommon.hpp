@@ -1,0 +1,41 @@
+#pragma once
+// kcommon.hpp -- shared pieces of the gfx950 kernel modules of libpraos_hip
+// (one header / signature per lane).
+//
+// Data layout in HBM (struct of arrays, one record per header per field,
+// records 8/16-byte aligned so each lane issues dwordx4 loads):
+//   slot u64[n] | cold_vk [n][32] | vrf_vk [n][32] | vrf_out [n][64] | vrf_proof [n][80]
+//   hot_vk [n][32] | ocert_n u64[n] | ocert_c0 u64[n] | ocert_sig [n][64]
+//   kes_sig [n][448] | body_off u64[n] | body_len u32[n] | body arena (8-aligned, +8 pad)
+// Outputs: bits u16[n] (OR-accumulated by the kernels), pool_idx i32[n],
+//   beta [n][64], leader [n][32] (big-endian natural), nonce [n][32].
+// Epoch tables: pool hash28 (7 words, sorted), vrf hash (8 words), x_raw (4 words).
+#include "praos_core.hpp"
+#include "leader.hpp"
+#include "praos_kernels.h"
+#include "launch.hpp"
+
+#define NT 256                      // threads per block (4 waves)
+#define DIG_BYTES (64 * 2 * NT)     // two digit planes
+
+__device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords) {
+  const uint4* q = (const uint4*)p;
+  for (int i = 0; i < nwords / 4; i++) {
+    const uint4 v = q[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int nwords) {
+  uint4* q = (uint4*)p;
+  for (int i = 0; i < nwords / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Stage the 8-entry niels table of B into LDS (all threads of the block).
+__device__ __forceinline__ const ge_niels* stage_btab(const ge_niels* __restrict__ g, ge_niels* s) {
+  const uint32_t* src = (const uint32_t*)g;
+  uint32_t* dst = (uint32_t*)s;
+  for (int i = threadIdx.x; i < 8 * 24; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  return s;
+}
+

@@ -1,0 +1,723 @@
+// praos_api.hip -- host side of libpraos_hip: context, device buffers, launches
+// and the sequential part of Praos.updateChainDepState (C++).
+// Single translation unit with the kernels (no relocatable device code).
+#include "praos_kernels.h"
+#include "launch.hpp"
+#include "host_util.hpp"
+
+static constexpr size_t NT = 256;                  // threads per block of the crypto kernels
+static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+struct praos_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  float kernel_ms[5] = {0, 0, 0, 0, 0};
+  std::string err;
+  ge_niels* btab = nullptr;
+  // epoch
+  bool have_epoch = false;
+  praos_params params{};
+  uint32_t eta0[8] = {0};
+  int eta0_neutral = 1;
+  uint32_t npools = 0;
+  uint32_t* d_pool_hash = nullptr;   // sorted, 7 words each
+  uint32_t* d_pool_vrf = nullptr;    // 8 words
+  uint32_t* d_pool_x = nullptr;      // 4 words
+  int32_t* d_pool_map = nullptr;     // sorted idx -> caller idx
+  uint32_t* d_eta0 = nullptr;
+  std::vector<praos_pool> pools;     // caller order
+  std::map<std::string, int32_t> pool_by_hash;
+};
+
+struct praos_batch {
+  size_t n = 0;
+  size_t body_bytes_len = 0;
+  uint64_t *slot = nullptr, *ocert_n = nullptr, *ocert_c0 = nullptr, *body_off = nullptr;
+  uint32_t* body_len = nullptr;
+  uint8_t *cold_vk = nullptr, *vrf_vk = nullptr, *vrf_out = nullptr, *vrf_proof = nullptr, *hot_vk = nullptr,
+          *ocert_sig = nullptr, *kes_sig = nullptr, *body = nullptr;
+  uint16_t* bits = nullptr;
+  int32_t *pool_idx = nullptr, *pool_sorted = nullptr;
+  uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
+  std::vector<void*> owned;
+};
+
+#define HIPCHK(ctx, x)                                                                    \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      (ctx)->err = std::string(#x) + ": " + hipGetErrorString(e_);                        \
+      return PRAOS_E_HIP;                                                                 \
+    }                                                                                     \
+  } while (0)
+
+static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+template <typename T>
+static hipError_t dalloc(praos_batch* b, T** p, size_t bytes) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+  if (e == hipSuccess) { b->owned.push_back(q); *p = (T*)q; }
+  return e;
+}
+
+extern "C" {
+
+int praos_abi_version(void) { return PRAOS_ABI_VERSION; }
+
+const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+praos_ctx* praos_open(int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+    fprintf(stderr, "praos_open: no HIP device %d (count %d)\n", device, ndev);
+    return nullptr;
+  }
+  praos_ctx* c = new praos_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  if (hipMalloc(&c->btab, 8 * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
+  launch_init_btab(dim3(1), dim3(64), c->stream, c->btab);
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
+    fprintf(stderr, "praos_open: init kernel failed\n");
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+static void free_epoch(praos_ctx* c) {
+  (void)hipFree(c->d_pool_hash); (void)hipFree(c->d_pool_vrf); (void)hipFree(c->d_pool_x);
+  (void)hipFree(c->d_pool_map); (void)hipFree(c->d_eta0);
+  c->d_pool_hash = nullptr; c->d_pool_vrf = nullptr; c->d_pool_x = nullptr; c->d_pool_map = nullptr; c->d_eta0 = nullptr;
+}
+
+void praos_close(praos_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  free_epoch(c);
+  (void)hipFree(c->btab);
+  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
+                    const praos_params* params) {
+  if (!c || !params || (npools && !pools) || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  free_epoch(c);
+  c->params = *params;
+  c->eta0_neutral = eta0 == nullptr;
+  std::memset(c->eta0, 0, 32);
+  if (eta0) std::memcpy(c->eta0, eta0, 32);
+  c->npools = npools;
+  c->pools.assign(pools, pools + npools);
+  c->pool_by_hash.clear();
+  std::vector<int32_t> order(npools);
+  for (uint32_t i = 0; i < npools; i++) order[i] = (int32_t)i;
+  std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return std::memcmp(pools[a].hash28, pools[b].hash28, 28) < 0;
+  });
+  std::vector<uint32_t> h(7 * (size_t)std::max(1u, npools)), v(8 * (size_t)std::max(1u, npools)),
+      x(4 * (size_t)std::max(1u, npools));
+  for (uint32_t s = 0; s < npools; s++) {
+    const praos_pool& p = pools[order[s]];
+    std::memcpy(&h[7 * s], p.hash28, 28);
+    std::memcpy(&v[8 * s], p.vrf_hash32, 32);
+    uint8_t xr[16];
+    if (!praos_host::leader_x_raw(xr, p.sigma_fp, params->c_raw)) {
+      c->err = "sigma * activeSlotLog out of range";
+      return PRAOS_E_ARG;
+    }
+    std::memcpy(&x[4 * s], xr, 16);
+    c->pool_by_hash[std::string((const char*)p.hash28, 28)] = order[s];
+  }
+  HIPCHK(c, hipMalloc(&c->d_pool_hash, h.size() * 4));
+  HIPCHK(c, hipMalloc(&c->d_pool_vrf, v.size() * 4));
+  HIPCHK(c, hipMalloc(&c->d_pool_x, x.size() * 4));
+  HIPCHK(c, hipMalloc(&c->d_pool_map, std::max<size_t>(1, npools) * 4));
+  HIPCHK(c, hipMalloc(&c->d_eta0, 32));
+  HIPCHK(c, hipMemcpy(c->d_pool_hash, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_pool_vrf, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_pool_x, x.data(), x.size() * 4, hipMemcpyHostToDevice));
+  if (npools) HIPCHK(c, hipMemcpy(c->d_pool_map, order.data(), npools * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->d_eta0, c->eta0, 32, hipMemcpyHostToDevice));
+  c->have_epoch = true;
+  return PRAOS_OK;
+}
+
+void praos_batch_free(praos_ctx* c, praos_batch* b) {
+  if (!b) return;
+  if (c) (void)hipSetDevice(c->device);
+  for (void* p : b->owned) (void)hipFree(p);
+  delete b;
+}
+
+praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
+  if (!c || !h) return nullptr;
+  if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+  praos_batch* b = new praos_batch();
+  const size_t n = h->n;
+  b->n = n;
+  // repack bodies 8-byte aligned (the SHA-512 feeder reads 64-bit words)
+  std::vector<uint64_t> off(n);
+  size_t total = 0;
+  bool bad_range = false;
+  for (size_t i = 0; i < n; i++) {
+    off[i] = total;
+    if (h->body_off[i] > h->body_bytes_len || h->body_len[i] > h->body_bytes_len - h->body_off[i]) bad_range = true;
+    total += (h->body_len[i] + 7) & ~(size_t)7;
+  }
+  std::vector<uint8_t> arena(total + 16, 0);
+  std::vector<uint32_t> len(n);
+  for (size_t i = 0; i < n; i++) {
+    const bool ok = h->body_off[i] <= h->body_bytes_len && h->body_len[i] <= h->body_bytes_len - h->body_off[i];
+    len[i] = ok ? h->body_len[i] : 0xffffffffu;  // marks out-of-range (kernel flags PRAOS_BIT_INPUT)
+    if (ok) std::memcpy(arena.data() + off[i], h->body_bytes + h->body_off[i], h->body_len[i]);
+  }
+  (void)bad_range;
+  b->body_bytes_len = total;
+  bool ok = true;
+  ok &= dalloc(b, &b->slot, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->ocert_n, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->ocert_c0, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body_off, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body_len, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->cold_vk, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_vk, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_out, 64 * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_proof, 80 * n) == hipSuccess;
+  ok &= dalloc(b, &b->hot_vk, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->ocert_sig, 64 * n) == hipSuccess;
+  ok &= dalloc(b, &b->kes_sig, 448 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body, total + 16) == hipSuccess;
+  ok &= dalloc(b, &b->bits, 2 * n) == hipSuccess;
+  ok &= dalloc(b, &b->pool_idx, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->pool_sorted, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->beta, 64 * n) == hipSuccess;
+  ok &= dalloc(b, &b->leader, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->nonce, 32 * n) == hipSuccess;
+  if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
+  auto up = [&](void* d, const void* s, size_t bytes) {
+    if (bytes) ok &= hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+  };
+  up(b->slot, h->slot, 8 * n);
+  up(b->ocert_n, h->ocert_n, 8 * n);
+  up(b->ocert_c0, h->ocert_c0, 8 * n);
+  up(b->body_off, off.data(), 8 * n);
+  up(b->body_len, len.data(), 4 * n);
+  up(b->cold_vk, h->cold_vk, 32 * n);
+  up(b->vrf_vk, h->vrf_vk, 32 * n);
+  up(b->vrf_out, h->vrf_out, 64 * n);
+  up(b->vrf_proof, h->vrf_proof, 80 * n);
+  up(b->hot_vk, h->hot_vk, 32 * n);
+  up(b->ocert_sig, h->ocert_sig, 64 * n);
+  up(b->kes_sig, h->kes_sig, 448 * n);
+  up(b->body, arena.data(), total + 16);
+  ok &= hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) { c->err = "upload failed"; praos_batch_free(c, b); return nullptr; }
+  return b;
+}
+
+int praos_batch_run(praos_ctx* c, praos_batch* b) {
+  if (!c || !b) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = b->n;
+  if (n == 0) return PRAOS_OK;
+  const praos_params& P = c->params;
+  HIPCHK(c, hipMemsetAsync(b->bits, 0, 2 * n, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  launch_ocert(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, b->cold_vk, b->hot_vk,
+                     b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, b->bits,
+                     (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  launch_kes(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, b->hot_vk, b->kes_sig,
+                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
+                     P.slots_per_kes_period, (const uint32_t*)nullptr, b->bits, (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, b->cold_vk, b->vrf_vk,
+                     b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                     c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, b->bits, b->pool_idx,
+                     b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+  launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, b->leader, b->pool_sorted,
+                     c->d_pool_x, (const uint32_t*)nullptr, (int)P.f_is_one, b->bits, (uint8_t*)nullptr,
+                     (int32_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  HIPCHK(c, hipGetLastError());
+  return PRAOS_OK;
+}
+
+int praos_batch_sync(praos_ctx* c) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < 4; k++) (void)hipEventElapsedTime(&c->kernel_ms[k], c->ev[k], c->ev[k + 1]);
+  (void)hipEventElapsedTime(&c->kernel_ms[4], c->ev[0], c->ev[4]);
+  return PRAOS_OK;
+}
+
+float praos_batch_kernel_ms(praos_ctx* c, int which) {
+  if (!c || which < 0 || which > 4) return -1.f;
+  return c->kernel_ms[which];
+}
+
+int praos_batch_download(praos_ctx* c, praos_batch* b, praos_out* out) {
+  if (!c || !b || !out || !out->bits) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t n = b->n;
+  if (n == 0) return PRAOS_OK;
+  HIPCHK(c, hipMemcpy(out->bits, b->bits, 2 * n, hipMemcpyDeviceToHost));
+  if (out->pool_idx) HIPCHK(c, hipMemcpy(out->pool_idx, b->pool_idx, 4 * n, hipMemcpyDeviceToHost));
+  if (out->beta) HIPCHK(c, hipMemcpy(out->beta, b->beta, 64 * n, hipMemcpyDeviceToHost));
+  if (out->leader) HIPCHK(c, hipMemcpy(out->leader, b->leader, 32 * n, hipMemcpyDeviceToHost));
+  if (out->nonce) HIPCHK(c, hipMemcpy(out->nonce, b->nonce, 32 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_verify_headers(praos_ctx* c, const praos_headers* h, praos_out* out) {
+  if (!c || !h || !out || !out->bits) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  if (h->n == 0) return PRAOS_OK;
+  praos_batch* b = praos_batch_upload(c, h);
+  if (!b) return PRAOS_E_OOM;
+  int r = praos_batch_run(c, b);
+  if (r == PRAOS_OK) r = praos_batch_sync(c);
+  if (r == PRAOS_OK) r = praos_batch_download(c, b, out);
+  praos_batch_free(c, b);
+  return r;
+}
+
+// ---------------------------------------------------------------- single-primitive batches
+}  // extern "C"
+namespace {
+struct Scratch {
+  praos_ctx* c;
+  std::vector<void*> ptrs;
+  bool ok = true;
+  explicit Scratch(praos_ctx* cc) : c(cc) {}
+  ~Scratch() { for (void* p : ptrs) (void)hipFree(p); }
+  template <typename T>
+  T* up(const T* src, size_t bytes) {
+    void* d = nullptr;
+    if (hipMalloc(&d, bytes ? bytes : 16) != hipSuccess) { ok = false; return nullptr; }
+    ptrs.push_back(d);
+    if (src && bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
+    return (T*)d;
+  }
+  template <typename T>
+  T* zeros(size_t bytes) {
+    T* d = up<T>(nullptr, bytes);
+    if (d && hipMemset(d, 0, bytes ? bytes : 16) != hipSuccess) ok = false;
+    return d;
+  }
+};
+}  // namespace
+extern "C" {
+
+int praos_verify_ocert(praos_ctx* c, size_t n, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
+                       const uint64_t* ocert_c0, const uint8_t* sig, uint8_t* ok) {
+  if (!c || (n && (!cold_vk || !hot_vk || !ocert_n || !ocert_c0 || !sig || !ok))) return PRAOS_E_ARG;
+  if (n == 0) return PRAOS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto dv = s.up(cold_vk, 32 * n);
+  auto dh = s.up(hot_vk, 32 * n);
+  auto dn = s.up(ocert_n, 8 * n);
+  auto dc = s.up(ocert_c0, 8 * n);
+  auto ds = s.up(sig, 64 * n);
+  auto dok = s.zeros<uint8_t>(n);
+  if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  launch_ocert(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, dv, dh, dn, dc, ds,
+                     (const uint64_t*)nullptr, (uint64_t)1, (uint64_t)0, (uint16_t*)nullptr, dok);
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&c->kernel_ms[0], c->ev[0], c->ev[1]);
+  HIPCHK(c, hipMemcpy(ok, dok, n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_verify_kes(praos_ctx* c, size_t n, const uint8_t* vk, const uint32_t* period, const uint8_t* sig,
+                     const uint64_t* msg_off, const uint32_t* msg_len, const uint8_t* msg_bytes, size_t msg_bytes_len,
+                     uint8_t* result) {
+  if (!c || (n && (!vk || !period || !sig || !msg_off || !msg_len || !result))) return PRAOS_E_ARG;
+  if (n == 0) return PRAOS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint64_t> off(n);
+  std::vector<uint32_t> len(n);
+  size_t total = 0;
+  for (size_t i = 0; i < n; i++) { off[i] = total; total += (msg_len[i] + 7) & ~(size_t)7; }
+  std::vector<uint8_t> arena(total + 16, 0);
+  for (size_t i = 0; i < n; i++) {
+    const bool okr = msg_off[i] <= msg_bytes_len && msg_len[i] <= msg_bytes_len - msg_off[i];
+    len[i] = okr ? msg_len[i] : 0xffffffffu;
+    if (okr && msg_len[i]) std::memcpy(arena.data() + off[i], msg_bytes + msg_off[i], msg_len[i]);
+  }
+  Scratch s(c);
+  auto dvk = s.up(vk, 32 * n);
+  auto dp = s.up(period, 4 * n);
+  auto dsig = s.up(sig, 448 * n);
+  auto doff = s.up(off.data(), 8 * n);
+  auto dlen = s.up(len.data(), 4 * n);
+  auto dmsg = s.up(arena.data(), arena.size());
+  auto dres = s.zeros<uint8_t>(n);
+  if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  launch_kes(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, dvk, dsig, doff, dlen, dmsg,
+                     total, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)1, dp, (uint16_t*)nullptr,
+                     dres);
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&c->kernel_ms[1], c->ev[0], c->ev[1]);
+  HIPCHK(c, hipMemcpy(result, dres, n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_verify_vrf(praos_ctx* c, size_t n, const uint8_t* vk, const uint8_t* proof, const uint8_t* alpha,
+                     uint8_t* ok, uint8_t* beta) {
+  if (!c || (n && (!vk || !proof || !alpha || !ok))) return PRAOS_E_ARG;
+  if (n == 0) return PRAOS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto dvk = s.up(vk, 32 * n);
+  auto dpr = s.up(proof, 80 * n);
+  auto dal = s.up(alpha, 32 * n);
+  auto dok = s.zeros<uint8_t>(n);
+  auto dbeta = s.zeros<uint8_t>(64 * n);
+  if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, (const uint8_t*)nullptr, dvk,
+                     (const uint8_t*)nullptr, dpr, (const uint64_t*)nullptr, (const uint32_t*)nullptr, 1,
+                     (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const int32_t*)nullptr, 0u, 0, dal,
+                     (uint16_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, dbeta, (uint8_t*)nullptr,
+                     (uint8_t*)nullptr, dok);
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&c->kernel_ms[2], c->ev[0], c->ev[1]);
+  HIPCHK(c, hipMemcpy(ok, dok, n, hipMemcpyDeviceToHost));
+  if (beta) HIPCHK(c, hipMemcpy(beta, dbeta, 64 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_check_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint8_t* sigma_fp,
+                       const praos_params* params, uint8_t* is_leader) {
+  if (!c || !params || (n && (!leader || !sigma_fp || !is_leader))) return PRAOS_E_ARG;
+  if (n == 0) return PRAOS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint32_t> x(4 * n);
+  for (size_t i = 0; i < n; i++) {
+    uint8_t xr[16];
+    if (!praos_host::leader_x_raw(xr, sigma_fp + 16 * i, params->c_raw)) { c->err = "x out of range"; return PRAOS_E_ARG; }
+    std::memcpy(&x[4 * i], xr, 16);
+  }
+  Scratch s(c);
+  auto dl = s.up(leader, 32 * n);
+  auto dx = s.up(x.data(), 16 * n);
+  auto dres = s.zeros<uint8_t>(n);
+  if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr,
+                     (const uint32_t*)nullptr, dx, (int)params->f_is_one, (uint16_t*)nullptr, dres, (int32_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  (void)hipEventElapsedTime(&c->kernel_ms[3], c->ev[0], c->ev[1]);
+  HIPCHK(c, hipMemcpy(is_leader, dres, n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+// ---------------------------------------------------------------- sequential part (host)
+// First-error-wins order of Praos.updateChainDepState (Praos.hs:441-459):
+// validateKESSignature (:567 c0<=kp, :568 kp<c0+maxKESEvo, :580 OCert, :582 KES,
+// :584-590 counter), then validateVRFSignature (:537 unknown, :539 vrf key,
+// :543 proof, :549 leader).  Counter source (:601-606): the counter map, else
+// 0 if the issuer is in the pool distribution, else missing.
+int praos_apply_batch(praos_ctx* c, const praos_headers* h, const praos_out* crypto, praos_counters* counters,
+                      uint8_t* verdict, size_t* chain_stop) {
+  if (!c || !h || !crypto || !crypto->bits || !verdict) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  std::map<std::string, uint64_t> cmap;
+  if (counters)
+    for (size_t k = 0; k < counters->m; k++)
+      cmap[std::string((const char*)counters->hash28 + 28 * k, 28)] = counters->counter[k];
+  size_t stop = h->n;
+  for (size_t i = 0; i < h->n; i++) {
+    const uint16_t b = crypto->bits[i];
+    std::string hk;
+    const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
+    if (pidx >= 0 && (uint32_t)pidx < c->npools) {
+      hk.assign((const char*)c->pools[pidx].hash28, 28);
+    } else {
+      uint8_t hh[28];
+      praos_host::blake2b(hh, 28, h->cold_vk + 32 * i, 32);
+      hk.assign((const char*)hh, 28);
+    }
+    const uint64_t n = h->ocert_n[i];
+    uint8_t v = PRAOS_V_OK;
+    if (b & PRAOS_BIT_INPUT) v = PRAOS_V_INPUT;
+    else if (b & PRAOS_BIT_KES_BEFORE_START) v = PRAOS_V_KES_BEFORE_START;
+    else if (b & PRAOS_BIT_KES_AFTER_END) v = PRAOS_V_KES_AFTER_END;
+    else if (b & PRAOS_BIT_OCERT_SIG) v = PRAOS_V_OCERT_SIG;
+    else if (b & (PRAOS_BIT_KES_MERKLE | PRAOS_BIT_KES_LEAF)) v = PRAOS_V_KES_SIG;
+    else {
+      auto it = cmap.find(hk);
+      bool have = true;
+      uint64_t m = 0;
+      if (it != cmap.end()) m = it->second;
+      else if (c->pool_by_hash.count(hk)) m = 0;
+      else have = false;
+      if (!have) v = PRAOS_V_COUNTER_MISSING;
+      else if (!(m <= n)) v = PRAOS_V_COUNTER_TOO_SMALL;
+      else if (!(n <= m + 1)) v = PRAOS_V_COUNTER_OVER_INC;
+      else if (b & PRAOS_BIT_VRF_KEY_UNKNOWN) v = PRAOS_V_VRF_KEY_UNKNOWN;
+      else if (b & PRAOS_BIT_VRF_KEY_WRONG) v = PRAOS_V_VRF_KEY_WRONG;
+      else if (b & (PRAOS_BIT_VRF_PROOF | PRAOS_BIT_VRF_OUTPUT)) v = PRAOS_V_VRF_BAD_PROOF;
+      else if (b & PRAOS_BIT_LEADER) v = PRAOS_V_LEADER_TOO_BIG;
+    }
+    verdict[i] = v;
+    if (v == PRAOS_V_OK) cmap[hk] = n;               // reupdateChainDepState, Praos.hs:484-485
+    else if (stop == h->n) stop = i;
+  }
+  if (chain_stop) *chain_stop = stop;
+  if (counters)
+    for (size_t k = 0; k < counters->m; k++)
+      counters->counter[k] = cmap[std::string((const char*)counters->hash28 + 28 * k, 28)];
+  return PRAOS_OK;
+}
+
+// ---------------------------------------------------------------- generator
+int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_params* params, const uint8_t eta0[32],
+                     praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out,
+                     uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig,
+                     uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes,
+                     uint8_t* corrupted) {
+  if (!c || !sp || !params || sp->npools == 0 || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = sp->n, np = sp->npools;
+  const size_t bstride = ((size_t)sp->body_len + 7) & ~(size_t)7;
+  Scratch s(c);
+  uint32_t master[8], e0[8] = {0};
+  std::memcpy(master, sp->seed, 32);
+  if (eta0) std::memcpy(e0, eta0, 32);
+  auto dmaster = s.up(master, 32);
+  auto de0 = s.up(e0, 32);
+  auto cold_seed = s.zeros<uint32_t>(32 * np);
+  auto cold_pk = s.zeros<uint32_t>(32 * np);
+  auto vrf_seed = s.zeros<uint32_t>(32 * np);
+  auto vrf_pk = s.zeros<uint32_t>(32 * np);
+  auto kes_seed = s.zeros<uint32_t>(32 * np);
+  auto ph = s.zeros<uint8_t>(28 * np);
+  auto pv = s.zeros<uint8_t>(32 * np);
+  auto leaf_seed = s.zeros<uint32_t>(32 * np * 64);
+  auto tree = s.zeros<uint32_t>(32 * np * 128);
+  auto scratch = s.zeros<uint8_t>(48 * n);
+  auto dslot = s.zeros<uint64_t>(8 * n);
+  auto dcold = s.zeros<uint8_t>(32 * n);
+  auto dvrfvk = s.zeros<uint8_t>(32 * n);
+  auto dvout = s.zeros<uint8_t>(64 * n);
+  auto dproof = s.zeros<uint8_t>(80 * n);
+  auto dhot = s.zeros<uint8_t>(32 * n);
+  auto dn = s.zeros<uint64_t>(8 * n);
+  auto dc0 = s.zeros<uint64_t>(8 * n);
+  auto dosig = s.zeros<uint8_t>(64 * n);
+  auto dksig = s.zeros<uint8_t>(448 * n);
+  auto doff = s.zeros<uint64_t>(8 * n);
+  auto dlen = s.zeros<uint32_t>(4 * n);
+  auto dbody = s.zeros<uint8_t>(bstride * n + 8);
+  auto dcor = s.zeros<uint8_t>(n);
+  if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
+  uint64_t salt = 0;
+  std::memcpy(&salt, sp->seed, 8);
+  launch_synth_pools(dim3(nblocks(np, NT)), dim3(NT), c->stream, (uint32_t)np, c->btab, dmaster,
+                     cold_seed, cold_pk, vrf_seed, vrf_pk, kes_seed, ph, pv);
+  launch_synth_kes_leaves(dim3(nblocks(np * 64, NT)), dim3(NT), c->stream, (uint32_t)np, c->btab,
+                     kes_seed, leaf_seed, tree);
+  launch_synth_kes_tree(dim3(nblocks(np, 64)), dim3(64), c->stream, (uint32_t)np, tree);
+  if (n) {
+    launch_synth_headers(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, (uint32_t)np,
+                       sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
+                       eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
+                       dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody);
+    launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
+                       salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor);
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<uint8_t> hh(28 * np), vv(32 * np);
+  HIPCHK(c, hipMemcpy(hh.data(), ph, 28 * np, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(vv.data(), pv, 32 * np, hipMemcpyDeviceToHost));
+  if (pools_out)
+    for (size_t p = 0; p < np; p++) {
+      std::memcpy(pools_out[p].hash28, &hh[28 * p], 28);
+      std::memcpy(pools_out[p].vrf_hash32, &vv[32 * p], 32);
+    }
+  if (n) {
+    auto dn2h = [&](void* h, const void* d, size_t bytes) -> int {
+      if (h) HIPCHK(c, hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost));
+      return PRAOS_OK;
+    };
+    int r = PRAOS_OK;
+    r |= dn2h(slot, dslot, 8 * n); r |= dn2h(cold_vk, dcold, 32 * n); r |= dn2h(vrf_vk, dvrfvk, 32 * n);
+    r |= dn2h(vrf_out, dvout, 64 * n); r |= dn2h(vrf_proof, dproof, 80 * n); r |= dn2h(hot_vk, dhot, 32 * n);
+    r |= dn2h(ocert_n, dn, 8 * n); r |= dn2h(ocert_c0, dc0, 8 * n); r |= dn2h(ocert_sig, dosig, 64 * n);
+    r |= dn2h(kes_sig, dksig, 448 * n); r |= dn2h(body_off, doff, 8 * n); r |= dn2h(body_len, dlen, 4 * n);
+    r |= dn2h(body_bytes, dbody, bstride * n + 8); r |= dn2h(corrupted, dcor, n);
+    if (r != PRAOS_OK) return PRAOS_E_HIP;
+  }
+  return PRAOS_OK;
+}
+
+// ---------------------------------------------------------------- debug entry points
+int praos_debug_fe(praos_ctx* c, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r) {
+  if (!c || !a || !r) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto da = s.up(a, 32 * n);
+  auto db = s.up(b ? b : a, 32 * n);
+  auto dr = s.zeros<uint8_t>(32 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_fe(dim3(nblocks(n, 64)), dim3(64), c->stream, op, n, da, db, dr);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(r, dr, 32 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_sha512(praos_ctx* c, size_t n, const uint8_t* prefix, const uint64_t* msg_off, const uint32_t* msg_len,
+                       const uint8_t* msg_bytes, size_t msg_bytes_len, uint8_t* out) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint64_t> off(n);
+  size_t total = 0;
+  for (size_t i = 0; i < n; i++) { off[i] = total; total += (msg_len[i] + 7) & ~(size_t)7; }
+  std::vector<uint8_t> arena(total + 16, 0);
+  for (size_t i = 0; i < n; i++)
+    if (msg_len[i]) std::memcpy(arena.data() + off[i], msg_bytes + msg_off[i], msg_len[i]);
+  (void)msg_bytes_len;
+  Scratch s(c);
+  auto dp = s.up(prefix, 64 * n);
+  auto doff = s.up(off.data(), 8 * n);
+  auto dlen = s.up(msg_len, 4 * n);
+  auto dmsg = s.up(arena.data(), arena.size());
+  auto dout = s.zeros<uint8_t>(64 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_sha512(dim3(nblocks(n, 64)), dim3(64), c->stream, n, dp, doff, dlen, dmsg, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, dout, 64 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_blake2b(praos_ctx* c, size_t n, const uint8_t* in64, uint8_t* out) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto di = s.up(in64, 64 * n);
+  auto dout = s.zeros<uint8_t>(32 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_blake2b(dim3(nblocks(n, 64)), dim3(64), c->stream, n, di, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, dout, 32 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_sc_reduce(praos_ctx* c, size_t n, const uint8_t* in64, uint8_t* out) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto di = s.up(in64, 64 * n);
+  auto dout = s.zeros<uint8_t>(32 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_sc_reduce(dim3(nblocks(n, 64)), dim3(64), c->stream, n, di, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, dout, 32 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_decode(praos_ctx* c, size_t n, const uint8_t* in32, uint8_t* out, uint8_t* ok) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto di = s.up(in32, 32 * n);
+  auto dout = s.zeros<uint8_t>(32 * n);
+  auto dok = s.zeros<uint8_t>(n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_decode(dim3(nblocks(n, 64)), dim3(64), c->stream, n, di, dout, dok);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, dout, 32 * n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(ok, dok, n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_scalarmult_base(praos_ctx* c, size_t n, const uint8_t* sc, uint8_t* out) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto di = s.up(sc, 32 * n);
+  auto dout = s.zeros<uint8_t>(32 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_smul_base(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, di, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, dout, 32 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint8_t* x_raw16, uint8_t* is_leader,
+                       int32_t* iters) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto dl = s.up(leader, 32 * n);
+  auto dx = s.up(x_raw16, 16 * n);
+  auto dres = s.zeros<uint8_t>(n);
+  auto dit = s.zeros<int32_t>(4 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr, (const uint32_t*)nullptr,
+                (const uint32_t*)dx, 0, (uint16_t*)nullptr, dres, dit);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(is_leader, dres, n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(iters, dit, 4 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_hash_to_curve(praos_ctx* c, size_t n, const uint8_t* pk, const uint8_t* alpha, uint8_t* out) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto dpk = s.up(pk, 32 * n);
+  auto dal = s.up(alpha, 32 * n);
+  auto dout = s.zeros<uint8_t>(32 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_debug_h2c(dim3(nblocks(n, 64)), dim3(64), c->stream, n, dpk, dal, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, dout, 32 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+}  // extern "C"

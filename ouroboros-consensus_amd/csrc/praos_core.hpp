@@ -1,0 +1,407 @@
+// praos_core.hpp -- per-lane verification procedures of the Praos header path.
+//
+//   ed25519_verify_core : libsodium 1.0.18 crypto_sign_ed25519_verify_detached
+//                         (via cardano-crypto-class Ed25519DSIGN; Praos.hs:580, KES leaf)
+//   kes_merkle          : cardano-crypto-class Sum6KES verifyKES tree walk (Praos.hs:582)
+//   vrf_verify_core     : IOG crypto_vrf_ietfdraft03_verify + proof_to_hash (Praos.hs:543)
+// plus the signing procedures used only by the synthetic-chain generator.
+#pragma once
+#include "hash.hpp"
+#include "scalarmult.hpp"
+#include "sc25519.hpp"
+
+FE_INLINE uint32_t fsh16(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbit(hi, lo, 16); }
+
+// SHA-512 of a message held in registers as LE u32 stream words S[0..NW),
+// already padded with the 0x80 byte; NBYTES = message length (pre-padding).
+template <int NW, int NBYTES>
+FE_INLINE void sha512_regs(uint32_t out[16], const uint32_t S[NW]) {
+  constexpr int NBLK = (NBYTES + 17 + 127) / 128;
+  uint64_t H[8];
+  sha512_init(H);
+#pragma unroll
+  for (int b = 0; b < NBLK; b++) {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      const int i0 = 32 * b + 2 * w, i1 = i0 + 1;
+      const uint32_t lo = i0 < NW ? S[i0] : 0u;
+      const uint32_t hi = i1 < NW ? S[i1] : 0u;
+      W[w] = bswap64(((uint64_t)hi << 32) | lo);
+    }
+    if (b == NBLK - 1) W[15] = (uint64_t)NBYTES * 8u;
+    sha512_block(H, W);
+  }
+  sha512_digest_words(out, H);
+}
+
+// stream = tag(2 bytes, LE u16) || parts (NP LE words) || 0x80
+template <int NP>
+FE_INLINE void stream2(uint32_t S[NP + 1], uint32_t tag16, const uint32_t P[NP]) {
+  S[0] = (tag16 & 0xffffu) | (P[0] << 16);
+#pragma unroll
+  for (int i = 1; i < NP; i++) S[i] = fsh16(P[i], P[i - 1]);
+  S[NP] = (P[NP - 1] >> 16) | (0x80u << 16);
+}
+
+// SHA-512 of (prefix[0..plen) || msg[0..len)); plen multiple of 8, <= 64.
+// msg is 8-byte aligned and readable up to round_up(len, 8).
+FE_INLINE void sha512_stream(uint32_t out[16], const uint32_t prefix[16], uint32_t plen,
+                             const uint8_t* __restrict__ msg, uint32_t len) {
+  uint64_t H[8];
+  sha512_init(H);
+  const uint32_t total = plen + len;
+  const uint32_t nblocks = (total + 17u + 127u) >> 7;
+  for (uint32_t blk = 0; blk < nblocks; blk++) {
+    uint64_t W[16];
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      const uint32_t off = blk * 128u + 8u * w;
+      uint64_t v;
+      if (blk == 0 && (uint32_t)(8 * w) < plen) {
+        v = be_word(prefix[2 * w], prefix[2 * w + 1]);
+      } else {
+        const uint32_t m = off - plen;
+        uint64_t raw = 0;
+        if (m < len) raw = *(const uint64_t*)(msg + m);
+        const uint32_t valid = len > m ? (len - m) : 0u;
+        if (valid < 8) {
+          const uint64_t keep = valid == 0 ? 0ULL : (~0ULL >> (64 - 8 * valid));
+          raw &= keep;
+          if (len >= m && len < m + 8) raw |= 0x80ULL << (8 * (len - m));
+        }
+        v = bswap64(raw);
+      }
+      W[w] = v;
+    }
+    if (blk == nblocks - 1) W[15] = (uint64_t)total * 8u;
+    sha512_block(H, W);
+  }
+  sha512_digest_words(out, H);
+}
+
+// ------------------------------------------------------------------ Ed25519
+// hram: SHA-512(R || A || M) digest words.  Checks in libsodium order; all
+// lanes do the full computation (rejections are folded in at the end).
+FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], const uint32_t S[8],
+                                   const uint32_t hram[16], DigitPlanes& dp, int t,
+                                   const ge_niels* __restrict__ btab) {
+  bool ok = sc_is_canonical(S) && !ge_has_small_order(R) && ge_is_canonical(pk) && !ge_has_small_order(pk);
+  ge_p3 A;
+  ok = ge_frombytes(A, pk, /*negate=*/true) && ok;
+  uint32_t h[8], s[8];
+  sc_reduce512(h, hram);
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;      // keep recoding in range
+  store_digits(dp, 0, t, h);
+  store_digits(dp, 1, t, s);
+  ge_p2 Rp;
+  ge_double_scalarmult_base(Rp, dp, 0, 1, t, A, 64, btab);   // [s]B - [h]A
+  uint32_t enc[8];
+  ge_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) eq &= enc[i] == R[i];
+  return ok && eq;
+}
+
+// OCert signable: hot_vk(32) || BE64(n) || BE64(c0)  -> SHA-512(R||A||M), 112 bytes
+FE_INLINE void ocert_hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], const uint32_t hot[8],
+                          uint64_t n, uint64_t c0) {
+  uint64_t H[8];
+  sha512_init(H);
+  uint64_t W[16];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    W[i] = be_word(R[2 * i], R[2 * i + 1]);
+    W[4 + i] = be_word(A[2 * i], A[2 * i + 1]);
+    W[8 + i] = be_word(hot[2 * i], hot[2 * i + 1]);
+  }
+  W[12] = n;                 // bytes are BE64(n): the big-endian word is n itself
+  W[13] = c0;
+  W[14] = 0x8000000000000000ULL;
+  W[15] = 0;
+  sha512_block(H, W);
+#pragma unroll
+  for (int i = 0; i < 15; i++) W[i] = 0;
+  W[15] = 112u * 8u;
+  sha512_block(H, W);
+  sha512_digest_words(out, H);
+}
+
+// ------------------------------------------------------------------ Sum6KES
+// Walks the tree top-down (Sum.verifyKES): at depth d the pair (vk0, vk1) is
+// sig[64 + 64*(d-1) ..); Blake2b-256(vk0||vk1) must equal the current vk;
+// t < 2^(d-1) selects vk0, else vk1 with t -= 2^(d-1).  Returns merkle_ok and
+// the leaf Ed25519 vk.  t is a Word (64-bit) as in the reference.
+FE_INLINE bool kes_merkle(uint32_t leaf_vk[8], const uint32_t vk[8], uint64_t t, const uint8_t* __restrict__ sig) {
+  uint32_t cur[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) cur[i] = vk[i];
+  bool ok = true;
+#pragma unroll
+  for (int d = 6; d >= 1; d--) {
+    uint32_t pair[16];
+    const uint4* p = (const uint4*)(sig + 64 + 64 * (d - 1));
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint4 v = p[q];
+      pair[4 * q] = v.x; pair[4 * q + 1] = v.y; pair[4 * q + 2] = v.z; pair[4 * q + 3] = v.w;
+    }
+    uint32_t h[8];
+    blake2b256_64(h, pair);
+#pragma unroll
+    for (int i = 0; i < 8; i++) ok &= h[i] == cur[i];
+    const uint64_t T = 1ull << (d - 1);
+    const bool right = t >= T;
+    t = right ? t - T : t;
+#pragma unroll
+    for (int i = 0; i < 8; i++) cur[i] = right ? pair[8 + i] : pair[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) leaf_vk[i] = cur[i];
+  return ok;
+}
+
+// ------------------------------------------------------------------ VRF draft-03
+__device__ __constant__ static const uint32_t FE_CURVE_A[8] = {486662u, 0, 0, 0, 0, 0, 0, 0};
+
+// libsodium ge25519_from_uniform (the VRF caller has cleared r's sign bit):
+// returns the point H = 8 * P and its encoding.
+FE_INLINE void vrf_from_uniform(ge_p3& H, uint32_t hs[8], const uint32_t r[8]) {
+  fe rr2, x, x2, x3, e, one, A;
+  fe_set(one, 1);
+  fe_const(A, FE_CURVE_A);
+  fe_frombytes32(rr2, r);
+  fe_sq(rr2, rr2);
+  fe_add(rr2, rr2, rr2);
+  fe_add(rr2, rr2, one);            // 1 + 2 r^2
+  fe_invert(rr2, rr2);
+  fe_mul(x, A, rr2);
+  fe_neg(x, x);                     // x = -A / (1 + 2 r^2)
+  fe_sq(x2, x);
+  fe_mul(x3, x, x2);
+  fe_add(e, x3, x);
+  fe_mul(x2, x2, A);
+  fe_add(e, x2, e);                 // e = x^3 + A x^2 + x
+  fe_chi(e, e);
+  fe ec;
+  fe_canon(ec, e);
+  const bool e_is_minus_1 = (ec.v[0] >> 8) & 1;   // libsodium: s[1] & 1 of the encoding
+  fe negx;
+  fe_neg(negx, x);
+  fe_cmov(x, negx, e_is_minus_1);
+  fe a2;
+  fe_set(a2, 0);
+  fe_cmov(a2, A, e_is_minus_1);
+  fe_sub(x, x, a2);
+  // y_ed = (x - 1) / (x + 1)
+  fe xp1, xm1, inv, yed;
+  fe_add(xp1, x, one);
+  fe_sub(xm1, x, one);
+  fe_invert(inv, xp1);
+  fe_mul(yed, xm1, inv);
+  uint32_t ys[8];
+  fe_tobytes32(ys, yed);            // sign bit 0
+  ge_p3 P;
+  ge_frombytes(P, ys, false);       // cannot fail (libsodium aborts otherwise)
+  ge_p3 Q;
+  ge_p3_dbl_to_p3(Q, P);
+  ge_p3_dbl_to_p3(P, Q);
+  ge_p3_dbl_to_p3(H, P);            // cofactor 8
+  ge_tobytes(hs, H.X, H.Y, H.Z);
+}
+
+// encoding of a point with Z == 1 (fresh from ge_frombytes)
+FE_INLINE void ge_enc_affine(uint32_t s[8], const ge_p3& P) {
+  fe_tobytes32(s, P.Y);
+  s[7] |= (uint32_t)fe_isnegative(P.X) << 31;
+}
+
+// r = first 32 bytes of SHA-512(0x04 || 0x01 || Y || alpha), sign bit cleared
+FE_INLINE void vrf_hash_to_curve(ge_p3& H, uint32_t hs[8], const uint32_t ys[8], const uint32_t alpha[8]) {
+  uint32_t P[16], S[17], d[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { P[i] = ys[i]; P[8 + i] = alpha[i]; }
+  stream2<16>(S, 0x0104u, P);
+  sha512_regs<17, 66>(d, S);
+  uint32_t r[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = d[i];
+  r[7] &= 0x7fffffffu;
+  vrf_from_uniform(H, hs, r);
+}
+
+// beta = SHA-512(0x04 || 0x03 || enc(8 Gamma))
+FE_INLINE void vrf_beta(uint32_t beta[16], const uint32_t g8[8]) {
+  uint32_t S[9];
+  stream2<8>(S, 0x0304u, g8);
+  sha512_regs<9, 34>(beta, S);
+}
+
+// c' = SHA-512(0x04 || 0x02 || H || Gamma || U || V)[0..16)
+FE_INLINE void vrf_hash_points(uint32_t c[4], const uint32_t h[8], const uint32_t g[8], const uint32_t u[8],
+                               const uint32_t v[8]) {
+  uint32_t P[32], S[33], d[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { P[i] = h[i]; P[8 + i] = g[i]; P[16 + i] = u[i]; P[24 + i] = v[i]; }
+  stream2<32>(S, 0x0204u, P);
+  sha512_regs<33, 130>(d, S);
+#pragma unroll
+  for (int i = 0; i < 4; i++) c[i] = d[i];
+}
+
+// Returns proof validity; beta always computed from Gamma (gamma_ok tells if it decoded).
+FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t pk[8], const uint32_t gamma[8],
+                               const uint32_t c4[4], const uint32_t s8[8], const uint32_t alpha[8],
+                               DigitPlanes& dp, int t, const ge_niels* __restrict__ btab) {
+  // vrf_validate_key: small order -> reject; ge25519_frombytes must succeed
+  bool ok = !ge_has_small_order(pk);
+  ge_p3 Y, G;
+  ok = ge_frombytes(Y, pk, false) && ok;
+  gamma_ok = ge_frombytes(G, gamma, false);
+  // s reduced mod L (sc25519_reduce of s || 0^32)
+  uint32_t sx[16], s[8], c[8];
+#pragma unroll
+  for (int i = 0; i < 16; i++) sx[i] = i < 8 ? s8[i] : 0u;
+  sc_reduce512(s, sx);
+#pragma unroll
+  for (int i = 0; i < 8; i++) c[i] = i < 4 ? c4[i] : 0u;
+  // H = hash_to_curve(canonical Y, alpha)
+  uint32_t ys[8], hs[8];
+  ge_enc_affine(ys, Y);
+  ge_p3 H;
+  vrf_hash_to_curve(H, hs, ys, alpha);
+  store_digits(dp, 0, t, c);
+  store_digits(dp, 1, t, s);
+  // U = [s]B - [c]Y
+  ge_p3 nY = Y;
+  fe_neg(nY.X, Y.X);
+  fe_neg(nY.T, Y.T);
+  ge_p2 U;
+  ge_double_scalarmult_base(U, dp, 0, 1, t, nY, 33, btab);
+  // V = [s]H - [c]Gamma
+  ge_p3 nG = G;
+  fe_neg(nG.X, G.X);
+  fe_neg(nG.T, G.T);
+  ge_p2 V;
+  ge_double_scalarmult_var(V, dp, 1, 0, t, H, nG, 33);
+  // 8 Gamma
+  ge_p3 G2, G4, G8;
+  ge_p3_dbl_to_p3(G2, G);
+  ge_p3_dbl_to_p3(G4, G2);
+  ge_p3_dbl_to_p3(G8, G4);
+  // batched inversion of U.Z, V.Z, G8.Z
+  fe zuv, zall, inv, iu, iv, ig;
+  fe_mul(zuv, U.Z, V.Z);
+  fe_mul(zall, zuv, G8.Z);
+  fe_invert(inv, zall);
+  fe_mul(ig, inv, zuv);             // 1/G8.Z
+  fe_mul(inv, inv, G8.Z);           // 1/(U.Z V.Z)
+  fe_mul(iu, inv, V.Z);
+  fe_mul(iv, inv, U.Z);
+  uint32_t us[8], vs[8], gs[8], g8s[8];
+  ge_tobytes_zi(us, U.X, U.Y, iu);
+  ge_tobytes_zi(vs, V.X, V.Y, iv);
+  ge_tobytes_zi(g8s, G8.X, G8.Y, ig);
+  ge_enc_affine(gs, G);
+  uint32_t cp[4];
+  vrf_hash_points(cp, hs, gs, us, vs);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 4; i++) eq &= cp[i] == c4[i];
+  vrf_beta(beta, g8s);
+  return ok && gamma_ok && eq;
+}
+
+// ------------------------------------------------------------------ signing (generator only)
+// az = SHA-512(seed), clamped
+FE_INLINE void ed25519_expand(uint32_t az[16], const uint32_t seed[8]) {
+  uint32_t S[9];
+#pragma unroll
+  for (int i = 0; i < 8; i++) S[i] = seed[i];
+  S[8] = 0x80u;
+  sha512_regs<9, 32>(az, S);
+  az[0] &= 0xfffffff8u;
+  az[7] &= 0x7fffffffu;
+  az[7] |= 0x40000000u;
+}
+
+FE_INLINE void ed25519_pk_from_az(uint32_t pk[8], const uint32_t az[16], DigitPlanes& dp, int t,
+                                  const ge_niels* __restrict__ btab) {
+  uint32_t a[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = az[i];
+  store_digits(dp, 1, t, a);
+  ge_p3 A;
+  ge_scalarmult_base(A, dp, 1, t, btab);
+  ge_tobytes(pk, A.X, A.Y, A.Z);
+}
+
+// RFC 8032 signature of msg (global memory, 8-aligned, len bytes)
+FE_INLINE void ed25519_sign_core(uint32_t sig[16], const uint32_t az[16], const uint32_t pk[8],
+                                 const uint8_t* __restrict__ msg, uint32_t len, DigitPlanes& dp, int t,
+                                 const ge_niels* __restrict__ btab) {
+  uint32_t pre[16], d[16], r[8], h[8], a[8];
+#pragma unroll
+  for (int i = 0; i < 16; i++) pre[i] = i < 8 ? az[8 + i] : 0u;
+  sha512_stream(d, pre, 32, msg, len);
+  sc_reduce512(r, d);
+  store_digits(dp, 1, t, r);
+  ge_p3 R;
+  ge_scalarmult_base(R, dp, 1, t, btab);
+  uint32_t rs[8];
+  ge_tobytes(rs, R.X, R.Y, R.Z);
+#pragma unroll
+  for (int i = 0; i < 8; i++) { pre[i] = rs[i]; pre[8 + i] = pk[i]; }
+  sha512_stream(d, pre, 64, msg, len);
+  sc_reduce512(h, d);
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = az[i];
+  uint32_t S[8];
+  sc_muladd(S, h, a, r);
+#pragma unroll
+  for (int i = 0; i < 8; i++) { sig[i] = rs[i]; sig[8 + i] = S[i]; }
+}
+
+// draft-03 prove (crypto_vrf_ietfdraft03_prove): proof = Gamma || c || s
+FE_INLINE void vrf_prove_core(uint32_t proof[20], const uint32_t az[16], const uint32_t pk[8],
+                              const uint32_t alpha[8], DigitPlanes& dp, int t, const ge_niels* __restrict__ btab) {
+  ge_p3 Y;
+  ge_frombytes(Y, pk, false);
+  uint32_t ys[8], hs[8];
+  ge_enc_affine(ys, Y);
+  ge_p3 H;
+  vrf_hash_to_curve(H, hs, ys, alpha);
+  uint32_t x[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = az[i];
+  store_digits(dp, 0, t, x);
+  ge_p3 G;
+  ge_scalarmult_var(G, dp, 0, t, H);
+  // k = SHA-512(az[32..64) || h_string) mod L
+  uint32_t S[17], d[16], k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) { S[i] = az[8 + i]; S[8 + i] = hs[i]; }
+  S[16] = 0x80u;
+  sha512_regs<17, 64>(d, S);
+  sc_reduce512(k, d);
+  store_digits(dp, 1, t, k);
+  ge_p3 kB, kH;
+  ge_scalarmult_base(kB, dp, 1, t, btab);
+  ge_scalarmult_var(kH, dp, 1, t, H);
+  uint32_t gs[8], kbs[8], khs[8];
+  ge_tobytes(gs, G.X, G.Y, G.Z);
+  ge_tobytes(kbs, kB.X, kB.Y, kB.Z);
+  ge_tobytes(khs, kH.X, kH.Y, kH.Z);
+  uint32_t c4[4];
+  vrf_hash_points(c4, hs, gs, kbs, khs);
+  uint32_t c[8], s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) c[i] = i < 4 ? c4[i] : 0u;
+  sc_muladd(s, c, x, k);
+#pragma unroll
+  for (int i = 0; i < 8; i++) { proof[i] = gs[i]; proof[12 + i] = s[i]; }
+#pragma unroll
+  for (int i = 0; i < 4; i++) proof[8 + i] = c4[i];
+}

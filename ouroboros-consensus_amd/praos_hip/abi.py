@@ -1,0 +1,401 @@
+"""ctypes binding of libpraos_hip.so (include/praos_hip.h).
+
+This is plumbing for tests and bench.py; the product is the C ABI itself.  The
+library is the gfx950 HIP build; there is deliberately no CPU fallback: every
+call here goes to the GPU, and a missing library raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "libpraos_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "praos_hip.h")
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u16p = ctypes.POINTER(ctypes.c_uint16)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+i32p = ctypes.POINTER(ctypes.c_int32)
+
+# bits (PRAOS_BIT_*)
+BIT_KES_BEFORE_START = 0x0001
+BIT_KES_AFTER_END = 0x0002
+BIT_OCERT_SIG = 0x0004
+BIT_KES_MERKLE = 0x0008
+BIT_KES_LEAF = 0x0010
+BIT_COUNTER_MISSING = 0x0020
+BIT_COUNTER_TOO_SMALL = 0x0040
+BIT_COUNTER_OVER_INC = 0x0080
+BIT_VRF_KEY_UNKNOWN = 0x0100
+BIT_VRF_KEY_WRONG = 0x0200
+BIT_VRF_PROOF = 0x0400
+BIT_VRF_OUTPUT = 0x0800
+BIT_LEADER = 0x1000
+BIT_INPUT = 0x8000
+
+# verdicts (enum praos_verdict)
+V_OK, V_KES_BEFORE_START, V_KES_AFTER_END, V_OCERT_SIG, V_KES_SIG, V_COUNTER_MISSING, \
+    V_COUNTER_TOO_SMALL, V_COUNTER_OVER_INC, V_VRF_KEY_UNKNOWN, V_VRF_KEY_WRONG, V_VRF_BAD_PROOF, \
+    V_LEADER_TOO_BIG, V_INPUT = range(13)
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("slots_per_kes_period", ctypes.c_uint64), ("max_kes_evo", ctypes.c_uint64),
+                ("f_is_one", ctypes.c_int32), ("vrf_check_output", ctypes.c_int32),
+                ("c_raw", ctypes.c_uint8 * 16)]
+
+
+class Pool(ctypes.Structure):
+    _fields_ = [("hash28", ctypes.c_uint8 * 28), ("vrf_hash32", ctypes.c_uint8 * 32),
+                ("sigma_fp", ctypes.c_uint8 * 16)]
+
+
+class Headers(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("slot", u64p), ("cold_vk", u8p), ("vrf_vk", u8p), ("vrf_out", u8p),
+                ("vrf_proof", u8p), ("hot_vk", u8p), ("ocert_n", u64p), ("ocert_c0", u64p), ("ocert_sig", u8p),
+                ("kes_sig", u8p), ("body_off", u64p), ("body_len", u32p), ("body_bytes", u8p),
+                ("body_bytes_len", ctypes.c_size_t)]
+
+
+class Out(ctypes.Structure):
+    _fields_ = [("bits", u16p), ("pool_idx", i32p), ("beta", u8p), ("leader", u8p), ("nonce", u8p)]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [("hash28", u8p), ("counter", u64p), ("m", ctypes.c_size_t)]
+
+
+class SynthParams(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("npools", ctypes.c_uint32), ("first_slot", ctypes.c_uint64),
+                ("slot_stride", ctypes.c_uint64), ("body_len", ctypes.c_uint32),
+                ("corrupt_per_10000", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32)]
+
+
+# every entry point declared in include/praos_hip.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "praos_abi_version": (ctypes.c_int, []),
+    "praos_open": (ctypes.c_void_p, [ctypes.c_int]),
+    "praos_close": (None, [ctypes.c_void_p]),
+    "praos_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "praos_set_epoch": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.POINTER(Pool), ctypes.c_uint32,
+                                       ctypes.POINTER(Params)]),
+    "praos_verify_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), ctypes.POINTER(Out)]),
+    "praos_batch_upload": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(Headers)]),
+    "praos_batch_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "praos_batch_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "praos_batch_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Out)]),
+    "praos_batch_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+    "praos_batch_kernel_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_int]),
+    "praos_verify_ocert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u64p, u64p, u8p, u8p]),
+    "praos_verify_kes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u32p, u8p, u64p, u32p, u8p,
+                                        ctypes.c_size_t, u8p]),
+    "praos_verify_vrf": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p, u8p, u8p]),
+    "praos_check_leader": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, ctypes.POINTER(Params), u8p]),
+    "praos_apply_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), ctypes.POINTER(Out),
+                                         ctypes.POINTER(Counters), u8p, ctypes.POINTER(ctypes.c_size_t)]),
+    "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
+                                        ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
+                                        u64p, u32p, u8p, u8p]),
+    "praos_debug_fe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, u8p, u8p, u8p]),
+    "praos_debug_sha512": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u64p, u32p, u8p, ctypes.c_size_t,
+                                          u8p]),
+    "praos_debug_blake2b": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p]),
+    "praos_debug_sc_reduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p]),
+    "praos_debug_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p]),
+    "praos_debug_scalarmult_base": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p]),
+    "praos_debug_leader": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p, i32p]),
+    "praos_debug_hash_to_curve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libpraos_hip.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with __graft_entry__.build() "
+                               "(make -C ouroboros-consensus_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def ptr(a, t=u8p):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(t)
+
+
+class PraosError(RuntimeError):
+    pass
+
+
+class Context:
+    """One praos_ctx (one GPU).  Mirrors the lifetime rules of the C ABI."""
+
+    def __init__(self, device: int = 0):
+        self.L = load()
+        self.h = self.L.praos_open(device)
+        if not self.h:
+            raise PraosError(f"praos_open({device}) failed (no HIP device?)")
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            self.L.praos_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def check(self, rc):
+        if rc != 0:
+            msg = self.L.praos_last_error(self.h)
+            raise PraosError(f"praos rc={rc}: {msg.decode() if msg else ''}")
+
+    # ---- epoch ----
+    def set_epoch(self, eta0, pools, params: Params):
+        """pools: list of (hash28: bytes, vrf_hash32: bytes, sigma_fp: int)."""
+        arr = (Pool * max(1, len(pools)))()
+        for i, (h, v, s) in enumerate(pools):
+            ctypes.memmove(arr[i].hash28, h, 28)
+            ctypes.memmove(arr[i].vrf_hash32, v, 32)
+            ctypes.memmove(arr[i].sigma_fp, int(s).to_bytes(16, "little"), 16)
+        e = None
+        if eta0 is not None:
+            eb = np.frombuffer(bytes(eta0), dtype=np.uint8).copy()
+            self._keep.append(eb)
+            e = ptr(eb)
+        self.check(self.L.praos_set_epoch(self.h, e, arr, len(pools), ctypes.byref(params)))
+        self._keep.append(arr)
+
+    # ---- headers ----
+    @staticmethod
+    def headers_struct(H: dict):
+        """H: dict of numpy arrays: slot u64[n], cold_vk u8[n,32], vrf_vk, vrf_out[n,64], vrf_proof[n,80],
+        hot_vk, ocert_n u64, ocert_c0 u64, ocert_sig[n,64], kes_sig[n,448], body_off u64, body_len u32,
+        body_bytes u8[]."""
+        s = Headers()
+        s.n = len(H["slot"])
+        s.slot = ptr(H["slot"], u64p)
+        for k in ("cold_vk", "vrf_vk", "vrf_out", "vrf_proof", "hot_vk", "ocert_sig", "kes_sig", "body_bytes"):
+            setattr(s, k, ptr(H[k]))
+        s.ocert_n = ptr(H["ocert_n"], u64p)
+        s.ocert_c0 = ptr(H["ocert_c0"], u64p)
+        s.body_off = ptr(H["body_off"], u64p)
+        s.body_len = ptr(H["body_len"], u32p)
+        s.body_bytes_len = len(H["body_bytes"])
+        return s
+
+    @staticmethod
+    def alloc_out(n):
+        return {"bits": np.zeros(n, np.uint16), "pool_idx": np.zeros(n, np.int32),
+                "beta": np.zeros((n, 64), np.uint8), "leader": np.zeros((n, 32), np.uint8),
+                "nonce": np.zeros((n, 32), np.uint8)}
+
+    @staticmethod
+    def out_struct(o):
+        s = Out()
+        s.bits = ptr(o["bits"], u16p)
+        s.pool_idx = ptr(o["pool_idx"], i32p)
+        s.beta = ptr(o["beta"])
+        s.leader = ptr(o["leader"])
+        s.nonce = ptr(o["nonce"])
+        return s
+
+    def verify_headers(self, H):
+        n = len(H["slot"])
+        o = self.alloc_out(n)
+        hs = self.headers_struct(H)
+        os_ = self.out_struct(o)
+        self.check(self.L.praos_verify_headers(self.h, ctypes.byref(hs), ctypes.byref(os_)))
+        return o
+
+    def upload(self, H):
+        hs = self.headers_struct(H)
+        b = self.L.praos_batch_upload(self.h, ctypes.byref(hs))
+        if not b:
+            self.check(-3)
+        return b
+
+    def run(self, b):
+        self.check(self.L.praos_batch_run(self.h, b))
+
+    def sync(self):
+        self.check(self.L.praos_batch_sync(self.h))
+
+    def kernel_ms(self, which):
+        return float(self.L.praos_batch_kernel_ms(self.h, which))
+
+    def download(self, b, n):
+        o = self.alloc_out(n)
+        os_ = self.out_struct(o)
+        self.check(self.L.praos_batch_download(self.h, b, ctypes.byref(os_)))
+        return o
+
+    def free(self, b):
+        self.L.praos_batch_free(self.h, b)
+
+    def apply_batch(self, H, crypto, counters=None):
+        """counters: dict hash28 -> int.  Returns (verdict u8[n], chain_stop, counters_out)."""
+        n = len(H["slot"])
+        hs = self.headers_struct(H)
+        os_ = self.out_struct(crypto)
+        verdict = np.zeros(n, np.uint8)
+        stop = ctypes.c_size_t(0)
+        cs = None
+        keys = list(counters.keys()) if counters else []
+        hk = np.frombuffer(b"".join(keys), dtype=np.uint8).copy() if keys else np.zeros(28, np.uint8)
+        cv = np.array([counters[k] for k in keys], dtype=np.uint64) if keys else np.zeros(1, np.uint64)
+        if counters is not None:
+            cs = Counters()
+            cs.hash28 = ptr(hk)
+            cs.counter = ptr(cv, u64p)
+            cs.m = len(keys)
+        self.check(self.L.praos_apply_batch(self.h, ctypes.byref(hs), ctypes.byref(os_),
+                                            ctypes.byref(cs) if cs is not None else None, ptr(verdict),
+                                            ctypes.byref(stop)))
+        out_counters = {k: int(cv[i]) for i, k in enumerate(keys)}
+        return verdict, stop.value, out_counters
+
+    # ---- single primitives ----
+    def verify_ocert(self, cold_vk, hot_vk, n_arr, c0_arr, sig):
+        n = len(n_arr)
+        ok = np.zeros(n, np.uint8)
+        self.check(self.L.praos_verify_ocert(self.h, n, ptr(cold_vk), ptr(hot_vk), ptr(n_arr, u64p),
+                                             ptr(c0_arr, u64p), ptr(sig), ptr(ok)))
+        return ok
+
+    def verify_kes(self, vk, period, sig, msgs):
+        n = len(period)
+        lens = np.array([len(m) for m in msgs], dtype=np.uint32)
+        offs = np.zeros(n, np.uint64)
+        if n > 1:
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        blob = np.frombuffer(b"".join(msgs) + b"\0" * 8, dtype=np.uint8).copy()
+        res = np.zeros(n, np.uint8)
+        self.check(self.L.praos_verify_kes(self.h, n, ptr(vk), ptr(period, u32p), ptr(sig), ptr(offs, u64p),
+                                           ptr(lens, u32p), ptr(blob), len(blob) - 8, ptr(res)))
+        return res
+
+    def verify_vrf(self, vk, proof, alpha):
+        n = len(vk)
+        ok = np.zeros(n, np.uint8)
+        beta = np.zeros((n, 64), np.uint8)
+        self.check(self.L.praos_verify_vrf(self.h, n, ptr(vk), ptr(proof), ptr(alpha), ptr(ok), ptr(beta)))
+        return ok, beta
+
+    def check_leader(self, leader_be, sigma_fp, params: Params):
+        n = len(leader_be)
+        res = np.zeros(n, np.uint8)
+        self.check(self.L.praos_check_leader(self.h, n, ptr(leader_be), ptr(sigma_fp), ctypes.byref(params),
+                                             ptr(res)))
+        return res
+
+    def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
+                   body_len=397, corrupt_per_10000=0):
+        sp = SynthParams()
+        sp.n = n
+        sp.npools = npools
+        sp.first_slot = first_slot
+        sp.slot_stride = slot_stride
+        sp.body_len = body_len
+        sp.corrupt_per_10000 = corrupt_per_10000
+        ctypes.memmove(sp.seed, seed, 32)
+        bstride = (body_len + 7) & ~7
+        H = {"slot": np.zeros(n, np.uint64), "cold_vk": np.zeros((n, 32), np.uint8),
+             "vrf_vk": np.zeros((n, 32), np.uint8), "vrf_out": np.zeros((n, 64), np.uint8),
+             "vrf_proof": np.zeros((n, 80), np.uint8), "hot_vk": np.zeros((n, 32), np.uint8),
+             "ocert_n": np.zeros(n, np.uint64), "ocert_c0": np.zeros(n, np.uint64),
+             "ocert_sig": np.zeros((n, 64), np.uint8), "kes_sig": np.zeros((n, 448), np.uint8),
+             "body_off": np.zeros(n, np.uint64), "body_len": np.zeros(n, np.uint32),
+             "body_bytes": np.zeros(bstride * n + 8, np.uint8)}
+        corrupted = np.zeros(n, np.uint8)
+        pools = (Pool * npools)()
+        e = None
+        if eta0 is not None:
+            eb = np.frombuffer(bytes(eta0), dtype=np.uint8).copy()
+            e = ptr(eb)
+        self.check(self.L.praos_synthesize(
+            self.h, ctypes.byref(sp), ctypes.byref(params), e, pools, ptr(H["slot"], u64p), ptr(H["cold_vk"]),
+            ptr(H["vrf_vk"]), ptr(H["vrf_out"]), ptr(H["vrf_proof"]), ptr(H["hot_vk"]), ptr(H["ocert_n"], u64p),
+            ptr(H["ocert_c0"], u64p), ptr(H["ocert_sig"]), ptr(H["kes_sig"]), ptr(H["body_off"], u64p),
+            ptr(H["body_len"], u32p), ptr(H["body_bytes"]), ptr(corrupted)))
+        H["body_bytes"] = H["body_bytes"][:bstride * n]
+        pool_list = [(bytes(p.hash28), bytes(p.vrf_hash32)) for p in pools]
+        return H, pool_list, corrupted
+
+    # ---- self tests ----
+    def debug_fe(self, op, a, b=None):
+        n = len(a)
+        r = np.zeros((n, 32), np.uint8)
+        self.check(self.L.praos_debug_fe(self.h, op, n, ptr(a), ptr(b if b is not None else a), ptr(r)))
+        return r
+
+    def debug_sha512(self, prefix, msgs):
+        n = len(msgs)
+        lens = np.array([len(m) for m in msgs], dtype=np.uint32)
+        offs = np.zeros(n, np.uint64)
+        if n > 1:
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        blob = np.frombuffer(b"".join(msgs) + b"\0" * 8, dtype=np.uint8).copy()
+        out = np.zeros((n, 64), np.uint8)
+        self.check(self.L.praos_debug_sha512(self.h, n, ptr(prefix), ptr(offs, u64p), ptr(lens, u32p), ptr(blob),
+                                             len(blob) - 8, ptr(out)))
+        return out
+
+    def debug_blake2b(self, in64):
+        out = np.zeros((len(in64), 32), np.uint8)
+        self.check(self.L.praos_debug_blake2b(self.h, len(in64), ptr(in64), ptr(out)))
+        return out
+
+    def debug_sc_reduce(self, in64):
+        out = np.zeros((len(in64), 32), np.uint8)
+        self.check(self.L.praos_debug_sc_reduce(self.h, len(in64), ptr(in64), ptr(out)))
+        return out
+
+    def debug_decode(self, in32):
+        n = len(in32)
+        out = np.zeros((n, 32), np.uint8)
+        ok = np.zeros(n, np.uint8)
+        self.check(self.L.praos_debug_decode(self.h, n, ptr(in32), ptr(out), ptr(ok)))
+        return out, ok
+
+    def debug_scalarmult_base(self, s):
+        out = np.zeros((len(s), 32), np.uint8)
+        self.check(self.L.praos_debug_scalarmult_base(self.h, len(s), ptr(s), ptr(out)))
+        return out
+
+    def debug_leader(self, leader_be, x_raw16):
+        n = len(leader_be)
+        res = np.zeros(n, np.uint8)
+        it = np.zeros(n, np.int32)
+        self.check(self.L.praos_debug_leader(self.h, n, ptr(leader_be), ptr(x_raw16), ptr(res), ptr(it, i32p)))
+        return res, it
+
+    def debug_hash_to_curve(self, pk, alpha):
+        out = np.zeros((len(pk), 32), np.uint8)
+        self.check(self.L.praos_debug_hash_to_curve(self.h, len(pk), ptr(pk), ptr(alpha), ptr(out)))
+        return out
+
+
+def params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=0, f_is_one=False, vrf_check_output=True):
+    p = Params()
+    p.slots_per_kes_period = slots_per_kes_period
+    p.max_kes_evo = max_kes_evo
+    p.f_is_one = int(bool(f_is_one))
+    p.vrf_check_output = int(bool(vrf_check_output))
+    ctypes.memmove(p.c_raw, (int(c_raw) & ((1 << 128) - 1)).to_bytes(16, "little"), 16)
+    return p

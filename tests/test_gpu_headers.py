@@ -1,0 +1,149 @@
+"""End-to-end header batches: GPU-synthesised chains (with seeded corruptions),
+validated by the GPU pipeline, checked header-by-header against the oracle's
+restatement of Praos.hs:558-606 / :528-556, and the sequential verdict order
+(praos_apply_batch) against a Python restatement of updateChainDepState."""
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from helpers import arr, b2b, corrupt, rng
+
+pytestmark = pytest.mark.gpu
+
+BITS_FROM_ORACLE = 0x0001 | 0x0002 | 0x0004 | 0x0008 | 0x0010 | 0x0100 | 0x0200 | 0x0400 | 0x0800 | 0x1000
+
+
+def _chain(ctx, n, npools, corrupt_per_10000, seed=b"\x42" * 32, f=Fraction(1, 20), eta0=None,
+           stride=20, body_len=397):
+    from praos_hip import abi, fixed
+    c_raw = fixed.active_slot_log(f)
+    p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw)
+    eta0 = eta0 if eta0 is not None else b2b(b"genesis")
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, seed, first_slot=1000, slot_stride=stride,
+                                         body_len=body_len, corrupt_per_10000=corrupt_per_10000)
+    # stake: sigma_i ~ 1/(i+10), exact rationals, normalised
+    w = [Fraction(1, i + 10) for i in range(npools)]
+    tot = sum(w)
+    sig = [fixed.from_rational(x / tot) for x in w]
+    pool_list = [(h, v, s) for (h, v), s in zip(pools, sig)]
+    ctx.set_epoch(eta0, pool_list, p)
+    return H, pool_list, corrupted, p, c_raw, eta0
+
+
+def _oracle_bits(oracle, H, pool_list, c_raw, eta0):
+    ep = oracle.make_epoch(eta0, 129600, 62, c_raw, pool_list)
+    out = []
+    for i in range(len(H["slot"])):
+        off, ln = int(H["body_off"][i]), int(H["body_len"][i])
+        h = {"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
+             "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
+             "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
+             "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
+             "body": bytes(H["body_bytes"][off:off + ln])}
+        out.append(oracle.praos_header(ep, h))
+    return out
+
+
+def test_synth_chain_parity(ctx, oracle):
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 300, 7, 1500)
+    o = ctx.verify_headers(H)
+    ref = _oracle_bits(oracle, H, pool_list, c_raw, eta0)
+    hash_of = {h: i for i, (h, _, _) in enumerate(pool_list)}
+    for i, r in enumerate(ref):
+        assert int(o["bits"][i]) & BITS_FROM_ORACLE == r["bits"], (i, hex(o["bits"][i]), hex(r["bits"]), corrupted[i])
+        assert bytes(o["beta"][i]) == r["beta"]
+        assert bytes(o["leader"][i]) == r["leader"]
+        assert bytes(o["nonce"][i]) == r["nonce"]
+        assert int(o["pool_idx"][i]) == hash_of.get(r["issuer_hash"], -1)
+    # uncorrupted headers carry valid crypto (only the leader check may fail)
+    clean = [i for i in range(len(ref)) if corrupted[i] == 0]
+    assert clean and all(int(o["bits"][i]) & ~0x1000 == 0 for i in clean)
+    assert any(corrupted) and any(int(o["bits"][i]) != 0 for i in range(len(ref)) if corrupted[i])
+
+
+def test_header_edge_inputs(ctx, oracle):
+    """Unknown issuer, wrong VRF key, KES period out of range, neutral nonce."""
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 64, 5, 0, seed=b"\x07" * 32)
+    n = len(H["slot"])
+    H["cold_vk"][1] = H["cold_vk"][0] if bytes(H["cold_vk"][0]) != bytes(H["cold_vk"][1]) else H["cold_vk"][2]
+    H["vrf_vk"][2] = np.frombuffer(b2b(b"x"), np.uint8)
+    H["ocert_c0"][3] = 10 ** 6                       # KESBeforeStart
+    H["slot"][4] = 129600 * 70                       # KESAfterEnd (kp - c0 >= 62)
+    H["cold_vk"][5] = np.frombuffer(b2b(b"nobody"), np.uint8)   # unknown pool
+    pools_wrong_vrf = list(pool_list)
+    o = ctx.verify_headers(H)
+    ref = _oracle_bits(oracle, H, pool_list, c_raw, eta0)
+    for i, r in enumerate(ref):
+        assert int(o["bits"][i]) & BITS_FROM_ORACLE == r["bits"], i
+    assert int(o["bits"][5]) & 0x0100
+    assert int(o["bits"][3]) & 0x0001 and int(o["bits"][4]) & 0x0002
+    # neutral epoch nonce: alpha = Blake2b256(BE64 slot)
+    ctx.set_epoch(None, pools_wrong_vrf, p)
+    o2 = ctx.verify_headers(H)
+    ref2 = _oracle_bits(oracle, H, pool_list, c_raw, None)
+    for i, r in enumerate(ref2):
+        assert int(o2["bits"][i]) & BITS_FROM_ORACLE == r["bits"], i
+
+
+def _apply_python(H, bits, pool_idx, pool_list, counters):
+    """Restatement of the first-error order of Praos.updateChainDepState."""
+    from praos_hip import abi
+    known = {h for h, _, _ in pool_list}
+    cm = dict(counters)
+    verdicts, stop = [], None
+    for i in range(len(H["slot"])):
+        b = int(bits[i])
+        hk = pool_list[pool_idx[i]][0] if pool_idx[i] >= 0 else b2b(bytes(H["cold_vk"][i]), 28)
+        n = int(H["ocert_n"][i])
+        if b & abi.BIT_INPUT:
+            v = abi.V_INPUT
+        elif b & abi.BIT_KES_BEFORE_START:
+            v = abi.V_KES_BEFORE_START
+        elif b & abi.BIT_KES_AFTER_END:
+            v = abi.V_KES_AFTER_END
+        elif b & abi.BIT_OCERT_SIG:
+            v = abi.V_OCERT_SIG
+        elif b & (abi.BIT_KES_MERKLE | abi.BIT_KES_LEAF):
+            v = abi.V_KES_SIG
+        else:
+            m = cm.get(hk, 0 if hk in known else None)
+            if m is None:
+                v = abi.V_COUNTER_MISSING
+            elif not m <= n:
+                v = abi.V_COUNTER_TOO_SMALL
+            elif not n <= m + 1:
+                v = abi.V_COUNTER_OVER_INC
+            elif b & abi.BIT_VRF_KEY_UNKNOWN:
+                v = abi.V_VRF_KEY_UNKNOWN
+            elif b & abi.BIT_VRF_KEY_WRONG:
+                v = abi.V_VRF_KEY_WRONG
+            elif b & (abi.BIT_VRF_PROOF | abi.BIT_VRF_OUTPUT):
+                v = abi.V_VRF_BAD_PROOF
+            elif b & abi.BIT_LEADER:
+                v = abi.V_LEADER_TOO_BIG
+            else:
+                v = abi.V_OK
+        verdicts.append(v)
+        if v == abi.V_OK:
+            cm[hk] = n
+        elif stop is None:
+            stop = i
+    return verdicts, (stop if stop is not None else len(H["slot"])), cm
+
+
+def test_apply_batch_order(ctx):
+    from praos_hip import abi, fixed
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 200, 6, 800, seed=b"\x09" * 32, f=Fraction(9, 10))
+    o = ctx.verify_headers(H)
+    r = rng(3)
+    # counters: some pools ahead (CounterTooSmall), some behind by 2 (OverIncremented)
+    counters = {pool_list[0][0]: 5, pool_list[1][0]: 0, b2b(b"retired", 28): 3}
+    H["ocert_n"][10] = 7
+    verdict, stop, cm = ctx.apply_batch(H, o, counters)
+    want, want_stop, want_cm = _apply_python(H, o["bits"], o["pool_idx"], pool_list, counters)
+    assert list(verdict) == want
+    assert stop == want_stop
+    for k in counters:
+        assert cm[k] == want_cm[k]
+    assert abi.V_OK in want and len(set(want)) >= 3
