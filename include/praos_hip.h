@@ -147,8 +147,13 @@ int praos_batch_run(praos_ctx* ctx, praos_batch* b);          /* async on the ct
 int praos_batch_sync(praos_ctx* ctx);
 int praos_batch_download(praos_ctx* ctx, praos_batch* b, praos_out* out);
 void praos_batch_free(praos_ctx* ctx, praos_batch* b);
+/* Options.  PRAOS_OPT_CONCURRENT (default 1): run the OCert, KES and VRF
+ * kernels on three streams so their tail waves overlap. */
+#define PRAOS_OPT_CONCURRENT 1
+int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
- * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run. */
+ * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run.  With concurrent
+ * streams, 0-2 are measured from the common start to each kernel's end. */
 float praos_batch_kernel_ms(praos_ctx* ctx, int which);
 
 /* ---- single-primitive batches (configs C2-C4); outputs 1 = valid, 0 = invalid ---- */

@@ -4,7 +4,7 @@
 // ------------------------------------------------------------------ OCert + KES period checks
 // bits |= KES_BEFORE_START / KES_AFTER_END / OCERT_SIG.  If ok_out != null the
 // kernel is the plain praos_verify_ocert batch (ok_out[i] = 1 when valid).
-__global__ void __launch_bounds__(NT) k_ocert(size_t n, const ge_niels* __restrict__ gbtab,
+__global__ void __launch_bounds__(NT, LB_ED) k_ocert(size_t n, const ge_niels* __restrict__ gbtab,
                                               const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ hot_vk,
                                               const uint64_t* __restrict__ ocert_n, const uint64_t* __restrict__ ocert_c0,
                                               const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot,
@@ -32,13 +32,13 @@ __global__ void __launch_bounds__(NT) k_ocert(size_t n, const ge_niels* __restri
   const uint64_t kp = slot[i] / slots_per_kes_period;        // Praos.hs:596-599
   if (!(c0 <= kp)) b |= PRAOS_BIT_KES_BEFORE_START;          // Praos.hs:567
   if (!(kp < c0 + max_kes_evo)) b |= PRAOS_BIT_KES_AFTER_END; // Praos.hs:568
-  bits[i] |= b;
+  bits[i] = b;
 }
 
 // ------------------------------------------------------------------ KES
 // Header mode: t = kp >= c0 ? kp - c0 : 0 (Praos.hs:570), result to bits.
 // Plain mode (result != null): t = period[i], result 0 ok / 1 Reject / 2 leaf.
-__global__ void __launch_bounds__(NT) k_kes(size_t n, const ge_niels* __restrict__ gbtab,
+__global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __restrict__ gbtab,
                                             const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig,
                                             const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len,
                                             const uint8_t* __restrict__ body, size_t body_bytes_len,
@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(NT) k_kes(size_t n, const ge_niels* __restrict
   if (!merkle_ok) b |= PRAOS_BIT_KES_MERKLE;
   else if (!leaf_ok) b |= PRAOS_BIT_KES_LEAF;
   if (!in_range) b |= PRAOS_BIT_INPUT;
-  bits[i] |= b;
+  bits[i] = b;
 }
 
 

@@ -40,29 +40,37 @@ __global__ void k_init_btab(ge_niels* btab) {
 __global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restrict__ leader_in,
                                                const int32_t* __restrict__ pool_sorted_idx,
                                                const uint32_t* __restrict__ pool_x, const uint32_t* __restrict__ x_item,
-                                               int f_is_one, uint16_t* __restrict__ bits,
-                                               uint8_t* __restrict__ is_leader, int32_t* __restrict__ iters) {
+                                               int f_is_one, const uint16_t* __restrict__ b_ocert,
+                                               const uint16_t* __restrict__ b_kes, const uint16_t* __restrict__ b_vrf,
+                                               uint16_t* __restrict__ bits, uint8_t* __restrict__ is_leader,
+                                               int32_t* __restrict__ iters) {
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
   uint32_t x[4];
+  bool skip = false;
+  uint16_t b = 0;
   if (x_item) {
 #pragma unroll
     for (int k = 0; k < 4; k++) x[k] = x_item[4 * i + k];
   } else {
+    b = b_ocert[i] | b_kes[i] | b_vrf[i];      // the three crypto kernels' bits
     const int32_t s = pool_sorted_idx[i];
-    if (s < 0) return;                       // VRFKeyUnknown precedes the leader check
+    skip = s < 0;                              // VRFKeyUnknown precedes the leader check
 #pragma unroll
-    for (int k = 0; k < 4; k++) x[k] = pool_x[4 * s + k];
+    for (int k = 0; k < 4; k++) x[k] = skip ? 0u : pool_x[4 * s + k];
   }
-  uint32_t raw[8], l[8];
-  load_words(raw, leader_in + 32 * i, 8);
-#pragma unroll
-  for (int k = 0; k < 8; k++) l[k] = __builtin_bswap32(raw[7 - k]);  // big-endian bytes -> LE words
+  bool lead = true;
   int it = 0;
-  const bool lead = f_is_one ? true : leader_check(l, x, &it);
+  if (!skip && !f_is_one) {
+    uint32_t raw[8], l[8];
+    load_words(raw, leader_in + 32 * i, 8);
+#pragma unroll
+    for (int k = 0; k < 8; k++) l[k] = __builtin_bswap32(raw[7 - k]);  // big-endian bytes -> LE words
+    lead = leader_check(l, x, &it);
+  }
   if (iters) iters[i] = it;
   if (is_leader) { is_leader[i] = lead ? 1 : 0; return; }
-  if (!lead) bits[i] |= PRAOS_BIT_LEADER;
+  bits[i] = b | (lead ? 0 : PRAOS_BIT_LEADER);
 }
 
 // ------------------------------------------------------------------ debug / self-test kernels
@@ -159,9 +167,6 @@ void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab)
   hipLaunchKernelGGL(k_init_btab, grid, block, 0, stream, btab);
 }
 
-void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* __restrict__ leader_in, const int32_t* __restrict__ pool_sorted_idx, const uint32_t* __restrict__ pool_x, const uint32_t* __restrict__ x_item, int f_is_one, uint16_t* __restrict__ bits, uint8_t* __restrict__ is_leader, int32_t* __restrict__ iters) {
-  hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one, bits, is_leader, iters);
-}
 
 void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r) {
   hipLaunchKernelGGL(k_debug_fe, grid, block, 0, stream, op, n, a, b, r);
@@ -189,4 +194,11 @@ void launch_debug_smul_base(dim3 grid, dim3 block, hipStream_t stream, size_t n,
 
 void launch_debug_h2c(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* pk, const uint8_t* alpha, uint8_t* out) {
   hipLaunchKernelGGL(k_debug_h2c, grid, block, 0, stream, n, pk, alpha, out);
+}
+void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in,
+                   const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one,
+                   const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits,
+                   uint8_t* is_leader, int32_t* iters) {
+  hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one, b_ocert,
+                     b_kes, b_vrf, bits, is_leader, iters);
 }

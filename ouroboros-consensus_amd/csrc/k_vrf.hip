@@ -5,7 +5,7 @@
 // Header mode: issuer hash -> pool (binary search), VRF key hash, alpha =
 // mkInputVRF(slot, eta0), proof verify, beta, output check, leader/nonce values.
 // Plain mode (ok_out != null): alpha given per item; ok_out, beta only.
-__global__ void __launch_bounds__(NT) k_vrf(size_t n, const ge_niels* __restrict__ gbtab,
+__global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const ge_niels* __restrict__ gbtab,
                                             const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ vrf_vk,
                                             const uint8_t* __restrict__ vrf_out, const uint8_t* __restrict__ vrf_proof,
                                             const uint64_t* __restrict__ slot, const uint32_t* __restrict__ eta0,
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(NT) k_vrf(size_t n, const ge_niels* __restrict
   if (beta_out) store_words(beta_out + 64 * i, beta, 16);
   pool_idx[i] = sidx < 0 ? -1 : pool_map[sidx];
   pool_sorted_idx[i] = sidx;
-  bits[i] |= b;
+  bits[i] = b;
 }
 
 

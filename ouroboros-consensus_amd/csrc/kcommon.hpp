@@ -16,6 +16,13 @@
 #include "launch.hpp"
 
 #define NT 256                      // threads per block (4 waves)
+// minimum waves per SIMD requested from the register allocator
+#ifndef LB_ED
+#define LB_ED 3
+#endif
+#ifndef LB_VRF
+#define LB_VRF 3
+#endif
 #define DIG_BYTES (64 * 2 * NT)     // two digit planes
 
 __device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords) {

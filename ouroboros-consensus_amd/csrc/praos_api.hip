@@ -18,7 +18,10 @@ static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
 struct praos_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};   // concurrent crypto kernels
+  int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   hipEvent_t ev[6] = {};
+  hipEvent_t side_ev[4] = {};
   float kernel_ms[5] = {0, 0, 0, 0, 0};
   std::string err;
   ge_niels* btab = nullptr;
@@ -45,6 +48,7 @@ struct praos_batch {
   uint8_t *cold_vk = nullptr, *vrf_vk = nullptr, *vrf_out = nullptr, *vrf_proof = nullptr, *hot_vk = nullptr,
           *ocert_sig = nullptr, *kes_sig = nullptr, *body = nullptr;
   uint16_t* bits = nullptr;
+  uint16_t* bits3 = nullptr;   // per-kernel bits: ocert | kes | vrf
   int32_t *pool_idx = nullptr, *pool_sorted = nullptr;
   uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
   std::vector<void*> owned;
@@ -88,6 +92,8 @@ praos_ctx* praos_open(int device) {
     return nullptr;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  for (auto& e : c->side_ev) (void)hipEventCreate(&e);
+  for (auto& st : c->side) (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
   if (hipMalloc(&c->btab, 8 * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
   launch_init_btab(dim3(1), dim3(64), c->stream, c->btab);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
@@ -111,6 +117,8 @@ void praos_close(praos_ctx* c) {
   free_epoch(c);
   (void)hipFree(c->btab);
   for (auto& e : c->ev) (void)hipEventDestroy(e);
+  for (auto& e : c->side_ev) (void)hipEventDestroy(e);
+  for (auto& st : c->side) (void)hipStreamDestroy(st);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -206,6 +214,7 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   ok &= dalloc(b, &b->kes_sig, 448 * n) == hipSuccess;
   ok &= dalloc(b, &b->body, total + 16) == hipSuccess;
   ok &= dalloc(b, &b->bits, 2 * n) == hipSuccess;
+  ok &= dalloc(b, &b->bits3, 6 * n) == hipSuccess;
   ok &= dalloc(b, &b->pool_idx, 4 * n) == hipSuccess;
   ok &= dalloc(b, &b->pool_sorted, 4 * n) == hipSuccess;
   ok &= dalloc(b, &b->beta, 64 * n) == hipSuccess;
@@ -240,35 +249,64 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   const size_t n = b->n;
   if (n == 0) return PRAOS_OK;
   const praos_params& P = c->params;
-  HIPCHK(c, hipMemsetAsync(b->bits, 0, 2 * n, c->stream));
+  uint16_t* bo = b->bits3;
+  uint16_t* bk = b->bits3 + n;
+  uint16_t* bv = b->bits3 + 2 * n;
+  const dim3 g(nblocks(n, NT)), blk(NT);
+  // The three crypto kernels are independent; run concurrently they fill each
+  // other's tail waves (one launch of 432k headers is ~3.3 rounds of resident
+  // waves).  Each writes its own bit array; k_leader joins and combines.
+  hipStream_t so = c->concurrent ? c->side[0] : c->stream;
+  hipStream_t sk = c->concurrent ? c->side[1] : c->stream;
+  hipStream_t sv = c->concurrent ? c->side[2] : c->stream;
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  launch_ocert(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, b->cold_vk, b->hot_vk,
-                     b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, b->bits,
-                     (uint8_t*)nullptr);
-  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
-  launch_kes(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, b->hot_vk, b->kes_sig,
-                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
-                     P.slots_per_kes_period, (const uint32_t*)nullptr, b->bits, (uint8_t*)nullptr);
-  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
-  launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, b->cold_vk, b->vrf_vk,
-                     b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
-                     c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, b->bits, b->pool_idx,
-                     b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr);
-  HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-  launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, b->leader, b->pool_sorted,
-                     c->d_pool_x, (const uint32_t*)nullptr, (int)P.f_is_one, b->bits, (uint8_t*)nullptr,
-                     (int32_t*)nullptr);
+  if (c->concurrent)
+    for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[0], 0));
+  launch_ocert(g, blk, so, n, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
+               P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->side_ev[0], so));
+  launch_kes(g, blk, sk, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body, b->body_bytes_len,
+             b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
+  launch_vrf(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->slot, c->d_eta0,
+             c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output,
+             (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta, b->leader, b->nonce,
+             (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
+  if (c->concurrent)
+    for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
+  launch_leader(g, blk, c->stream, n, b->leader, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
+                (int)P.f_is_one, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   HIPCHK(c, hipGetLastError());
   return PRAOS_OK;
+}
+
+int praos_set_option(praos_ctx* c, int opt, int value) {
+  if (!c) return PRAOS_E_ARG;
+  if (opt == PRAOS_OPT_CONCURRENT) { c->concurrent = value != 0; return PRAOS_OK; }
+  return PRAOS_E_ARG;
 }
 
 int praos_batch_sync(praos_ctx* c) {
   if (!c) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (int k = 0; k < 4; k++) (void)hipEventElapsedTime(&c->kernel_ms[k], c->ev[k], c->ev[k + 1]);
-  (void)hipEventElapsedTime(&c->kernel_ms[4], c->ev[0], c->ev[4]);
+  // per-kernel: from the common start event to each kernel's end event (with
+  // concurrent streams these overlap; which = 4 is the whole run)
+  float t[3] = {0, 0, 0};
+  for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&t[k], c->ev[0], c->side_ev[k]);
+  if (c->concurrent) {
+    for (int k = 0; k < 3; k++) c->kernel_ms[k] = t[k];
+  } else {
+    c->kernel_ms[0] = t[0];
+    c->kernel_ms[1] = t[1] - t[0];
+    c->kernel_ms[2] = t[2] - t[1];
+  }
+  float all = 0;
+  (void)hipEventElapsedTime(&all, c->ev[0], c->ev[4]);
+  c->kernel_ms[3] = all - (c->concurrent ? std::max(t[0], std::max(t[1], t[2])) : t[2]);
+  c->kernel_ms[4] = all;
   return PRAOS_OK;
 }
 
@@ -437,7 +475,8 @@ int praos_check_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr,
-                     (const uint32_t*)nullptr, dx, (int)params->f_is_one, (uint16_t*)nullptr, dres, (int32_t*)nullptr);
+                (const uint32_t*)nullptr, dx, (int)params->f_is_one, (const uint16_t*)nullptr,
+                (const uint16_t*)nullptr, (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, (int32_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -697,7 +736,8 @@ int praos_debug_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   auto dit = s.zeros<int32_t>(4 * n);
   if (!s.ok) return PRAOS_E_OOM;
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr, (const uint32_t*)nullptr,
-                (const uint32_t*)dx, 0, (uint16_t*)nullptr, dres, dit);
+                (const uint32_t*)dx, 0, (const uint16_t*)nullptr, (const uint16_t*)nullptr,
+                (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, dit);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(is_leader, dres, n, hipMemcpyDeviceToHost));

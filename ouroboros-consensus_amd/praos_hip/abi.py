@@ -11,6 +11,8 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG), "libpraos_hip.so")
+# A/B experiments only: load an alternative in-tree build (same ABI)
+LIB_PATH = os.environ.get("PRAOS_HIP_LIB", LIB_PATH)
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG)), "include", "praos_hip.h")
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -88,6 +90,7 @@ SIGNATURES = {
     "praos_batch_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Out)]),
     "praos_batch_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "praos_batch_kernel_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_int]),
+    "praos_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "praos_verify_ocert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u64p, u64p, u8p, u8p]),
     "praos_verify_kes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u32p, u8p, u64p, u32p, u8p,
                                         ctypes.c_size_t, u8p]),
@@ -235,6 +238,9 @@ class Context:
 
     def sync(self):
         self.check(self.L.praos_batch_sync(self.h))
+
+    def set_option(self, opt, value):
+        self.check(self.L.praos_set_option(self.h, opt, value))
 
     def kernel_ms(self, which):
         return float(self.L.praos_batch_kernel_ms(self.h, which))
