@@ -2,25 +2,29 @@
 """bench.py -- Praos header-crypto validation throughput on MI355X.
 
 Metric (BASELINE.json): Praos headers validated/sec (VRF + KES + OCert + leader).
-Workload: configs[4], a mainnet-shaped epoch replay: 432,000 Praos (Babbage)
-headers per GPU, 3000-pool stake distribution (sigma_i ~ 1/(i+10)), one epoch
-nonce, f = 1/20, slotsPerKESPeriod 129600, maxKESEvo 62, 397-byte signed
-bodies, 1% of headers corrupted with the consensus-testlib +1-byte model.  The
-chain is synthesised on the GPU by the library's generator (real Ed25519 /
-Sum6KES / ECVRF-draft03 signatures; db-synthesizer analogue) and is resident in
-HBM before the timed region.  One step = one full validation pass (all four
-kernels) over the GPU's shard.  Multi-GPU: one process per GPU; each rank owns
-a contiguous slot range of its own 432k headers (weak scaling, no collective on
-the data path; only the timing max-reduce).
+Default workload (no flags) = configs[4], a mainnet-shaped epoch replay:
+432,000 Praos (Babbage) headers per GPU, 3000-pool stake distribution
+(sigma_i ~ 1/(i+10), exact rationals), one epoch nonce, f = 1/20,
+slotsPerKESPeriod 129600, maxKESEvo 62, 397-byte signed bodies, 1% of headers
+corrupted with the consensus-testlib +1-byte model.  The chain is synthesised
+on the GPU by the library's generator (real Ed25519 / Sum6KES / ECVRF-draft03
+signatures; db-synthesizer analogue) and is resident in HBM before the timed
+region.  One step = one full validation pass (all kernels) over the GPU's
+shard.  Multi-GPU: one process per GPU; each rank owns a contiguous slot range
+of its own 432k headers (weak scaling, no collective on the data path; only
+the timing max-reduce).
+
+--config c2|c3|c4 measure the single-primitive configs (1M OCert verifies with
+distinct keys, 1M VRF verifies + leader checks, 1M Sum6KES verifies), c1 the
+10k-header / 100-pool CPU config (GPU and oracle side by side).
 
 CPU baseline: the C oracle (oracle/, a port of the reference semantics; the
 Haskell reference cannot run here) timed on the host over a bounded sample of
-the same headers with a process pool, cores stated; it also cross-checks the
-GPU bits on that sample.
+the same inputs with a process pool, cores stated; it also cross-checks the
+GPU result on that sample.
 """
 import argparse
 import json
-import math
 import multiprocessing as mp
 import os
 import sys
@@ -32,75 +36,102 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 
-# Algorithmic work per header (int32 lane-ops), counted from the kernel schedule
-# (DESIGN.md "Work model"): field mul 154, square 130, add/sub 17, SHA-512 block
-# 5000, BLAKE2b block 2700 int32 ops.
+# Algorithmic work per unit (int32 lane-ops), counted from the kernel schedule
+# (DESIGN.md sec. 4 "Work model"): field mul 154, square 130, add/sub 17,
+# SHA-512 block 5000, BLAKE2b block 2700 int32 ops.
 W_OCERT = 529_000
 W_KES = 555_000
 W_VRF = 1_150_000
 W_LEADER = 3_000
 W_HEADER = W_OCERT + W_KES + W_VRF + W_LEADER
-PEAK_INT32 = 256 * 64 * 2.4e9      # VOP3 integer issue: 64 lane-ops/clk/CU (measured: tools/microbench)
+PEAK_INT32 = 256 * 64 * 2.4e9      # VOP3 integer issue: 64 lane-ops/clk/CU (tools/microbench)
+MASK = {"ocert": 1, "kes": 2, "vrf": 4}
+
+CONFIGS = {
+    "c1": dict(headers=10_000, pools=100, kernels=7, nkes=0, metric="Praos headers validated/sec (CPU config C1)",
+               workload="configs[0]: 10k-header Praos (Babbage) chain, 100 pools (GPU and oracle side by side)"),
+    "c2": dict(headers=1_000_000, pools=None, kernels=1, nkes=64, metric="OCert Ed25519 verifications/sec",
+               workload="configs[1]: 1M OCert Ed25519 verifications, distinct cold keys, 1% corrupted"),
+    "c3": dict(headers=1_000_000, pools=3000, kernels=4, nkes=0,
+               metric="ECVRF-draft03 verifies + leader checks/sec",
+               workload="configs[2]: 1M ECVRF-ED25519-SHA512-Elligator2 verifies + leader checks, single eta0, "
+                        "3000 pools, 1% corrupted"),
+    "c4": dict(headers=1_000_000, pools=3000, kernels=2, nkes=0, metric="Sum6KES verifications/sec",
+               workload="configs[3]: 1M Sum6KES verifies (depth-6 Blake2b-256 Merkle path + Ed25519 leaf), "
+                        "397-byte messages, 1% corrupted"),
+    "c5": dict(headers=432_000, pools=3000, kernels=7, nkes=0,
+               metric="Praos headers validated/sec (VRF+KES+OCert+leader)",
+               workload="configs[4]: mainnet-shaped epoch replay, 432k Praos headers per GPU, 3000-pool stake "
+                        "distribution, single eta0, 1% corrupted"),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def epoch_setup(npools, f=Fraction(1, 20)):
-    import hashlib
-    from praos_hip import abi, fixed
-    c_raw = fixed.active_slot_log(f)
-    p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw, vrf_check_output=True)
-    eta0 = hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest()
+def stake(npools):
+    from praos_hip import fixed
     w = [Fraction(1, i + 10) for i in range(npools)]
     tot = sum(w)
-    sig = [fixed.from_rational(x / tot) for x in w]
-    return p, eta0, c_raw, sig
+    return [fixed.from_rational(x / tot) for x in w]
+
+
+def _hdr_dict(H, i):
+    off, ln = int(H["body_off"][i]), int(H["body_len"][i])
+    return {"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
+            "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
+            "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
+            "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
+            "body": bytes(H["body_bytes"][off:off + ln])}
 
 
 def _oracle_worker(payload):
+    """Checks one chunk with the oracle; returns (result bits, busy seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    eta0, c_raw, pools, headers = payload
-    ep = oracle.make_epoch(eta0, 129600, 62, c_raw, pools)
-    t0 = time.perf_counter()
-    bits = [oracle.praos_header(ep, h)["bits"] for h in headers]
-    return bits, time.perf_counter() - t0
+    kind, eta0, c_raw, pools, items = payload
+    out = []
+    if kind == "header":
+        ep = oracle.make_epoch(eta0, 129600, 62, c_raw, pools)
+        t0 = time.perf_counter()
+        out = [oracle.praos_header(ep, h)["bits"] for h in items]
+    elif kind == "ocert":
+        t0 = time.perf_counter()
+        for h in items:
+            m = h["hot_vk"] + h["n"].to_bytes(8, "big") + h["c0"].to_bytes(8, "big")
+            out.append(0 if oracle.ed25519_verify(h["cold_vk"], m, h["ocert_sig"]) else 0x0004)
+    elif kind == "kes":
+        t0 = time.perf_counter()
+        for h in items:
+            t = h["slot"] // 129600 - h["c0"]
+            r = oracle.kes_verify(h["hot_vk"], max(t, 0), h["body"], h["kes_sig"])
+            out.append({0: 0, 1: 0x0008, 2: 0x0010}[r])
+    else:
+        raise ValueError(kind)
+    return out, time.perf_counter() - t0
 
 
-def cpu_baseline(H, out_bits, eta0, c_raw, pool_list, seconds, workers):
-    """Times the oracle (port of the reference path) on a bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    oracle.lib()
-    per_hdr = 1.4e-3
+def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, pool_list, seconds, workers, per_item, mask):
     n_total = len(H["slot"])
-    n_sample = int(min(n_total, max(workers * 8, seconds * workers / per_hdr)))
+    n_sample = int(min(n_total, max(workers * 8, seconds * workers / per_item)))
     idx = np.linspace(0, n_total - 1, n_sample).astype(np.int64)
-    hs = []
-    for i in idx:
-        off, ln = int(H["body_off"][i]), int(H["body_len"][i])
-        hs.append({"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
-                   "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
-                   "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
-                   "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
-                   "body": bytes(H["body_bytes"][off:off + ln])})
-    chunks = [hs[k::workers] for k in range(workers)]
+    items = [_hdr_dict(H, i) for i in idx]
+    chunks = [items[k::workers] for k in range(workers)]
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(workers) as pool:
-        res = pool.map(_oracle_worker, [(eta0, c_raw, pool_list, c) for c in chunks])
+        res = pool.map(_oracle_worker, [(kind, eta0, c_raw, pool_list, c) for c in chunks])
     wall = time.perf_counter() - t0
     busy = max(r[1] for r in res)
     bits = [None] * n_sample
     for k, (b, _) in enumerate(res):
         for j, v in enumerate(b):
             bits[k + j * workers] = v
-    mask = 0x1F1F
-    agree = sum(1 for j, i in enumerate(idx) if (int(out_bits[i]) & mask) == bits[j])
-    return {"value": n_sample / busy, "unit": "headers/s", "cores": workers, "kind": "port",
-            "sample": f"{n_sample} headers evenly spaced over the benchmark chain, C oracle (oracle/praos.c) "
-                      f"in {workers} processes; busy {busy:.1f}s, wall {wall:.1f}s",
+    agree = sum(1 for j, i in enumerate(idx) if (int(gpu_bits[i]) & mask) == (bits[j] & mask))
+    return {"value": round(n_sample / busy, 1), "unit": "items/s" if kind != "header" else "headers/s",
+            "cores": workers, "kind": "port",
+            "sample": f"{n_sample} items evenly spaced over the benchmark input, C oracle (oracle/) in "
+                      f"{workers} processes; busy {busy:.1f}s, wall {wall:.1f}s",
             "parity_sample": {"n": n_sample, "bit_exact": agree}}
 
 
@@ -109,14 +140,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--headers", type=int, default=432_000, help="headers per GPU")
-    ap.add_argument("--pools", type=int, default=3000)
+    ap.add_argument("--config", default="c5", choices=sorted(CONFIGS))
+    ap.add_argument("--headers", type=int, default=None, help="items per GPU (default: the config's)")
+    ap.add_argument("--pools", type=int, default=None)
     ap.add_argument("--corrupt-per-10000", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,19 +163,30 @@ def main():
     import torch
 
     import praos_hip
+    from praos_hip import abi, fixed
+
     ctx = praos_hip.Context(local)
     ctx.set_option(1, args.concurrent)
-    n = args.headers
-    stride = 20                                    # 432k headers ~ 8.64M slots at f = 1/20
-    p, eta0, c_raw, sig = epoch_setup(args.pools)
+    ctx.set_option(2, cfg["kernels"])
+    n = args.headers or cfg["headers"]
+    npools = args.pools or cfg["pools"] or n           # c2: one distinct cold key per item
+    stride = 20                                        # one header per ~1/f slots
+    c_raw = fixed.active_slot_log(Fraction(1, 20))
+    p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw, vrf_check_output=True)
+    import hashlib
+    eta0 = hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest()
     t0 = time.perf_counter()
-    H, pools, corrupted = ctx.synthesize(n, args.pools, p, eta0, (b"\x5a" * 28) + rank.to_bytes(4, "little"),
-                                         first_slot=rank * n * stride, slot_stride=stride, body_len=397,
-                                         corrupt_per_10000=args.corrupt_per_10000)
-    pool_list = [(h, v, s) for (h, v), s in zip(pools, sig)]
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, (b"\x5a" * 27) + bytes([int(args.config[1])]) +
+                                         rank.to_bytes(4, "little"), first_slot=rank * n * stride,
+                                         slot_stride=stride, body_len=397, corrupt_per_10000=args.corrupt_per_10000,
+                                         nkes=cfg["nkes"])
+    if cfg["pools"] is None:
+        pool_list = []                                 # OCert-only config: no stake distribution needed
+    else:
+        pool_list = [(h, v, s) for (h, v), s in zip(pools, stake(npools))]
     ctx.set_epoch(eta0, pool_list, p)
     b = ctx.upload(H)
-    log(f"[rank {rank}] synthesised + uploaded {n} headers in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] {args.config}: synthesised + uploaded {n} items in {time.perf_counter() - t0:.1f}s")
 
     for _ in range(args.warmup):
         ctx.run(b)
@@ -154,7 +198,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.run(b)
-        ctx.sync()                                 # per-step HIP-event kernel times
+        ctx.sync()                                     # per-step HIP-event kernel times
         kms += [ctx.kernel_ms(k) for k in range(5)]
     torch.cuda.synchronize()
     if dist:
@@ -177,11 +221,15 @@ def main():
     out = ctx.download(b, n)
     ctx.free(b)
 
-    # self-check on the whole shard: clean headers must pass all crypto checks
+    # self-check on the whole shard: clean items must pass every check that ran
     clean = corrupted == 0
     crypto_bits = out["bits"] & ~np.uint16(0x1000)
     clean_ok = int((crypto_bits[clean] == 0).sum())
     corrupt_caught = int((crypto_bits[~clean] != 0).sum())
+    # corruptions that land in a field the config does not check cannot be caught
+    relevant = {1: (1,), 2: (2, 5), 4: (3, 4), 7: (1, 2, 3, 4, 5)}[cfg["kernels"]]
+    rel = np.isin(corrupted, relevant)
+    corrupt_caught_rel = int((crypto_bits[rel] != 0).sum())
 
     if rank != 0:
         return
@@ -189,36 +237,40 @@ def main():
     ms_step = dt * 1e3 / steps
     value = world * n * steps / dt
     kms /= steps
-    k_total = kms[4]                               # whole pipeline per step (HIP events)
-    achieved = n * W_HEADER / (k_total * 1e-3)
     per_kernel = {"ocert": kser[0], "kes": kser[1], "vrf": kser[2], "leader": kser[3]}
-    dominant = max(("ocert", "kes", "vrf"), key=lambda k: per_kernel[k])
+    ran = [k for k in ("ocert", "kes", "vrf") if cfg["kernels"] & MASK[k]]
+    dominant = max(ran, key=lambda k: per_kernel[k])
     wk = {"ocert": W_OCERT, "kes": W_KES, "vrf": W_VRF}[dominant]
     dom_achieved = n * wk / (per_kernel[dominant] * 1e-3)
+    w_pipe = sum({"ocert": W_OCERT, "kes": W_KES, "vrf": W_VRF + W_LEADER}[k] for k in ran)
+    pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
     line = {
-        "metric": "Praos headers validated/sec (VRF+KES+OCert+leader)",
-        "value": round(value, 1), "unit": "headers/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "metric": cfg["metric"],
+        "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
+        "n_gpus": world, "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u32 (GF(2^255-19) radix-2^32 limbs; Fixed E34 bignum)", "data": "synthetic",
-        "config": {"workload": "configs[4]: mainnet-shaped epoch replay, 432k Praos headers per GPU, "
-                               "3000-pool stake distribution, single eta0, 1% corrupted",
-                   "headers_per_gpu": n, "pools": args.pools, "active_slot_coeff": "1/20",
-                   "body_bytes": 397, "parallelism": f"shard-by-slot-range x{world}"},
+        "config": {"workload": cfg["workload"], "items_per_gpu": n, "pools": npools if cfg["pools"] else None,
+                   "active_slot_coeff": "1/20", "body_bytes": 397, "parallelism": f"shard-by-slot-range x{world}"},
         "roofline": {"bound": "valu-int32", "kernel": f"k_{dominant}",
                      "achieved": round(dom_achieved / 1e12, 3), "peak": round(PEAK_INT32 / 1e12, 2),
                      "unit": "T int32-ops/s", "frac": round(dom_achieved / PEAK_INT32, 4), "traffic": None,
-                     "pipeline_achieved": round(achieved / 1e12, 3),
-                     "pipeline_frac": round(achieved / PEAK_INT32, 4),
-                     "work_per_header": W_HEADER,
+                     "work_per_unit": wk, "pipeline_achieved": round(pipe_achieved / 1e12, 3),
+                     "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": w_pipe,
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},
-                     "pipeline_ms": round(k_total, 3), "concurrent_streams": bool(args.concurrent)},
-        "self_check": {"clean_headers": int(clean.sum()), "clean_crypto_ok": clean_ok,
-                       "corrupted": int((~clean).sum()), "corrupted_rejected": corrupt_caught,
-                       "leader_pass": int(((out["bits"] & 0x1000) == 0).sum())},
+                     "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent)},
+        "self_check": {"clean": int(clean.sum()), "clean_ok": clean_ok, "corrupted": int((~clean).sum()),
+                       "corrupted_rejected": corrupt_caught, "corrupted_in_checked_fields": int(rel.sum()),
+                       "corrupted_in_checked_fields_rejected": corrupt_caught_rel,
+                       "leader_pass": int(((out["bits"] & 0x1000) == 0).sum()) if cfg["kernels"] & 4 else None},
     }
     if world == 1 and not args.no_cpu:
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-        line["cpu_baseline"] = cpu_baseline(H, out["bits"], eta0, c_raw, pool_list, args.cpu_seconds, workers)
+        kind, per_item, mask = {7: ("header", 1.4e-3, 0x1F1F), 1: ("ocert", 0.3e-3, 0x0004),
+                                2: ("kes", 0.35e-3, 0x0018), 4: ("header", 1.4e-3, 0x1F00)}[cfg["kernels"]]
+        seconds = args.cpu_seconds if args.config != "c1" else 1e9      # c1: the whole chain on CPU
+        line["cpu_baseline"] = cpu_baseline(kind, H, out["bits"], eta0, c_raw, pool_list, seconds, workers,
+                                            per_item, mask)
         line["gpu_vs_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     print(json.dumps(line), flush=True)
     ctx.close()

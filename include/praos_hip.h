@@ -150,6 +150,10 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
 /* Options.  PRAOS_OPT_CONCURRENT (default 1): run the OCert, KES and VRF
  * kernels on three streams so their tail waves overlap. */
 #define PRAOS_OPT_CONCURRENT 1
+/* PRAOS_OPT_KERNELS: bit mask of the crypto kernels praos_batch_run launches
+ * (1 = OCert + KES-period checks, 2 = Sum6KES, 4 = VRF + leader; default 7).
+ * Used by the single-primitive benchmark configs; skipped checks report 0 bits. */
+#define PRAOS_OPT_KERNELS 2
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
  * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run.  With concurrent
@@ -198,6 +202,7 @@ typedef struct {
   uint64_t slot_stride;           /* slot of header i = first_slot + i * slot_stride */
   uint32_t body_len;              /* synthetic signed body length (CBOR-like bytes) */
   uint32_t corrupt_per_10000;     /* seeded corruptions (Corruption.hs model: +1 at a byte) */
+  uint32_t nkes;                  /* distinct Sum6KES keys (0 = one per pool); header of pool p uses key p mod nkes */
   uint8_t seed[32];
 } praos_synth_params;
 

@@ -128,7 +128,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 
 // per header: body bytes, OCert signature, KES signature, VRF proof/output.
 __global__ void __launch_bounds__(NT) k_synth_headers(
-    size_t n, const ge_niels* gbtab, uint32_t npools, uint64_t first_slot, uint64_t slot_stride,
+    size_t n, const ge_niels* gbtab, uint32_t npools, uint32_t nkes, uint64_t first_slot, uint64_t slot_stride,
     uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral,
     const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk,
     const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk,
@@ -147,7 +147,8 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   const uint64_t t = kp - c0;                   // < 60 <= maxKESEvo (62)
   const uint64_t nn = c0 / 60u;                 // issue number grows with each new OCert
   slot[i] = s; ocert_n[i] = nn; ocert_c0[i] = c0;
-  const uint32_t* T = tree + (size_t)p * 128 * 8;
+  const uint32_t kk = p % nkes;                 // KES key of this pool
+  const uint32_t* T = tree + (size_t)kk * 128 * 8;
   uint32_t hv[8], cpk[8], vpk[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) { hv[k] = T[8 + k]; cpk[k] = cold_pk[8 * p + k]; vpk[k] = vrf_pk[8 * p + k]; }
@@ -178,7 +179,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   const uint32_t leaf = (uint32_t)t;
   uint32_t lpk[8];
 #pragma unroll
-  for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)p * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
+  for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)kk * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
   ed25519_expand(az, seed);
   ed25519_sign_core(sig, az, lpk, body_bytes + boff, blen, dp, threadIdx.x, btab);
   uint8_t* ks = kes_sig + 448 * i;
@@ -247,8 +248,8 @@ void launch_synth_kes_tree(dim3 grid, dim3 block, hipStream_t stream, uint32_t n
   hipLaunchKernelGGL(k_synth_kes_tree, grid, block, 0, stream, npools, tree);
 }
 
-void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, uint32_t npools, uint64_t first_slot, uint64_t slot_stride, uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral, const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk, const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes) {
-  hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, first_slot, slot_stride, slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n, ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes);
+void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, uint32_t npools, uint32_t nkes, uint64_t first_slot, uint64_t slot_stride, uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral, const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk, const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes) {
+  hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, nkes, first_slot, slot_stride, slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n, ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes);
 }
 
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted) {

@@ -20,6 +20,7 @@ struct praos_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};   // concurrent crypto kernels
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
+  int kernels = 7;                                     // PRAOS_OPT_KERNELS
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   float kernel_ms[5] = {0, 0, 0, 0, 0};
@@ -262,16 +263,28 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[0], 0));
-  launch_ocert(g, blk, so, n, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
-               P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+  if (c->kernels & 1)
+    launch_ocert(g, blk, so, n, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
+                 P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+  else
+    HIPCHK(c, hipMemsetAsync(bo, 0, 2 * n, so));
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
-  launch_kes(g, blk, sk, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body, b->body_bytes_len,
-             b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr);
+  if (c->kernels & 2)
+    launch_kes(g, blk, sk, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body, b->body_bytes_len,
+               b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr);
+  else
+    HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
-  launch_vrf(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->slot, c->d_eta0,
-             c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output,
-             (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta, b->leader, b->nonce,
-             (uint8_t*)nullptr);
+  const bool do_vrf = (c->kernels & 4) != 0;
+  if (do_vrf)
+    launch_vrf(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->slot, c->d_eta0,
+               c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output,
+               (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta, b->leader, b->nonce,
+               (uint8_t*)nullptr);
+  else {
+    HIPCHK(c, hipMemsetAsync(bv, 0, 2 * n, sv));
+    HIPCHK(c, hipMemsetAsync(b->pool_sorted, 0xff, 4 * n, sv));   // no pool -> leader kernel skips
+  }
   HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
@@ -285,6 +298,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
 int praos_set_option(praos_ctx* c, int opt, int value) {
   if (!c) return PRAOS_E_ARG;
   if (opt == PRAOS_OPT_CONCURRENT) { c->concurrent = value != 0; return PRAOS_OK; }
+  if (opt == PRAOS_OPT_KERNELS) { c->kernels = value & 7; return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 
@@ -567,8 +581,9 @@ int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_par
   auto kes_seed = s.zeros<uint32_t>(32 * np);
   auto ph = s.zeros<uint8_t>(28 * np);
   auto pv = s.zeros<uint8_t>(32 * np);
-  auto leaf_seed = s.zeros<uint32_t>(32 * np * 64);
-  auto tree = s.zeros<uint32_t>(32 * np * 128);
+  const size_t nk = sp->nkes ? std::min<size_t>(sp->nkes, np) : np;
+  auto leaf_seed = s.zeros<uint32_t>(32 * nk * 64);
+  auto tree = s.zeros<uint32_t>(32 * nk * 128);
   auto scratch = s.zeros<uint8_t>(48 * n);
   auto dslot = s.zeros<uint64_t>(8 * n);
   auto dcold = s.zeros<uint8_t>(32 * n);
@@ -589,12 +604,12 @@ int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_par
   std::memcpy(&salt, sp->seed, 8);
   launch_synth_pools(dim3(nblocks(np, NT)), dim3(NT), c->stream, (uint32_t)np, c->btab, dmaster,
                      cold_seed, cold_pk, vrf_seed, vrf_pk, kes_seed, ph, pv);
-  launch_synth_kes_leaves(dim3(nblocks(np * 64, NT)), dim3(NT), c->stream, (uint32_t)np, c->btab,
+  launch_synth_kes_leaves(dim3(nblocks(nk * 64, NT)), dim3(NT), c->stream, (uint32_t)nk, c->btab,
                      kes_seed, leaf_seed, tree);
-  launch_synth_kes_tree(dim3(nblocks(np, 64)), dim3(64), c->stream, (uint32_t)np, tree);
+  launch_synth_kes_tree(dim3(nblocks(nk, 64)), dim3(64), c->stream, (uint32_t)nk, tree);
   if (n) {
     launch_synth_headers(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, (uint32_t)np,
-                       sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
+                       (uint32_t)nk, sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
                        dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,

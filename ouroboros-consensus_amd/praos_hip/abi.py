@@ -72,7 +72,7 @@ class Counters(ctypes.Structure):
 class SynthParams(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("npools", ctypes.c_uint32), ("first_slot", ctypes.c_uint64),
                 ("slot_stride", ctypes.c_uint64), ("body_len", ctypes.c_uint32),
-                ("corrupt_per_10000", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32)]
+                ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32)]
 
 
 # every entry point declared in include/praos_hip.h: name -> (restype, argtypes)
@@ -311,7 +311,7 @@ class Context:
         return res
 
     def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
-                   body_len=397, corrupt_per_10000=0):
+                   body_len=397, corrupt_per_10000=0, nkes=0):
         sp = SynthParams()
         sp.n = n
         sp.npools = npools
@@ -319,6 +319,7 @@ class Context:
         sp.slot_stride = slot_stride
         sp.body_len = body_len
         sp.corrupt_per_10000 = corrupt_per_10000
+        sp.nkes = nkes
         ctypes.memmove(sp.seed, seed, 32)
         bstride = (body_len + 7) & ~7
         H = {"slot": np.zeros(n, np.uint64), "cold_vk": np.zeros((n, 32), np.uint8),
