@@ -60,6 +60,9 @@ extern "C" {
 #define PRAOS_BIT_VRF_OUTPUT         0x0800u /* VRFKeyBadProof: certified output != proof_to_hash */
 #define PRAOS_BIT_LEADER             0x1000u /* VRFLeaderValueTooBig */
 #define PRAOS_BIT_INPUT              0x8000u /* malformed batch entry (e.g. body out of range) */
+/* TPraos (praos_verify_tpraos_headers) reuses bits 0-4, 8, 9, 12 and replaces 10/11: */
+#define PRAOS_BIT_TP_VRF_NONCE       0x0400u /* VRFKeyBadNonce (eta cert: proof or output) */
+#define PRAOS_BIT_TP_VRF_LEADER      0x0800u /* VRFKeyBadLeaderValue (leader cert) */
 
 /* ---- verdict codes of praos_apply_batch (first failing check, Praos.hs order) ---- */
 enum praos_verdict {
@@ -160,6 +163,26 @@ int praos_set_option(praos_ctx* ctx, int opt, int value);
  * streams, 0-2 are measured from the common start to each kernel's end. */
 float praos_batch_kernel_ms(praos_ctx* ctx, int which);
 
+/* ---- TPraos (Shelley..Alonzo), the d = 0 path of cardano-protocol-tpraos ----
+ * Replaces SL.updateChainDepState's crypto (TPraos.hs:378-387): OVERLAY
+ * praosVrfChecks (pool, VRF key, eta cert with mkSeed seedEta, leader cert with
+ * mkSeed seedL, checkLeaderValue on the 64-byte leader output, bound 2^512) and
+ * the OCERT rule (same predicates as Praos a2).  Overlay slots (d > 0, genesis
+ * delegates) are not handled. */
+typedef struct {
+  praos_headers h;                /* vrf_out / vrf_proof = bheaderEta; body = the signed BHBody bytes */
+  const uint8_t* leader_out;      /* bheaderL certified output, n*64 */
+  const uint8_t* leader_proof;    /* n*80 */
+} praos_tpraos_headers;
+typedef struct {
+  uint16_t* bits;                 /* n: PRAOS_BIT_* / PRAOS_BIT_TP_* */
+  int32_t* pool_idx;              /* n */
+  uint8_t* beta_eta;              /* n*64 */
+  uint8_t* beta_leader;           /* n*64 */
+  uint8_t* nonce;                 /* n*32: mkNonceFromOutputVRF (Blake2b-256 of the eta output) */
+} praos_tpraos_out;
+int praos_verify_tpraos_headers(praos_ctx* ctx, const praos_tpraos_headers* h, praos_tpraos_out* out);
+
 /* ---- single-primitive batches (configs C2-C4); outputs 1 = valid, 0 = invalid ---- */
 /* Ed25519 over the OCert signable hot_vk || BE64(n) || BE64(c0). */
 int praos_verify_ocert(praos_ctx* ctx, size_t n, const uint8_t* cold_vk, const uint8_t* hot_vk,
@@ -214,6 +237,15 @@ int praos_synthesize(praos_ctx* ctx, const praos_synth_params* sp, const praos_p
                      uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n,
                      uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off,
                      uint32_t* body_len, uint8_t* body_bytes, uint8_t* corrupted);
+
+/* TPraos variant of the generator: the VRF cert pair uses mkSeed alphas;
+ * leader_out/leader_proof receive the leader cert (n*64, n*80). */
+int praos_synthesize_tpraos(praos_ctx* ctx, const praos_synth_params* sp, const praos_params* params,
+                            const uint8_t eta0[32], praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk,
+                            uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n,
+                            uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off,
+                            uint32_t* body_len, uint8_t* body_bytes, uint8_t* leader_out, uint8_t* leader_proof,
+                            uint8_t* corrupted);
 
 /* ---- self-test entry points (unit tests of the device arithmetic) ---- */
 /* op: 0 mul, 1 sq, 2 add, 3 sub, 4 invert, 5 pow22523, 6 canon; inputs/outputs n*32 bytes LE */

@@ -128,6 +128,34 @@ typedef struct {
 
 void orc_praos_header(const orc_epoch *ep, const orc_header *h, orc_result *r);
 
+/* ---- TPraos header (Shelley..Alonzo), d = 0 path ----
+ * cardano-protocol-tpraos (>= 1.0.1 < 1.1, ouroboros-consensus-cardano.cabal:132):
+ * OVERLAY praosVrfChecks then OCERT (TPraos.hs:378-398 calls SL.updateChainDepState).
+ *   seed alpha = Blake2b256(BE64 slot || eta0) XOR Blake2b256(BE64 k), k = 0 (eta), 1 (leader)
+ *   leader value = certified leader output (64 B) as a big-endian natural < 2^512
+ *   nonce        = Blake2b256(certified eta output)                                   */
+enum {
+  ORC_BIT_TP_VRF_NONCE   = 1u << 10,  /* VRFKeyBadNonce (proof rejected or output mismatch) */
+  ORC_BIT_TP_VRF_LEADER  = 1u << 11,  /* VRFKeyBadLeaderValue */
+};
+typedef struct {
+  orc_header h;             /* vrf_out / vrf_proof = the eta certificate */
+  uint8_t leader_out[64];
+  uint8_t leader_proof[80];
+} orc_tp_header;
+typedef struct {
+  uint32_t bits;
+  int32_t pool_idx;
+  uint8_t beta_eta[64];
+  uint8_t beta_leader[64];
+  uint8_t nonce[32];
+} orc_tp_result;
+void orc_tpraos_seed(uint8_t out[32], uint64_t slot, const uint8_t eta0[32], int eta0_neutral, uint64_t k);
+void orc_tpraos_header(const orc_epoch *ep, const orc_tp_header *h, orc_tp_result *r);
+/* leader check against a 512-bit big-endian value (TPraos checkLeaderValue) */
+int orc_check_leader512(const uint8_t leader_be[64], const uint8_t sigma_fp[16], const uint8_t c_raw[16],
+                        int f_is_one, int *iters);
+
 #ifdef __cplusplus
 }
 #endif

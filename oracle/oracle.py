@@ -42,6 +42,9 @@ def lib():
         L.orc_point_order_divides.argtypes = [c.c_char_p, c.c_int]
         L.orc_praos_header.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p]
         L.orc_scalarmult_base.argtypes = [c.c_char_p, c.c_char_p]
+        L.orc_tpraos_header.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p]
+        L.orc_tpraos_seed.argtypes = [c.c_char_p, c.c_uint64, c.c_char_p, c.c_int, c.c_uint64]
+        L.orc_check_leader512.argtypes = [c.c_char_p, c.c_char_p, c.c_char_p, c.c_int, c.POINTER(c.c_int)]
         L.orc_ge_reencode.argtypes = [c.c_char_p, c.c_char_p]
         L.orc_vrf_hash_to_curve.argtypes = [c.c_char_p, c.c_char_p, c.c_char_p, c.c_size_t]
         _lib = L
@@ -225,3 +228,46 @@ def praos_header(ep, h: dict) -> dict:
     lib().orc_praos_header(ctypes.byref(ep), ctypes.byref(H), ctypes.byref(R))
     return {"bits": R.bits, "pool_idx": R.pool_idx, "beta": bytes(R.beta),
             "leader": bytes(R.leader), "nonce": bytes(R.nonce), "issuer_hash": bytes(R.issuer_hash)}
+
+
+class TPHeader(ctypes.Structure):
+    _fields_ = [("h", Header), ("leader_out", ctypes.c_uint8 * 64), ("leader_proof", ctypes.c_uint8 * 80)]
+
+
+class TPResult(ctypes.Structure):
+    _fields_ = [("bits", ctypes.c_uint32), ("pool_idx", ctypes.c_int32), ("beta_eta", ctypes.c_uint8 * 64),
+                ("beta_leader", ctypes.c_uint8 * 64), ("nonce", ctypes.c_uint8 * 32)]
+
+
+def tpraos_seed(slot: int, eta0, k: int) -> bytes:
+    o = ctypes.create_string_buffer(32)
+    lib().orc_tpraos_seed(o, slot, eta0 if eta0 is not None else bytes(32), int(eta0 is None), k)
+    return o.raw
+
+
+def check_leader512(leader_be: bytes, sigma_fp: int, c_raw: int, f_is_one: bool = False):
+    it = ctypes.c_int(0)
+    r = lib().orc_check_leader512(leader_be, sigma_fp.to_bytes(16, "little"),
+                                  (c_raw & ((1 << 128) - 1)).to_bytes(16, "little"), int(bool(f_is_one)),
+                                  ctypes.byref(it))
+    return bool(r), it.value
+
+
+def tpraos_header(ep, h: dict) -> dict:
+    """h: praos_header fields (vrf_out/vrf_proof = eta cert) + leader_out, leader_proof."""
+    T = TPHeader()
+    H = T.h
+    H.slot = h["slot"]
+    for k in ("cold_vk", "vrf_vk", "vrf_out", "vrf_proof", "hot_vk", "ocert_sig", "kes_sig"):
+        _fill(getattr(H, k), h[k])
+    H.ocert_n = h["n"]
+    H.ocert_c0 = h["c0"]
+    body = ctypes.create_string_buffer(h["body"], len(h["body"]))
+    H.body = ctypes.cast(body, ctypes.c_void_p)
+    H.body_len = len(h["body"])
+    _fill(T.leader_out, h["leader_out"])
+    _fill(T.leader_proof, h["leader_proof"])
+    R = TPResult()
+    lib().orc_tpraos_header(ctypes.byref(ep), ctypes.byref(T), ctypes.byref(R))
+    return {"bits": R.bits, "pool_idx": R.pool_idx, "beta_eta": bytes(R.beta_eta),
+            "beta_leader": bytes(R.beta_leader), "nonce": bytes(R.nonce)}

@@ -77,7 +77,7 @@ int orc_kes_sign(uint8_t sig[ORC_KES_SIG_BYTES], const uint8_t seed[32], uint32_
  * Bignums are little-endian uint32 arrays; division is bit-serial.
  * Call site: Praos.hs:549 (validateVRFSignature), Praos.hs:505-526.
  * ------------------------------------------------------------------------ */
-#define BW 16  /* 512-bit capacity */
+#define BW 32  /* 1024-bit capacity (TPraos: 2^512 * 10^34 products) */
 typedef struct { uint32_t w[BW]; } bn;
 
 static void bn_zero(bn *a) { memset(a, 0, sizeof *a); }
@@ -138,16 +138,16 @@ static void bn_from_be(bn *a, const uint8_t *b, int n) {
 static void bn_pow10(bn *a, int e) { bn_zero(a); a->w[0] = 1; for (int i = 0; i < e; i++) bn_mul_small(a, a, 10); }
 static int bn_is_zero(const bn *a) { for (int i = 0; i < BW; i++) if (a->w[i]) return 0; return 1; }
 
-int orc_check_leader(const uint8_t leader_be[32], const uint8_t sigma_fp[16],
-                     const uint8_t c_raw[16], int f_is_one, int *iters) {
+static int check_leader_n(const uint8_t *leader_be, int nbytes, const uint8_t sigma_fp[16],
+                          const uint8_t c_raw[16], int f_is_one, int *iters) {
   if (iters) *iters = 0;
   if (f_is_one) return 1;
   bn R, l, D, N, q, sig, c, P, x, rem, two256;
   bn_pow10(&R, 34);
-  bn_from_be(&l, leader_be, 32);
-  bn_zero(&two256); two256.w[8] = 1;
-  bn_sub(&D, &two256, &l);                     /* D = 2^256 - l  (>= 1) */
-  bn_mul(&N, &two256, &R);                     /* N = 2^256 * R */
+  bn_from_be(&l, leader_be, nbytes);
+  bn_zero(&two256); two256.w[nbytes / 4] = 1;  /* certNatMax = 2^(8 * nbytes) */
+  bn_sub(&D, &two256, &l);                     /* D = max - l  (>= 1) */
+  bn_mul(&N, &two256, &R);                     /* N = max * R */
   bn_divmod(&q, NULL, &N, &D);                 /* recip_q raw */
   bn_from_le(&sig, sigma_fp, 16);
   /* c_raw is a signed 128-bit value, must be <= 0: |c| = -c */
@@ -182,6 +182,15 @@ int orc_check_leader(const uint8_t leader_be[32], const uint8_t sigma_fp[16],
     }
     err = errp; acc = accp;
   }
+}
+
+int orc_check_leader(const uint8_t leader_be[32], const uint8_t sigma_fp[16],
+                     const uint8_t c_raw[16], int f_is_one, int *iters) {
+  return check_leader_n(leader_be, 32, sigma_fp, c_raw, f_is_one, iters);
+}
+int orc_check_leader512(const uint8_t leader_be[64], const uint8_t sigma_fp[16],
+                        const uint8_t c_raw[16], int f_is_one, int *iters) {
+  return check_leader_n(leader_be, 64, sigma_fp, c_raw, f_is_one, iters);
 }
 
 /* ------------------------------------------------------------------------
@@ -251,5 +260,43 @@ void orc_praos_header(const orc_epoch *ep, const orc_header *h, orc_result *r) {
   orc_blake2b(nv, 32, lb, 65);
   orc_blake2b(r->nonce, 32, nv, 32);                      /* vrfNonceValue, Praos/VRF.hs:116-131 */
   if (idx >= 0 && !orc_check_leader(r->leader, ep->pools[idx].sigma_fp, ep->c_raw, ep->f_is_one, NULL))
+    r->bits |= ORC_BIT_LEADER;
+}
+
+/* ------------------------------------------------------------------------
+ * TPraos (cardano-protocol-tpraos), d = 0: praosVrfChecks (OVERLAY) then OCERT.
+ * The OCERT predicates are the same as Praos.hs:567-590 (a2).
+ * ------------------------------------------------------------------------ */
+void orc_tpraos_seed(uint8_t out[32], uint64_t slot, const uint8_t eta0[32], int eta0_neutral, uint64_t k) {
+  uint8_t in[40], h[32], kb[8], uc[32];
+  be64(in, slot);
+  memcpy(in + 8, eta0, 32);
+  orc_blake2b(h, 32, in, eta0_neutral ? 8 : 40);           /* mkSeed: hash of BE64 slot || eta0 */
+  be64(kb, k);
+  orc_blake2b(uc, 32, kb, 8);                               /* mkNonceFromNumber k */
+  for (int i = 0; i < 32; i++) out[i] = h[i] ^ uc[i];       /* Hash.xor */
+}
+
+void orc_tpraos_header(const orc_epoch *ep, const orc_tp_header *th, orc_tp_result *r) {
+  const orc_header *h = &th->h;
+  orc_result pr;
+  memset(r, 0, sizeof *r);
+  /* OCERT predicates and key lookups are shared with the Praos restatement */
+  orc_praos_header(ep, h, &pr);
+  r->bits = pr.bits & (ORC_BIT_KES_BEFORE_START | ORC_BIT_KES_AFTER_END | ORC_BIT_OCERT_SIG |
+                       ORC_BIT_KES_MERKLE | ORC_BIT_KES_LEAF | ORC_BIT_VRF_KEY_UNKNOWN | ORC_BIT_VRF_KEY_WRONG);
+  r->pool_idx = pr.pool_idx;
+  uint8_t a_eta[32], a_l[32], beta[64];
+  orc_tpraos_seed(a_eta, h->slot, ep->eta0, ep->eta0_neutral, 0);
+  orc_tpraos_seed(a_l, h->slot, ep->eta0, ep->eta0_neutral, 1);
+  if (orc_vrf_verify(beta, h->vrf_vk, h->vrf_proof, a_eta, 32) != 0) r->bits |= ORC_BIT_TP_VRF_NONCE;
+  if (orc_vrf_proof_to_hash(r->beta_eta, h->vrf_proof) != 0) memset(r->beta_eta, 0, 64);
+  if (memcmp(r->beta_eta, h->vrf_out, 64) != 0) r->bits |= ORC_BIT_TP_VRF_NONCE;
+  if (orc_vrf_verify(beta, h->vrf_vk, th->leader_proof, a_l, 32) != 0) r->bits |= ORC_BIT_TP_VRF_LEADER;
+  if (orc_vrf_proof_to_hash(r->beta_leader, th->leader_proof) != 0) memset(r->beta_leader, 0, 64);
+  if (memcmp(r->beta_leader, th->leader_out, 64) != 0) r->bits |= ORC_BIT_TP_VRF_LEADER;
+  orc_blake2b(r->nonce, 32, h->vrf_out, 64);                 /* mkNonceFromOutputVRF */
+  if (r->pool_idx >= 0 &&
+      !orc_check_leader512(th->leader_out, ep->pools[r->pool_idx].sigma_fp, ep->c_raw, ep->f_is_one, NULL))
     r->bits |= ORC_BIT_LEADER;
 }

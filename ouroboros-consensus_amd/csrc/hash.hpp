@@ -220,3 +220,22 @@ H_INLINE void mk_input_vrf(uint32_t out[8], uint64_t slot, const uint32_t eta0[8
 #pragma unroll
   for (int i = 0; i < 4; i++) { out[2 * i] = (uint32_t)h[i]; out[2 * i + 1] = (uint32_t)(h[i] >> 32); }
 }
+
+// TPraos mkSeed (cardano-protocol-tpraos BHeader.mkSeed): Blake2b256(BE64(slot) || eta0)
+// XOR ucNonce, ucNonce = mkNonceFromNumber k = Blake2b256(BE64(k)), k = 0 (seedEta), 1 (seedL).
+H_INLINE void tpraos_seed(uint32_t out[8], uint64_t slot, const uint32_t eta0[8], bool neutral, uint64_t k) {
+  uint32_t h[8], uc[8];
+  mk_input_vrf(h, slot, eta0, neutral);
+  uint64_t m[16];
+  m[0] = bswap64(k);
+#pragma unroll
+  for (int i = 1; i < 16; i++) m[i] = 0;
+  uint64_t hh[4];
+  blake2b_1block(hh, m, 8, 32);
+#pragma unroll
+  for (int i = 0; i < 4; i++) { uc[2 * i] = (uint32_t)hh[i]; uc[2 * i + 1] = (uint32_t)(hh[i] >> 32); }
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = h[i] ^ uc[i];
+}
+// mkNonceFromOutputVRF: Blake2b256 of the 64-byte VRF output (16 LE words)
+H_INLINE void blake2b256_of64(uint32_t out[8], const uint32_t in[16]) { blake2b256_64(out, in); }

@@ -40,7 +40,7 @@ __global__ void k_init_btab(ge_niels* btab) {
 __global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restrict__ leader_in,
                                                const int32_t* __restrict__ pool_sorted_idx,
                                                const uint32_t* __restrict__ pool_x, const uint32_t* __restrict__ x_item,
-                                               int f_is_one, const uint16_t* __restrict__ b_ocert,
+                                               int f_is_one, int leader_words, const uint16_t* __restrict__ b_ocert,
                                                const uint16_t* __restrict__ b_kes, const uint16_t* __restrict__ b_vrf,
                                                uint16_t* __restrict__ bits, uint8_t* __restrict__ is_leader,
                                                int32_t* __restrict__ iters) {
@@ -62,11 +62,19 @@ __global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restri
   bool lead = true;
   int it = 0;
   if (!skip && !f_is_one) {
-    uint32_t raw[8], l[8];
-    load_words(raw, leader_in + 32 * i, 8);
+    if (leader_words == 16) {                  // TPraos: raw 64-byte output, bound 2^512
+      uint32_t raw[16], l[16];
+      load_words(raw, leader_in + 64 * i, 16);
 #pragma unroll
-    for (int k = 0; k < 8; k++) l[k] = __builtin_bswap32(raw[7 - k]);  // big-endian bytes -> LE words
-    lead = leader_check(l, x, &it);
+      for (int k = 0; k < 16; k++) l[k] = __builtin_bswap32(raw[15 - k]);
+      lead = leader_check_t<16>(l, x, &it);
+    } else {                                   // Praos: Blake2b-256 range extension, bound 2^256
+      uint32_t raw[8], l[8];
+      load_words(raw, leader_in + 32 * i, 8);
+#pragma unroll
+      for (int k = 0; k < 8; k++) l[k] = __builtin_bswap32(raw[7 - k]);  // big-endian bytes -> LE words
+      lead = leader_check(l, x, &it);
+    }
   }
   if (iters) iters[i] = it;
   if (is_leader) { is_leader[i] = lead ? 1 : 0; return; }
@@ -197,8 +205,9 @@ void launch_debug_h2c(dim3 grid, dim3 block, hipStream_t stream, size_t n, const
 }
 void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in,
                    const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one,
-                   const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits,
+                   int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits,
                    uint8_t* is_leader, int32_t* iters) {
-  hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one, b_ocert,
+  hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one,
+                     leader_words, b_ocert,
                      b_kes, b_vrf, bits, is_leader, iters);
 }

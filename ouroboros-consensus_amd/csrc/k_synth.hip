@@ -133,7 +133,8 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk,
     const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk,
     uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
-    uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes) {
+    uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos,
+    uint8_t* l_out, uint8_t* l_proof) {
   __shared__ ge_niels sbtab[8];
   __shared__ int8_t sdig[DIG_BYTES];
   const ge_niels* btab = stage_btab(gbtab, sbtab);
@@ -191,31 +192,34 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     store_words(ks + 64 * d + 32, T + (2 * parent + 1) * 8, 8);
     node = parent;
   }
-  // VRF proof for alpha = mkInputVRF(slot, eta0); output = proof_to_hash
+  // VRF proof(s): Praos alpha = mkInputVRF(slot, eta0); TPraos: the eta cert
+  // with mkSeed seedEta and the leader cert with mkSeed seedL.  output = beta.
   uint32_t e0[8], alpha[8], proof[20];
 #pragma unroll
   for (int k = 0; k < 8; k++) { e0[k] = eta0[k]; seed[k] = vrf_seed[8 * p + k]; }
-  mk_input_vrf(alpha, s, e0, eta0_neutral != 0);
   ed25519_expand(az, seed);
-  vrf_prove_core(proof, az, vpk, alpha, dp, threadIdx.x, btab);
-  store_words(vrf_proof + 80 * i, proof, 20);
-  // beta = SHA-512(0x04||0x03||enc(8 Gamma))
-  ge_p3 G, G2, G4, G8;
-  ge_frombytes(G, proof, false);
-  ge_p3_dbl_to_p3(G2, G);
-  ge_p3_dbl_to_p3(G4, G2);
-  ge_p3_dbl_to_p3(G8, G4);
-  uint32_t g8s[8], beta[16];
-  ge_tobytes(g8s, G8.X, G8.Y, G8.Z);
-  vrf_beta(beta, g8s);
-  store_words(vrf_out + 64 * i, beta, 16);
+  for (int cert = 0; cert < (tpraos ? 2 : 1); cert++) {
+    if (tpraos) tpraos_seed(alpha, s, e0, eta0_neutral != 0, (uint64_t)cert);
+    else mk_input_vrf(alpha, s, e0, eta0_neutral != 0);
+    vrf_prove_core(proof, az, vpk, alpha, dp, threadIdx.x, btab);
+    store_words((cert ? l_proof : vrf_proof) + 80 * i, proof, 20);
+    ge_p3 G, G2, G4, G8;
+    ge_frombytes(G, proof, false);
+    ge_p3_dbl_to_p3(G2, G);
+    ge_p3_dbl_to_p3(G4, G2);
+    ge_p3_dbl_to_p3(G8, G4);
+    uint32_t g8s[8], beta[16];
+    ge_tobytes(g8s, G8.X, G8.Y, G8.Z);
+    vrf_beta(beta, g8s);
+    store_words((cert ? l_out : vrf_out) + 64 * i, beta, 16);
+  }
 }
 
 // Corruption model (consensus-testlib Test/Util/Corruption.hs:29-35): increment
 // the byte at offset k mod len of one chosen field.
 __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig,
                                 uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off,
-                                const uint32_t* body_len, uint8_t* corrupted) {
+                                const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t r = mix64(i ^ salt ^ 0xc0ffee);
@@ -227,7 +231,9 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
   switch (which) {
     case 0: ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1; break;
     case 1: kes_sig[448 * i + k % 448] += 1; corrupted[i] = 2; break;
-    case 2: vrf_proof[80 * i + k % 80] += 1; corrupted[i] = 3; break;
+    case 2:
+      if (l_proof && (k & 0x10000)) { l_proof[80 * i + k % 80] += 1; corrupted[i] = 6; break; }
+      vrf_proof[80 * i + k % 80] += 1; corrupted[i] = 3; break;
     case 3: vrf_out[64 * i + k % 64] += 1; corrupted[i] = 4; break;
     default:
       if (body_len[i] == 0) { ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1; break; }
@@ -248,10 +254,25 @@ void launch_synth_kes_tree(dim3 grid, dim3 block, hipStream_t stream, uint32_t n
   hipLaunchKernelGGL(k_synth_kes_tree, grid, block, 0, stream, npools, tree);
 }
 
-void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, uint32_t npools, uint32_t nkes, uint64_t first_slot, uint64_t slot_stride, uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral, const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk, const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes) {
-  hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, nkes, first_slot, slot_stride, slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n, ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes);
-}
 
-void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted) {
-  hipLaunchKernelGGL(k_synth_corrupt, grid, block, 0, stream, n, per10000, salt, ocert_sig, kes_sig, vrf_proof, vrf_out, body_bytes, body_off, body_len, corrupted);
+void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, uint32_t npools,
+                          uint32_t nkes, uint64_t first_slot, uint64_t slot_stride, uint64_t slots_per_kes_period,
+                          uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral,
+                          const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed,
+                          const uint32_t* vrf_pk, const uint32_t* leaf_seed, const uint32_t* tree,
+                          uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out,
+                          uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
+                          uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len,
+                          uint8_t* body_bytes, int tpraos, uint8_t* l_out, uint8_t* l_proof) {
+  hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, nkes, first_slot, slot_stride,
+                     slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk,
+                     leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
+                     ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, tpraos, l_out, l_proof);
+}
+void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt,
+                          uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out,
+                          uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len,
+                          uint8_t* corrupted, uint8_t* l_proof) {
+  hipLaunchKernelGGL(k_synth_corrupt, grid, block, 0, stream, n, per10000, salt, ocert_sig, kes_sig, vrf_proof,
+                     vrf_out, body_bytes, body_off, body_len, corrupted, l_proof);
 }

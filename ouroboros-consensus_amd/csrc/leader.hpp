@@ -124,21 +124,25 @@ FE_INLINE void mp_div_small(uint32_t q[8], const uint32_t a[8], uint32_t k) {
   }
 }
 
-// Returns true = leader (BELOW).  l_le: leader value as 8 LE words (natural);
+// Returns true = leader (BELOW).  l_le: leader value as LW LE words (natural,
+// bound certNatMax = 2^(32 LW): LW = 8 for Praos (Blake2b-256 range extension,
+// Praos/VRF.hs:103-112), LW = 16 for TPraos (raw 64-byte VRF output);
 // x: Fixed raw x (4 words, >= 0).
-FE_INLINE bool leader_check(const uint32_t l_le[8], const uint32_t x[4], int* iters_out) {
-  // D = 2^256 - l  (9 words)
-  uint32_t D[9];
+template <int LW>
+FE_INLINE bool leader_check_t(const uint32_t l_le[LW], const uint32_t x[4], int* iters_out) {
+  constexpr int NW = LW + 5;          // N = 2^(32 LW) * R, plus one zero word
+  constexpr int PW = 8 + LW + 1;      // (8-word value) * D
+  // D = 2^(32 LW) - l  (LW + 1 words)
+  uint32_t D[LW + 1];
   uint32_t bw = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) D[i] = subb(0u, l_le[i], bw, &bw);
-  D[8] = 1u - bw;            // l == 0 -> D = 2^256
-  // N = 2^256 * R  (12 words, low 8 zero)
-  uint32_t N[13];
+  for (int i = 0; i < LW; i++) D[i] = subb(0u, l_le[i], bw, &bw);
+  D[LW] = 1u - bw;           // l == 0 -> D = 2^(32 LW)
+  uint32_t N[NW];
 #pragma unroll
-  for (int i = 0; i < 13; i++) N[i] = 0;
+  for (int i = 0; i < NW; i++) N[i] = 0;
 #pragma unroll
-  for (int i = 0; i < 4; i++) N[8 + i] = FX_R[i];
+  for (int i = 0; i < 4; i++) N[LW + i] = FX_R[i];
   uint32_t err[8], acc[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) { err[i] = i < 4 ? x[i] : 0; acc[i] = i < 4 ? FX_R[i] : 0; }
@@ -171,19 +175,23 @@ FE_INLINE bool leader_check(const uint32_t l_le[8], const uint32_t x[4], int* it
       c = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) hi[i] = addc(accp[i], e[i], c, &c);
-      uint32_t hd[17];
-      mp_mul<8, 9>(hd, hi, D);
-      const bool hd_big = (hd[13] | hd[14] | hd[15] | hd[16]) != 0;
-      const bool above = !hd_big && mp_cmp<13>(N, hd) >= 0;
+      uint32_t hd[PW];
+      mp_mul<8, LW + 1>(hd, hi, D);
+      uint32_t big = 0;
+#pragma unroll
+      for (int i = NW; i < PW; i++) big |= hd[i];
+      const bool above = big == 0 && mp_cmp<NW>(N, hd) >= 0;
       // lo = acc' - e (if non-negative); BELOW iff N < lo * D
       uint32_t lo[8];
       uint32_t b = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) lo[i] = subb(accp[i], e[i], b, &b);
-      uint32_t ld[17];
-      mp_mul<8, 9>(ld, lo, D);
-      const bool ld_big = (ld[13] | ld[14] | ld[15] | ld[16]) != 0;
-      const bool below = b == 0 && (ld_big || mp_cmp<13>(N, ld) < 0);
+      uint32_t ld[PW];
+      mp_mul<8, LW + 1>(ld, lo, D);
+      uint32_t lbig = 0;
+#pragma unroll
+      for (int i = NW; i < PW; i++) lbig |= ld[i];
+      const bool below = b == 0 && (lbig != 0 || mp_cmp<NW>(N, ld) < 0);
       if (above) { res = 0; iters = n + 1; }
       else if (below) { res = 1; iters = n + 1; }
 #pragma unroll
@@ -194,4 +202,8 @@ FE_INLINE bool leader_check(const uint32_t l_le[8], const uint32_t x[4], int* it
   const bool result = res == 1;                 // MaxReached -> not leader
   if (iters_out) *iters_out = iters;
   return result;
+}
+
+FE_INLINE bool leader_check(const uint32_t l_le[8], const uint32_t x[4], int* iters_out) {
+  return leader_check_t<8>(l_le, x, iters_out);
 }

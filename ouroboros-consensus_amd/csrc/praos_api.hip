@@ -289,7 +289,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
   launch_leader(g, blk, c->stream, n, b->leader, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
-                (int)P.f_is_one, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr);
+                (int)P.f_is_one, 8, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   HIPCHK(c, hipGetLastError());
   return PRAOS_OK;
@@ -489,7 +489,7 @@ int praos_check_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr,
-                (const uint32_t*)nullptr, dx, (int)params->f_is_one, (const uint16_t*)nullptr,
+                (const uint32_t*)nullptr, dx, (int)params->f_is_one, 8, (const uint16_t*)nullptr,
                 (const uint16_t*)nullptr, (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, (int32_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
@@ -559,11 +559,13 @@ int praos_apply_batch(praos_ctx* c, const praos_headers* h, const praos_out* cry
 }
 
 // ---------------------------------------------------------------- generator
-int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_params* params, const uint8_t eta0[32],
-                     praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out,
-                     uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig,
-                     uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes,
-                     uint8_t* corrupted) {
+}  // extern "C"
+static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const praos_params* params,
+                           const uint8_t eta0[32], praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk,
+                           uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n,
+                           uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off,
+                           uint32_t* body_len, uint8_t* body_bytes, uint8_t* corrupted, int tpraos,
+                           uint8_t* leader_out, uint8_t* leader_proof) {
   if (!c || !sp || !params || sp->npools == 0 || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = sp->n, np = sp->npools;
@@ -599,6 +601,8 @@ int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_par
   auto dlen = s.zeros<uint32_t>(4 * n);
   auto dbody = s.zeros<uint8_t>(bstride * n + 8);
   auto dcor = s.zeros<uint8_t>(n);
+  auto dlout = s.zeros<uint8_t>(tpraos ? 64 * n : 16);
+  auto dlproof = s.zeros<uint8_t>(tpraos ? 80 * n : 16);
   if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
   uint64_t salt = 0;
   std::memcpy(&salt, sp->seed, 8);
@@ -611,9 +615,9 @@ int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_par
     launch_synth_headers(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, (uint32_t)np,
                        (uint32_t)nk, sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
-                       dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody);
+                       dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
-                       salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor);
+                       salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr);
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -636,9 +640,80 @@ int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_par
     r |= dn2h(ocert_n, dn, 8 * n); r |= dn2h(ocert_c0, dc0, 8 * n); r |= dn2h(ocert_sig, dosig, 64 * n);
     r |= dn2h(kes_sig, dksig, 448 * n); r |= dn2h(body_off, doff, 8 * n); r |= dn2h(body_len, dlen, 4 * n);
     r |= dn2h(body_bytes, dbody, bstride * n + 8); r |= dn2h(corrupted, dcor, n);
+    if (tpraos) { r |= dn2h(leader_out, dlout, 64 * n); r |= dn2h(leader_proof, dlproof, 80 * n); }
     if (r != PRAOS_OK) return PRAOS_E_HIP;
   }
   return PRAOS_OK;
+}
+extern "C" {
+
+int praos_synthesize(praos_ctx* c, const praos_synth_params* sp, const praos_params* params, const uint8_t eta0[32],
+                     praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out,
+                     uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig,
+                     uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes,
+                     uint8_t* corrupted) {
+  return synthesize_impl(c, sp, params, eta0, pools_out, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
+                         ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, corrupted, 0, nullptr, nullptr);
+}
+
+int praos_synthesize_tpraos(praos_ctx* c, const praos_synth_params* sp, const praos_params* params,
+                            const uint8_t eta0[32], praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk,
+                            uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n,
+                            uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off,
+                            uint32_t* body_len, uint8_t* body_bytes, uint8_t* leader_out, uint8_t* leader_proof,
+                            uint8_t* corrupted) {
+  if (!leader_out || !leader_proof) return PRAOS_E_ARG;
+  return synthesize_impl(c, sp, params, eta0, pools_out, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
+                         ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, corrupted, 1, leader_out,
+                         leader_proof);
+}
+
+// TPraos batch: OCert + KES kernels are shared with Praos; VRF checks use the
+// two-certificate kernel and the leader test the 2^512 bound.
+int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, praos_tpraos_out* out) {
+  if (!c || !th || !out || !out->bits || !th->leader_out || !th->leader_proof) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  const size_t n = th->h.n;
+  if (n == 0) return PRAOS_OK;
+  praos_batch* b = praos_batch_upload(c, &th->h);
+  if (!b) return PRAOS_E_OOM;
+  uint8_t *dlout = nullptr, *dlproof = nullptr, *dbeta_l = nullptr;
+  int rc = PRAOS_OK;
+  if (dalloc(b, &dlout, 64 * n) != hipSuccess || dalloc(b, &dlproof, 80 * n) != hipSuccess ||
+      dalloc(b, &dbeta_l, 64 * n) != hipSuccess) {
+    praos_batch_free(c, b);
+    return PRAOS_E_OOM;
+  }
+  const praos_params& P = c->params;
+  const dim3 g(nblocks(n, NT)), blk(NT);
+  uint16_t* bo = b->bits3;
+  uint16_t* bk = b->bits3 + n;
+  uint16_t* bv = b->bits3 + 2 * n;
+  auto body = [&]() -> int {
+    HIPCHK(c, hipMemcpy(dlout, th->leader_out, 64 * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
+    launch_ocert(g, blk, c->stream, n, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
+                 P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+    launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
+               b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk,
+               (uint8_t*)nullptr);
+    launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
+                  b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
+                  (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce);
+    launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
+                  (int)P.f_is_one, 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out->bits, b->bits, 2 * n, hipMemcpyDeviceToHost));
+    if (out->pool_idx) HIPCHK(c, hipMemcpy(out->pool_idx, b->pool_idx, 4 * n, hipMemcpyDeviceToHost));
+    if (out->beta_eta) HIPCHK(c, hipMemcpy(out->beta_eta, b->beta, 64 * n, hipMemcpyDeviceToHost));
+    if (out->beta_leader) HIPCHK(c, hipMemcpy(out->beta_leader, dbeta_l, 64 * n, hipMemcpyDeviceToHost));
+    if (out->nonce) HIPCHK(c, hipMemcpy(out->nonce, b->nonce, 32 * n, hipMemcpyDeviceToHost));
+    return PRAOS_OK;
+  };
+  rc = body();
+  praos_batch_free(c, b);
+  return rc;
 }
 
 // ---------------------------------------------------------------- debug entry points
@@ -751,7 +826,7 @@ int praos_debug_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   auto dit = s.zeros<int32_t>(4 * n);
   if (!s.ok) return PRAOS_E_OOM;
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr, (const uint32_t*)nullptr,
-                (const uint32_t*)dx, 0, (const uint16_t*)nullptr, (const uint16_t*)nullptr,
+                (const uint32_t*)dx, 0, 8, (const uint16_t*)nullptr, (const uint16_t*)nullptr,
                 (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, dit);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));

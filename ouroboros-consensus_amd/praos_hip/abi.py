@@ -36,6 +36,8 @@ BIT_VRF_PROOF = 0x0400
 BIT_VRF_OUTPUT = 0x0800
 BIT_LEADER = 0x1000
 BIT_INPUT = 0x8000
+BIT_TP_VRF_NONCE = 0x0400
+BIT_TP_VRF_LEADER = 0x0800
 
 # verdicts (enum praos_verdict)
 V_OK, V_KES_BEFORE_START, V_KES_AFTER_END, V_OCERT_SIG, V_KES_SIG, V_COUNTER_MISSING, \
@@ -63,6 +65,14 @@ class Headers(ctypes.Structure):
 
 class Out(ctypes.Structure):
     _fields_ = [("bits", u16p), ("pool_idx", i32p), ("beta", u8p), ("leader", u8p), ("nonce", u8p)]
+
+
+class TPHeaders(ctypes.Structure):
+    _fields_ = [("h", Headers), ("leader_out", u8p), ("leader_proof", u8p)]
+
+
+class TPOut(ctypes.Structure):
+    _fields_ = [("bits", u16p), ("pool_idx", i32p), ("beta_eta", u8p), ("beta_leader", u8p), ("nonce", u8p)]
 
 
 class Counters(ctypes.Structure):
@@ -101,6 +111,11 @@ SIGNATURES = {
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
+    "praos_verify_tpraos_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders),
+                                                   ctypes.POINTER(TPOut)]),
+    "praos_synthesize_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params),
+                                               u8p, ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p,
+                                               u8p, u8p, u64p, u32p, u8p, u8p, u8p, u8p]),
     "praos_debug_fe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, u8p, u8p, u8p]),
     "praos_debug_sha512": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u64p, u32p, u8p, ctypes.c_size_t,
                                           u8p]),
@@ -226,6 +241,25 @@ class Context:
         self.check(self.L.praos_verify_headers(self.h, ctypes.byref(hs), ctypes.byref(os_)))
         return o
 
+    def verify_tpraos_headers(self, H):
+        """H as for verify_headers plus leader_out [n,64] / leader_proof [n,80] (the bheaderL cert)."""
+        n = len(H["slot"])
+        th = TPHeaders()
+        th.h = self.headers_struct(H)
+        th.leader_out = ptr(H["leader_out"])
+        th.leader_proof = ptr(H["leader_proof"])
+        o = {"bits": np.zeros(n, np.uint16), "pool_idx": np.zeros(n, np.int32),
+             "beta_eta": np.zeros((n, 64), np.uint8), "beta_leader": np.zeros((n, 64), np.uint8),
+             "nonce": np.zeros((n, 32), np.uint8)}
+        to = TPOut()
+        to.bits = ptr(o["bits"], u16p)
+        to.pool_idx = ptr(o["pool_idx"], i32p)
+        to.beta_eta = ptr(o["beta_eta"])
+        to.beta_leader = ptr(o["beta_leader"])
+        to.nonce = ptr(o["nonce"])
+        self.check(self.L.praos_verify_tpraos_headers(self.h, ctypes.byref(th), ctypes.byref(to)))
+        return o
+
     def upload(self, H):
         hs = self.headers_struct(H)
         b = self.L.praos_batch_upload(self.h, ctypes.byref(hs))
@@ -311,7 +345,7 @@ class Context:
         return res
 
     def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
-                   body_len=397, corrupt_per_10000=0, nkes=0):
+                   body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False):
         sp = SynthParams()
         sp.n = n
         sp.npools = npools
@@ -335,11 +369,17 @@ class Context:
         if eta0 is not None:
             eb = np.frombuffer(bytes(eta0), dtype=np.uint8).copy()
             e = ptr(eb)
-        self.check(self.L.praos_synthesize(
-            self.h, ctypes.byref(sp), ctypes.byref(params), e, pools, ptr(H["slot"], u64p), ptr(H["cold_vk"]),
-            ptr(H["vrf_vk"]), ptr(H["vrf_out"]), ptr(H["vrf_proof"]), ptr(H["hot_vk"]), ptr(H["ocert_n"], u64p),
-            ptr(H["ocert_c0"], u64p), ptr(H["ocert_sig"]), ptr(H["kes_sig"]), ptr(H["body_off"], u64p),
-            ptr(H["body_len"], u32p), ptr(H["body_bytes"]), ptr(corrupted)))
+        common = (self.h, ctypes.byref(sp), ctypes.byref(params), e, pools, ptr(H["slot"], u64p), ptr(H["cold_vk"]),
+                  ptr(H["vrf_vk"]), ptr(H["vrf_out"]), ptr(H["vrf_proof"]), ptr(H["hot_vk"]),
+                  ptr(H["ocert_n"], u64p), ptr(H["ocert_c0"], u64p), ptr(H["ocert_sig"]), ptr(H["kes_sig"]),
+                  ptr(H["body_off"], u64p), ptr(H["body_len"], u32p), ptr(H["body_bytes"]))
+        if tpraos:
+            H["leader_out"] = np.zeros((n, 64), np.uint8)
+            H["leader_proof"] = np.zeros((n, 80), np.uint8)
+            self.check(self.L.praos_synthesize_tpraos(*common, ptr(H["leader_out"]), ptr(H["leader_proof"]),
+                                                      ptr(corrupted)))
+        else:
+            self.check(self.L.praos_synthesize(*common, ptr(corrupted)))
         H["body_bytes"] = H["body_bytes"][:bstride * n]
         pool_list = [(bytes(p.hash28), bytes(p.vrf_hash32)) for p in pools]
         return H, pool_list, corrupted
