@@ -20,4 +20,4 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES G
   rc=$?
   if [ $rc -ge 124 ]; then echo "pmc pass $n rc=$rc, stopping"; exit $rc; fi
 done
-find $OUT -name "*.csv" | head -40
+python3 tools/prof_summary.py $OUT $TAG > $OUT/summary.txt && echo summary written
