@@ -132,6 +132,11 @@ typedef struct {
 } praos_out;
 
 /* ---- context ---- */
+/* device >= 0: a HIP device.  PRAOS_HOST_ONLY: a context without a device that
+ * supports only the host-side sequential part (praos_set_epoch, praos_apply_batch,
+ * praos_update_chain_dep_state); every GPU entry point then returns PRAOS_E_STATE.
+ * There is no CPU crypto path. */
+#define PRAOS_HOST_ONLY (-1)
 praos_ctx* praos_open(int device);               /* NULL on failure */
 void praos_close(praos_ctx* ctx);
 const char* praos_last_error(praos_ctx* ctx);
@@ -213,6 +218,52 @@ typedef struct {
 
 int praos_apply_batch(praos_ctx* ctx, const praos_headers* h, const praos_out* crypto,
                       praos_counters* counters, uint8_t* verdict, size_t* chain_stop);
+
+/* ---- full chain-dependent state fold (tickChainDepState + updateChainDepState +
+ *      reupdateChainDepState, Praos.hs:407-502) over a batch ----
+ * Nonce = NeutralNonce | Nonce (32-byte hash); a ⭒ b = Blake2b-256(a || b), Neutral is
+ * the identity.  Epochs: fixed size from a base (epoch of slot s =
+ * base_no + (s - base_slot) / length); stability_window = computeStabilityWindow k f
+ * (Praos.hs:497-498; ceiling(3k/f), computed by the caller).
+ * Per header i, in order: tick (isNewEpoch last_slot slot_i, Ledger/Util.hs:20-40:
+ * epoch_nonce := candidate ⭒ last_epoch_block, last_epoch_block := lab); the ticked
+ * epoch nonce must equal the ctx's eta0 (the nonce the crypto outputs were computed
+ * with), else the fold stops there (*processed = i) so the caller can set_epoch and
+ * verify the rest; verdict as praos_apply_batch; on OK the ticked state is kept and
+ * reupdated: last_slot := slot, lab := prevHashToNonce prev_hash, evolving :=
+ * evolving ⭒ vrfNonceValue, candidate := evolving' if slot + stability_window <
+ * firstSlotNextEpoch, counters[hk] := n (new keys appended; PRAOS_E_ARG past cap). */
+typedef struct {
+  uint8_t hash[32];
+  int32_t neutral;                /* 1 = NeutralNonce */
+} praos_nonce;
+
+typedef struct {
+  int32_t last_slot_origin;       /* praosStateLastSlot = Origin */
+  uint64_t last_slot;
+  uint8_t* counter_hash28;        /* praosStateOCertCounters: cap*28 */
+  uint64_t* counter;              /* cap */
+  size_t m;                       /* entries in use (in/out) */
+  size_t cap;
+  praos_nonce evolving;           /* praosStateEvolvingNonce */
+  praos_nonce candidate;          /* praosStateCandidateNonce */
+  praos_nonce epoch_nonce;        /* praosStateEpochNonce */
+  praos_nonce lab;                /* praosStateLabNonce */
+  praos_nonce last_epoch_block;   /* praosStateLastEpochBlockNonce */
+} praos_chain_state;
+
+typedef struct {
+  uint64_t epoch_base_slot;
+  uint64_t epoch_base_no;
+  uint64_t epoch_length;          /* > 0 */
+  uint64_t stability_window;
+} praos_epoch_info;
+
+/* prev_hash: n*32 (hvPrevHash); prev_is_genesis: n flags (GenesisHash), may be NULL. */
+int praos_update_chain_dep_state(praos_ctx* ctx, const praos_headers* h, const uint8_t* prev_hash,
+                                 const uint8_t* prev_is_genesis, const praos_out* crypto,
+                                 const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict,
+                                 size_t* chain_stop, size_t* processed);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

@@ -57,6 +57,10 @@ struct praos_batch {
 
 #define HIPCHK(ctx, x)                                                                    \
   do {                                                                                    \
+    if ((ctx)->device < 0) {                                                              \
+      (ctx)->err = "host-only context: no HIP device";                                    \
+      return PRAOS_E_STATE;                                                               \
+    }                                                                                     \
     hipError_t e_ = (x);                                                                  \
     if (e_ != hipSuccess) {                                                               \
       (ctx)->err = std::string(#x) + ": " + hipGetErrorString(e_);                        \
@@ -81,6 +85,11 @@ int praos_abi_version(void) { return PRAOS_ABI_VERSION; }
 const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
 praos_ctx* praos_open(int device) {
+  if (device == PRAOS_HOST_ONLY) {
+    praos_ctx* c = new praos_ctx();
+    c->device = -1;
+    return c;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
     fprintf(stderr, "praos_open: no HIP device %d (count %d)\n", device, ndev);
@@ -113,6 +122,7 @@ static void free_epoch(praos_ctx* c) {
 
 void praos_close(praos_ctx* c) {
   if (!c) return;
+  if (c->device < 0) { delete c; return; }
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_epoch(c);
@@ -127,8 +137,10 @@ void praos_close(praos_ctx* c) {
 int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
                     const praos_params* params) {
   if (!c || !params || (npools && !pools) || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
-  HIPCHK(c, hipSetDevice(c->device));
-  free_epoch(c);
+  if (c->device >= 0) {
+    HIPCHK(c, hipSetDevice(c->device));
+    free_epoch(c);
+  }
   c->params = *params;
   c->eta0_neutral = eta0 == nullptr;
   std::memset(c->eta0, 0, 32);
@@ -154,6 +166,10 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
     }
     std::memcpy(&x[4 * s], xr, 16);
     c->pool_by_hash[std::string((const char*)p.hash28, 28)] = order[s];
+  }
+  if (c->device < 0) {          // host-only context: the sequential part needs no tables
+    c->have_epoch = true;
+    return PRAOS_OK;
   }
   HIPCHK(c, hipMalloc(&c->d_pool_hash, h.size() * 4));
   HIPCHK(c, hipMalloc(&c->d_pool_vrf, v.size() * 4));
@@ -505,6 +521,55 @@ int praos_check_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
 // :584-590 counter), then validateVRFSignature (:537 unknown, :539 vrf key,
 // :543 proof, :549 leader).  Counter source (:601-606): the counter map, else
 // 0 if the issuer is in the pool distribution, else missing.
+}  // extern "C"
+
+// First failing check of one header in the reference order (Praos.hs:449-455 with
+// validateKESSignature :558-606 and validateVRFSignature :528-556).  has_counter / m
+// = the counter-map lookup of :601-606 (PoolDistr membership counts as m = 0).
+static uint8_t header_verdict(uint16_t b, bool have, uint64_t m, uint64_t n) {
+  if (b & PRAOS_BIT_INPUT) return PRAOS_V_INPUT;
+  if (b & PRAOS_BIT_KES_BEFORE_START) return PRAOS_V_KES_BEFORE_START;
+  if (b & PRAOS_BIT_KES_AFTER_END) return PRAOS_V_KES_AFTER_END;
+  if (b & PRAOS_BIT_OCERT_SIG) return PRAOS_V_OCERT_SIG;
+  if (b & (PRAOS_BIT_KES_MERKLE | PRAOS_BIT_KES_LEAF)) return PRAOS_V_KES_SIG;
+  if (!have) return PRAOS_V_COUNTER_MISSING;
+  if (!(m <= n)) return PRAOS_V_COUNTER_TOO_SMALL;
+  if (!(n <= m + 1)) return PRAOS_V_COUNTER_OVER_INC;
+  if (b & PRAOS_BIT_VRF_KEY_UNKNOWN) return PRAOS_V_VRF_KEY_UNKNOWN;
+  if (b & PRAOS_BIT_VRF_KEY_WRONG) return PRAOS_V_VRF_KEY_WRONG;
+  if (b & (PRAOS_BIT_VRF_PROOF | PRAOS_BIT_VRF_OUTPUT)) return PRAOS_V_VRF_BAD_PROOF;
+  if (b & PRAOS_BIT_LEADER) return PRAOS_V_LEADER_TOO_BIG;
+  return PRAOS_V_OK;
+}
+
+static std::string issuer_hash(const praos_ctx* c, const praos_headers* h, const praos_out* crypto, size_t i) {
+  const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
+  if (pidx >= 0 && (uint32_t)pidx < c->npools) return std::string((const char*)c->pools[pidx].hash28, 28);
+  uint8_t hh[28];
+  praos_host::blake2b(hh, 28, h->cold_vk + 32 * i, 32);
+  return std::string((const char*)hh, 28);
+}
+
+// a ⭒ b (Nonce semigroup): Neutral is the identity, else Blake2b-256(a || b).
+static praos_nonce nonce_combine(const praos_nonce& a, const praos_nonce& b) {
+  if (a.neutral) return b;
+  if (b.neutral) return a;
+  uint8_t m[64];
+  std::memcpy(m, a.hash, 32);
+  std::memcpy(m + 32, b.hash, 32);
+  praos_nonce r{};
+  praos_host::blake2b(r.hash, 32, m, 64);
+  r.neutral = 0;
+  return r;
+}
+
+static bool nonce_eq(const praos_nonce& a, const praos_nonce& b) {
+  if (a.neutral || b.neutral) return a.neutral && b.neutral;
+  return std::memcmp(a.hash, b.hash, 32) == 0;
+}
+
+extern "C" {
+
 int praos_apply_batch(praos_ctx* c, const praos_headers* h, const praos_out* crypto, praos_counters* counters,
                       uint8_t* verdict, size_t* chain_stop) {
   if (!c || !h || !crypto || !crypto->bits || !verdict) return PRAOS_E_ARG;
@@ -515,38 +580,11 @@ int praos_apply_batch(praos_ctx* c, const praos_headers* h, const praos_out* cry
       cmap[std::string((const char*)counters->hash28 + 28 * k, 28)] = counters->counter[k];
   size_t stop = h->n;
   for (size_t i = 0; i < h->n; i++) {
-    const uint16_t b = crypto->bits[i];
-    std::string hk;
-    const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
-    if (pidx >= 0 && (uint32_t)pidx < c->npools) {
-      hk.assign((const char*)c->pools[pidx].hash28, 28);
-    } else {
-      uint8_t hh[28];
-      praos_host::blake2b(hh, 28, h->cold_vk + 32 * i, 32);
-      hk.assign((const char*)hh, 28);
-    }
+    const std::string hk = issuer_hash(c, h, crypto, i);
     const uint64_t n = h->ocert_n[i];
-    uint8_t v = PRAOS_V_OK;
-    if (b & PRAOS_BIT_INPUT) v = PRAOS_V_INPUT;
-    else if (b & PRAOS_BIT_KES_BEFORE_START) v = PRAOS_V_KES_BEFORE_START;
-    else if (b & PRAOS_BIT_KES_AFTER_END) v = PRAOS_V_KES_AFTER_END;
-    else if (b & PRAOS_BIT_OCERT_SIG) v = PRAOS_V_OCERT_SIG;
-    else if (b & (PRAOS_BIT_KES_MERKLE | PRAOS_BIT_KES_LEAF)) v = PRAOS_V_KES_SIG;
-    else {
-      auto it = cmap.find(hk);
-      bool have = true;
-      uint64_t m = 0;
-      if (it != cmap.end()) m = it->second;
-      else if (c->pool_by_hash.count(hk)) m = 0;
-      else have = false;
-      if (!have) v = PRAOS_V_COUNTER_MISSING;
-      else if (!(m <= n)) v = PRAOS_V_COUNTER_TOO_SMALL;
-      else if (!(n <= m + 1)) v = PRAOS_V_COUNTER_OVER_INC;
-      else if (b & PRAOS_BIT_VRF_KEY_UNKNOWN) v = PRAOS_V_VRF_KEY_UNKNOWN;
-      else if (b & PRAOS_BIT_VRF_KEY_WRONG) v = PRAOS_V_VRF_KEY_WRONG;
-      else if (b & (PRAOS_BIT_VRF_PROOF | PRAOS_BIT_VRF_OUTPUT)) v = PRAOS_V_VRF_BAD_PROOF;
-      else if (b & PRAOS_BIT_LEADER) v = PRAOS_V_LEADER_TOO_BIG;
-    }
+    auto it = cmap.find(hk);
+    const bool have = it != cmap.end() || c->pool_by_hash.count(hk);
+    const uint8_t v = header_verdict(crypto->bits[i], have, it != cmap.end() ? it->second : 0, n);
     verdict[i] = v;
     if (v == PRAOS_V_OK) cmap[hk] = n;               // reupdateChainDepState, Praos.hs:484-485
     else if (stop == h->n) stop = i;
@@ -555,6 +593,75 @@ int praos_apply_batch(praos_ctx* c, const praos_headers* h, const praos_out* cry
   if (counters)
     for (size_t k = 0; k < counters->m; k++)
       counters->counter[k] = cmap[std::string((const char*)counters->hash28 + 28 * k, 28)];
+  return PRAOS_OK;
+}
+
+int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash,
+                                 const uint8_t* prev_is_genesis, const praos_out* crypto,
+                                 const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict,
+                                 size_t* chain_stop, size_t* processed) {
+  if (!c || !h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash ||
+      ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter)))
+    return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  praos_nonce eta0{};
+  eta0.neutral = c->eta0_neutral;
+  if (!c->eta0_neutral) std::memcpy(eta0.hash, c->eta0, 32);
+  auto epoch_of = [&](uint64_t s, bool* ok) -> uint64_t {
+    *ok = s >= ei->epoch_base_slot;
+    return ei->epoch_base_no + (*ok ? (s - ei->epoch_base_slot) / ei->epoch_length : 0);
+  };
+  std::map<std::string, size_t> where;
+  for (size_t k = 0; k < st->m; k++) where[std::string((const char*)st->counter_hash28 + 28 * k, 28)] = k;
+  size_t stop = h->n, i = 0;
+  for (; i < h->n; i++) {
+    const uint64_t slot = h->slot[i];
+    bool ok = true;
+    const uint64_t e_new = epoch_of(slot, &ok);
+    if (!ok) { c->err = "slot before the epoch base"; return PRAOS_E_ARG; }
+    // tickChainDepState (Praos.hs:407-431) with isNewEpoch (Ledger/Util.hs:27-40)
+    const uint64_t e_old = st->last_slot_origin ? 0 : epoch_of(st->last_slot, &ok);
+    praos_nonce tick_epoch = st->epoch_nonce, tick_leb = st->last_epoch_block;
+    if (e_new > e_old) {
+      tick_epoch = nonce_combine(st->candidate, st->last_epoch_block);
+      tick_leb = st->lab;
+    }
+    if (!nonce_eq(tick_epoch, eta0)) break;        // crypto outputs were computed for another epoch nonce
+    const std::string hk = issuer_hash(c, h, crypto, i);
+    const uint64_t n = h->ocert_n[i];
+    auto it = where.find(hk);
+    const bool have = it != where.end() || c->pool_by_hash.count(hk);
+    const uint8_t v = header_verdict(crypto->bits[i], have, it != where.end() ? st->counter[it->second] : 0, n);
+    verdict[i] = v;
+    if (v != PRAOS_V_OK) {
+      if (stop == h->n) stop = i;
+      continue;
+    }
+    // reupdateChainDepState (Praos.hs:468-502)
+    st->epoch_nonce = tick_epoch;
+    st->last_epoch_block = tick_leb;
+    st->last_slot_origin = 0;
+    st->last_slot = slot;
+    st->lab.neutral = prev_is_genesis && prev_is_genesis[i];
+    std::memset(st->lab.hash, 0, 32);
+    if (!st->lab.neutral) std::memcpy(st->lab.hash, prev_hash + 32 * i, 32);
+    praos_nonce eta{};
+    std::memcpy(eta.hash, crypto->nonce + 32 * i, 32);
+    eta.neutral = 0;
+    st->evolving = nonce_combine(st->evolving, eta);
+    const uint64_t first_next = ei->epoch_base_slot + (e_new - ei->epoch_base_no + 1) * ei->epoch_length;
+    if (slot + ei->stability_window < first_next) st->candidate = st->evolving;
+    if (it != where.end()) {
+      st->counter[it->second] = n;
+    } else {
+      if (st->m >= st->cap) { c->err = "counter map capacity exceeded"; return PRAOS_E_ARG; }
+      std::memcpy(st->counter_hash28 + 28 * st->m, hk.data(), 28);
+      st->counter[st->m] = n;
+      where[hk] = st->m++;
+    }
+  }
+  if (chain_stop) *chain_stop = std::min(stop, i);
+  if (processed) *processed = i;
   return PRAOS_OK;
 }
 

@@ -36,6 +36,7 @@ BIT_VRF_PROOF = 0x0400
 BIT_VRF_OUTPUT = 0x0800
 BIT_LEADER = 0x1000
 BIT_INPUT = 0x8000
+HOST_ONLY = -1
 BIT_TP_VRF_NONCE = 0x0400
 BIT_TP_VRF_LEADER = 0x0800
 
@@ -75,6 +76,22 @@ class TPOut(ctypes.Structure):
     _fields_ = [("bits", u16p), ("pool_idx", i32p), ("beta_eta", u8p), ("beta_leader", u8p), ("nonce", u8p)]
 
 
+class Nonce(ctypes.Structure):
+    _fields_ = [("hash", ctypes.c_uint8 * 32), ("neutral", ctypes.c_int32)]
+
+
+class ChainState(ctypes.Structure):
+    _fields_ = [("last_slot_origin", ctypes.c_int32), ("last_slot", ctypes.c_uint64),
+                ("counter_hash28", u8p), ("counter", u64p), ("m", ctypes.c_size_t), ("cap", ctypes.c_size_t),
+                ("evolving", Nonce), ("candidate", Nonce), ("epoch_nonce", Nonce), ("lab", Nonce),
+                ("last_epoch_block", Nonce)]
+
+
+class EpochInfo(ctypes.Structure):
+    _fields_ = [("epoch_base_slot", ctypes.c_uint64), ("epoch_base_no", ctypes.c_uint64),
+                ("epoch_length", ctypes.c_uint64), ("stability_window", ctypes.c_uint64)]
+
+
 class Counters(ctypes.Structure):
     _fields_ = [("hash28", u8p), ("counter", u64p), ("m", ctypes.c_size_t)]
 
@@ -108,6 +125,10 @@ SIGNATURES = {
     "praos_check_leader": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, ctypes.POINTER(Params), u8p]),
     "praos_apply_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), ctypes.POINTER(Out),
                                          ctypes.POINTER(Counters), u8p, ctypes.POINTER(ctypes.c_size_t)]),
+    "praos_update_chain_dep_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), u8p, u8p,
+                                                    ctypes.POINTER(Out), ctypes.POINTER(EpochInfo),
+                                                    ctypes.POINTER(ChainState), u8p, ctypes.POINTER(ctypes.c_size_t),
+                                                    ctypes.POINTER(ctypes.c_size_t)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -287,6 +308,51 @@ class Context:
 
     def free(self, b):
         self.L.praos_batch_free(self.h, b)
+
+    def update_chain_dep_state(self, H, crypto, prev_hash, state: dict, epoch_info, prev_is_genesis=None):
+        """state: dict(last_slot (None = Origin), counters {hash28: n}, evolving, candidate, epoch_nonce,
+        lab, leb) with nonces None (Neutral) or 32 bytes; updated in place.  epoch_info: (base_slot,
+        base_no, length, stability_window).  Returns (verdict u8[n], chain_stop, processed)."""
+        n = len(H["slot"])
+        hs = self.headers_struct(H)
+        os_ = self.out_struct(crypto)
+        keys = list(state["counters"].keys())
+        cap = len(keys) + n
+        hk = np.zeros(28 * max(cap, 1), np.uint8)
+        cv = np.zeros(max(cap, 1), np.uint64)
+        for k, key in enumerate(keys):
+            hk[28 * k:28 * k + 28] = np.frombuffer(key, np.uint8)
+            cv[k] = state["counters"][key]
+        st = ChainState()
+        st.last_slot_origin = int(state["last_slot"] is None)
+        st.last_slot = state["last_slot"] or 0
+        st.counter_hash28, st.counter, st.m, st.cap = ptr(hk), ptr(cv, u64p), len(keys), cap
+
+        def setn(dst, v):
+            dst.neutral = int(v is None)
+            if v is not None:
+                ctypes.memmove(dst.hash, v, 32)
+
+        def getn(src):
+            return None if src.neutral else bytes(src.hash)
+        for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),
+                     ("lab", "lab"), ("last_epoch_block", "leb")):
+            setn(getattr(st, a), state[b])
+        ei = EpochInfo(*epoch_info)
+        ph = np.ascontiguousarray(prev_hash, dtype=np.uint8)
+        pg = None if prev_is_genesis is None else np.ascontiguousarray(prev_is_genesis, dtype=np.uint8)
+        verdict = np.zeros(n, np.uint8)
+        stop, done = ctypes.c_size_t(0), ctypes.c_size_t(0)
+        self.check(self.L.praos_update_chain_dep_state(self.h, ctypes.byref(hs), ptr(ph),
+                                                       ptr(pg) if pg is not None else None, ctypes.byref(os_),
+                                                       ctypes.byref(ei), ctypes.byref(st), ptr(verdict),
+                                                       ctypes.byref(stop), ctypes.byref(done)))
+        state["last_slot"] = None if st.last_slot_origin else int(st.last_slot)
+        state["counters"] = {bytes(hk[28 * k:28 * k + 28]): int(cv[k]) for k in range(st.m)}
+        for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),
+                     ("lab", "lab"), ("last_epoch_block", "leb")):
+            state[b] = getn(getattr(st, a))
+        return verdict, stop.value, done.value
 
     def apply_batch(self, H, crypto, counters=None):
         """counters: dict hash28 -> int.  Returns (verdict u8[n], chain_stop, counters_out)."""

@@ -1,0 +1,120 @@
+"""The host-side sequential part (Praos.hs:407-502) through the C ABI on a host-only
+context (no GPU: crypto bits are synthetic), against oracle/chainstate.py."""
+import hashlib
+import random
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+import chainstate as cs
+
+
+def _b2b(m, n=32):
+    return hashlib.blake2b(m, digest_size=n).digest()
+
+
+@pytest.fixture(scope="module")
+def hctx():
+    from praos_hip import abi
+    c = abi.Context(abi.HOST_ONLY)
+    yield c
+    c.close()
+
+
+def _batch(r, n, pools, first_slot, stride):
+    H = {"slot": np.array([first_slot + i * stride + r.randrange(stride) for i in range(n)], np.uint64),
+         "cold_vk": np.frombuffer(bytes(r.getrandbits(8) for _ in range(32 * n)), np.uint8).reshape(n, 32).copy(),
+         "vrf_vk": np.zeros((n, 32), np.uint8), "vrf_out": np.zeros((n, 64), np.uint8),
+         "vrf_proof": np.zeros((n, 80), np.uint8), "hot_vk": np.zeros((n, 32), np.uint8),
+         "ocert_n": np.zeros(n, np.uint64), "ocert_c0": np.zeros(n, np.uint64),
+         "ocert_sig": np.zeros((n, 64), np.uint8), "kes_sig": np.zeros((n, 448), np.uint8),
+         "body_off": np.zeros(n, np.uint64), "body_len": np.zeros(n, np.uint32), "body_bytes": np.zeros(8, np.uint8)}
+    weights = [(0, 80), (cs.BIT_OCERT_SIG, 2), (cs.BIT_KES_LEAF, 2), (cs.BIT_VRF_PROOF, 2), (cs.BIT_LEADER, 3),
+               (cs.BIT_VRF_KEY_WRONG, 1), (cs.BIT_KES_AFTER_END, 1), (cs.BIT_INPUT, 1)]
+    bits = np.array([r.choices([b for b, _ in weights], [w for _, w in weights])[0] for _ in range(n)], np.uint16)
+    pidx = np.array([r.randrange(len(pools)) if r.random() > 0.02 else -1 for _ in range(n)], np.int32)
+    for i in range(n):
+        H["ocert_n"][i] = r.choice([0, 0, 1, 1, 2, 5])
+    crypto = {"bits": bits, "pool_idx": pidx, "beta": np.zeros((n, 64), np.uint8),
+              "leader": np.zeros((n, 32), np.uint8),
+              "nonce": np.frombuffer(bytes(r.getrandbits(8) for _ in range(32 * n)), np.uint8).reshape(n, 32).copy()}
+    prev = np.frombuffer(bytes(r.getrandbits(8) for _ in range(32 * n)), np.uint8).reshape(n, 32).copy()
+    hk = [pools[p][0] if p >= 0 else _b2b(bytes(H["cold_vk"][i]), 28) for i, p in enumerate(pidx)]
+    return H, crypto, prev, hk
+
+
+def _pools(r, k):
+    from praos_hip import fixed
+    return [(_b2b(b"pool" + bytes([i]), 28), _b2b(b"vrf" + bytes([i])), fixed.from_rational(Fraction(1, k)))
+            for i in range(k)]
+
+
+def _params():
+    from praos_hip import abi, fixed
+    return abi.params(c_raw=fixed.active_slot_log(Fraction(1, 20)))
+
+
+def test_apply_batch_host_only(hctx):
+    r = random.Random(5)
+    pools = _pools(r, 8)
+    hctx.set_epoch(_b2b(b"e"), pools, _params())
+    H, crypto, prev, hk = _batch(r, 400, pools, 1000, 7)
+    counters = {pools[0][0]: 1, pools[1][0]: 4, _b2b(b"gone", 28): 2}
+    v, stop, cm = hctx.apply_batch(H, crypto, counters)
+    want, want_stop, want_cm = cs.apply_batch(hk, crypto["bits"], H["ocert_n"], {p[0] for p in pools}, counters)
+    assert list(v) == want and stop == want_stop
+    assert all(cm[k] == want_cm[k] for k in counters)
+    assert len(set(want)) >= 6
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_chain_dep_state_fold_across_epochs(hctx, seed):
+    """Two epochs of 600 slots, stability window 180: the fold stops at the boundary
+    (the ticked epoch nonce differs from the context's), resumes after set_epoch with
+    the nonce the state computed, and matches the restatement step for step."""
+    r = random.Random(seed)
+    pools = _pools(r, 6)
+    base, length, window = 3000, 600, 180
+    H, crypto, prev, hk = _batch(r, 160, pools, base + 40, 7)      # slots 3040 .. ~4160: epochs 0, 1
+    genesis = np.zeros(160, np.uint8)
+    genesis[0] = 1
+    eta_a = _b2b(b"epoch-a")
+    st = {"last_slot": None, "counters": {pools[2][0]: 0}, "evolving": _b2b(b"ev"), "candidate": _b2b(b"cand"),
+          "epoch_nonce": eta_a, "lab": None, "leb": _b2b(b"leb")}
+    ref = {k: (dict(v) if isinstance(v, dict) else v) for k, v in st.items()}
+    known = {p[0] for p in pools}
+    ei = (base, 0, length, window)
+    prev_l = [None if genesis[i] else bytes(prev[i]) for i in range(160)]
+    done_total, calls = 0, 0
+    eta = eta_a
+    for _ in range(3):
+        calls += 1
+        hctx.set_epoch(eta, pools, _params())
+        sl = slice(done_total, None)
+        Hs = {k: (v[sl] if k not in ("body_bytes",) else v) for k, v in H.items()}
+        Hs = {k: np.ascontiguousarray(v) for k, v in Hs.items()}
+        cr = {k: np.ascontiguousarray(v[sl]) for k, v in crypto.items()}
+        v, stop, done = hctx.update_chain_dep_state(Hs, cr, prev[sl], st, ei, prev_is_genesis=genesis[sl])
+        wv, wstop, wdone = cs.fold(ref, hk[sl], Hs["slot"], cr["bits"], Hs["ocert_n"], cr["nonce"], prev_l[sl],
+                                   known, eta, base, 0, length, window)
+        assert done == wdone and stop == wstop
+        assert list(v[:done]) == wv
+        assert st == ref
+        done_total += done
+        if done_total == 160:
+            break
+        # the state ticks into the next epoch: eta = candidate ⭒ lastEpochBlock
+        eta = cs.combine(ref["candidate"], ref["leb"])
+    assert done_total == 160 and calls == 2
+    assert ref["epoch_nonce"] == eta != eta_a
+
+
+def test_host_only_refuses_gpu_calls(hctx):
+    from praos_hip import abi
+    r = random.Random(9)
+    pools = _pools(r, 2)
+    hctx.set_epoch(None, pools, _params())
+    H, crypto, prev, hk = _batch(r, 4, pools, 0, 5)
+    with pytest.raises(abi.PraosError):
+        hctx.verify_headers(H)

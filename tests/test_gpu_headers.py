@@ -147,3 +147,23 @@ def test_apply_batch_order(ctx):
     for k in counters:
         assert cm[k] == want_cm[k]
     assert abi.V_OK in want and len(set(want)) >= 3
+
+
+def test_chain_dep_state_fold_gpu(ctx):
+    """praos_update_chain_dep_state over a GPU-verified synthetic chain: the nonce fold
+    uses the GPU's vrfNonceValue outputs; checked against oracle/chainstate.py."""
+    import chainstate as cs
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 300, 5, 300, seed=b"\x0b" * 32, f=Fraction(9, 10))
+    o = ctx.verify_headers(H)
+    n = len(H["slot"])
+    prev = np.stack([np.frombuffer(b2b(i.to_bytes(8, "big")), np.uint8) for i in range(n)])
+    st = {"last_slot": None, "counters": {}, "evolving": eta0, "candidate": eta0, "epoch_nonce": eta0,
+          "lab": None, "leb": None}
+    ref = dict(st, counters={})
+    base = int(H["slot"][0]) - int(H["slot"][0]) % 432000
+    ei = (base, 0, 432000, 129600)
+    v, stop, done = ctx.update_chain_dep_state(H, o, prev, st, ei)
+    hk = [pool_list[pi][0] if pi >= 0 else b2b(bytes(H["cold_vk"][i]), 28) for i, pi in enumerate(o["pool_idx"])]
+    wv, wstop, wdone = cs.fold(ref, hk, H["slot"], o["bits"], H["ocert_n"], o["nonce"], [bytes(x) for x in prev],
+                               {q[0] for q in pool_list}, eta0, base, 0, 432000, 129600)
+    assert (done, stop) == (wdone, wstop) and list(v) == wv and st == ref
