@@ -36,13 +36,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 
-# Algorithmic work per unit (int32 lane-ops), counted from the kernel schedule
-# (DESIGN.md sec. 4 "Work model"): field mul 154, square 130, add/sub 17,
-# SHA-512 block 5000, BLAKE2b block 2700 int32 ops.
-W_OCERT = 529_000
-W_KES = 555_000
-W_VRF = 1_150_000
-W_LEADER = 3_000
+# Algorithmic work per unit (int32 lane-ops), counted by construction from the
+# kernel schedules (tools/workmodel.py; DESIGN.md sec. 4 "Work model").
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from workmodel import W_OCERT, W_KES, W_VRF, W_LEADER  # noqa: E402
 W_HEADER = W_OCERT + W_KES + W_VRF + W_LEADER
 PEAK_INT32 = 256 * 64 * 2.4e9      # VOP3 integer issue: 64 lane-ops/clk/CU (tools/microbench)
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}

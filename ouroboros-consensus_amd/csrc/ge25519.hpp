@@ -132,10 +132,36 @@ FE_INLINE void ge_tobytes_zi(uint32_t s[8], const fe& X, const fe& Y, const fe& 
   s[7] ^= (uint32_t)fe_isnegative(x) << 31;
 }
 
+// x = sqrt(u / v) exactly as libsodium ge25519_frombytes computes it:
+// x = u v^3 (u v^7)^((p-5)/8), multiplied by sqrt(-1) when v x^2 != u.
+// Returns false when u / v is not a square (neither v x^2 == u nor == -u).
+FE_INLINE bool fe_sqrt_ratio(fe& x, const fe& u, const fe& v) {
+  fe v3, vxx, chk;
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);                 // v^3
+  fe_sq(x, v3);
+  fe_mul(x, x, v);
+  fe_mul(x, x, u);                   // u v^7
+  fe_pow22523(x, x);
+  fe_mul(x, x, v3);
+  fe_mul(x, x, u);                   // u v^3 (u v^7)^((p-5)/8)
+  fe_sq(vxx, x);
+  fe_mul(vxx, vxx, v);
+  fe_sub(chk, vxx, u);
+  const bool has_m_root = fe_iszero(chk);
+  fe_add(chk, vxx, u);
+  const bool has_p_root = fe_iszero(chk);
+  fe xs, sq;
+  fe_const(sq, FE_SQRTM1);
+  fe_mul(xs, x, sq);
+  fe_cmov(x, xs, !has_m_root);
+  return has_m_root || has_p_root;
+}
+
 // libsodium ge25519_frombytes; negate=true gives ge25519_frombytes_negate_vartime.
 // Returns false when the encoding is not on the curve.
 FE_INLINE bool ge_frombytes(ge_p3& h, const uint32_t s[8], bool negate) {
-  fe u, v, v3, vxx, chk, one, d;
+  fe u, v, one, d;
   fe_set(one, 1);
   fe_const(d, FE_D);
   fe_frombytes32(h.Y, s);
@@ -144,47 +170,14 @@ FE_INLINE bool ge_frombytes(ge_p3& h, const uint32_t s[8], bool negate) {
   fe_mul(v, u, d);
   fe_sub(u, u, one);                 // u = y^2 - 1
   fe_add(v, v, one);                 // v = d y^2 + 1
-  fe_sq(v3, v);
-  fe_mul(v3, v3, v);                 // v^3
-  fe_sq(h.X, v3);
-  fe_mul(h.X, h.X, v);
-  fe_mul(h.X, h.X, u);               // u v^7
-  fe_pow22523(h.X, h.X);
-  fe_mul(h.X, h.X, v3);
-  fe_mul(h.X, h.X, u);               // u v^3 (u v^7)^((p-5)/8)
-  fe_sq(vxx, h.X);
-  fe_mul(vxx, vxx, v);
-  fe_sub(chk, vxx, u);
-  const bool has_m_root = fe_iszero(chk);
-  fe_add(chk, vxx, u);
-  const bool has_p_root = fe_iszero(chk);
-  fe xs, sq;
-  fe_const(sq, FE_SQRTM1);
-  fe_mul(xs, h.X, sq);
-  fe_cmov(h.X, xs, !has_m_root);
+  const bool ok = fe_sqrt_ratio(h.X, u, v);
   const bool sign = (s[7] >> 31) != 0;
   const bool flip = negate ? (fe_isnegative(h.X) == sign) : (fe_isnegative(h.X) != sign);
   fe nx;
   fe_neg(nx, h.X);
   fe_cmov(h.X, nx, flip);
   fe_mul(h.T, h.X, h.Y);
-  return has_m_root || has_p_root;
-}
-
-// ---- scalar recoding: 256-bit LE scalar (top bit clear) -> 64 signed radix-16 digits
-FE_INLINE void sc_signed_radix16(int8_t e[64], const uint32_t s[8]) {
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-#pragma unroll
-    for (int j = 0; j < 8; j++) e[8 * i + j] = (int8_t)((s[i] >> (4 * j)) & 15);
-  int carry = 0;
-#pragma unroll
-  for (int i = 0; i < 63; i++) {
-    int v = e[i] + carry;
-    carry = (v + 8) >> 4;
-    e[i] = (int8_t)(v - (carry << 4));
-  }
-  e[63] = (int8_t)(e[63] + carry);
+  return ok;
 }
 
 // ---- small-order blacklist and canonicity (libsodium ed25519_ref10.c)

@@ -10,12 +10,10 @@ __global__ void __launch_bounds__(NT, LB_ED) k_ocert(size_t n, const ge_niels* _
                                               const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot,
                                               uint64_t slots_per_kes_period, uint64_t max_kes_evo,
                                               uint16_t* __restrict__ bits, uint8_t* __restrict__ ok_out) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[BTAB_N];
+  const ge_niels* btab = stage_btab<1>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  DigitPlanes dp{sdig, NT, 2};
   uint32_t pk[8], hot[8], sg[16];
   load_words(pk, cold_vk + 32 * i, 8);
   load_words(hot, hot_vk + 32 * i, 8);
@@ -23,7 +21,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_ocert(size_t n, const ge_niels* _
   const uint64_t nn = ocert_n[i], c0 = ocert_c0[i];
   uint32_t hram[16];
   ocert_hram(hram, sg, pk, hot, nn, c0);
-  const bool ok = ed25519_verify_core(pk, sg, sg + 8, hram, dp, threadIdx.x, btab);
+  const bool ok = ed25519_verify_core(pk, sg, sg + 8, hram, btab);
   if (ok_out) {
     ok_out[i] = ok ? 1 : 0;
     return;
@@ -45,12 +43,10 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
                                             const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0,
                                             uint64_t slots_per_kes_period, const uint32_t* __restrict__ period,
                                             uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[BTAB_N];
+  const ge_niels* btab = stage_btab<1>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  DigitPlanes dp{sdig, NT, 2};
   uint64_t t;
   if (period) {
     t = period[i];
@@ -71,7 +67,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
 #pragma unroll
   for (int k = 0; k < 8; k++) { pre[k] = sg[k]; pre[8 + k] = leaf[k]; }
   sha512_stream(hram, pre, 64, body + off, len);
-  const bool leaf_ok = ed25519_verify_core(leaf, sg, sg + 8, hram, dp, threadIdx.x, btab);
+  const bool leaf_ok = ed25519_verify_core(leaf, sg, sg + 8, hram, btab);
   if (result) {
     result[i] = !in_range ? 3 : (!merkle_ok ? 1 : (leaf_ok ? 0 : 2));
     return;

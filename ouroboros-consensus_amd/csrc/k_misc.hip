@@ -2,14 +2,22 @@
 #include "kcommon.hpp"
 
 // ------------------------------------------------------------------ init
-// btab[k] = (k+1) B as affine niels (y+x, y-x, 2dxy); one lane per entry.
+// btab[k] = (k+1) B and btab[BTAB_N + k] = (k+1) 2^128 B (k < BTAB_N) as
+// affine niels (y+x, y-x, 2dxy); one lane per entry (runs once per context).
 __global__ void k_init_btab(ge_niels* btab) {
-  const int k = threadIdx.x;
-  if (k >= 8) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * BTAB_N) return;
+  const int k = e % BTAB_N;
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   ge_p3 B, acc;
   ge_frombytes(B, benc, false);
+  if (e >= BTAB_N) {
+    for (int i = 0; i < 128; i++) {
+      ge_p3_dbl_to_p3(acc, B);
+      B = acc;
+    }
+  }
   acc = B;
   ge_cached bc;
   ge_p3_to_cached(bc, B);
@@ -30,7 +38,7 @@ __global__ void k_init_btab(ge_niels* btab) {
   fe_mul(xy, x, y);
   fe_const(d2, FE_D2);
   fe_mul(n.xy2d, xy, d2);
-  btab[k] = n;
+  btab[e] = n;
 }
 
 // ------------------------------------------------------------------ leader
@@ -139,19 +147,18 @@ __global__ void k_debug_decode(size_t n, const uint8_t* in, uint8_t* out, uint8_
   store_words(out + 32 * i, e, 8);
 }
 
+// [s mod L] B (B has order L, so this is [s]B for any 256-bit s)
 __global__ void __launch_bounds__(NT) k_debug_smul_base(size_t n, const ge_niels* gbtab, const uint8_t* s,
                                                         uint8_t* out) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  DigitPlanes dp{sdig, NT, 2};
-  uint32_t w[8], e[8];
+  uint32_t w[8], r[8], e[8];
   load_words(w, s + 32 * i, 8);
-  store_digits(dp, 1, threadIdx.x, w);
+  sc_reduce256(r, w);
   ge_p3 R;
-  ge_scalarmult_base(R, dp, 1, threadIdx.x, btab);
+  ge_scalarmult_base(R, r, btab);
   ge_tobytes(e, R.X, R.Y, R.Z);
   store_words(out + 32 * i, e, 8);
 }
@@ -165,7 +172,8 @@ __global__ void k_debug_h2c(size_t n, const uint8_t* pk, const uint8_t* alpha, u
   ge_p3 Y, H;
   ge_frombytes(Y, w, false);
   ge_enc_affine(ys, Y);
-  vrf_hash_to_curve(H, hs, ys, a);
+  vrf_hash_to_curve(H, ys, a);
+  ge_tobytes(hs, H.X, H.Y, H.Z);
   store_words(out + 32 * i, hs, 8);
 }
 

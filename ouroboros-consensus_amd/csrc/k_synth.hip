@@ -51,12 +51,10 @@ __global__ void __launch_bounds__(NT) k_synth_pools(uint32_t npools, const ge_ni
                                                     uint32_t* cold_seed, uint32_t* cold_pk, uint32_t* vrf_seed,
                                                     uint32_t* vrf_pk, uint32_t* kes_seed, uint8_t* pool_hash28,
                                                     uint8_t* pool_vrf32) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
   const uint32_t p = blockIdx.x * NT + threadIdx.x;
   if (p >= npools) return;
-  DigitPlanes dp{sdig, NT, 2};
   uint32_t ms[8], cs[8], vs[8], ks[8], az[16], cpk[8], vpk[8], h[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) ms[k] = master[k];
@@ -64,9 +62,9 @@ __global__ void __launch_bounds__(NT) k_synth_pools(uint32_t npools, const ge_ni
   derive_seed(vs, 2, ms, p);
   derive_seed(ks, 3, ms, p);
   ed25519_expand(az, cs);
-  ed25519_pk_from_az(cpk, az, dp, threadIdx.x, btab);
+  ed25519_pk_from_az(cpk, az, btab);
   ed25519_expand(az, vs);
-  ed25519_pk_from_az(vpk, az, dp, threadIdx.x, btab);
+  ed25519_pk_from_az(vpk, az, btab);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     cold_seed[8 * p + k] = cs[k]; cold_pk[8 * p + k] = cpk[k];
@@ -84,12 +82,10 @@ __global__ void __launch_bounds__(NT) k_synth_pools(uint32_t npools, const ge_ni
 __global__ void __launch_bounds__(NT) k_synth_kes_leaves(uint32_t npools, const ge_niels* gbtab,
                                                          const uint32_t* kes_seed, uint32_t* leaf_seed,
                                                          uint32_t* tree) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
   const uint32_t g = blockIdx.x * NT + threadIdx.x;
   if (g >= npools * 64u) return;
-  DigitPlanes dp{sdig, NT, 2};
   const uint32_t p = g / 64, j = g % 64;
   uint32_t s[8], r[8], az[16], pk[8];
 #pragma unroll
@@ -100,7 +96,7 @@ __global__ void __launch_bounds__(NT) k_synth_kes_leaves(uint32_t npools, const 
     for (int k = 0; k < 8; k++) s[k] = r[k];
   }
   ed25519_expand(az, s);
-  ed25519_pk_from_az(pk, az, dp, threadIdx.x, btab);
+  ed25519_pk_from_az(pk, az, btab);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     leaf_seed[8 * g + k] = s[k];
@@ -135,12 +131,10 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
     uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos,
     uint8_t* l_out, uint8_t* l_proof) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  DigitPlanes dp{sdig, NT, 2};
   const uint32_t p = (uint32_t)(mix64(i ^ salt) % npools);
   const uint64_t s = first_slot + i * slot_stride;
   const uint64_t kp = s / slots_per_kes_period;
@@ -174,7 +168,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
 #pragma unroll
   for (int k = 0; k < 8; k++) seed[k] = cold_seed[8 * p + k];
   ed25519_expand(az, seed);
-  ed25519_sign_core(sig, az, cpk, msg, 48, dp, threadIdx.x, btab);
+  ed25519_sign_core(sig, az, cpk, msg, 48, btab);
   store_words(ocert_sig + 64 * i, sig, 16);
   // KES: leaf t signs the body; path pairs from the tree (leaf level first)
   const uint32_t leaf = (uint32_t)t;
@@ -182,7 +176,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
 #pragma unroll
   for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)kk * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
   ed25519_expand(az, seed);
-  ed25519_sign_core(sig, az, lpk, body_bytes + boff, blen, dp, threadIdx.x, btab);
+  ed25519_sign_core(sig, az, lpk, body_bytes + boff, blen, btab);
   uint8_t* ks = kes_sig + 448 * i;
   store_words(ks, sig, 16);
   uint32_t node = 64 + leaf;
@@ -201,7 +195,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   for (int cert = 0; cert < (tpraos ? 2 : 1); cert++) {
     if (tpraos) tpraos_seed(alpha, s, e0, eta0_neutral != 0, (uint64_t)cert);
     else mk_input_vrf(alpha, s, e0, eta0_neutral != 0);
-    vrf_prove_core(proof, az, vpk, alpha, dp, threadIdx.x, btab);
+    vrf_prove_core(proof, az, vpk, alpha, btab);
     store_words((cert ? l_proof : vrf_proof) + 80 * i, proof, 20);
     ge_p3 G, G2, G4, G8;
     ge_frombytes(G, proof, false);

@@ -16,12 +16,10 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const ge_niels* __
                                             int32_t* __restrict__ pool_sorted_idx, uint8_t* __restrict__ beta_out,
                                             uint8_t* __restrict__ leader_out, uint8_t* __restrict__ nonce_out,
                                             uint8_t* __restrict__ ok_out) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  DigitPlanes dp{sdig, NT, 2};
   uint32_t pk[8], pr[20], alpha[8];
   load_words(pk, vrf_vk + 32 * i, 8);
   load_words(pr, vrf_proof + 80 * i, 20);
@@ -63,7 +61,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const ge_niels* __
   }
   uint32_t beta[16];
   bool gamma_ok;
-  const bool proof_ok = vrf_verify_core(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, dp, threadIdx.x, btab);
+  const bool proof_ok = vrf_verify_core(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab);
   if (!gamma_ok) {
 #pragma unroll
     for (int k = 0; k < 16; k++) beta[k] = 0;
@@ -107,12 +105,10 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map, uint32_t npools, int check_output,
     uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx, int32_t* __restrict__ pool_sorted_idx,
     uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_l, uint8_t* __restrict__ nonce_out) {
-  __shared__ ge_niels sbtab[8];
-  __shared__ int8_t sdig[DIG_BYTES];
-  const ge_niels* btab = stage_btab(gbtab, sbtab);
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  DigitPlanes dp{sdig, NT, 2};
   uint32_t pk[8], e0[8];
   load_words(pk, vrf_vk + 32 * i, 8);
 #pragma unroll
@@ -151,7 +147,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     load_words(out, (cert ? l_out : eta_out) + 64 * i, 16);
     tpraos_seed(alpha, s, e0, eta0_neutral != 0, (uint64_t)cert);
     bool gamma_ok;
-    const bool ok = vrf_verify_core(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, dp, threadIdx.x, btab);
+    const bool ok = vrf_verify_core(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab);
     if (!gamma_ok) {
 #pragma unroll
       for (int k = 0; k < 16; k++) beta[k] = 0;

@@ -23,7 +23,6 @@
 #ifndef LB_VRF
 #define LB_VRF 3
 #endif
-#define DIG_BYTES (64 * 2 * NT)     // two digit planes
 
 __device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords) {
   const uint4* q = (const uint4*)p;
@@ -37,12 +36,13 @@ __device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int n
   for (int i = 0; i < nwords / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
-// Stage the 8-entry niels table of B into LDS (all threads of the block).
+// Stage NTAB fixed-base niels tables (B, then B' = 2^128 B; BTAB_N entries
+// each) into LDS (all threads of the block).
+template <int NTAB>
 __device__ __forceinline__ const ge_niels* stage_btab(const ge_niels* __restrict__ g, ge_niels* s) {
-  const uint32_t* src = (const uint32_t*)g;
-  uint32_t* dst = (uint32_t*)s;
-  for (int i = threadIdx.x; i < 8 * 24; i += blockDim.x) dst[i] = src[i];
+  const uint4* src = (const uint4*)g;
+  uint4* dst = (uint4*)s;
+  for (int i = threadIdx.x; i < NTAB * BTAB_WORDS / 4; i += blockDim.x) dst[i] = src[i];
   __syncthreads();
   return s;
 }
-

@@ -7,6 +7,7 @@
 
 static constexpr size_t NT = 256;                  // threads per block of the crypto kernels
 static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
+static constexpr size_t BTAB_N = 128;              // entries per fixed-base table (scalarmult.hpp)
 
 #include <algorithm>
 #include <cstdio>
@@ -104,8 +105,8 @@ praos_ctx* praos_open(int device) {
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
   for (auto& st : c->side) (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-  if (hipMalloc(&c->btab, 8 * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
-  launch_init_btab(dim3(1), dim3(64), c->stream, c->btab);
+  if (hipMalloc(&c->btab, 2 * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
+  launch_init_btab(dim3(1), dim3(2 * BTAB_N), c->stream, c->btab);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
     fprintf(stderr, "praos_open: init kernel failed\n");
     delete c;

@@ -84,19 +84,23 @@ FE_INLINE void sha512_stream(uint32_t out[16], const uint32_t prefix[16], uint32
 // hram: SHA-512(R || A || M) digest words.  Checks in libsodium order; all
 // lanes do the full computation (rejections are folded in at the end).
 FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], const uint32_t S[8],
-                                   const uint32_t hram[16], DigitPlanes& dp, int t,
-                                   const ge_niels* __restrict__ btab) {
+                                   const uint32_t hram[16], const ge_niels* __restrict__ btab) {
   bool ok = sc_is_canonical(S) && !ge_has_small_order(R) && ge_is_canonical(pk) && !ge_has_small_order(pk);
   ge_p3 A;
   ok = ge_frombytes(A, pk, /*negate=*/true) && ok;
   uint32_t h[8], s[8];
   sc_reduce512(h, hram);
 #pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;      // keep recoding in range
-  store_digits(dp, 0, t, h);
-  store_digits(dp, 1, t, s);
+  for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;      // keep the recoding in range (S < L)
+  ge_cached tab[8];
+  build_cached_table(tab, A);
+  uint32_t hw[8], sw[8];
+  sc_recode16(hw, h);
+  sc_recode256(sw, s);
+  ge_p1p1 x;
+  straus<64, 64, 0, 32, false>(x, tab, hw, nullptr, nullptr, btab, sw);   // [s]B - [h]A
   ge_p2 Rp;
-  ge_double_scalarmult_base(Rp, dp, 0, 1, t, A, 64, btab);   // [s]B - [h]A
+  ge_p1p1_to_p2(Rp, x);
   uint32_t enc[8];
   ge_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
   bool eq = true;
@@ -166,50 +170,74 @@ FE_INLINE bool kes_merkle(uint32_t leaf_vk[8], const uint32_t vk[8], uint64_t t,
 // ------------------------------------------------------------------ VRF draft-03
 __device__ __constant__ static const uint32_t FE_CURVE_A[8] = {486662u, 0, 0, 0, 0, 0, 0, 0};
 
-// libsodium ge25519_from_uniform (the VRF caller has cleared r's sign bit):
-// returns the point H = 8 * P and its encoding.
-FE_INLINE void vrf_from_uniform(ge_p3& H, uint32_t hs[8], const uint32_t r[8]) {
-  fe rr2, x, x2, x3, e, one, A;
-  fe_set(one, 1);
+// libsodium ge25519_from_uniform (the VRF caller has cleared r's sign bit),
+// restated without its two field inversions: returns H = 8 * P projective
+// (the encoding is deferred to the caller's batched inversion).
+//   w = 1 + 2 r^2, Montgomery x = -A / w, e = x^3 + A x^2 + x.
+//   chi(e) = chi(-A w Q) with Q = A^2 - A^2 w + w^2 (e = -A Q / w^3).
+//   u = x (chi(e) != -1) or -x - A = A (1 - w) / w (chi(e) = -1), and
+//   y = (u - 1) / (u + 1) = N / D:  N = -(A + w), D = w - A  resp.
+//                                   N = A - A w - w, D = A - A w + w.
+//   libsodium inverts u + 1 = 0 to 0 (y = 0): D = 0 gives N/D = 0/1.
+// P = ge25519_frombytes(y, sign 0): x = sqrt((y^2 - 1) / (d y^2 + 1)) computed
+// as sqrt((N^2 - D^2) / (d N^2 + D^2)) with the same root/parity rules, so P =
+// (x D : N : D : x N) is exactly libsodium's point.
+FE_INLINE void vrf_from_uniform(ge_p3& H, const uint32_t r[8]) {
+  fe A, one, w, t, q, e, A2;
   fe_const(A, FE_CURVE_A);
-  fe_frombytes32(rr2, r);
-  fe_sq(rr2, rr2);
-  fe_add(rr2, rr2, rr2);
-  fe_add(rr2, rr2, one);            // 1 + 2 r^2
-  fe_invert(rr2, rr2);
-  fe_mul(x, A, rr2);
-  fe_neg(x, x);                     // x = -A / (1 + 2 r^2)
-  fe_sq(x2, x);
-  fe_mul(x3, x, x2);
-  fe_add(e, x3, x);
-  fe_mul(x2, x2, A);
-  fe_add(e, x2, e);                 // e = x^3 + A x^2 + x
+  fe_set(one, 1);
+  fe_frombytes32(w, r);
+  fe_sq(w, w);
+  fe_add(w, w, w);
+  fe_add(w, w, one);                // w = 1 + 2 r^2 (never 0: -1/2 is a non-square)
+  fe_sq(A2, A);
+  fe Aw;
+  fe_mul(Aw, A, w);
+  fe_mul(t, A2, w);
+  fe_sub(q, A2, t);
+  fe_sq(t, w);
+  fe_add(q, q, t);                  // Q
+  fe_mul(q, q, Aw);
+  fe_neg(e, q);                     // -A w Q
   fe_chi(e, e);
   fe ec;
   fe_canon(ec, e);
   const bool e_is_minus_1 = (ec.v[0] >> 8) & 1;   // libsodium: s[1] & 1 of the encoding
+  fe N, D, N2, D2;
+  fe_add(N, A, w);
+  fe_neg(N, N);
+  fe_sub(D, w, A);
+  fe_sub(t, A, Aw);
+  fe_sub(N2, t, w);
+  fe_add(D2, t, w);
+  fe_cmov(N, N2, e_is_minus_1);
+  fe_cmov(D, D2, e_is_minus_1);
+  const bool dz = fe_iszero(D);
+  fe zero;
+  fe_set(zero, 0);
+  fe_cmov(N, zero, dz);
+  fe_cmov(D, one, dz);
+  // x^2 = (N^2 - D^2) / (d N^2 + D^2)
+  fe nn, dd, u, v, d, x;
+  fe_sq(nn, N);
+  fe_sq(dd, D);
+  fe_sub(u, nn, dd);
+  fe_const(d, FE_D);
+  fe_mul(v, nn, d);
+  fe_add(v, v, dd);
+  fe_sqrt_ratio(x, u, v);           // cannot fail: the point exists
   fe negx;
   fe_neg(negx, x);
-  fe_cmov(x, negx, e_is_minus_1);
-  fe a2;
-  fe_set(a2, 0);
-  fe_cmov(a2, A, e_is_minus_1);
-  fe_sub(x, x, a2);
-  // y_ed = (x - 1) / (x + 1)
-  fe xp1, xm1, inv, yed;
-  fe_add(xp1, x, one);
-  fe_sub(xm1, x, one);
-  fe_invert(inv, xp1);
-  fe_mul(yed, xm1, inv);
-  uint32_t ys[8];
-  fe_tobytes32(ys, yed);            // sign bit 0
+  fe_cmov(x, negx, fe_isnegative(x));   // sign bit 0
   ge_p3 P;
-  ge_frombytes(P, ys, false);       // cannot fail (libsodium aborts otherwise)
+  fe_mul(P.X, x, D);
+  P.Y = N;
+  P.Z = D;
+  fe_mul(P.T, x, N);
   ge_p3 Q;
   ge_p3_dbl_to_p3(Q, P);
   ge_p3_dbl_to_p3(P, Q);
   ge_p3_dbl_to_p3(H, P);            // cofactor 8
-  ge_tobytes(hs, H.X, H.Y, H.Z);
 }
 
 // encoding of a point with Z == 1 (fresh from ge_frombytes)
@@ -218,8 +246,8 @@ FE_INLINE void ge_enc_affine(uint32_t s[8], const ge_p3& P) {
   s[7] |= (uint32_t)fe_isnegative(P.X) << 31;
 }
 
-// r = first 32 bytes of SHA-512(0x04 || 0x01 || Y || alpha), sign bit cleared
-FE_INLINE void vrf_hash_to_curve(ge_p3& H, uint32_t hs[8], const uint32_t ys[8], const uint32_t alpha[8]) {
+// H from r = first 32 bytes of SHA-512(0x04 || 0x01 || Y || alpha), sign bit cleared
+FE_INLINE void vrf_hash_to_curve(ge_p3& H, const uint32_t ys[8], const uint32_t alpha[8]) {
   uint32_t P[16], S[17], d[16];
 #pragma unroll
   for (int i = 0; i < 8; i++) { P[i] = ys[i]; P[8 + i] = alpha[i]; }
@@ -229,7 +257,7 @@ FE_INLINE void vrf_hash_to_curve(ge_p3& H, uint32_t hs[8], const uint32_t ys[8],
 #pragma unroll
   for (int i = 0; i < 8; i++) r[i] = d[i];
   r[7] &= 0x7fffffffu;
-  vrf_from_uniform(H, hs, r);
+  vrf_from_uniform(H, r);
 }
 
 // beta = SHA-512(0x04 || 0x03 || enc(8 Gamma))
@@ -252,9 +280,12 @@ FE_INLINE void vrf_hash_points(uint32_t c[4], const uint32_t h[8], const uint32_
 }
 
 // Returns proof validity; beta always computed from Gamma (gamma_ok tells if it decoded).
+//   U = [s]B - [c]Y  : 33-window chain, s split over B and B' = 2^128 B (radix 256)
+//   V = [s]H - [c]Gamma : 64-window chain, both bases per lane (radix 16)
+// One batched inversion encodes H, U, V and 8 Gamma.
 FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t pk[8], const uint32_t gamma[8],
                                const uint32_t c4[4], const uint32_t s8[8], const uint32_t alpha[8],
-                               DigitPlanes& dp, int t, const ge_niels* __restrict__ btab) {
+                               const ge_niels* __restrict__ btab) {
   // vrf_validate_key: small order -> reject; ge25519_frombytes must succeed
   bool ok = !ge_has_small_order(pk);
   ge_p3 Y, G;
@@ -268,39 +299,57 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
 #pragma unroll
   for (int i = 0; i < 8; i++) c[i] = i < 4 ? c4[i] : 0u;
   // H = hash_to_curve(canonical Y, alpha)
-  uint32_t ys[8], hs[8];
+  uint32_t ys[8];
   ge_enc_affine(ys, Y);
   ge_p3 H;
-  vrf_hash_to_curve(H, hs, ys, alpha);
-  store_digits(dp, 0, t, c);
-  store_digits(dp, 1, t, s);
-  // U = [s]B - [c]Y
-  ge_p3 nY = Y;
-  fe_neg(nY.X, Y.X);
-  fe_neg(nY.T, Y.T);
-  ge_p2 U;
-  ge_double_scalarmult_base(U, dp, 0, 1, t, nY, 33, btab);
-  // V = [s]H - [c]Gamma
-  ge_p3 nG = G;
-  fe_neg(nG.X, G.X);
-  fe_neg(nG.T, G.T);
-  ge_p2 V;
-  ge_double_scalarmult_var(V, dp, 1, 0, t, H, nG, 33);
+  vrf_hash_to_curve(H, ys, alpha);
+  ge_p2 U, V;
+  {  // U = [s]B - [c]Y
+    ge_p3 nY = Y;
+    fe_neg(nY.X, Y.X);
+    fe_neg(nY.T, Y.T);
+    ge_cached ty[8];
+    build_cached_table(ty, nY);
+    uint32_t cw[8], sw[8];
+    sc_recode16(cw, c);
+    sc_recode256(sw, s);
+    ge_p1p1 x;
+    straus<33, 33, 0, 16, true>(x, ty, cw, nullptr, nullptr, btab, sw);
+    ge_p1p1_to_p2(U, x);
+  }
+  {  // V = [s]H - [c]Gamma
+    ge_p3 nG = G;
+    fe_neg(nG.X, G.X);
+    fe_neg(nG.T, G.T);
+    ge_cached th[8], tg[8];
+    build_cached_table(th, H);
+    build_cached_table(tg, nG);
+    uint32_t sw[8], cw[8];
+    sc_recode16(sw, s);
+    sc_recode16(cw, c);
+    ge_p1p1 x;
+    straus<64, 64, 33, 0, false>(x, th, sw, tg, cw, nullptr, nullptr);
+    ge_p1p1_to_p2(V, x);
+  }
   // 8 Gamma
   ge_p3 G2, G4, G8;
   ge_p3_dbl_to_p3(G2, G);
   ge_p3_dbl_to_p3(G4, G2);
   ge_p3_dbl_to_p3(G8, G4);
-  // batched inversion of U.Z, V.Z, G8.Z
-  fe zuv, zall, inv, iu, iv, ig;
-  fe_mul(zuv, U.Z, V.Z);
-  fe_mul(zall, zuv, G8.Z);
-  fe_invert(inv, zall);
-  fe_mul(ig, inv, zuv);             // 1/G8.Z
+  // batched inversion of U.Z, V.Z, G8.Z, H.Z
+  fe z12, z123, z1234, inv, iu, iv, ig, ih;
+  fe_mul(z12, U.Z, V.Z);
+  fe_mul(z123, z12, G8.Z);
+  fe_mul(z1234, z123, H.Z);
+  fe_invert(inv, z1234);
+  fe_mul(ih, inv, z123);            // 1/H.Z
+  fe_mul(inv, inv, H.Z);            // 1/(U.Z V.Z G8.Z)
+  fe_mul(ig, inv, z12);             // 1/G8.Z
   fe_mul(inv, inv, G8.Z);           // 1/(U.Z V.Z)
   fe_mul(iu, inv, V.Z);
   fe_mul(iv, inv, U.Z);
-  uint32_t us[8], vs[8], gs[8], g8s[8];
+  uint32_t hs[8], us[8], vs[8], gs[8], g8s[8];
+  ge_tobytes_zi(hs, H.X, H.Y, ih);
   ge_tobytes_zi(us, U.X, U.Y, iu);
   ge_tobytes_zi(vs, V.X, V.Y, iv);
   ge_tobytes_zi(g8s, G8.X, G8.Y, ig);
@@ -327,29 +376,32 @@ FE_INLINE void ed25519_expand(uint32_t az[16], const uint32_t seed[8]) {
   az[7] |= 0x40000000u;
 }
 
-FE_INLINE void ed25519_pk_from_az(uint32_t pk[8], const uint32_t az[16], DigitPlanes& dp, int t,
-                                  const ge_niels* __restrict__ btab) {
-  uint32_t a[8];
+// reduce a 256-bit scalar mod L ([a]P = [a mod L]P for P in the prime-order subgroup)
+FE_INLINE void sc_reduce256(uint32_t r[8], const uint32_t a[8]) {
+  uint32_t x[16];
 #pragma unroll
-  for (int i = 0; i < 8; i++) a[i] = az[i];
-  store_digits(dp, 1, t, a);
+  for (int i = 0; i < 16; i++) x[i] = i < 8 ? a[i] : 0u;
+  sc_reduce512(r, x);
+}
+
+FE_INLINE void ed25519_pk_from_az(uint32_t pk[8], const uint32_t az[16], const ge_niels* __restrict__ btab) {
+  uint32_t a[8];
+  sc_reduce256(a, az);
   ge_p3 A;
-  ge_scalarmult_base(A, dp, 1, t, btab);
+  ge_scalarmult_base(A, a, btab);
   ge_tobytes(pk, A.X, A.Y, A.Z);
 }
 
 // RFC 8032 signature of msg (global memory, 8-aligned, len bytes)
 FE_INLINE void ed25519_sign_core(uint32_t sig[16], const uint32_t az[16], const uint32_t pk[8],
-                                 const uint8_t* __restrict__ msg, uint32_t len, DigitPlanes& dp, int t,
-                                 const ge_niels* __restrict__ btab) {
+                                 const uint8_t* __restrict__ msg, uint32_t len, const ge_niels* __restrict__ btab) {
   uint32_t pre[16], d[16], r[8], h[8], a[8];
 #pragma unroll
   for (int i = 0; i < 16; i++) pre[i] = i < 8 ? az[8 + i] : 0u;
   sha512_stream(d, pre, 32, msg, len);
   sc_reduce512(r, d);
-  store_digits(dp, 1, t, r);
   ge_p3 R;
-  ge_scalarmult_base(R, dp, 1, t, btab);
+  ge_scalarmult_base(R, r, btab);
   uint32_t rs[8];
   ge_tobytes(rs, R.X, R.Y, R.Z);
 #pragma unroll
@@ -366,19 +418,18 @@ FE_INLINE void ed25519_sign_core(uint32_t sig[16], const uint32_t az[16], const 
 
 // draft-03 prove (crypto_vrf_ietfdraft03_prove): proof = Gamma || c || s
 FE_INLINE void vrf_prove_core(uint32_t proof[20], const uint32_t az[16], const uint32_t pk[8],
-                              const uint32_t alpha[8], DigitPlanes& dp, int t, const ge_niels* __restrict__ btab) {
+                              const uint32_t alpha[8], const ge_niels* __restrict__ btab) {
   ge_p3 Y;
   ge_frombytes(Y, pk, false);
   uint32_t ys[8], hs[8];
   ge_enc_affine(ys, Y);
   ge_p3 H;
-  vrf_hash_to_curve(H, hs, ys, alpha);
+  vrf_hash_to_curve(H, ys, alpha);
+  ge_tobytes(hs, H.X, H.Y, H.Z);
   uint32_t x[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) x[i] = az[i];
-  store_digits(dp, 0, t, x);
+  sc_reduce256(x, az);
   ge_p3 G;
-  ge_scalarmult_var(G, dp, 0, t, H);
+  ge_scalarmult_var(G, x, H);
   // k = SHA-512(az[32..64) || h_string) mod L
   uint32_t S[17], d[16], k[8];
 #pragma unroll
@@ -386,10 +437,9 @@ FE_INLINE void vrf_prove_core(uint32_t proof[20], const uint32_t az[16], const u
   S[16] = 0x80u;
   sha512_regs<17, 64>(d, S);
   sc_reduce512(k, d);
-  store_digits(dp, 1, t, k);
   ge_p3 kB, kH;
-  ge_scalarmult_base(kB, dp, 1, t, btab);
-  ge_scalarmult_var(kH, dp, 1, t, H);
+  ge_scalarmult_base(kB, k, btab);
+  ge_scalarmult_var(kH, k, H);
   uint32_t gs[8], kbs[8], khs[8];
   ge_tobytes(gs, G.X, G.Y, G.Z);
   ge_tobytes(kbs, kB.X, kB.Y, kB.Z);

@@ -1,36 +1,63 @@
 // scalarmult.hpp -- per-lane multi-scalar multiplication for gfx950.
 //
-// All scalar multiplications on the Praos path are Straus/Shamir sums over
-// 64 signed radix-16 windows (Horner: 4 doublings per window):
-//   * fixed base B: 8-entry affine-niels table {1..8}B shared by the block in
-//     LDS (computed once per context by k_init_basetab);
-//   * per-lane variable bases: 8-entry cached tables {1..8}P in private
-//     memory (scratch: indexed by a per-lane digit, so not register-resident).
-// Digits are recoded once into LDS (int8, lane-interleaved: conflict-free).
-// Results are mathematically exact group elements, so verdicts depend only on
-// the encodings, exactly as in libsodium (which uses a different schedule).
+// Every scalar multiplication on the Praos path is one Straus/Horner chain
+// over 4-bit windows (4 doublings between windows, shared by all terms):
+//   * per-lane variable bases P, Q: signed radix-16 digits in [-8, 7], 8-entry
+//     cached tables {1..8}P in private memory (indexed by a per-lane digit);
+//   * the fixed base B (and B' = 2^128 B): signed radix-256 digits in
+//     [-128, 127] with 128-entry affine-niels tables {1..128}B, {1..128}B'
+//     staged in LDS per block (k_init_btab builds them once per context).
+//     A fixed-base digit is added every other window (one byte = 2 windows),
+//     which halves the fixed-base additions of a radix-16 schedule.
+//
+// Digits are produced on the fly from the scalar kept in registers, recoded
+// once as w = s + 0x88..88 (radix 16) or s + 0x80..80 (radix 256): the
+// signed digit j is then nibble/byte j of w minus 8/128 (exact for s < 2^253,
+// which holds for every scalar here: values reduced mod L, or < 2^128).  The
+// register is shifted left by one window per step, so no digit array exists.
+//
+// Window schedules are uniform across the wave (no divergence): digits may be
+// zero (identity added), exactly as in a constant-time schedule.  Results are
+// exact group elements, so verdicts depend only on the encodings, as in
+// libsodium (which uses a different, sliding-window schedule).
 #pragma once
 #include "ge25519.hpp"
 
-// LDS layout helpers: digit j of lane t in plane k: dig[(j * NPLANE + k) * nthreads + t]
-struct DigitPlanes {
-  int8_t* base;
-  int nthreads;
-  int nplane;
-  FE_INLINE int8_t get(int j, int k, int t) const { return base[(j * nplane + k) * nthreads + t]; }
-  FE_INLINE void put(int j, int k, int t, int8_t v) { base[(j * nplane + k) * nthreads + t] = v; }
-};
+#define BTAB_N 128                     // entries per fixed-base table
+#define BTAB_WORDS (BTAB_N * 24)       // u32 words per table (niels = 3 fe)
 
-FE_INLINE void store_digits(DigitPlanes& dp, int plane, int t, const uint32_t s[8]) {
-  int8_t e[64];
-  sc_signed_radix16(e, s);
+// w = s + 0x8888...88 (radix-16 signed recoding); requires s < 2^253
+FE_INLINE void sc_recode16(uint32_t w[8], const uint32_t s[8]) {
+  uint32_t c = 0;
 #pragma unroll
-  for (int j = 0; j < 64; j++) dp.put(j, plane, t, e[j]);
+  for (int i = 0; i < 8; i++) w[i] = addc(s[i], 0x88888888u, c, &c);
+}
+// w = s + 0x8080...80 (radix-256 signed recoding); requires s < 2^253
+FE_INLINE void sc_recode256(uint32_t w[8], const uint32_t s[8]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = addc(s[i], 0x80808080u, c, &c);
+}
+
+template <int NW, int SH>
+FE_INLINE void shl_small(uint32_t w[NW]) {          // w <<= SH, 0 < SH < 32
+#pragma unroll
+  for (int i = NW - 1; i > 0; i--) w[i] = __builtin_amdgcn_alignbit(w[i], w[i - 1], 32 - SH);
+  w[0] <<= SH;
+}
+template <int NW, int BITS>
+FE_INLINE void shl_const(uint32_t w[NW]) {          // w <<= BITS (compile-time)
+  constexpr int WS = BITS / 32, B = BITS % 32;
+  if constexpr (WS > 0) {
+#pragma unroll
+    for (int i = NW - 1; i >= 0; i--) w[i] = i >= WS ? w[i - WS] : 0u;
+  }
+  if constexpr (B > 0) shl_small<NW, B>(w);
 }
 
 // table[k] = (k+1) * P in cached form
 FE_INLINE void build_cached_table(ge_cached tab[8], const ge_p3& P) {
-  ge_p3 acc = P, P2;
+  ge_p3 acc, P2;
   ge_p1p1 t;
   ge_p3_to_cached(tab[0], P);
   ge_p3_dbl_to_p3(P2, P);
@@ -63,102 +90,101 @@ FE_INLINE void select_niels(ge_niels& c, const ge_niels* __restrict__ tab, int d
   ge_niels_cneg(c, d < 0);
 }
 
-// 4 doublings: p2 -> p3
-FE_INLINE void dbl4(ge_p3& r, const ge_p2& p) {
-  ge_p1p1 t;
-  ge_p2 q = p;
-  ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t);
-  ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t);
-  ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t);
-  ge_p2_dbl(t, q); ge_p1p1_to_p3(r, t);
+// x (p1p1) <- 4 doublings of acc (p2); the last one is left unconverted
+FE_INLINE void dbl4_p1p1(ge_p1p1& x, const ge_p2& acc) {
+  ge_p2 q = acc;
+  ge_p2_dbl(x, q); ge_p1p1_to_p2(q, x);
+  ge_p2_dbl(x, q); ge_p1p1_to_p2(q, x);
+  ge_p2_dbl(x, q); ge_p1p1_to_p2(q, x);
+  ge_p2_dbl(x, q);
 }
 
-// R = [s]B + [a]P   (digit planes: plane_a for a, plane_s for s)
-// nwin_a: windows (from 0) in which a may have non-zero digits (<= 64).
-FE_INLINE void ge_double_scalarmult_base(ge_p2& R, const DigitPlanes& dp, int plane_a, int plane_s, int t,
-                                         const ge_p3& P, int nwin_a, const ge_niels* __restrict__ btab) {
+FE_INLINE void ge_p1p1_identity(ge_p1p1& x) { fe_set(x.X, 0); fe_set(x.Y, 1); fe_set(x.Z, 1); fe_set(x.T, 1); }
+
+// out = sum over terms, as p1p1 (caller converts to p2 or p3):
+//   [p] P  with p's radix-16 recoding pw, digits j < NP      (tp: table of P)
+//   [q] Q  with q's radix-16 recoding qw, digits j < NQ      (tq: table of Q)
+//   [b] B  with b's radix-256 recoding fw:
+//          NB = 32:             all 32 bytes on B            (btab[0..128))
+//          NB = 16 and TWO_B:   bytes 0..15 on B, bytes 16..31 on B' = 2^128 B
+//                               (btab[128..256)), i.e. a 128-window-bit chain
+// over nibble windows j = NWIN-1 .. 0 (fixed-base bytes k at windows 2k).
+template <int NWIN, int NP, int NQ, int NB, bool TWO_B>
+FE_INLINE void straus(ge_p1p1& out, const ge_cached* tp, uint32_t pw[8], const ge_cached* tq, uint32_t qw[8],
+                      const ge_niels* __restrict__ btab, uint32_t fw[8]) {
+  static_assert(NWIN >= 1 && NWIN <= 64 && NP <= NWIN && NQ <= NWIN, "window counts");
+  static_assert(NB == 0 || (NB == 32 && !TWO_B) || (NB == 16 && TWO_B), "fixed-base layout");
+  static_assert(NB == 0 || 2 * (NB - 1) <= NWIN - 1, "fixed-base bytes beyond the chain");
+  static_assert(NB == 0 || NWIN - 1 <= 2 * NB, "chain starts above the top fixed-base byte");
+  // align nibble NWIN-1 to the top of pw / qw
+  if constexpr (NP > 0) shl_const<8, 4 * (64 - NWIN)>(pw);
+  if constexpr (NQ > 0) shl_const<8, 4 * (64 - NWIN)>(qw);
+  ge_p2 acc;
+  ge_p1p1 x;
+  ge_p3 a3;
+#pragma clang loop unroll(disable)
+  for (int j = NWIN - 1; j >= 0; j--) {
+    if (j == NWIN - 1) ge_p1p1_identity(x);
+    else dbl4_p1p1(x, acc);
+    if constexpr (NP > 0) {
+      if (j < NP) {
+        ge_cached c;
+        select_cached(c, tp, (int)(pw[7] >> 28) - 8);
+        ge_p1p1_to_p3(a3, x);
+        ge_add(x, a3, c);
+      }
+      shl_small<8, 4>(pw);
+    }
+    if constexpr (NQ > 0) {
+      if (j < NQ) {
+        ge_cached c;
+        select_cached(c, tq, (int)(qw[7] >> 28) - 8);
+        ge_p1p1_to_p3(a3, x);
+        ge_add(x, a3, c);
+      }
+      shl_small<8, 4>(qw);
+    }
+    if constexpr (NB > 0) {
+      if ((j & 1) == 0 && (j >> 1) < NB) {
+        ge_niels nb;
+        if constexpr (TWO_B) {
+          select_niels(nb, btab, (int)(fw[3] >> 24) - 128);
+          ge_p1p1_to_p3(a3, x);
+          ge_madd(x, a3, nb);
+          select_niels(nb, btab + BTAB_N, (int)(fw[7] >> 24) - 128);
+          ge_p1p1_to_p3(a3, x);
+          ge_madd(x, a3, nb);
+          shl_small<4, 8>(fw);
+          shl_small<4, 8>(fw + 4);
+        } else {
+          select_niels(nb, btab, (int)(fw[7] >> 24) - 128);
+          ge_p1p1_to_p3(a3, x);
+          ge_madd(x, a3, nb);
+          shl_small<8, 8>(fw);
+        }
+      }
+    }
+    if (j > 0) ge_p1p1_to_p2(acc, x);
+  }
+  out = x;
+}
+
+// R = [s]B (fixed base only), s < 2^253 (reduce mod L first)
+FE_INLINE void ge_scalarmult_base(ge_p3& R, const uint32_t s[8], const ge_niels* __restrict__ btab) {
+  uint32_t fw[8];
+  sc_recode256(fw, s);
+  ge_p1p1 x;
+  straus<31, 0, 0, 16, true>(x, nullptr, nullptr, nullptr, nullptr, btab, fw);
+  ge_p1p1_to_p3(R, x);
+}
+
+// R = [s]P (single per-lane base), s < 2^253
+FE_INLINE void ge_scalarmult_var(ge_p3& R, const uint32_t s[8], const ge_p3& P) {
   ge_cached tab[8];
   build_cached_table(tab, P);
-  ge_p2 acc;
-  ge_p2_identity(acc);
+  uint32_t pw[8];
+  sc_recode16(pw, s);
   ge_p1p1 x;
-  ge_p3 a3;
-#pragma clang loop unroll(disable)
-  for (int j = 63; j >= 0; j--) {
-    dbl4(a3, acc);
-    if (j < nwin_a) {
-      ge_cached c;
-      select_cached(c, tab, dp.get(j, plane_a, t));
-      ge_add(x, a3, c);
-      ge_p1p1_to_p3(a3, x);
-    }
-    ge_niels nb;
-    select_niels(nb, btab, dp.get(j, plane_s, t));
-    ge_madd(x, a3, nb);
-    ge_p1p1_to_p2(acc, x);
-  }
-  R = acc;
-}
-
-// R = [a]P + [b]Q   (two per-lane bases; b may be short: nwin_b windows)
-FE_INLINE void ge_double_scalarmult_var(ge_p2& R, const DigitPlanes& dp, int plane_a, int plane_b, int t,
-                                        const ge_p3& P, const ge_p3& Q, int nwin_b) {
-  ge_cached tp[8], tq[8];
-  build_cached_table(tp, P);
-  build_cached_table(tq, Q);
-  ge_p2 acc;
-  ge_p2_identity(acc);
-  ge_p1p1 x;
-  ge_p3 a3;
-#pragma clang loop unroll(disable)
-  for (int j = 63; j >= 0; j--) {
-    dbl4(a3, acc);
-    ge_cached c;
-    if (j < nwin_b) {
-      select_cached(c, tq, dp.get(j, plane_b, t));
-      ge_add(x, a3, c);
-      ge_p1p1_to_p3(a3, x);
-    }
-    select_cached(c, tp, dp.get(j, plane_a, t));
-    ge_add(x, a3, c);
-    ge_p1p1_to_p2(acc, x);
-  }
-  R = acc;
-}
-
-// R = [s]B (fixed base only), s < 2^255
-FE_INLINE void ge_scalarmult_base(ge_p3& R, const DigitPlanes& dp, int plane_s, int t,
-                                  const ge_niels* __restrict__ btab) {
-  ge_p2 acc;
-  ge_p2_identity(acc);
-  ge_p1p1 x;
-  ge_p3 a3;
-#pragma clang loop unroll(disable)
-  for (int j = 63; j >= 0; j--) {
-    dbl4(a3, acc);
-    ge_niels nb;
-    select_niels(nb, btab, dp.get(j, plane_s, t));
-    ge_madd(x, a3, nb);
-    if (j == 0) ge_p1p1_to_p3(R, x);
-    else ge_p1p1_to_p2(acc, x);
-  }
-}
-
-// R = [s]P (single per-lane base)
-FE_INLINE void ge_scalarmult_var(ge_p3& R, const DigitPlanes& dp, int plane_s, int t, const ge_p3& P) {
-  ge_cached tab[8];
-  build_cached_table(tab, P);
-  ge_p2 acc;
-  ge_p2_identity(acc);
-  ge_p1p1 x;
-  ge_p3 a3;
-#pragma clang loop unroll(disable)
-  for (int j = 63; j >= 0; j--) {
-    dbl4(a3, acc);
-    ge_cached c;
-    select_cached(c, tab, dp.get(j, plane_s, t));
-    ge_add(x, a3, c);
-    if (j == 0) ge_p1p1_to_p3(R, x);
-    else ge_p1p1_to_p2(acc, x);
-  }
+  straus<64, 64, 0, 0, false>(x, tab, pw, nullptr, nullptr, nullptr, nullptr);
+  ge_p1p1_to_p3(R, x);
 }

@@ -1,0 +1,74 @@
+"""Algorithmic work model of the HIP kernels (int32 VALU lane-ops per item).
+
+The roofline in bench.py prices each kernel by the field operations its
+schedule performs (counted here by construction, mirroring the code in
+ouroboros-consensus_amd/csrc/*.hpp) times the int32 instruction count of
+each operation in the radix-2^32 implementation (fe25519.hpp):
+
+    M   field multiply   64 v_mad_u64_u32 + 64 carry adds + 26 reduction  = 154
+    S   field square     28 cross MACs x 2 + doubling + 8 diagonals + red. = 130
+    A   add / sub / neg  8 + 8 carry-propagating adds + fold                =  17
+    SHA-512 compression  80 rounds on 64-bit words in VGPR pairs            = 5000
+    BLAKE2b compression  12 rounds                                          = 2700
+    X   exponentiation   (p-2, (p-5)/8, (p-1)/2): 254 S + 11 M (+ canon)
+
+Everything else (digit extraction, table selection, sign handling, loads,
+loop control) is overhead and not counted: `frac` therefore reports how much
+of the integer-VALU issue rate goes into the counted arithmetic.
+
+Run `python tools/workmodel.py` to print the per-item figures.
+"""
+M, S, A = 154, 130, 17
+SHA, B2B = 5000, 2700
+CANON = 30
+X = 254 * S + 11 * M + CANON            # one exponentiation chain
+
+# group operations (ge25519.hpp)
+DBL = 4 * S + 6 * A                     # ge_p2_dbl -> p1p1
+ADD = 4 * M + 6 * A + 2 * A             # ge_add (incl. Y+X, Y-X of p)
+MADD = 3 * M + 6 * A + 2 * A            # ge_madd
+TO_P2, TO_P3 = 3 * M, 4 * M
+CNEG = A                                # negation of the selected entry
+TABLE8 = 8 * (M + 2 * A) + (DBL + TO_P3) + 6 * (ADD + TO_P3)   # {1..8}P cached
+DECODE = X + 2 * S + 10 * M + 3 * A + 3 * CANON                # ge_frombytes (sqrt ratio)
+ENCODE = X + 2 * M + CANON                                     # ge_tobytes (one inversion)
+SC_REDUCE = 600
+
+
+def straus(nwin, np_, nq, nfixed_adds):
+    """Horner chain: (nwin-1) x 4 doublings, per-lane adds, fixed-base madds."""
+    w = (nwin - 1) * (4 * DBL + 3 * TO_P2)          # dbl4 (last one left as p1p1)
+    w += (np_ + nq) * (TO_P3 + ADD + CNEG)
+    w += nfixed_adds * (TO_P3 + MADD + CNEG)
+    w += (nwin - 1) * TO_P2
+    return w
+
+
+def ed25519_verify(sha_blocks):
+    return (sha_blocks * SHA + SC_REDUCE + DECODE + TABLE8 + straus(64, 64, 0, 32)
+            + TO_P2 + ENCODE + 200)
+
+
+def vrf_verify():
+    w = 2 * DECODE                                   # Y, Gamma
+    w += SHA                                         # hash_to_curve digest
+    w += X + 10 * M + 6 * S + 12 * A + CANON         # Elligator2 chi + numerators
+    w += DECODE - X + X                              # sqrt ratio of the point on N/D
+    w += 3 * (DBL + TO_P3)                           # cofactor 8
+    w += TABLE8 + straus(33, 33, 0, 32) + TO_P2      # U = [s]B - [c]Y (B, 2^128 B)
+    w += 2 * TABLE8 + straus(64, 64, 33, 0) + TO_P2  # V = [s]H - [c]Gamma
+    w += 3 * (DBL + TO_P3)                           # 8 Gamma
+    w += X + 10 * M + 4 * (2 * M + CANON)            # batched inversion + 4 encodings
+    w += 3 * SHA + SC_REDUCE                         # c' (2 blocks), beta (1 block)
+    return w
+
+
+W_OCERT = ed25519_verify(2)
+W_KES = ed25519_verify(4) + 6 * B2B
+W_VRF = vrf_verify() + 6 * B2B + 1000                # mkInputVRF, issuer/key hashes, L/N, search
+W_LEADER = 3000
+
+if __name__ == "__main__":
+    for k, v in (("ocert", W_OCERT), ("kes", W_KES), ("vrf", W_VRF), ("leader", W_LEADER)):
+        print(f"W_{k:7s} {v:>10,d} int32 ops / item")
+    print(f"W_header  {W_OCERT + W_KES + W_VRF + W_LEADER:>10,d}")
