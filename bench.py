@@ -39,7 +39,8 @@ sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 # Algorithmic work per unit (int32 lane-ops), counted by construction from the
 # kernel schedules (tools/workmodel.py; DESIGN.md sec. 4 "Work model").
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-from workmodel import W_OCERT, W_KES, W_VRF, W_LEADER  # noqa: E402
+from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  # noqa: E402
+                       W_KEY_COLD, W_KEY_VRF)
 W_HEADER = W_OCERT + W_KES + W_VRF + W_LEADER
 PEAK_INT32 = 256 * 64 * 2.4e9      # VOP3 integer issue: 64 lane-ops/clk/CU (tools/microbench)
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
@@ -145,6 +146,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
+    ap.add_argument("--keycache", type=int, default=2,
+                    help="min uses of a public key for the per-batch key cache (0 = off)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -165,6 +168,7 @@ def main():
     ctx = praos_hip.Context(local)
     ctx.set_option(1, args.concurrent)
     ctx.set_option(2, cfg["kernels"])
+    ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
     n = args.headers or cfg["headers"]
     npools = args.pools or cfg["pools"] or n           # c2: one distinct cold key per item
     stride = 20                                        # one header per ~1/f slots
@@ -215,6 +219,7 @@ def main():
         kser += [ctx.kernel_ms(k) for k in range(5)]
     kser /= 3
     ctx.set_option(1, args.concurrent)
+    kst = ctx.batch_stats(b)
     out = ctx.download(b, n)
     ctx.free(b)
 
@@ -236,10 +241,17 @@ def main():
     kms /= steps
     per_kernel = {"ocert": kser[0], "kes": kser[1], "vrf": kser[2], "leader": kser[3]}
     ran = [k for k in ("ocert", "kes", "vrf") if cfg["kernels"] & MASK[k]]
+    # algorithmic work of one run (tools/workmodel.py): headers on cached keys
+    # run the short chains, plus the per-key precomputation
+    work = {"ocert": kst["cold_hits"] * W_OCERT_CK + kst["cold_misses"] * W_OCERT + kst["cold_keys"] * W_KEY_COLD,
+            "kes": n * W_KES,
+            "vrf": kst["vrf_hits"] * W_VRF_CK + kst["vrf_misses"] * W_VRF + kst["vrf_keys"] * W_KEY_VRF}
+    if args.keycache == 0:
+        work["ocert"], work["vrf"] = n * W_OCERT, n * W_VRF
     dominant = max(ran, key=lambda k: per_kernel[k])
-    wk = {"ocert": W_OCERT, "kes": W_KES, "vrf": W_VRF}[dominant]
-    dom_achieved = n * wk / (per_kernel[dominant] * 1e-3)
-    w_pipe = sum({"ocert": W_OCERT, "kes": W_KES, "vrf": W_VRF + W_LEADER}[k] for k in ran)
+    wk = work[dominant] / n
+    dom_achieved = work[dominant] / (per_kernel[dominant] * 1e-3)
+    w_pipe = (sum(work[k] for k in ran) + (n * W_LEADER if "vrf" in ran else 0)) / n
     pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
     line = {
         "metric": cfg["metric"],
@@ -252,10 +264,11 @@ def main():
         "roofline": {"bound": "valu-int32", "kernel": f"k_{dominant}",
                      "achieved": round(dom_achieved / 1e12, 3), "peak": round(PEAK_INT32 / 1e12, 2),
                      "unit": "T int32-ops/s", "frac": round(dom_achieved / PEAK_INT32, 4), "traffic": None,
-                     "work_per_unit": wk, "pipeline_achieved": round(pipe_achieved / 1e12, 3),
-                     "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": w_pipe,
+                     "work_per_unit": round(wk), "pipeline_achieved": round(pipe_achieved / 1e12, 3),
+                     "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": round(w_pipe),
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},
                      "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent)},
+        "keycache": dict(kst, min_uses=args.keycache),
         "self_check": {"clean": int(clean.sum()), "clean_ok": clean_ok, "corrupted": int((~clean).sum()),
                        "corrupted_rejected": corrupt_caught, "corrupted_in_checked_fields": int(rel.sum()),
                        "corrupted_in_checked_fields_rejected": corrupt_caught_rel,

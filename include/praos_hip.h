@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 1
+#define PRAOS_ABI_VERSION 2
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -162,7 +162,17 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * (1 = OCert + KES-period checks, 2 = Sum6KES, 4 = VRF + leader; default 7).
  * Used by the single-primitive benchmark configs; skipped checks report 0 bits. */
 #define PRAOS_OPT_KERNELS 2
+/* PRAOS_OPT_KEYCACHE (default 2): a public key (cold key, VRF key) used by at
+ * least this many headers of a batch is decoded once per run and expanded into
+ * multi-power tables, so those headers' OCert / VRF-U scalar chains are 16
+ * windows long instead of 64 (k_keys.hip).  0 disables the cache.  Verdicts
+ * are identical either way (keys are matched byte for byte). */
+#define PRAOS_OPT_KEYCACHE 3
 int praos_set_option(praos_ctx* ctx, int opt, int value);
+/* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
+ * out[0..2] = cold keys cached, OCert items on cached keys, OCert items
+ * uncached; out[3..5] = the same for VRF keys.  Returns 0. */
+int praos_batch_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[6]);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
  * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run.  With concurrent
  * streams, 0-2 are measured from the common start to each kernel's end. */

@@ -4,33 +4,74 @@
 // ------------------------------------------------------------------ OCert + KES period checks
 // bits |= KES_BEFORE_START / KES_AFTER_END / OCERT_SIG.  If ok_out != null the
 // kernel is the plain praos_verify_ocert batch (ok_out[i] = 1 when valid).
-__global__ void __launch_bounds__(NT, LB_ED) k_ocert(size_t n, const ge_niels* __restrict__ gbtab,
-                                              const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ hot_vk,
-                                              const uint64_t* __restrict__ ocert_n, const uint64_t* __restrict__ ocert_c0,
-                                              const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot,
-                                              uint64_t slots_per_kes_period, uint64_t max_kes_evo,
-                                              uint16_t* __restrict__ bits, uint8_t* __restrict__ ok_out) {
-  __shared__ ge_niels sbtab[BTAB_N];
-  const ge_niels* btab = stage_btab<1>(gbtab, sbtab);
-  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= n) return;
-  uint32_t pk[8], hot[8], sg[16];
-  load_words(pk, cold_vk + 32 * i, 8);
-  load_words(hot, hot_vk + 32 * i, 8);
-  load_words(sg, sig + 64 * i, 16);
-  const uint64_t nn = ocert_n[i], c0 = ocert_c0[i];
-  uint32_t hram[16];
-  ocert_hram(hram, sg, pk, hot, nn, c0);
-  const bool ok = ed25519_verify_core(pk, sg, sg + 8, hram, btab);
-  if (ok_out) {
-    ok_out[i] = ok ? 1 : 0;
+// Items: i in [0, n), or list[0 .. *count) when list != null (key-cache
+// partition, k_keys.hip): k_ocert takes the misses, k_ocert_ck the hits.
+struct OcertIn {
+  const uint8_t* __restrict__ cold_vk;
+  const uint8_t* __restrict__ hot_vk;
+  const uint64_t* __restrict__ ocert_n;
+  const uint64_t* __restrict__ ocert_c0;
+  const uint8_t* __restrict__ sig;
+  const uint64_t* __restrict__ slot;
+  uint64_t slots_per_kes_period, max_kes_evo;
+  uint16_t* __restrict__ bits;
+  uint8_t* __restrict__ ok_out;
+};
+
+__device__ __forceinline__ void ocert_store(const OcertIn& a, size_t i, bool ok) {
+  if (a.ok_out) {
+    a.ok_out[i] = ok ? 1 : 0;
     return;
   }
   uint16_t b = ok ? 0 : PRAOS_BIT_OCERT_SIG;
-  const uint64_t kp = slot[i] / slots_per_kes_period;        // Praos.hs:596-599
-  if (!(c0 <= kp)) b |= PRAOS_BIT_KES_BEFORE_START;          // Praos.hs:567
-  if (!(kp < c0 + max_kes_evo)) b |= PRAOS_BIT_KES_AFTER_END; // Praos.hs:568
-  bits[i] = b;
+  const uint64_t c0 = a.ocert_c0[i];
+  const uint64_t kp = a.slot[i] / a.slots_per_kes_period;     // Praos.hs:596-599
+  if (!(c0 <= kp)) b |= PRAOS_BIT_KES_BEFORE_START;            // Praos.hs:567
+  if (!(kp < c0 + a.max_kes_evo)) b |= PRAOS_BIT_KES_AFTER_END; // Praos.hs:568
+  a.bits[i] = b;
+}
+
+__device__ __forceinline__ void ocert_load(const OcertIn& a, size_t i, uint32_t sg[16], uint32_t hram[16],
+                                           uint32_t pk[8]) {
+  uint32_t hot[8];
+  load_words(pk, a.cold_vk + 32 * i, 8);
+  load_words(hot, a.hot_vk + 32 * i, 8);
+  load_words(sg, a.sig + 64 * i, 16);
+  ocert_hram(hram, sg, pk, hot, a.ocert_n[i], a.ocert_c0[i]);
+}
+
+__global__ void __launch_bounds__(NT, LB_ED) k_ocert(size_t n, const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ count,
+                                                     const ge_niels* __restrict__ gbtab, OcertIn a) {
+  const size_t items = list ? (size_t)*count : n;
+  if ((size_t)blockIdx.x * NT >= items) return;                // whole block idle
+  __shared__ ge_niels sbtab[BTAB_N];
+  const ge_niels* btab = stage_btab<1>(gbtab, sbtab);
+  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (t >= items) return;
+  const size_t i = list ? list[t] : t;
+  uint32_t pk[8], sg[16], hram[16];
+  ocert_load(a, i, sg, hram, pk);
+  ocert_store(a, i, ed25519_verify_core(pk, sg, sg + 8, hram, btab));
+}
+
+__global__ void __launch_bounds__(NT, LB_ED) k_ocert_ck(const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ count,
+                                                        const int32_t* __restrict__ item_entry,
+                                                        const ge_cached* __restrict__ ktab,
+                                                        const uint32_t* __restrict__ kinfo,
+                                                        const ge_niels* __restrict__ gbtab, OcertIn a) {
+  const size_t items = *count;
+  if ((size_t)blockIdx.x * NT >= items) return;
+  __shared__ ge_niels sbtab[4 * BTAB_N];
+  const ge_niels* btab = stage_btab<15>(gbtab, sbtab);
+  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (t >= items) return;
+  const size_t i = list[t];
+  const size_t e = (size_t)item_entry[i];
+  uint32_t pk[8], sg[16], hram[16];
+  ocert_load(a, i, sg, hram, pk);
+  ocert_store(a, i, ed25519_verify_cached(sg, sg + 8, hram, kinfo[9 * e], ktab + e * KT_STRIDE, btab));
 }
 
 // ------------------------------------------------------------------ KES
@@ -43,6 +84,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
                                             const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0,
                                             uint64_t slots_per_kes_period, const uint32_t* __restrict__ period,
                                             uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {
+  if ((size_t)blockIdx.x * NT >= n) return;
   __shared__ ge_niels sbtab[BTAB_N];
   const ge_niels* btab = stage_btab<1>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
@@ -81,8 +123,20 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
 
 
 // ---- host launchers (kernels are only launchable from their own module)
-void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ hot_vk, const uint64_t* __restrict__ ocert_n, const uint64_t* __restrict__ ocert_c0, const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo, uint16_t* __restrict__ bits, uint8_t* __restrict__ ok_out) {
-  hipLaunchKernelGGL(k_ocert, grid, block, 0, stream, n, gbtab, cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out);
+void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                  const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
+                  const uint64_t* ocert_c0, const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period,
+                  uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out) {
+  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out};
+  hipLaunchKernelGGL(k_ocert, grid, block, 0, stream, n, list, count, gbtab, a);
+}
+void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                     const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
+                     const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo,
+                     uint16_t* bits, uint8_t* ok_out) {
+  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out};
+  hipLaunchKernelGGL(k_ocert_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }
 
 void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {

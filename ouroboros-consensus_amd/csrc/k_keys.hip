@@ -1,0 +1,147 @@
+// k_keys.hip -- per-batch public-key cache (cold keys, VRF keys).
+//
+// A Praos batch repeats the same public keys many times (each pool signs its
+// OCerts with one cold key and proves leadership with one VRF key: a 432k-
+// header epoch of 3000 pools has ~144 headers per key).  The cache decodes
+// each recurring key once and expands it into the multi-power tables of
+// scalarmult.hpp (KT_CHUNKS x {1..8} 2^(64k) (-P)), so the per-header chains
+// of those headers are 16 windows long instead of 64.  Keys are compared
+// byte for byte (open addressing on the 32 key bytes), so a cached header
+// sees exactly the point, validity flags and encoding its own bytes give.
+//
+//   k_key_insert     per item: insert key into the hash set, count uses
+//   k_key_assign     per slot: keys used >= min_count get a cache entry
+//   k_key_partition  per item: entry id, hit list / miss list (wave-aggregated)
+//   k_key_precompute per entry: checks, decode, tables (and Y's encoding)
+#include "kcommon.hpp"
+
+__device__ __forceinline__ uint32_t key_hash(const uint32_t k[8]) {
+  uint32_t h = k[0] * 0x9E3779B1u;
+  h ^= k[1] + 0x7F4A7C15u + (h << 6) + (h >> 2);
+  h ^= k[5] + (h << 6) + (h >> 2);
+  return h;
+}
+
+__global__ void k_key_insert(size_t n, const uint8_t* __restrict__ keys, uint32_t mask, uint32_t* slot_rep,
+                             uint32_t* slot_cnt, int32_t* __restrict__ item_slot) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  load_words(k, keys + 32 * i, 8);
+  uint32_t h = key_hash(k) & mask;
+  for (uint32_t probe = 0; probe <= mask; probe++) {
+    const uint32_t cur = atomicCAS(&slot_rep[h], 0u, (uint32_t)i + 1u);
+    if (cur == 0u) break;                              // new key, this item represents it
+    uint32_t o[8];
+    load_words(o, keys + 32 * (size_t)(cur - 1u), 8);
+    bool same = true;
+#pragma unroll
+    for (int q = 0; q < 8; q++) same &= o[q] == k[q];
+    if (same) break;
+    h = (h + 1u) & mask;
+  }
+  atomicAdd(&slot_cnt[h], 1u);
+  item_slot[i] = (int32_t)h;
+}
+
+// counters: [0] entries, [1] hits, [2] misses
+__global__ void k_key_assign(uint32_t cap, const uint32_t* __restrict__ slot_rep, const uint32_t* __restrict__ slot_cnt,
+                             uint32_t min_count, uint32_t max_entries, int32_t* __restrict__ slot_entry,
+                             uint32_t* __restrict__ entry_rep, uint32_t* counters) {
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= cap) return;
+  int32_t e = -1;
+  if (slot_rep[h] != 0u && slot_cnt[h] >= min_count) {
+    const uint32_t k = atomicAdd(&counters[0], 1u);
+    if (k < max_entries) {
+      e = (int32_t)k;
+      entry_rep[k] = slot_rep[h] - 1u;
+    }
+  }
+  slot_entry[h] = e;
+}
+
+// appends i to list (wave-aggregated atomic: one atomic per wave and list)
+__device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t* counter, uint32_t* list) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  const uint32_t lane = __lane_id();
+  uint32_t base = 0;
+  if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  if (pred) {
+    const uint32_t below = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    list[base + below] = value;
+  }
+}
+
+__global__ void k_key_partition(size_t n, const int32_t* __restrict__ item_slot, const int32_t* __restrict__ slot_entry,
+                                int32_t* __restrict__ item_entry, uint32_t* __restrict__ hit_list,
+                                uint32_t* __restrict__ miss_list, uint32_t* counters) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n;
+  const int32_t e = in ? slot_entry[item_slot[i]] : -1;
+  if (in) item_entry[i] = e;
+  wave_append(in && e >= 0, (uint32_t)i, &counters[1], hit_list);
+  wave_append(in && e < 0, (uint32_t)i, &counters[2], miss_list);
+}
+
+// kind 0 (cold key, Ed25519): flag = ge_is_canonical && !ge_has_small_order &&
+//        decodes; tables of -A (ge25519_frombytes_negate_vartime), 4 chunks.
+// kind 1 (VRF key): flag = !ge_has_small_order && decodes (vrf_validate_key);
+//        kinfo[1..8] = canonical encoding of Y; tables of -Y, 3 chunks.
+__global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t* __restrict__ counters,
+                                                        uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
+                                                        const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
+                                                        uint32_t* __restrict__ kinfo) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ne = min(counters[0], max_entries);
+  if (e >= ne) return;
+  uint32_t pk[8];
+  load_words(pk, keys + 32 * (size_t)entry_rep[e], 8);
+  ge_p3 P;
+  bool ok;
+  uint32_t* info = kinfo + 9 * (size_t)e;
+  if (kind == 0) {
+    ok = ge_is_canonical(pk) && !ge_has_small_order(pk);
+    ok = ge_frombytes(P, pk, /*negate=*/true) && ok;
+  } else {
+    ok = !ge_has_small_order(pk);
+    ge_p3 Y;
+    ok = ge_frombytes(Y, pk, false) && ok;
+    uint32_t ys[8];
+    ge_enc_affine(ys, Y);
+#pragma unroll
+    for (int q = 0; q < 8; q++) info[1 + q] = ys[q];
+    P = Y;
+    fe_neg(P.X, Y.X);
+    fe_neg(P.T, Y.T);
+  }
+  info[0] = ok ? 1u : 0u;
+  build_key_tables(ktab + (size_t)e * KT_STRIDE, P, kind == 0 ? 4 : 3);
+}
+
+// ---- host launchers
+void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* keys, uint32_t mask,
+                       uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot) {
+  hipLaunchKernelGGL(k_key_insert, grid, block, 0, stream, n, keys, mask, slot_rep, slot_cnt, item_slot);
+}
+void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
+                       const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
+                       uint32_t* entry_rep, uint32_t* counters) {
+  hipLaunchKernelGGL(k_key_assign, grid, block, 0, stream, cap, slot_rep, slot_cnt, min_count, max_entries, slot_entry,
+                     entry_rep, counters);
+}
+void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const int32_t* item_slot,
+                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* hit_list, uint32_t* miss_list,
+                          uint32_t* counters) {
+  hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, item_slot, slot_entry, item_entry, hit_list,
+                     miss_list, counters);
+}
+void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
+                           uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
+                           uint32_t* kinfo) {
+  hipLaunchKernelGGL(k_key_precompute, grid, block, 0, stream, kind, counters, max_entries, entry_rep, keys, ktab,
+                     kinfo);
+}

@@ -2,18 +2,18 @@
 #include "kcommon.hpp"
 
 // ------------------------------------------------------------------ init
-// btab[k] = (k+1) B and btab[BTAB_N + k] = (k+1) 2^128 B (k < BTAB_N) as
-// affine niels (y+x, y-x, 2dxy); one lane per entry (runs once per context).
+// btab[BTAB_N t + k] = (k+1) 2^(64 t) B (t < 4, k < BTAB_N) as affine niels
+// (y+x, y-x, 2dxy); one lane per entry (runs once per context).
 __global__ void k_init_btab(ge_niels* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 2 * BTAB_N) return;
-  const int k = e % BTAB_N;
+  if (e >= 4 * BTAB_N) return;
+  const int k = e % BTAB_N, tb = e / BTAB_N;
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   ge_p3 B, acc;
   ge_frombytes(B, benc, false);
-  if (e >= BTAB_N) {
-    for (int i = 0; i < 128; i++) {
+  if (tb > 0) {
+    for (int i = 0; i < 64 * tb; i++) {
       ge_p3_dbl_to_p3(acc, B);
       B = acc;
     }
@@ -151,7 +151,7 @@ __global__ void k_debug_decode(size_t n, const uint8_t* in, uint8_t* out, uint8_
 __global__ void __launch_bounds__(NT) k_debug_smul_base(size_t n, const ge_niels* gbtab, const uint8_t* s,
                                                         uint8_t* out) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8], r[8], e[8];

@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(NT) k_synth_pools(uint32_t npools, const ge_ni
                                                     uint32_t* vrf_pk, uint32_t* kes_seed, uint8_t* pool_hash28,
                                                     uint8_t* pool_vrf32) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const uint32_t p = blockIdx.x * NT + threadIdx.x;
   if (p >= npools) return;
   uint32_t ms[8], cs[8], vs[8], ks[8], az[16], cpk[8], vpk[8], h[8];
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(NT) k_synth_kes_leaves(uint32_t npools, const 
                                                          const uint32_t* kes_seed, uint32_t* leaf_seed,
                                                          uint32_t* tree) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const uint32_t g = blockIdx.x * NT + threadIdx.x;
   if (g >= npools * 64u) return;
   const uint32_t p = g / 64, j = g % 64;
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos,
     uint8_t* l_out, uint8_t* l_proof) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
   const uint32_t p = (uint32_t)(mix64(i ^ salt) % npools);

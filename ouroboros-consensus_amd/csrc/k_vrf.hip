@@ -5,49 +5,68 @@
 // Header mode: issuer hash -> pool (binary search), VRF key hash, alpha =
 // mkInputVRF(slot, eta0), proof verify, beta, output check, leader/nonce values.
 // Plain mode (ok_out != null): alpha given per item; ok_out, beta only.
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const ge_niels* __restrict__ gbtab,
-                                            const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ vrf_vk,
-                                            const uint8_t* __restrict__ vrf_out, const uint8_t* __restrict__ vrf_proof,
-                                            const uint64_t* __restrict__ slot, const uint32_t* __restrict__ eta0,
-                                            int eta0_neutral, const uint32_t* __restrict__ pool_hash,
-                                            const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map,
-                                            uint32_t npools, int check_output, const uint8_t* __restrict__ alpha_in,
-                                            uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx,
-                                            int32_t* __restrict__ pool_sorted_idx, uint8_t* __restrict__ beta_out,
-                                            uint8_t* __restrict__ leader_out, uint8_t* __restrict__ nonce_out,
-                                            uint8_t* __restrict__ ok_out) {
-  __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
-  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= n) return;
+// Items: i in [0, n) or list[0 .. *count) (key-cache partition, k_keys.hip):
+// k_vrf takes the misses, k_vrf_ck the hits (cached VRF key, short U chain).
+struct VrfIn {
+  const uint8_t* __restrict__ cold_vk;
+  const uint8_t* __restrict__ vrf_vk;
+  const uint8_t* __restrict__ vrf_out;
+  const uint8_t* __restrict__ vrf_proof;
+  const uint64_t* __restrict__ slot;
+  const uint32_t* __restrict__ eta0;
+  int eta0_neutral;
+  const uint32_t* __restrict__ pool_hash;
+  const uint32_t* __restrict__ pool_vrf;
+  const int32_t* __restrict__ pool_map;
+  uint32_t npools;
+  int check_output;
+  const uint8_t* __restrict__ alpha_in;
+  uint16_t* __restrict__ bits;
+  int32_t* __restrict__ pool_idx;
+  int32_t* __restrict__ pool_sorted_idx;
+  uint8_t* __restrict__ beta_out;
+  uint8_t* __restrict__ leader_out;
+  uint8_t* __restrict__ nonce_out;
+  uint8_t* __restrict__ ok_out;
+};
+
+// issuer pool: hashKey (Blake2b-224 of the cold vk, Praos.hs:552) -> sorted index or -1
+__device__ __forceinline__ int32_t pool_search(const uint32_t hk[8], const uint32_t* __restrict__ pool_hash,
+                                               uint32_t npools) {
+  int lo = 0, hi = (int)npools - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint32_t* ph = pool_hash + 7 * mid;
+    int c = 0;
+    for (int k = 0; k < 7 && c == 0; k++) {
+      const uint32_t x = __builtin_bswap32(ph[k]), q = __builtin_bswap32(hk[k]);   // byte order
+      c = x < q ? -1 : (x > q ? 1 : 0);
+    }
+    if (c == 0) return mid;
+    if (c < 0) lo = mid + 1; else hi = mid - 1;
+  }
+  return -1;
+}
+
+template <bool CACHED>
+__device__ __forceinline__ void vrf_item(const VrfIn& a, size_t i, const ge_niels* __restrict__ btab,
+                                         const ge_cached* __restrict__ ktab, const uint32_t* __restrict__ kinfo) {
   uint32_t pk[8], pr[20], alpha[8];
-  load_words(pk, vrf_vk + 32 * i, 8);
-  load_words(pr, vrf_proof + 80 * i, 20);
+  load_words(pk, a.vrf_vk + 32 * i, 8);
+  load_words(pr, a.vrf_proof + 80 * i, 20);
   uint16_t b = 0;
   int32_t sidx = -1;
-  if (alpha_in) {
-    load_words(alpha, alpha_in + 32 * i, 8);
+  if (a.alpha_in) {
+    load_words(alpha, a.alpha_in + 32 * i, 8);
   } else {
     uint32_t e0[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) e0[k] = eta0[k];
-    mk_input_vrf(alpha, slot[i], e0, eta0_neutral != 0);          // Praos/VRF.hs:55-69
-    // issuer pool: hashKey (Blake2b-224 of the cold vk), Praos.hs:552
+    for (int k = 0; k < 8; k++) e0[k] = a.eta0[k];
+    mk_input_vrf(alpha, a.slot[i], e0, a.eta0_neutral != 0);     // Praos/VRF.hs:55-69
     uint32_t cv[8], hk[8];
-    load_words(cv, cold_vk + 32 * i, 8);
+    load_words(cv, a.cold_vk + 32 * i, 8);
     blake2b_32(hk, cv, 28);
-    int lo = 0, hi = (int)npools - 1;
-    while (lo <= hi) {
-      const int mid = (lo + hi) >> 1;
-      const uint32_t* ph = pool_hash + 7 * mid;
-      int c = 0;
-      for (int k = 0; k < 7 && c == 0; k++) {
-        const uint32_t a = __builtin_bswap32(ph[k]), q = __builtin_bswap32(hk[k]);   // byte order
-        c = a < q ? -1 : (a > q ? 1 : 0);
-      }
-      if (c == 0) { sidx = mid; break; }
-      if (c < 0) lo = mid + 1; else hi = mid - 1;
-    }
+    sidx = pool_search(hk, a.pool_hash, a.npools);
     if (sidx < 0) {
       b |= PRAOS_BIT_VRF_KEY_UNKNOWN;                              // Praos.hs:537
     } else {
@@ -55,40 +74,70 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const ge_niels* __
       blake2b_32(vh, pk, 32);                                      // hashVerKeyVRF
       bool same = true;
 #pragma unroll
-      for (int k = 0; k < 8; k++) same &= vh[k] == pool_vrf[8 * sidx + k];
+      for (int k = 0; k < 8; k++) same &= vh[k] == a.pool_vrf[8 * sidx + k];
       if (!same) b |= PRAOS_BIT_VRF_KEY_WRONG;                     // Praos.hs:539-541
     }
   }
   uint32_t beta[16];
   bool gamma_ok;
-  const bool proof_ok = vrf_verify_core(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab);
+  const bool proof_ok =
+      vrf_verify_core<CACHED>(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab, ktab, kinfo);
   if (!gamma_ok) {
 #pragma unroll
     for (int k = 0; k < 16; k++) beta[k] = 0;
   }
-  if (ok_out) {
-    ok_out[i] = proof_ok ? 1 : 0;
-    if (beta_out) store_words(beta_out + 64 * i, beta, 16);
+  if (a.ok_out) {
+    a.ok_out[i] = proof_ok ? 1 : 0;
+    if (a.beta_out) store_words(a.beta_out + 64 * i, beta, 16);
     return;
   }
   uint32_t out[16];
-  load_words(out, vrf_out + 64 * i, 16);
+  load_words(out, a.vrf_out + 64 * i, 16);
   bool out_eq = true;
 #pragma unroll
   for (int k = 0; k < 16; k++) out_eq &= out[k] == beta[k];
   if (!proof_ok) b |= PRAOS_BIT_VRF_PROOF;                         // Praos.hs:543-547
-  if (!out_eq && check_output) b |= PRAOS_BIT_VRF_OUTPUT;
+  if (!out_eq && a.check_output) b |= PRAOS_BIT_VRF_OUTPUT;
   // range extension of the CERTIFIED output (Praos/VRF.hs:88-131)
   uint32_t lv[8], nv[8], nn[8];
   blake2b256_tag64(lv, 'L', out);
   blake2b256_tag64(nv, 'N', out);
   blake2b_32(nn, nv, 32);
-  if (leader_out) store_words(leader_out + 32 * i, lv, 8);
-  if (nonce_out) store_words(nonce_out + 32 * i, nn, 8);
-  if (beta_out) store_words(beta_out + 64 * i, beta, 16);
-  pool_idx[i] = sidx < 0 ? -1 : pool_map[sidx];
-  pool_sorted_idx[i] = sidx;
-  bits[i] = b;
+  if (a.leader_out) store_words(a.leader_out + 32 * i, lv, 8);
+  if (a.nonce_out) store_words(a.nonce_out + 32 * i, nn, 8);
+  if (a.beta_out) store_words(a.beta_out + 64 * i, beta, 16);
+  a.pool_idx[i] = sidx < 0 ? -1 : a.pool_map[sidx];
+  a.pool_sorted_idx[i] = sidx;
+  a.bits[i] = b;
+}
+
+__global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ count,
+                                                    const ge_niels* __restrict__ gbtab, VrfIn a) {
+  const size_t items = list ? (size_t)*count : n;
+  if ((size_t)blockIdx.x * NT >= items) return;
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
+  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (t >= items) return;
+  vrf_item<false>(a, list ? list[t] : t, btab, nullptr, nullptr);
+}
+
+__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_ck(const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ count,
+                                                       const int32_t* __restrict__ item_entry,
+                                                       const ge_cached* __restrict__ ktab,
+                                                       const uint32_t* __restrict__ kinfo,
+                                                       const ge_niels* __restrict__ gbtab, VrfIn a) {
+  const size_t items = *count;
+  if ((size_t)blockIdx.x * NT >= items) return;
+  __shared__ ge_niels sbtab[4 * BTAB_N];
+  const ge_niels* btab = stage_btab<15>(gbtab, sbtab);
+  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (t >= items) return;
+  const size_t i = list[t];
+  const size_t e = (size_t)item_entry[i];
+  vrf_item<true>(a, i, btab, ktab + e * KT_STRIDE, kinfo + 9 * e);
 }
 
 
@@ -105,8 +154,9 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map, uint32_t npools, int check_output,
     uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx, int32_t* __restrict__ pool_sorted_idx,
     uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_l, uint8_t* __restrict__ nonce_out) {
+  if ((size_t)blockIdx.x * NT >= n) return;
   __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<2>(gbtab, sbtab);
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
   uint32_t pk[8], e0[8];
@@ -117,19 +167,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
   uint32_t cv[8], hk[8];
   load_words(cv, cold_vk + 32 * i, 8);
   blake2b_32(hk, cv, 28);
-  int32_t sidx = -1;
-  int lo = 0, hi = (int)npools - 1;
-  while (lo <= hi) {
-    const int mid = (lo + hi) >> 1;
-    const uint32_t* ph = pool_hash + 7 * mid;
-    int c = 0;
-    for (int k = 0; k < 7 && c == 0; k++) {
-      const uint32_t a = __builtin_bswap32(ph[k]), q = __builtin_bswap32(hk[k]);
-      c = a < q ? -1 : (a > q ? 1 : 0);
-    }
-    if (c == 0) { sidx = mid; break; }
-    if (c < 0) lo = mid + 1; else hi = mid - 1;
-  }
+  const int32_t sidx = pool_search(hk, pool_hash, npools);
   if (sidx < 0) {
     b |= PRAOS_BIT_VRF_KEY_UNKNOWN;
   } else {
@@ -147,7 +185,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     load_words(out, (cert ? l_out : eta_out) + 64 * i, 16);
     tpraos_seed(alpha, s, e0, eta0_neutral != 0, (uint64_t)cert);
     bool gamma_ok;
-    const bool ok = vrf_verify_core(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab);
+    const bool ok = vrf_verify_core<false>(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab);
     if (!gamma_ok) {
 #pragma unroll
       for (int k = 0; k < 16; k++) beta[k] = 0;
@@ -170,8 +208,26 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
 }
 
 // ---- host launchers (kernels are only launchable from their own module)
-void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ vrf_vk, const uint8_t* __restrict__ vrf_out, const uint8_t* __restrict__ vrf_proof, const uint64_t* __restrict__ slot, const uint32_t* __restrict__ eta0, int eta0_neutral, const uint32_t* __restrict__ pool_hash, const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map, uint32_t npools, int check_output, const uint8_t* __restrict__ alpha_in, uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx, int32_t* __restrict__ pool_sorted_idx, uint8_t* __restrict__ beta_out, uint8_t* __restrict__ leader_out, uint8_t* __restrict__ nonce_out, uint8_t* __restrict__ ok_out) {
-  hipLaunchKernelGGL(k_vrf, grid, block, 0, stream, n, gbtab, cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools, check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out);
+void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
+                const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
+                const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
+                int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
+                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out) {
+  VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools,
+          check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out};
+  hipLaunchKernelGGL(k_vrf, grid, block, 0, stream, n, list, count, gbtab, a);
+}
+void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                   const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                   const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
+                   const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash,
+                   const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
+                   const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
+                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out) {
+  VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools,
+          check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out};
+  hipLaunchKernelGGL(k_vrf_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk,
                    const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out,

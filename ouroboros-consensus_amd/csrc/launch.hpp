@@ -5,9 +5,41 @@
 #include <cstddef>
 #include <cstdint>
 struct ge_niels;
-void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ hot_vk, const uint64_t* __restrict__ ocert_n, const uint64_t* __restrict__ ocert_c0, const uint8_t* __restrict__ sig, const uint64_t* __restrict__ slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo, uint16_t* __restrict__ bits, uint8_t* __restrict__ ok_out);
+struct ge_cached;
+void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                  const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
+                  const uint64_t* ocert_c0, const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period,
+                  uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out);
+void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                     const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
+                     const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo,
+                     uint16_t* bits, uint8_t* ok_out);
+void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
+                const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
+                const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
+                int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
+                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out);
+void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                   const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                   const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
+                   const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash,
+                   const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
+                   const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
+                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out);
+void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* keys, uint32_t mask,
+                       uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot);
+void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
+                       const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
+                       uint32_t* entry_rep, uint32_t* counters);
+void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const int32_t* item_slot,
+                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* hit_list, uint32_t* miss_list,
+                          uint32_t* counters);
+void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
+                           uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
+                           uint32_t* kinfo);
 void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result);
-void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ cold_vk, const uint8_t* __restrict__ vrf_vk, const uint8_t* __restrict__ vrf_out, const uint8_t* __restrict__ vrf_proof, const uint64_t* __restrict__ slot, const uint32_t* __restrict__ eta0, int eta0_neutral, const uint32_t* __restrict__ pool_hash, const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map, uint32_t npools, int check_output, const uint8_t* __restrict__ alpha_in, uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx, int32_t* __restrict__ pool_sorted_idx, uint8_t* __restrict__ beta_out, uint8_t* __restrict__ leader_out, uint8_t* __restrict__ nonce_out, uint8_t* __restrict__ ok_out);
 void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab);
 void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in, const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one, int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits, uint8_t* is_leader, int32_t* iters);
 void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);

@@ -22,6 +22,7 @@ struct praos_ctx {
   hipStream_t side[3] = {nullptr, nullptr, nullptr};   // concurrent crypto kernels
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
+  int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   float kernel_ms[5] = {0, 0, 0, 0, 0};
@@ -53,8 +54,20 @@ struct praos_batch {
   uint16_t* bits3 = nullptr;   // per-kernel bits: ocert | kes | vrf
   int32_t *pool_idx = nullptr, *pool_sorted = nullptr;
   uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
+  // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys
+  struct KeyCache {
+    uint32_t cap = 0, max_entries = 0;
+    uint32_t *slot_rep = nullptr, *slot_cnt = nullptr, *entry_rep = nullptr, *kinfo = nullptr;
+    int32_t *slot_entry = nullptr, *item_slot = nullptr, *item_entry = nullptr;
+    uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
+    ge_cached* ktab = nullptr;
+  } kc[2];
+  bool kc_used = false;
   std::vector<void*> owned;
 };
+
+static constexpr size_t KT_BYTES = 4 * 8 * 4 * 32;  // per cached key: 4 tables x 8 cached points
+static constexpr uint32_t KC_MAX_ENTRIES = 1u << 16;
 
 #define HIPCHK(ctx, x)                                                                    \
   do {                                                                                    \
@@ -105,8 +118,8 @@ praos_ctx* praos_open(int device) {
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
   for (auto& st : c->side) (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-  if (hipMalloc(&c->btab, 2 * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
-  launch_init_btab(dim3(1), dim3(2 * BTAB_N), c->stream, c->btab);
+  if (hipMalloc(&c->btab, 4 * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
+  launch_init_btab(dim3(2), dim3(2 * BTAB_N), c->stream, c->btab);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
     fprintf(stderr, "praos_open: init kernel failed\n");
     delete c;
@@ -238,6 +251,22 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   ok &= dalloc(b, &b->beta, 64 * n) == hipSuccess;
   ok &= dalloc(b, &b->leader, 32 * n) == hipSuccess;
   ok &= dalloc(b, &b->nonce, 32 * n) == hipSuccess;
+  for (auto& k : b->kc) {
+    k.cap = 256;
+    while (k.cap < 2 * n) k.cap <<= 1;
+    k.max_entries = (uint32_t)std::min<size_t>(n / 2 + 1, KC_MAX_ENTRIES);
+    ok &= dalloc(b, &k.slot_rep, 4 * (size_t)k.cap) == hipSuccess;
+    ok &= dalloc(b, &k.slot_cnt, 4 * (size_t)k.cap) == hipSuccess;
+    ok &= dalloc(b, &k.slot_entry, 4 * (size_t)k.cap) == hipSuccess;
+    ok &= dalloc(b, &k.item_slot, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.item_entry, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.hit, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.miss, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.counters, 16) == hipSuccess;
+    ok &= dalloc(b, &k.entry_rep, 4 * (size_t)k.max_entries) == hipSuccess;
+    ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
+    ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
+  }
   if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
   auto up = [&](void* d, const void* s, size_t bytes) {
     if (bytes) ok &= hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess;
@@ -280,11 +309,39 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[0], 0));
-  if (c->kernels & 1)
-    launch_ocert(g, blk, so, n, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
-                 P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
-  else
+  const bool kc = c->keycache > 0 && n >= 2;
+  b->kc_used = kc;
+  // key cache prepass on the kernel's own stream: hash set, entries, hit/miss lists, tables
+  auto keycache_prepass = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) -> int {
+    HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
+    HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
+    HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
+    launch_key_insert(g, blk, st, n, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
+    launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)c->keycache,
+                      k.max_entries, k.slot_entry, k.entry_rep, k.counters);
+    launch_key_partition(g, blk, st, n, k.item_slot, k.slot_entry, k.item_entry, k.hit, k.miss, k.counters);
+    launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries,
+                          k.entry_rep, keys, k.ktab, k.kinfo);
+    return PRAOS_OK;
+  };
+  if (c->kernels & 1) {
+    if (kc) {
+      praos_batch::KeyCache& k = b->kc[0];
+      int r = keycache_prepass(k, b->cold_vk, 0, so);
+      if (r != PRAOS_OK) return r;
+      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
+                      b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
+                      P.max_kes_evo, bo, (uint8_t*)nullptr);
+      launch_ocert(g, blk, so, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+    } else {
+      launch_ocert(g, blk, so, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk,
+                   b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo,
+                   bo, (uint8_t*)nullptr);
+    }
+  } else {
     HIPCHK(c, hipMemsetAsync(bo, 0, 2 * n, so));
+  }
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
   if (c->kernels & 2)
     launch_kes(g, blk, sk, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body, b->body_bytes_len,
@@ -293,11 +350,26 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
   const bool do_vrf = (c->kernels & 4) != 0;
-  if (do_vrf)
-    launch_vrf(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->slot, c->d_eta0,
-               c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output,
-               (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta, b->leader, b->nonce,
-               (uint8_t*)nullptr);
+  if (do_vrf) {
+    if (kc) {
+      praos_batch::KeyCache& k = b->kc[1];
+      int r = keycache_prepass(k, b->vrf_vk, 1, sv);
+      if (r != PRAOS_OK) return r;
+      launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk, b->vrf_vk,
+                    b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                    c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
+                    b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr);
+      launch_vrf(g, blk, sv, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
+                 b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
+                 (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
+                 b->leader, b->nonce, (uint8_t*)nullptr);
+    } else {
+      launch_vrf(g, blk, sv, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk, b->vrf_vk,
+                 b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                 c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
+                 b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr);
+    }
+  }
   else {
     HIPCHK(c, hipMemsetAsync(bv, 0, 2 * n, sv));
     HIPCHK(c, hipMemsetAsync(b->pool_sorted, 0xff, 4 * n, sv));   // no pool -> leader kernel skips
@@ -312,10 +384,27 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   return PRAOS_OK;
 }
 
+int praos_batch_stats(praos_ctx* c, praos_batch* b, uint32_t out[6]) {
+  if (!c || !b || !out) return PRAOS_E_ARG;
+  for (int k = 0; k < 6; k++) out[k] = 0;
+  if (!b->kc_used) return PRAOS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int t = 0; t < 2; t++) {
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    HIPCHK(c, hipMemcpy(cnt, b->kc[t].counters, 16, hipMemcpyDeviceToHost));
+    out[3 * t] = std::min(cnt[0], b->kc[t].max_entries);
+    out[3 * t + 1] = cnt[1];
+    out[3 * t + 2] = cnt[2];
+  }
+  return PRAOS_OK;
+}
+
 int praos_set_option(praos_ctx* c, int opt, int value) {
   if (!c) return PRAOS_E_ARG;
   if (opt == PRAOS_OPT_CONCURRENT) { c->concurrent = value != 0; return PRAOS_OK; }
   if (opt == PRAOS_OPT_KERNELS) { c->kernels = value & 7; return PRAOS_OK; }
+  if (opt == PRAOS_OPT_KEYCACHE) { c->keycache = value < 0 ? 0 : value; return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 
@@ -414,7 +503,7 @@ int praos_verify_ocert(praos_ctx* c, size_t n, const uint8_t* cold_vk, const uin
   auto dok = s.zeros<uint8_t>(n);
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  launch_ocert(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, dv, dh, dn, dc, ds,
+  launch_ocert(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, nullptr, nullptr, c->btab, dv, dh, dn, dc, ds,
                      (const uint64_t*)nullptr, (uint64_t)1, (uint64_t)0, (uint16_t*)nullptr, dok);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
@@ -474,7 +563,7 @@ int praos_verify_vrf(praos_ctx* c, size_t n, const uint8_t* vk, const uint8_t* p
   auto dbeta = s.zeros<uint8_t>(64 * n);
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, (const uint8_t*)nullptr, dvk,
+  launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, nullptr, nullptr, c->btab, (const uint8_t*)nullptr, dvk,
                      (const uint8_t*)nullptr, dpr, (const uint64_t*)nullptr, (const uint32_t*)nullptr, 1,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const int32_t*)nullptr, 0u, 0, dal,
                      (uint16_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, dbeta, (uint8_t*)nullptr,
@@ -800,7 +889,7 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
   auto body = [&]() -> int {
     HIPCHK(c, hipMemcpy(dlout, th->leader_out, 64 * n, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
-    launch_ocert(g, blk, c->stream, n, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
+    launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
                  P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
     launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
                b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk,

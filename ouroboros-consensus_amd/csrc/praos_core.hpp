@@ -109,6 +109,32 @@ FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], co
   return ok && eq;
 }
 
+// Same verification with the public key cached (k_keys.hip): kflag bit 0 =
+// ge_is_canonical(pk) && !ge_has_small_order(pk) && decode ok; ktab = tables of
+// -A at 2^0, 2^64, 2^128, 2^192; btab = the four fixed-base tables in LDS.
+FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], const uint32_t hram[16],
+                                     uint32_t kflag, const ge_cached* __restrict__ ktab,
+                                     const ge_niels* __restrict__ btab) {
+  bool ok = sc_is_canonical(S) && !ge_has_small_order(R) && (kflag & 1u) != 0;
+  uint32_t h[8], s[8];
+  sc_reduce512(h, hram);
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;
+  uint32_t hw[8], sw[8];
+  sc_recode16(hw, h);
+  sc_recode256(sw, s);
+  ge_p1p1 x;
+  straus_chunked<4, false>(x, ktab, hw, btab, sw);   // [s]B - [h]A, 16-window chain
+  ge_p2 Rp;
+  ge_p1p1_to_p2(Rp, x);
+  uint32_t enc[8];
+  ge_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
+  bool eq = true;
+#pragma unroll
+  for (int i = 0; i < 8; i++) eq &= enc[i] == R[i];
+  return ok && eq;
+}
+
 // OCert signable: hot_vk(32) || BE64(n) || BE64(c0)  -> SHA-512(R||A||M), 112 bytes
 FE_INLINE void ocert_hram(uint32_t out[16], const uint32_t R[8], const uint32_t A[8], const uint32_t hot[8],
                           uint64_t n, uint64_t c0) {
@@ -283,13 +309,27 @@ FE_INLINE void vrf_hash_points(uint32_t c[4], const uint32_t h[8], const uint32_
 //   U = [s]B - [c]Y  : 33-window chain, s split over B and B' = 2^128 B (radix 256)
 //   V = [s]H - [c]Gamma : 64-window chain, both bases per lane (radix 16)
 // One batched inversion encodes H, U, V and 8 Gamma.
+// CACHED: the VRF key comes from k_keys.hip (kinfo[0] bit 0 = key valid,
+// kinfo[1..8] = canonical encoding of Y, ktab = tables of -Y at 2^0, 2^64,
+// 2^128) and U runs on a 16-window chain over the four fixed-base tables.
+template <bool CACHED>
 FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t pk[8], const uint32_t gamma[8],
                                const uint32_t c4[4], const uint32_t s8[8], const uint32_t alpha[8],
-                               const ge_niels* __restrict__ btab) {
+                               const ge_niels* __restrict__ btab, const ge_cached* __restrict__ ktab = nullptr,
+                               const uint32_t* __restrict__ kinfo = nullptr) {
   // vrf_validate_key: small order -> reject; ge25519_frombytes must succeed
-  bool ok = !ge_has_small_order(pk);
+  bool ok;
   ge_p3 Y, G;
-  ok = ge_frombytes(Y, pk, false) && ok;
+  uint32_t ys[8];
+  if constexpr (CACHED) {
+    ok = (kinfo[0] & 1u) != 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) ys[i] = kinfo[1 + i];
+  } else {
+    ok = !ge_has_small_order(pk);
+    ok = ge_frombytes(Y, pk, false) && ok;
+    ge_enc_affine(ys, Y);
+  }
   gamma_ok = ge_frombytes(G, gamma, false);
   // s reduced mod L (sc25519_reduce of s || 0^32)
   uint32_t sx[16], s[8], c[8];
@@ -299,12 +339,17 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
 #pragma unroll
   for (int i = 0; i < 8; i++) c[i] = i < 4 ? c4[i] : 0u;
   // H = hash_to_curve(canonical Y, alpha)
-  uint32_t ys[8];
-  ge_enc_affine(ys, Y);
   ge_p3 H;
   vrf_hash_to_curve(H, ys, alpha);
   ge_p2 U, V;
-  {  // U = [s]B - [c]Y
+  if constexpr (CACHED) {  // U = [s]B - [c]Y, cached -Y
+    uint32_t cw[8], sw[8];
+    sc_recode16(cw, c);
+    sc_recode256(sw, s);
+    ge_p1p1 x;
+    straus_chunked<2, true>(x, ktab, cw, btab, sw);
+    ge_p1p1_to_p2(U, x);
+  } else {  // U = [s]B - [c]Y
     ge_p3 nY = Y;
     fe_neg(nY.X, Y.X);
     fe_neg(nY.T, Y.T);

@@ -188,3 +188,87 @@ FE_INLINE void ge_scalarmult_var(ge_p3& R, const uint32_t s[8], const ge_p3& P) 
   straus<64, 64, 0, 0, false>(x, tab, pw, nullptr, nullptr, nullptr, nullptr);
   ge_p1p1_to_p3(R, x);
 }
+
+// ---------------------------------------------------------------- cached keys
+// A public key that recurs in a batch (pool cold keys, VRF keys) is decoded
+// once and expanded into KT_CHUNKS tables {1..8} (2^(64k) P) in global memory
+// (k_keys.hip).  A scalar below 2^256 is then 4 chunks of 64 bits sharing one
+// 16-window (64-bit) chain instead of a 64-window one: 4x fewer doublings.
+// The fixed base uses the matching tables 2^(64k) B (radix 256) in LDS.
+#define KT_CHUNKS 4
+#define KT_STRIDE (KT_CHUNKS * 8)      // ge_cached entries per cached key
+
+template <int NW, int SH>
+FE_INLINE void shl64_chunks(uint32_t w[NW]) {      // each 64-bit chunk (w[2k], w[2k+1]) <<= SH
+#pragma unroll
+  for (int k = 0; k < NW / 2; k++) {
+    w[2 * k + 1] = __builtin_amdgcn_alignbit(w[2 * k + 1], w[2 * k], 32 - SH);
+    w[2 * k] <<= SH;
+  }
+}
+
+// out = [p] P + [b] B (as p1p1) with P cached (ktab: KT_CHUNKS tables of P):
+//   p: radix-16 recoding pw; chunks k < NPC use table k at nibble 16k + m;
+//      P_TOP: digit 32 (in {0, 1} for p < 2^128) comes from table NPC at m = 0;
+//   b: radix-256 recoding fw (b < 2^253); byte 8k + m/2 on btab + 128 k at even m.
+template <int NPC, bool P_TOP>
+FE_INLINE void straus_chunked(ge_p1p1& out, const ge_cached* __restrict__ ktab, uint32_t pw[8],
+                              const ge_niels* __restrict__ btab, uint32_t fw[8]) {
+  static_assert(NPC >= 1 && NPC + (P_TOP ? 1 : 0) <= KT_CHUNKS, "chunk count");
+  const int dtop = P_TOP ? (int)(pw[2 * NPC] & 15u) - 8 : 0;
+  ge_p2 acc;
+  ge_p1p1 x;
+  ge_p3 a3;
+#pragma clang loop unroll(disable)
+  for (int m = 15; m >= 0; m--) {
+    if (m == 15) ge_p1p1_identity(x);
+    else dbl4_p1p1(x, acc);
+#pragma unroll
+    for (int k = 0; k < NPC; k++) {
+      ge_cached c;
+      select_cached(c, ktab + 8 * k, (int)(pw[2 * k + 1] >> 28) - 8);
+      ge_p1p1_to_p3(a3, x);
+      ge_add(x, a3, c);
+    }
+    shl64_chunks<2 * NPC, 4>(pw);
+    if (P_TOP && m == 0) {
+      ge_cached c;
+      select_cached(c, ktab + 8 * NPC, dtop);
+      ge_p1p1_to_p3(a3, x);
+      ge_add(x, a3, c);
+    }
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        ge_niels nb;
+        select_niels(nb, btab + BTAB_N * k, (int)(fw[2 * k + 1] >> 24) - 128);
+        ge_p1p1_to_p3(a3, x);
+        ge_madd(x, a3, nb);
+      }
+      shl64_chunks<8, 8>(fw);
+    }
+    if (m > 0) ge_p1p1_to_p2(acc, x);
+  }
+  out = x;
+}
+
+// ktab[8k + j] = (j+1) 2^(64k) P for k < nchunks (global memory)
+FE_INLINE void build_key_tables(ge_cached* __restrict__ ktab, const ge_p3& P, int nchunks) {
+  ge_p3 Q = P;
+#pragma clang loop unroll(disable)
+  for (int k = 0; k < nchunks; k++) {
+    ge_cached tab[8];
+    build_cached_table(tab, Q);
+#pragma unroll
+    for (int j = 0; j < 8; j++) ktab[8 * k + j] = tab[j];
+    if (k + 1 < nchunks) {
+      ge_p2 q;
+      ge_p1p1 t;
+      ge_p3_to_p2(q, Q);
+#pragma clang loop unroll(disable)
+      for (int d = 0; d < 63; d++) { ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t); }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(Q, t);
+    }
+  }
+}

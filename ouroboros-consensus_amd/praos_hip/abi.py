@@ -118,6 +118,7 @@ SIGNATURES = {
     "praos_batch_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "praos_batch_kernel_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_int]),
     "praos_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "praos_batch_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u32p]),
     "praos_verify_ocert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u64p, u64p, u8p, u8p]),
     "praos_verify_kes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u32p, u8p, u64p, u32p, u8p,
                                         ctypes.c_size_t, u8p]),
@@ -172,6 +173,9 @@ def ptr(a, t=u8p):
         return None
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(t)
+
+
+OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE = 1, 2, 3     # praos_set_option (include/praos_hip.h)
 
 
 class PraosError(RuntimeError):
@@ -296,6 +300,13 @@ class Context:
 
     def set_option(self, opt, value):
         self.check(self.L.praos_set_option(self.h, opt, value))
+
+    def batch_stats(self, b):
+        """Key-cache statistics of the last run: dict of cold/vrf entries, hits, misses."""
+        out = np.zeros(6, np.uint32)
+        self.check(self.L.praos_batch_stats(self.h, b, ptr(out, u32p)))
+        return {"cold_keys": int(out[0]), "cold_hits": int(out[1]), "cold_misses": int(out[2]),
+                "vrf_keys": int(out[3]), "vrf_hits": int(out[4]), "vrf_misses": int(out[5])}
 
     def kernel_ms(self, which):
         return float(self.L.praos_batch_kernel_ms(self.h, which))

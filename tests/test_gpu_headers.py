@@ -62,6 +62,52 @@ def test_synth_chain_parity(ctx, oracle):
     assert any(corrupted) and any(int(o["bits"][i]) != 0 for i in range(len(ref)) if corrupted[i])
 
 
+def _run_batch(ctx, H, keycache):
+    from praos_hip import abi
+    ctx.set_option(abi.OPT_KEYCACHE, keycache)
+    try:
+        b = ctx.upload(H)
+        ctx.run(b)
+        ctx.sync()
+        st = ctx.batch_stats(b)
+        o = ctx.download(b, len(H["slot"]))
+        ctx.free(b)
+    finally:
+        ctx.set_option(abi.OPT_KEYCACHE, 2)
+    return o, st
+
+
+def test_keycache_equivalence(ctx, oracle):
+    """Per-batch key cache (k_keys.hip): cached and uncached chains give identical
+    outputs, including repeated invalid keys (small order, non-canonical, not on
+    the curve) that take the cached path with their validity flags."""
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 1500, 23, 1500, seed=b"\x33" * 32)
+    p_plus_2 = (2 ** 255 - 19 + 2).to_bytes(32, "little")            # non-canonical y
+    ident = (1).to_bytes(32, "little")                                 # small order (identity)
+    not_on_curve = None
+    for y in range(2, 200):                                            # first y with no x
+        if not oracle.decode_ok(y.to_bytes(32, "little")):
+            not_on_curve = y.to_bytes(32, "little")
+            break
+    assert not_on_curve is not None
+    for k, bad in enumerate((p_plus_2, ident, not_on_curve)):
+        for j in range(3):                                             # repeated: cached
+            H["cold_vk"][10 + 3 * k + j] = np.frombuffer(bad, np.uint8)
+            H["vrf_vk"][40 + 3 * k + j] = np.frombuffer(bad, np.uint8)
+    o1, st1 = _run_batch(ctx, H, 2)
+    o0, st0 = _run_batch(ctx, H, 0)
+    assert st1["cold_keys"] >= 23 and st1["cold_hits"] > 1300 and st1["vrf_hits"] > 1300
+    assert st0["cold_keys"] == 0 and st0["cold_hits"] == 0
+    assert st1["cold_hits"] + st1["cold_misses"] == len(H["slot"])
+    for key in ("bits", "beta", "leader", "nonce", "pool_idx"):
+        assert np.array_equal(o1[key], o0[key]), key
+    ref = _oracle_bits(oracle, H, pool_list, c_raw, eta0)
+    for i, r in enumerate(ref):
+        assert int(o1["bits"][i]) & BITS_FROM_ORACLE == r["bits"], (i, hex(o1["bits"][i]), hex(r["bits"]))
+        assert bytes(o1["beta"][i]) == r["beta"]
+    assert all(int(o1["bits"][10 + j]) & 0x0004 for j in range(9))    # OCert rejected for the bad cold keys
+
+
 def test_header_edge_inputs(ctx, oracle):
     """Unknown issuer, wrong VRF key, KES period out of range, neutral nonce."""
     H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 64, 5, 0, seed=b"\x07" * 32)

@@ -63,12 +63,31 @@ def vrf_verify():
     return w
 
 
+def straus_chunked(npc, p_top):
+    """16-window chain over cached multi-power key tables (scalarmult.hpp)."""
+    w = 15 * (4 * DBL + 3 * TO_P2) + 15 * TO_P2
+    w += (16 * npc + (1 if p_top else 0)) * (TO_P3 + ADD + CNEG)
+    w += 32 * (TO_P3 + MADD + CNEG)                  # 4 fixed-base tables at 8 even windows
+    return w
+
+
+def key_precompute(nchunks):
+    """k_key_precompute: decode, nchunks tables, 64 doublings between chunks."""
+    return DECODE + nchunks * TABLE8 + (nchunks - 1) * 64 * (DBL + TO_P2)
+
+
 W_OCERT = ed25519_verify(2)
 W_KES = ed25519_verify(4) + 6 * B2B
 W_VRF = vrf_verify() + 6 * B2B + 1000                # mkInputVRF, issuer/key hashes, L/N, search
 W_LEADER = 3000
+# key-cache path (k_keys.hip): per header on a cached key, and per cached key
+W_OCERT_CK = W_OCERT - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_chunked(4, False)
+W_VRF_CK = W_VRF - DECODE - TABLE8 - straus(33, 33, 0, 32) + straus_chunked(2, True)
+W_KEY_COLD = key_precompute(4)
+W_KEY_VRF = key_precompute(3) + CANON
 
 if __name__ == "__main__":
-    for k, v in (("ocert", W_OCERT), ("kes", W_KES), ("vrf", W_VRF), ("leader", W_LEADER)):
+    for k, v in (("ocert", W_OCERT), ("kes", W_KES), ("vrf", W_VRF), ("leader", W_LEADER),
+                 ("ocert_ck", W_OCERT_CK), ("vrf_ck", W_VRF_CK), ("key_cold", W_KEY_COLD), ("key_vrf", W_KEY_VRF)):
         print(f"W_{k:7s} {v:>10,d} int32 ops / item")
     print(f"W_header  {W_OCERT + W_KES + W_VRF + W_LEADER:>10,d}")
