@@ -18,6 +18,11 @@
  *                            (Praos.hs:543; PraosVRF -> crypto_vrf_ietfdraft03_verify)
  *   praos_check_leader    <- checkLeaderNatValue (vrfLeaderValue cert) sigma f
  *                            (Praos.hs:549)
+ *   praos_decode_headers  <- DecCBOR (Annotator (Header c)) + HeaderBody decoding, the
+ *                            signable re-serialisation and headerHash
+ *                            (Praos/Header.hs:90-94, :147-151, :187-231) over stored
+ *                            header bytes (ImmutableDB chunk + secondary index)
+ *   praos_verify_header_bytes <- decode + praos_verify_headers in one device pass
  *   praos_apply_batch     <- the first-error-wins order of updateChainDepState plus
  *                            the OCert counter rule (Praos.hs:584-606) and the
  *                            reupdateChainDepState counter/nonce update (Praos.hs:468-502)
@@ -36,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 2
+#define PRAOS_ABI_VERSION 3
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -174,9 +179,74 @@ int praos_set_option(praos_ctx* ctx, int opt, int value);
  * uncached; out[3..5] = the same for VRF keys.  Returns 0. */
 int praos_batch_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[6]);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
- * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run.  With concurrent
+ * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run, 5 = header
+ * decode (batches from praos_batch_upload_bytes; 0 otherwise).  With concurrent
  * streams, 0-2 are measured from the common start to each kernel's end. */
 float praos_batch_kernel_ms(praos_ctx* ctx, int which);
+
+/* ---- stored headers: decode on the GPU ----
+ * Input: a byte arena (e.g. an ImmutableDB chunk file as read) and per header
+ * the (offset, length) of its CBOR item -- blockOffset + headerOffset and
+ * headerSize from the secondary index (ImmutableDB/Impl/Index/Secondary.hs:93-128).
+ * The header is HeaderRaw = [body, kesSig] (Praos/Header.hs:201-231) with the
+ * 10-field HeaderBody (:160-199).  The KES message is the canonical
+ * re-serialisation of the decoded body (`serialize' hb`, :90-94): equal to the
+ * stored slice when that is canonical, re-encoded on the GPU otherwise.
+ * header_hash = Blake2b-256 of the stored header bytes (headerHash, :147-151). */
+typedef struct {
+  size_t n;
+  const uint8_t* bytes;           /* arena */
+  size_t bytes_len;
+  const uint64_t* off;            /* n: header i = bytes[off[i], off[i] + len[i]) */
+  const uint32_t* len;            /* n */
+} praos_header_bytes;
+
+/* decode status (uint16 per header): the first failure, or 0 / NONCANONICAL */
+#define PRAOS_DEC_RANGE        0x01u /* slice outside the arena */
+#define PRAOS_DEC_SYNTAX       0x02u /* truncated / wrong major type / wrong array length */
+#define PRAOS_DEC_SIZE         0x04u /* fixed-size byte string of the wrong length */
+#define PRAOS_DEC_UNSUPPORTED  0x08u /* indefinite-length item or tag (never emitted by the reference) */
+#define PRAOS_DEC_TRAILING     0x10u /* bytes after the header item within len */
+#define PRAOS_DEC_NONCANONICAL 0x20u /* informational: stored body not canonical; signed bytes re-encoded */
+#define PRAOS_DEC_OVERFLOW     0x40u /* integer out of range (bodySize > Word32) */
+#define PRAOS_DEC_FAILED       0x5Fu /* mask of the failure bits */
+#define PRAOS_SIGNED_STRIDE    448   /* bytes per header in praos_decoded.signed_body */
+
+/* Decoded fields (caller buffers; every pointer may be NULL = not returned).
+ * A header that fails to decode has all fields zero and signed_len 0xffffffff. */
+typedef struct {
+  uint16_t* status;               /* n: PRAOS_DEC_* */
+  uint64_t* block_no;             /* hbBlockNo */
+  uint64_t* slot;                 /* hbSlotNo */
+  uint8_t* prev_hash;             /* n*32 hbPrev (zeros when GenesisHash) */
+  uint8_t* prev_is_genesis;       /* n */
+  uint8_t* cold_vk;               /* n*32 hbVk */
+  uint8_t* vrf_vk;                /* n*32 hbVrfVk */
+  uint8_t* vrf_out;               /* n*64 */
+  uint8_t* vrf_proof;             /* n*80 */
+  uint32_t* body_size;            /* hbBodySize */
+  uint8_t* body_hash;             /* n*32 hbBodyHash */
+  uint8_t* hot_vk;                /* n*32 ocertVkHot */
+  uint64_t* ocert_n;
+  uint64_t* ocert_c0;
+  uint8_t* ocert_sig;             /* n*64 */
+  uint64_t* prot_major;
+  uint64_t* prot_minor;
+  uint8_t* kes_sig;               /* n*448 */
+  uint32_t* signed_len;           /* n: length of the KES message */
+  uint8_t* signed_body;           /* n*PRAOS_SIGNED_STRIDE: the KES message (serialize' hb) */
+  uint8_t* header_hash;           /* n*32 */
+} praos_decoded;
+
+int praos_decode_headers(praos_ctx* ctx, const praos_header_bytes* in, praos_decoded* out);
+/* Decode + full header validation on the device.  bits gets PRAOS_BIT_INPUT for
+ * a header that does not decode; dec may be NULL. */
+int praos_verify_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, praos_out* out, praos_decoded* dec);
+/* Device-resident form: the batch keeps the arena; praos_batch_run decodes and
+ * then validates (bench / streaming replay).  praos_batch_download_decoded
+ * copies the decoded fields of the last run. */
+praos_batch* praos_batch_upload_bytes(praos_ctx* ctx, const praos_header_bytes* in);
+int praos_batch_download_decoded(praos_ctx* ctx, praos_batch* b, praos_decoded* dec);
 
 /* ---- TPraos (Shelley..Alonzo), the d = 0 path of cardano-protocol-tpraos ----
  * Replaces SL.updateChainDepState's crypto (TPraos.hs:378-387): OVERLAY
@@ -284,14 +354,17 @@ typedef struct {
   uint32_t npools;
   uint64_t first_slot;
   uint64_t slot_stride;           /* slot of header i = first_slot + i * slot_stride */
-  uint32_t body_len;              /* synthetic signed body length (CBOR-like bytes) */
+  uint32_t body_len;              /* > 0: pseudo-random signed bodies of this length;
+                                     0: the genuine canonical HeaderBody CBOR of each header
+                                     (Praos only; PRAOS_SIGNED_STRIDE bytes per header) */
   uint32_t corrupt_per_10000;     /* seeded corruptions (Corruption.hs model: +1 at a byte) */
   uint32_t nkes;                  /* distinct Sum6KES keys (0 = one per pool); header of pool p uses key p mod nkes */
   uint8_t seed[32];
 } praos_synth_params;
 
 /* Fills caller buffers (same layout as praos_headers; body_off/body_len/body_bytes
- * sized n, n, n*round_up(body_len, 8)+8).  Also returns the pool table
+ * sized n, n, n*stride+8 with stride = round_up(body_len, 8), or PRAOS_SIGNED_STRIDE
+ * when body_len = 0).  Also returns the pool table
  * (npools entries, sigma_fp left for the caller to set). */
 int praos_synthesize(praos_ctx* ctx, const praos_synth_params* sp, const praos_params* params,
                      const uint8_t eta0[32], praos_pool* pools_out, uint64_t* slot, uint8_t* cold_vk,

@@ -122,6 +122,23 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// byte writer of the canonical CBOR body (generator only)
+struct SynthWr {
+  uint8_t* o;
+  uint32_t n;
+};
+__device__ __forceinline__ void sw_byte(SynthWr& w, uint32_t b) { w.o[w.n++] = (uint8_t)b; }
+__device__ void sw_head(SynthWr& w, uint32_t mt, uint64_t v) {
+  if (v < 24) { sw_byte(w, (mt << 5) | (uint32_t)v); return; }
+  const int nb = v < 256 ? 1 : v < 65536 ? 2 : v < (1ull << 32) ? 4 : 8;
+  sw_byte(w, (mt << 5) | (nb == 1 ? 24u : nb == 2 ? 25u : nb == 4 ? 26u : 27u));
+  for (int k = nb - 1; k >= 0; k--) sw_byte(w, (uint32_t)(v >> (8 * k)));
+}
+__device__ void sw_bytes(SynthWr& w, const uint8_t* src, uint32_t n) {
+  sw_head(w, 2, n);
+  for (uint32_t k = 0; k < n; k++) sw_byte(w, src[k]);
+}
+
 // per header: body bytes, OCert signature, KES signature, VRF proof/output.
 __global__ void __launch_bounds__(NT) k_synth_headers(
     size_t n, const ge_niels* gbtab, uint32_t npools, uint32_t nkes, uint64_t first_slot, uint64_t slot_stride,
@@ -150,16 +167,6 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   store_words(hot_vk + 32 * i, hv, 8);
   store_words(cold_vk + 32 * i, cpk, 8);
   store_words(vrf_vk + 32 * i, vpk, 8);
-  // body: deterministic pseudo-random bytes (the signed HeaderBody stand-in)
-  const uint64_t boff = (uint64_t)i * (((uint64_t)blen + 7) & ~7ull);
-  body_off[i] = boff;
-  body_len[i] = blen;
-  uint64_t st = mix64(i * 0x9e3779b97f4a7c15ULL ^ salt ^ 0xb0d1);
-  for (uint32_t k = 0; k < blen; k += 8) {
-    st = mix64(st + k);
-    *(uint64_t*)(body_bytes + boff + k) = st;
-  }
-  for (uint32_t k = blen; k < ((blen + 7) & ~7u); k++) body_bytes[boff + k] = 0;
   // OCert signature over hot_vk || BE64(n) || BE64(c0)
   uint8_t* msg = msg_scratch + 48 * i;
   store_words(msg, hv, 8);
@@ -170,22 +177,6 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   ed25519_expand(az, seed);
   ed25519_sign_core(sig, az, cpk, msg, 48, btab);
   store_words(ocert_sig + 64 * i, sig, 16);
-  // KES: leaf t signs the body; path pairs from the tree (leaf level first)
-  const uint32_t leaf = (uint32_t)t;
-  uint32_t lpk[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)kk * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
-  ed25519_expand(az, seed);
-  ed25519_sign_core(sig, az, lpk, body_bytes + boff, blen, btab);
-  uint8_t* ks = kes_sig + 448 * i;
-  store_words(ks, sig, 16);
-  uint32_t node = 64 + leaf;
-  for (int d = 1; d <= 6; d++) {                // level d pair = children of the ancestor at height d
-    const uint32_t parent = node >> 1;
-    store_words(ks + 64 * d, T + (2 * parent) * 8, 8);
-    store_words(ks + 64 * d + 32, T + (2 * parent + 1) * 8, 8);
-    node = parent;
-  }
   // VRF proof(s): Praos alpha = mkInputVRF(slot, eta0); TPraos: the eta cert
   // with mkSeed seedEta and the leader cert with mkSeed seedL.  output = beta.
   uint32_t e0[8], alpha[8], proof[20];
@@ -207,15 +198,98 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     vrf_beta(beta, g8s);
     store_words((cert ? l_out : vrf_out) + 64 * i, beta, 16);
   }
+  // body: blen > 0: deterministic pseudo-random bytes (a signed-message stand-in);
+  // blen == 0: the genuine canonical HeaderBody CBOR (Praos/Header.hs:160-185) of
+  // this header, 448-byte stride, so the header bytes can be decoded and the KES
+  // message is exactly `serialize' hb`.
+  const uint64_t bstride = blen ? (((uint64_t)blen + 7) & ~7ull) : 448ull;
+  const uint64_t boff = (uint64_t)i * bstride;
+  uint32_t bl = blen;
+  uint64_t st = mix64(i * 0x9e3779b97f4a7c15ULL ^ salt ^ 0xb0d1);
+  if (blen) {
+    for (uint32_t k = 0; k < blen; k += 8) {
+      st = mix64(st + k);
+      *(uint64_t*)(body_bytes + boff + k) = st;
+    }
+    for (uint32_t k = blen; k < ((blen + 7) & ~7u); k++) body_bytes[boff + k] = 0;
+  } else {
+    SynthWr w{body_bytes + boff, 0};
+    sw_head(w, 4, 10);
+    sw_head(w, 0, first_slot / slot_stride + i);                // blockNo
+    sw_head(w, 0, s);                                           // slotNo
+    sw_head(w, 2, 32);                                          // prevHash (pseudo-random)
+    for (int k = 0; k < 4; k++) { st = mix64(st + k); for (int b = 0; b < 8; b++) sw_byte(w, (uint32_t)(st >> (8 * b))); }
+    sw_bytes(w, cold_vk + 32 * i, 32);
+    sw_bytes(w, vrf_vk + 32 * i, 32);
+    sw_head(w, 4, 2);
+    sw_bytes(w, vrf_out + 64 * i, 64);
+    sw_bytes(w, vrf_proof + 80 * i, 80);
+    st = mix64(st + 17);
+    sw_head(w, 0, st & 0xffffu);                                // bodySize
+    sw_head(w, 2, 32);                                          // bodyHash (pseudo-random)
+    for (int k = 0; k < 4; k++) { st = mix64(st + k); for (int b = 0; b < 8; b++) sw_byte(w, (uint32_t)(st >> (8 * b))); }
+    sw_head(w, 4, 4);
+    sw_bytes(w, hot_vk + 32 * i, 32);
+    sw_head(w, 0, nn);
+    sw_head(w, 0, c0);
+    sw_bytes(w, ocert_sig + 64 * i, 64);
+    sw_head(w, 4, 2);
+    sw_head(w, 0, 8);                                           // protocol version 8.0 (Babbage)
+    sw_head(w, 0, 0);
+    bl = w.n;
+    for (uint32_t k = bl; k < ((bl + 7) & ~7u); k++) body_bytes[boff + k] = 0;
+  }
+  body_off[i] = boff;
+  body_len[i] = bl;
+  // KES: leaf t signs the body; path pairs from the tree (leaf level first)
+  const uint32_t leaf = (uint32_t)t;
+  uint32_t lpk[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)kk * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
+  ed25519_expand(az, seed);
+  ed25519_sign_core(sig, az, lpk, body_bytes + boff, bl, btab);
+  uint8_t* ks = kes_sig + 448 * i;
+  store_words(ks, sig, 16);
+  uint32_t node = 64 + leaf;
+  for (int d = 1; d <= 6; d++) {                // level d pair = children of the ancestor at height d
+    const uint32_t parent = node >> 1;
+    store_words(ks + 64 * d, T + (2 * parent) * 8, 8);
+    store_words(ks + 64 * d + 32, T + (2 * parent + 1) * 8, 8);
+    node = parent;
+  }
 }
 
 // Corruption model (consensus-testlib Test/Util/Corruption.hs:29-35): increment
 // the byte at offset k mod len of one chosen field.
 __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig,
                                 uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off,
-                                const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof) {
+                                const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // CBOR bodies carry copies of the OCert signature and the VRF cert: a corruption
+  // of those fields is applied to the copy as well, so the stored header bytes
+  // (praos_hip/chunk.py) hold exactly the corrupted header.
+  int32_t at_vrf_out = -1, at_vrf_proof = -1, at_ocert_sig = -1;
+  if (cbor_body) {
+    const uint8_t* b = body_bytes + body_off[i];
+    auto ulen = [](uint32_t ib) -> int32_t {
+      const uint32_t ai = ib & 31u;
+      return ai < 24 ? 1 : ai == 24 ? 2 : ai == 25 ? 3 : ai == 26 ? 5 : 9;
+    };
+    int32_t q = 1;
+    q += ulen(b[q]);                       // blockNo
+    q += ulen(b[q]);                       // slotNo
+    q += 34 + 34 + 34 + 1;                 // prevHash, vk, vrfVk, [ of the cert
+    at_vrf_out = q + 2;
+    q += 66;
+    at_vrf_proof = q + 2;
+    q += 82;
+    q += ulen(b[q]);                       // bodySize
+    q += 34 + 1 + 34;                      // bodyHash, [ of the OCert, hotVk
+    q += ulen(b[q]);                       // n
+    q += ulen(b[q]);                       // c0
+    at_ocert_sig = q + 2;
+  }
   const uint64_t r = mix64(i ^ salt ^ 0xc0ffee);
   const bool c = (r % 10000u) < per10000;
   corrupted[i] = c ? 1 : 0;
@@ -223,12 +297,20 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
   const uint32_t which = (uint32_t)((r >> 20) % 5u);
   const uint32_t k = (uint32_t)(r >> 32);
   switch (which) {
-    case 0: ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1; break;
+    case 0:
+      ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1;
+      if (at_ocert_sig >= 0) body_bytes[body_off[i] + at_ocert_sig + k % 64] += 1;
+      break;
     case 1: kes_sig[448 * i + k % 448] += 1; corrupted[i] = 2; break;
     case 2:
       if (l_proof && (k & 0x10000)) { l_proof[80 * i + k % 80] += 1; corrupted[i] = 6; break; }
-      vrf_proof[80 * i + k % 80] += 1; corrupted[i] = 3; break;
-    case 3: vrf_out[64 * i + k % 64] += 1; corrupted[i] = 4; break;
+      vrf_proof[80 * i + k % 80] += 1; corrupted[i] = 3;
+      if (at_vrf_proof >= 0) body_bytes[body_off[i] + at_vrf_proof + k % 80] += 1;
+      break;
+    case 3:
+      vrf_out[64 * i + k % 64] += 1; corrupted[i] = 4;
+      if (at_vrf_out >= 0) body_bytes[body_off[i] + at_vrf_out + k % 64] += 1;
+      break;
     default:
       if (body_len[i] == 0) { ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1; break; }
       body_bytes[body_off[i] + k % body_len[i]] += 1; corrupted[i] = 5; break;
@@ -266,7 +348,7 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt,
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out,
                           uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len,
-                          uint8_t* corrupted, uint8_t* l_proof) {
+                          uint8_t* corrupted, uint8_t* l_proof, int cbor_body) {
   hipLaunchKernelGGL(k_synth_corrupt, grid, block, 0, stream, n, per10000, salt, ocert_sig, kes_sig, vrf_proof,
-                     vrf_out, body_bytes, body_off, body_len, corrupted, l_proof);
+                     vrf_out, body_bytes, body_off, body_len, corrupted, l_proof, cbor_body);
 }

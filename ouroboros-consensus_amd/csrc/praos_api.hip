@@ -25,7 +25,8 @@ struct praos_ctx {
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
-  float kernel_ms[5] = {0, 0, 0, 0, 0};
+  float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
+  bool last_from_bytes = false;
   std::string err;
   ge_niels* btab = nullptr;
   // epoch
@@ -63,6 +64,15 @@ struct praos_batch {
     ge_cached* ktab = nullptr;
   } kc[2];
   bool kc_used = false;
+  // batches from stored bytes (praos_batch_upload_bytes): the arena and the
+  // decoded HeaderBody fields beyond the SoA above (k_decode.hip)
+  bool from_bytes = false;
+  uint8_t* arena = nullptr;
+  size_t arena_len = 0;
+  uint64_t *hoff = nullptr, *block_no = nullptr, *prot_major = nullptr, *prot_minor = nullptr;
+  uint32_t *hlen = nullptr, *body_size = nullptr;
+  uint8_t *prev_hash = nullptr, *prev_genesis = nullptr, *body_hash = nullptr, *header_hash = nullptr;
+  uint16_t* dec_status = nullptr;
   std::vector<void*> owned;
 };
 
@@ -206,6 +216,48 @@ void praos_batch_free(praos_ctx* c, praos_batch* b) {
   delete b;
 }
 
+// device buffers of a batch: header SoA, body arena, outputs, key caches
+static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
+  bool ok = true;
+  ok &= dalloc(b, &b->slot, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->ocert_n, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->ocert_c0, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body_off, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body_len, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->cold_vk, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_vk, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_out, 64 * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_proof, 80 * n) == hipSuccess;
+  ok &= dalloc(b, &b->hot_vk, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->ocert_sig, 64 * n) == hipSuccess;
+  ok &= dalloc(b, &b->kes_sig, 448 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body, body_arena_bytes) == hipSuccess;
+  ok &= dalloc(b, &b->bits, 2 * n) == hipSuccess;
+  ok &= dalloc(b, &b->bits3, 6 * n) == hipSuccess;
+  ok &= dalloc(b, &b->pool_idx, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->pool_sorted, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->beta, 64 * n) == hipSuccess;
+  ok &= dalloc(b, &b->leader, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->nonce, 32 * n) == hipSuccess;
+  for (auto& k : b->kc) {
+    k.cap = 256;
+    while (k.cap < 2 * n) k.cap <<= 1;
+    k.max_entries = (uint32_t)std::min<size_t>(n / 2 + 1, KC_MAX_ENTRIES);
+    ok &= dalloc(b, &k.slot_rep, 4 * (size_t)k.cap) == hipSuccess;
+    ok &= dalloc(b, &k.slot_cnt, 4 * (size_t)k.cap) == hipSuccess;
+    ok &= dalloc(b, &k.slot_entry, 4 * (size_t)k.cap) == hipSuccess;
+    ok &= dalloc(b, &k.item_slot, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.item_entry, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.hit, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.miss, 4 * n) == hipSuccess;
+    ok &= dalloc(b, &k.counters, 16) == hipSuccess;
+    ok &= dalloc(b, &k.entry_rep, 4 * (size_t)k.max_entries) == hipSuccess;
+    ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
+    ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
+  }
+  return ok;
+}
+
 praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   if (!c || !h) return nullptr;
   if (hipSetDevice(c->device) != hipSuccess) return nullptr;
@@ -230,43 +282,7 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   }
   (void)bad_range;
   b->body_bytes_len = total;
-  bool ok = true;
-  ok &= dalloc(b, &b->slot, 8 * n) == hipSuccess;
-  ok &= dalloc(b, &b->ocert_n, 8 * n) == hipSuccess;
-  ok &= dalloc(b, &b->ocert_c0, 8 * n) == hipSuccess;
-  ok &= dalloc(b, &b->body_off, 8 * n) == hipSuccess;
-  ok &= dalloc(b, &b->body_len, 4 * n) == hipSuccess;
-  ok &= dalloc(b, &b->cold_vk, 32 * n) == hipSuccess;
-  ok &= dalloc(b, &b->vrf_vk, 32 * n) == hipSuccess;
-  ok &= dalloc(b, &b->vrf_out, 64 * n) == hipSuccess;
-  ok &= dalloc(b, &b->vrf_proof, 80 * n) == hipSuccess;
-  ok &= dalloc(b, &b->hot_vk, 32 * n) == hipSuccess;
-  ok &= dalloc(b, &b->ocert_sig, 64 * n) == hipSuccess;
-  ok &= dalloc(b, &b->kes_sig, 448 * n) == hipSuccess;
-  ok &= dalloc(b, &b->body, total + 16) == hipSuccess;
-  ok &= dalloc(b, &b->bits, 2 * n) == hipSuccess;
-  ok &= dalloc(b, &b->bits3, 6 * n) == hipSuccess;
-  ok &= dalloc(b, &b->pool_idx, 4 * n) == hipSuccess;
-  ok &= dalloc(b, &b->pool_sorted, 4 * n) == hipSuccess;
-  ok &= dalloc(b, &b->beta, 64 * n) == hipSuccess;
-  ok &= dalloc(b, &b->leader, 32 * n) == hipSuccess;
-  ok &= dalloc(b, &b->nonce, 32 * n) == hipSuccess;
-  for (auto& k : b->kc) {
-    k.cap = 256;
-    while (k.cap < 2 * n) k.cap <<= 1;
-    k.max_entries = (uint32_t)std::min<size_t>(n / 2 + 1, KC_MAX_ENTRIES);
-    ok &= dalloc(b, &k.slot_rep, 4 * (size_t)k.cap) == hipSuccess;
-    ok &= dalloc(b, &k.slot_cnt, 4 * (size_t)k.cap) == hipSuccess;
-    ok &= dalloc(b, &k.slot_entry, 4 * (size_t)k.cap) == hipSuccess;
-    ok &= dalloc(b, &k.item_slot, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.item_entry, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.hit, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.miss, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.counters, 16) == hipSuccess;
-    ok &= dalloc(b, &k.entry_rep, 4 * (size_t)k.max_entries) == hipSuccess;
-    ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
-    ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
-  }
+  bool ok = alloc_soa(b, n, total + 16);
   if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
   auto up = [&](void* d, const void* s, size_t bytes) {
     if (bytes) ok &= hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess;
@@ -289,6 +305,54 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   return b;
 }
 
+praos_batch* praos_batch_upload_bytes(praos_ctx* c, const praos_header_bytes* in) {
+  if (!c || !in || (in->n && (!in->off || !in->len || (!in->bytes && in->bytes_len)))) return nullptr;
+  if (c->device < 0) { c->err = "host-only context: no HIP device"; return nullptr; }
+  if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+  praos_batch* b = new praos_batch();
+  const size_t n = in->n;
+  b->n = n;
+  b->from_bytes = true;
+  b->arena_len = in->bytes_len;
+  b->body_bytes_len = (size_t)PRAOS_SIGNED_STRIDE * n;
+  bool ok = alloc_soa(b, n, b->body_bytes_len + 16);
+  ok &= dalloc(b, &b->arena, ((in->bytes_len + 7) & ~(size_t)7) + 16) == hipSuccess;  // +16: ld64u pad
+  ok &= dalloc(b, &b->hoff, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->hlen, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->block_no, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prot_major, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prot_minor, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body_size, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prev_hash, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prev_genesis, n) == hipSuccess;
+  ok &= dalloc(b, &b->body_hash, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->header_hash, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->dec_status, 2 * n) == hipSuccess;
+  if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
+  const size_t pad = ((in->bytes_len + 7) & ~(size_t)7) + 16 - in->bytes_len;
+  ok &= hipMemsetAsync(b->arena + in->bytes_len, 0, pad, c->stream) == hipSuccess;
+  if (in->bytes_len)
+    ok &= hipMemcpyAsync(b->arena, in->bytes, in->bytes_len, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+  if (n) {
+    ok &= hipMemcpyAsync(b->hoff, in->off, 8 * n, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    ok &= hipMemcpyAsync(b->hlen, in->len, 4 * n, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+  }
+  ok &= hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) { c->err = "upload failed"; praos_batch_free(c, b); return nullptr; }
+  return b;
+}
+
+// k_decode_praos over a from-bytes batch, on the ctx stream
+static int batch_decode(praos_ctx* c, praos_batch* b) {
+  if (b->n == 0) return PRAOS_OK;
+  launch_decode_praos(dim3(nblocks(b->n, NT)), dim3(NT), c->stream, b->n, b->arena, b->arena_len, b->hoff, b->hlen,
+                      b->slot, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->hot_vk, b->ocert_sig, b->kes_sig,
+                      b->ocert_n, b->ocert_c0, b->body_off, b->body_len, b->body, b->block_no, b->prev_hash,
+                      b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor, b->header_hash,
+                      b->dec_status);
+  return hipGetLastError() == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
+}
+
 int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (!c || !b) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
@@ -306,6 +370,13 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   hipStream_t so = c->concurrent ? c->side[0] : c->stream;
   hipStream_t sk = c->concurrent ? c->side[1] : c->stream;
   hipStream_t sv = c->concurrent ? c->side[2] : c->stream;
+  c->last_from_bytes = b->from_bytes;
+  if (b->from_bytes) {
+    // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
+    HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+    const int rd = batch_decode(c, b);
+    if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
+  }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[0], 0));
@@ -423,15 +494,17 @@ int praos_batch_sync(praos_ctx* c) {
     c->kernel_ms[1] = t[1] - t[0];
     c->kernel_ms[2] = t[2] - t[1];
   }
-  float all = 0;
+  float all = 0, dec = 0;
   (void)hipEventElapsedTime(&all, c->ev[0], c->ev[4]);
+  if (c->last_from_bytes) (void)hipEventElapsedTime(&dec, c->ev[5], c->ev[0]);
   c->kernel_ms[3] = all - (c->concurrent ? std::max(t[0], std::max(t[1], t[2])) : t[2]);
-  c->kernel_ms[4] = all;
+  c->kernel_ms[4] = all + dec;
+  c->kernel_ms[5] = dec;
   return PRAOS_OK;
 }
 
 float praos_batch_kernel_ms(praos_ctx* c, int which) {
-  if (!c || which < 0 || which > 4) return -1.f;
+  if (!c || which < 0 || which > 5) return -1.f;
   return c->kernel_ms[which];
 }
 
@@ -458,6 +531,65 @@ int praos_verify_headers(praos_ctx* c, const praos_headers* h, praos_out* out) {
   int r = praos_batch_run(c, b);
   if (r == PRAOS_OK) r = praos_batch_sync(c);
   if (r == PRAOS_OK) r = praos_batch_download(c, b, out);
+  praos_batch_free(c, b);
+  return r;
+}
+
+int praos_batch_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d) {
+  if (!c || !b || !d || !b->from_bytes) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t n = b->n;
+  if (n == 0) return PRAOS_OK;
+  auto dn = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    return dst ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+  };
+  HIPCHK(c, dn(d->status, b->dec_status, 2 * n));
+  HIPCHK(c, dn(d->block_no, b->block_no, 8 * n));
+  HIPCHK(c, dn(d->slot, b->slot, 8 * n));
+  HIPCHK(c, dn(d->prev_hash, b->prev_hash, 32 * n));
+  HIPCHK(c, dn(d->prev_is_genesis, b->prev_genesis, n));
+  HIPCHK(c, dn(d->cold_vk, b->cold_vk, 32 * n));
+  HIPCHK(c, dn(d->vrf_vk, b->vrf_vk, 32 * n));
+  HIPCHK(c, dn(d->vrf_out, b->vrf_out, 64 * n));
+  HIPCHK(c, dn(d->vrf_proof, b->vrf_proof, 80 * n));
+  HIPCHK(c, dn(d->body_size, b->body_size, 4 * n));
+  HIPCHK(c, dn(d->body_hash, b->body_hash, 32 * n));
+  HIPCHK(c, dn(d->hot_vk, b->hot_vk, 32 * n));
+  HIPCHK(c, dn(d->ocert_n, b->ocert_n, 8 * n));
+  HIPCHK(c, dn(d->ocert_c0, b->ocert_c0, 8 * n));
+  HIPCHK(c, dn(d->ocert_sig, b->ocert_sig, 64 * n));
+  HIPCHK(c, dn(d->prot_major, b->prot_major, 8 * n));
+  HIPCHK(c, dn(d->prot_minor, b->prot_minor, 8 * n));
+  HIPCHK(c, dn(d->kes_sig, b->kes_sig, 448 * n));
+  HIPCHK(c, dn(d->signed_len, b->body_len, 4 * n));
+  HIPCHK(c, dn(d->signed_body, b->body, (size_t)PRAOS_SIGNED_STRIDE * n));
+  HIPCHK(c, dn(d->header_hash, b->header_hash, 32 * n));
+  return PRAOS_OK;
+}
+
+int praos_decode_headers(praos_ctx* c, const praos_header_bytes* in, praos_decoded* out) {
+  if (!c || !in || !out) return PRAOS_E_ARG;
+  if (c->device < 0) { c->err = "host-only context: no HIP device"; return PRAOS_E_STATE; }
+  if (in->n == 0) return PRAOS_OK;
+  praos_batch* b = praos_batch_upload_bytes(c, in);
+  if (!b) return PRAOS_E_OOM;
+  int r = batch_decode(c, b);
+  if (r == PRAOS_OK) r = praos_batch_download_decoded(c, b, out);
+  praos_batch_free(c, b);
+  return r;
+}
+
+int praos_verify_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec) {
+  if (!c || !in || !out || !out->bits) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  if (in->n == 0) return PRAOS_OK;
+  praos_batch* b = praos_batch_upload_bytes(c, in);
+  if (!b) return PRAOS_E_OOM;
+  int r = praos_batch_run(c, b);
+  if (r == PRAOS_OK) r = praos_batch_sync(c);
+  if (r == PRAOS_OK) r = praos_batch_download(c, b, out);
+  if (r == PRAOS_OK && dec) r = praos_batch_download_decoded(c, b, dec);
   praos_batch_free(c, b);
   return r;
 }
@@ -766,7 +898,9 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
   if (!c || !sp || !params || sp->npools == 0 || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = sp->n, np = sp->npools;
-  const size_t bstride = ((size_t)sp->body_len + 7) & ~(size_t)7;
+  // body_len 0: genuine CBOR HeaderBody (Praos only), PRAOS_SIGNED_STRIDE bytes per header
+  if (sp->body_len == 0 && tpraos) return PRAOS_E_ARG;
+  const size_t bstride = sp->body_len ? (((size_t)sp->body_len + 7) & ~(size_t)7) : (size_t)PRAOS_SIGNED_STRIDE;
   Scratch s(c);
   uint32_t master[8], e0[8] = {0};
   std::memcpy(master, sp->seed, 32);
@@ -814,7 +948,8 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
                        dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
-                       salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr);
+                       salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
+                       sp->body_len == 0 ? 1 : 0);
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));

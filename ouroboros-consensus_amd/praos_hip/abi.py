@@ -102,6 +102,32 @@ class SynthParams(ctypes.Structure):
                 ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32)]
 
 
+class HeaderBytes(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("bytes", u8p), ("bytes_len", ctypes.c_size_t), ("off", u64p),
+                ("len", u32p)]
+
+
+DECODED_FIELDS = (  # name, dtype, record shape (praos_decoded, include/praos_hip.h)
+    ("status", np.uint16, ()), ("block_no", np.uint64, ()), ("slot", np.uint64, ()), ("prev_hash", np.uint8, (32,)),
+    ("prev_is_genesis", np.uint8, ()), ("cold_vk", np.uint8, (32,)), ("vrf_vk", np.uint8, (32,)),
+    ("vrf_out", np.uint8, (64,)), ("vrf_proof", np.uint8, (80,)), ("body_size", np.uint32, ()),
+    ("body_hash", np.uint8, (32,)), ("hot_vk", np.uint8, (32,)), ("ocert_n", np.uint64, ()),
+    ("ocert_c0", np.uint64, ()), ("ocert_sig", np.uint8, (64,)), ("prot_major", np.uint64, ()),
+    ("prot_minor", np.uint64, ()), ("kes_sig", np.uint8, (448,)), ("signed_len", np.uint32, ()),
+    ("signed_body", np.uint8, (448,)), ("header_hash", np.uint8, (32,)))
+_CT = {np.uint8: u8p, np.uint16: u16p, np.uint32: u32p, np.uint64: u64p}
+
+
+class Decoded(ctypes.Structure):
+    _fields_ = [(name, _CT[dt]) for name, dt, _ in DECODED_FIELDS]
+
+
+# decode status (PRAOS_DEC_*)
+DEC_RANGE, DEC_SYNTAX, DEC_SIZE, DEC_UNSUPPORTED, DEC_TRAILING, DEC_NONCANONICAL, DEC_OVERFLOW = \
+    0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40
+DEC_FAILED = 0x5F
+SIGNED_STRIDE = 448
+
 # every entry point declared in include/praos_hip.h: name -> (restype, argtypes)
 SIGNATURES = {
     "praos_abi_version": (ctypes.c_int, []),
@@ -138,6 +164,11 @@ SIGNATURES = {
     "praos_synthesize_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params),
                                                u8p, ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p,
                                                u8p, u8p, u64p, u32p, u8p, u8p, u8p, u8p]),
+    "praos_decode_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.POINTER(Decoded)]),
+    "praos_verify_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.POINTER(Out),
+                                                 ctypes.POINTER(Decoded)]),
+    "praos_batch_upload_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
+    "praos_batch_download_decoded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Decoded)]),
     "praos_debug_fe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, u8p, u8p, u8p]),
     "praos_debug_sha512": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u64p, u32p, u8p, ctypes.c_size_t,
                                           u8p]),
@@ -320,6 +351,64 @@ class Context:
     def free(self, b):
         self.L.praos_batch_free(self.h, b)
 
+    # ---- stored header bytes (GPU decode, k_decode.hip) ----
+    @staticmethod
+    def header_bytes_struct(arena, off, length):
+        s = HeaderBytes()
+        s.n = len(off)
+        s.bytes = ptr(arena)
+        s.bytes_len = len(arena)
+        s.off = ptr(off, u64p)
+        s.len = ptr(length, u32p)
+        return s
+
+    @staticmethod
+    def alloc_decoded(n):
+        D = {name: np.zeros((n,) + shp, dt) for name, dt, shp in DECODED_FIELDS}
+        d = Decoded()
+        for name, dt, _ in DECODED_FIELDS:
+            setattr(d, name, ptr(D[name], _CT[dt]))
+        return D, d
+
+    @staticmethod
+    def _chunk(arena, off, length):
+        return (np.ascontiguousarray(np.frombuffer(arena, np.uint8) if isinstance(arena, (bytes, bytearray))
+                                     else arena, dtype=np.uint8),
+                np.ascontiguousarray(off, dtype=np.uint64), np.ascontiguousarray(length, dtype=np.uint32))
+
+    def decode_headers(self, arena, off, length):
+        """Decode stored Praos headers arena[off[i]:off[i]+len[i]] on the GPU; returns a dict of arrays
+        (DECODED_FIELDS)."""
+        arena, off, length = self._chunk(arena, off, length)
+        hb = self.header_bytes_struct(arena, off, length)
+        D, d = self.alloc_decoded(len(off))
+        self.check(self.L.praos_decode_headers(self.h, ctypes.byref(hb), ctypes.byref(d)))
+        return D
+
+    def verify_header_bytes(self, arena, off, length, decoded=False):
+        arena, off, length = self._chunk(arena, off, length)
+        n = len(off)
+        hb = self.header_bytes_struct(arena, off, length)
+        o = self.alloc_out(n)
+        os_ = self.out_struct(o)
+        D, d = self.alloc_decoded(n) if decoded else (None, None)
+        self.check(self.L.praos_verify_header_bytes(self.h, ctypes.byref(hb), ctypes.byref(os_),
+                                                    ctypes.byref(d) if d is not None else None))
+        return (o, D) if decoded else o
+
+    def upload_bytes(self, arena, off, length):
+        arena, off, length = self._chunk(arena, off, length)
+        hb = self.header_bytes_struct(arena, off, length)
+        b = self.L.praos_batch_upload_bytes(self.h, ctypes.byref(hb))
+        if not b:
+            self.check(-3)
+        return b
+
+    def download_decoded(self, b, n):
+        D, d = self.alloc_decoded(n)
+        self.check(self.L.praos_batch_download_decoded(self.h, b, ctypes.byref(d)))
+        return D
+
     def update_chain_dep_state(self, H, crypto, prev_hash, state: dict, epoch_info, prev_is_genesis=None):
         """state: dict(last_slot (None = Origin), counters {hash28: n}, evolving, candidate, epoch_nonce,
         lab, leb) with nonces None (Neutral) or 32 bytes; updated in place.  epoch_info: (base_slot,
@@ -432,7 +521,7 @@ class Context:
         sp.corrupt_per_10000 = corrupt_per_10000
         sp.nkes = nkes
         ctypes.memmove(sp.seed, seed, 32)
-        bstride = (body_len + 7) & ~7
+        bstride = (body_len + 7) & ~7 if body_len else SIGNED_STRIDE   # 0: genuine CBOR bodies
         H = {"slot": np.zeros(n, np.uint64), "cold_vk": np.zeros((n, 32), np.uint8),
              "vrf_vk": np.zeros((n, 32), np.uint8), "vrf_out": np.zeros((n, 64), np.uint8),
              "vrf_proof": np.zeros((n, 80), np.uint8), "hot_vk": np.zeros((n, 32), np.uint8),

@@ -41,11 +41,13 @@ def test_struct_sizes_match_c_layout():
     assert ctypes.sizeof(abi.Params) == 40
     assert ctypes.sizeof(abi.Pool) == 76
     assert ctypes.sizeof(abi.Headers) == 15 * 8
+    assert ctypes.sizeof(abi.HeaderBytes) == 5 * 8
+    assert ctypes.sizeof(abi.Decoded) == 21 * 8
 
 
 def test_abi_version():
     from praos_hip import abi
-    assert abi.load().praos_abi_version() == 2
+    assert abi.load().praos_abi_version() == 3
 
 
 def test_no_silent_fallback_without_gpu():

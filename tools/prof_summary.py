@@ -16,7 +16,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_ocert", "k_kes", "k_vrf", "k_vrf_tp", "k_leader", "k_synth_headers")
+KERNELS = ("k_ocert", "k_ocert_ck", "k_kes", "k_vrf", "k_vrf_ck", "k_vrf_tp", "k_leader", "k_key_precompute", "k_synth_headers")
 
 
 def short(name):
@@ -35,6 +35,26 @@ def main():
             for r in csv.DictReader(f):
                 lines.append(f"{short(r['Name'])[:28]:28s} {int(r['Calls']):6d} {float(r['AverageNs'])/1e6:10.3f} "
                              f"{float(r['MinNs'])/1e6:10.3f} {float(r['MaxNs'])/1e6:10.3f} {float(r['Percentage']):7.2f}")
+        lines.append("")
+    trace = glob.glob(os.path.join(d, "kt", "*kernel_trace.csv"))
+    if trace:
+        # bench.py times each crypto kernel alone (serial launches after the timed
+        # region) for the roofline; the timed steps run them concurrently on three
+        # streams, which stretches each launch.  Split the trace the same way.
+        with open(trace[0]) as f:
+            rows = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                    for r in csv.DictReader(f)]
+        crypto = [r for r in rows if r[0] in KERNELS and not r[0].startswith("k_synth") and r[2] - r[1] > 100_000]
+        iso, conc = defaultdict(list), defaultdict(list)
+        for k, s, e in crypto:
+            overl = any(o is not None and o[1] < e and s < o[2] for o in crypto if o != (k, s, e))
+            (conc if overl else iso)[k].append((e - s) / 1e6)
+        lines.append("== per-launch durations split by overlap (launches > 0.1 ms) ==")
+        lines.append(f"{'kernel':16s} {'isolated n':>10s} {'avg ms':>8s} {'concurrent n':>12s} {'avg ms':>8s}")
+        for k in sorted(set(iso) | set(conc)):
+            a = iso.get(k, [])
+            b = conc.get(k, [])
+            lines.append(f"{k:16s} {len(a):10d} {sum(a)/max(1,len(a)):8.3f} {len(b):12d} {sum(b)/max(1,len(b)):8.3f}")
         lines.append("")
     bench = os.path.join(d, "kt_bench.json")
     if os.path.exists(bench):
