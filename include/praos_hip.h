@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 3
+#define PRAOS_ABI_VERSION 4
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -247,6 +247,28 @@ int praos_verify_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, prao
  * copies the decoded fields of the last run. */
 praos_batch* praos_batch_upload_bytes(praos_ctx* ctx, const praos_header_bytes* in);
 int praos_batch_download_decoded(praos_ctx* ctx, praos_batch* b, praos_decoded* dec);
+
+/* ---- ImmutableDB block-integrity batch ----
+ * Replaces verifyBlockIntegrity spkp blk (Shelley/Ledger/Integrity.hs:14-20), the
+ * check ImmutableDB validation runs per stored block (--validate-all-blocks):
+ *   verifyHeaderIntegrity (Shelley/Protocol/Praos.hs:84-101): Sum6KES verify of the
+ *     header at t = kp - c0 if kp >= c0 else 0 (no OCert / VRF / maxKESEvo checks);
+ *   blockMatchesHeader (Shelley/Ledger/Block.hs:150-158): hashTxSeq of the stored
+ *     segments (Blake2b-256 over the segments' Blake2b-256 hashes) == hbBodyHash.
+ * Input: praos_header_bytes whose (off, len) describe whole stored blocks: the
+ * HardForkBlock wrapper [eraTag 6|7, [header, s1..s4]] or a bare [header, s1..s3|s4].
+ * result[i] = 0 (verifyBlockIntegrity True) or PRAOS_BLK_* bits; body_hash (may be
+ * NULL) gets the computed hashTxSeq (zeros when the block does not decode). */
+#define PRAOS_BLK_DECODE    0x01u /* block envelope, a segment or the header does not decode */
+#define PRAOS_BLK_KES       0x02u /* verifyHeaderIntegrity False */
+#define PRAOS_BLK_BODY_HASH 0x04u /* blockMatchesHeader False */
+int praos_verify_block_integrity(praos_ctx* ctx, const praos_header_bytes* blocks, uint64_t slots_per_kes_period,
+                                 uint8_t* result, uint8_t* body_hash);
+/* Device-resident form (bench / streaming ImmutableDB validation): upload once,
+ * run any number of times, download the last run's results. */
+praos_batch* praos_block_batch_upload(praos_ctx* ctx, const praos_header_bytes* blocks);
+int praos_block_batch_run(praos_ctx* ctx, praos_batch* b, uint64_t slots_per_kes_period);
+int praos_block_batch_download(praos_ctx* ctx, praos_batch* b, uint8_t* result, uint8_t* body_hash);
 
 /* ---- TPraos (Shelley..Alonzo), the d = 0 path of cardano-protocol-tpraos ----
  * Replaces SL.updateChainDepState's crypto (TPraos.hs:378-387): OVERLAY

@@ -1,0 +1,241 @@
+// k_block.hip -- ImmutableDB block-integrity batch.
+//
+// verifyBlockIntegrity spkp blk = verifyHeaderIntegrity spkp hdr && blockMatchesHeader hdr blk
+// (Shelley/Ledger/Integrity.hs:14-20).  The header half is k_kes in header mode
+// (t = max(0, kp - c0), Shelley/Protocol/Praos.hs:84-101) over the k_decode SoA;
+// this module supplies the block half:
+//   k_block_split   one lane per stored block: the era wrapper [eraTag, [header, s1..s4]]
+//                   (eraTag 6/7) or a bare [header, s1..s3|s4]; every segment must be one
+//                   well-formed CBOR item.  Emits the header span (k_decode's input) and
+//                   the segment spans, segment-major ([k][i]).
+//   k_seg_hash      one lane per (segment k, block i), segment-major so a wave hashes the
+//                   same segment kind of 64 neighbouring blocks (similar lengths, little
+//                   divergence): Blake2b-256 of the stored segment bytes.
+//   k_block_join    one lane per block: hashTxSeq = Blake2b-256 of the concatenated segment
+//                   hashes (one 96/128-byte compression), compared with hbBodyHash
+//                   (blockMatchesHeader, Shelley/Ledger/Block.hs:150-158); folds the KES
+//                   and decode bits into the result byte.
+// CPU restatement: oracle/block_integrity.py (same decode rules, same result bits).
+//
+// Roofline: HBM-bound in principle (every block byte is read once by k_seg_hash, the
+// header bytes once more by k_decode), but Blake2b is ~12 rounds x 8 G per 128 bytes,
+// ~1.4k int ops per 128 B, so at 8 TB/s the integer rate (~39 T ops/s) is the bound:
+// ~3.6 TB/s of block bytes.  The KES verify per block dominates for small blocks.
+#include "kcommon.hpp"
+#include "arena.hpp"
+
+namespace {
+
+constexpr uint32_t MAX_INDEF = 16;          // nested indefinite items (oracle MAX_INDEF)
+constexpr uint64_t BIG = 1ull << 62;        // "at an indefinite level" marker for `need`
+
+struct Cur {
+  const uint8_t* __restrict__ a;
+  uint64_t p, end;
+  bool ok;
+};
+
+// item head: major type, additional info, argument (indef = true for ai 31)
+__device__ __forceinline__ bool head(Cur& c, uint32_t& mt, uint32_t& ai, uint64_t& arg, bool& indef) {
+  if (c.p >= c.end) return false;
+  const uint32_t ib = c.a[c.p++];
+  mt = ib >> 5;
+  ai = ib & 31u;
+  indef = false;
+  if (ai < 24) { arg = ai; return true; }
+  if (ai <= 27) {
+    const uint32_t nb = 1u << (ai - 24);
+    if (nb > c.end - c.p) return false;
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < nb; k++) v = (v << 8) | c.a[c.p + k];
+    c.p += nb;
+    arg = v;
+    return true;
+  }
+  if (ai == 31 && (mt == 2 || mt == 3 || mt == 4 || mt == 5 || mt == 7)) { indef = true; arg = 0; return true; }
+  return false;   // 28..30 reserved; indefinite uint / nint / tag
+}
+
+// advance c.p past ONE well-formed CBOR item (oracle block_integrity.cbor_skip)
+__device__ bool cbor_skip(Cur& c) {
+  uint64_t need = 1;
+  uint64_t st_need[MAX_INDEF];
+  uint8_t st_kind[MAX_INDEF];
+  uint32_t sp = 0;
+  while (need || sp) {
+    if (c.p >= c.end) return false;
+    if (c.a[c.p] == 0xFF) {
+      if (!sp || need != BIG) return false;
+      need = st_need[--sp];
+      c.p++;
+      continue;
+    }
+    uint32_t mt, ai;
+    uint64_t arg;
+    bool indef;
+    if (!head(c, mt, ai, arg, indef)) return false;
+    if (sp && need == BIG && st_kind[sp - 1] != 0 && (mt != st_kind[sp - 1] || indef)) return false;
+    if (need != BIG) need -= 1;
+    if (mt == 2 || mt == 3) {
+      if (indef) {
+        if (sp == MAX_INDEF) return false;
+        st_need[sp] = need; st_kind[sp] = (uint8_t)mt; sp++;
+        need = BIG;
+      } else {
+        if (arg > c.end - c.p) return false;
+        c.p += arg;
+      }
+    } else if (mt == 4 || mt == 5) {
+      if (indef) {
+        if (sp == MAX_INDEF) return false;
+        st_need[sp] = need; st_kind[sp] = 0; sp++;
+        need = BIG;
+      } else {
+        const uint64_t k = mt == 5 ? 2 * arg : arg;
+        if (arg > c.end - c.p || k > c.end - c.p) return false;   // each item takes >= 1 byte
+        need += k;
+      }
+    } else if (mt == 6) {
+      need += 1;
+    } else if (mt == 7) {
+      if (ai == 24 && arg < 32) return false;
+    }
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(NT) k_block_split(size_t n, const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                    uint64_t* __restrict__ off_io, uint32_t* __restrict__ len_io,
+                                                    uint64_t* __restrict__ seg_off, uint32_t* __restrict__ seg_len,
+                                                    uint8_t* __restrict__ nseg, uint8_t* __restrict__ status) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t off = off_io[i];
+  const uint32_t len = len_io[i];
+  bool ok = off <= arena_len && len <= arena_len - off;
+  Cur c{arena, off, off + len, true};
+  uint64_t sp_off[5];
+  uint32_t sp_len[5];
+  uint32_t nitems = 0;
+  if (ok) {
+    uint32_t mt, ai;
+    uint64_t arg;
+    bool indef;
+    ok = head(c, mt, ai, arg, indef) && mt == 4 && !indef;
+    bool wrapped = false;
+    if (ok && arg == 2) {
+      uint64_t tag;
+      ok = head(c, mt, ai, tag, indef) && mt == 0 && (tag == 6 || tag == 7);   // Babbage, Conway
+      ok = ok && head(c, mt, ai, arg, indef) && mt == 4 && !indef && arg == 5;
+      wrapped = true;
+    }
+    ok = ok && (wrapped || arg == 4 || arg == 5);
+    if (ok) {
+      nitems = (uint32_t)arg;
+      for (uint32_t k = 0; k < nitems && ok; k++) {
+        const uint64_t s = c.p;
+        ok = cbor_skip(c);
+        sp_off[k] = s;
+        sp_len[k] = (uint32_t)(c.p - s);
+      }
+      ok = ok && c.p == c.end;
+    }
+  }
+  if (!ok) {
+    off_io[i] = 0;
+    len_io[i] = 0;   // k_decode then reports SYNTAX; k_block_join reports DECODE
+    nseg[i] = 0;
+    status[i] = 1;
+    return;
+  }
+  off_io[i] = sp_off[0];
+  len_io[i] = sp_len[0];
+  for (uint32_t k = 1; k < 5; k++) {
+    seg_off[(size_t)(k - 1) * n + i] = k < nitems ? sp_off[k] : 0;
+    seg_len[(size_t)(k - 1) * n + i] = k < nitems ? sp_len[k] : 0;
+  }
+  nseg[i] = (uint8_t)(nitems - 1);
+  status[i] = 0;
+}
+
+__global__ void __launch_bounds__(NT) k_seg_hash(size_t n, const uint8_t* __restrict__ arena,
+                                                 const uint64_t* __restrict__ seg_off,
+                                                 const uint32_t* __restrict__ seg_len, const uint8_t* __restrict__ nseg,
+                                                 uint8_t* __restrict__ seg_hash) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 4 * n) return;
+  const size_t k = j / n, i = j - k * n;
+  if (k >= nseg[i]) return;
+  uint32_t h[8];
+  b2b256_range(h, arena, seg_off[j], seg_len[j]);
+  store_words(seg_hash + 32 * j, h, 8);
+}
+
+__global__ void __launch_bounds__(NT) k_block_join(size_t n, const uint8_t* __restrict__ nseg,
+                                                   const uint8_t* __restrict__ split_status,
+                                                   const uint16_t* __restrict__ dec_status,
+                                                   const uint16_t* __restrict__ kes_bits,
+                                                   const uint8_t* __restrict__ seg_hash,
+                                                   const uint8_t* __restrict__ body_hash,
+                                                   uint8_t* __restrict__ result, uint8_t* __restrict__ calc_hash) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  if (split_status[i] || (dec_status[i] & PRAOS_DEC_FAILED)) {
+    result[i] = PRAOS_BLK_DECODE;
+    ((uint4*)(calc_hash + 32 * i))[0] = z;
+    ((uint4*)(calc_hash + 32 * i))[1] = z;
+    return;
+  }
+  // hashTxSeq: Blake2b-256 of hash(s1) || ... || hash(sk), one 128-byte block
+  const uint32_t k = nseg[i];
+  uint64_t m[16];
+#pragma unroll
+  for (uint32_t s = 0; s < 4; s++) {
+    const uint4* q = (const uint4*)(seg_hash + 32 * ((size_t)s * n + i));
+    const uint4 a = s < k ? q[0] : z, b = s < k ? q[1] : z;
+    m[4 * s + 0] = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    m[4 * s + 1] = (uint64_t)a.z | ((uint64_t)a.w << 32);
+    m[4 * s + 2] = (uint64_t)b.x | ((uint64_t)b.y << 32);
+    m[4 * s + 3] = (uint64_t)b.z | ((uint64_t)b.w << 32);
+  }
+  uint64_t h[8];
+#pragma unroll
+  for (int w = 0; w < 8; w++) h[w] = B2B_IV[w];
+  h[0] ^= 0x01010000ULL ^ 32u;
+  b2b_compress(h, m, 32ull * k, true);
+  const uint4* e = (const uint4*)(body_hash + 32 * i);
+  const uint4 e0 = e[0], e1 = e[1];
+  const uint4 c0 = make_uint4((uint32_t)h[0], (uint32_t)(h[0] >> 32), (uint32_t)h[1], (uint32_t)(h[1] >> 32));
+  const uint4 c1 = make_uint4((uint32_t)h[2], (uint32_t)(h[2] >> 32), (uint32_t)h[3], (uint32_t)(h[3] >> 32));
+  ((uint4*)(calc_hash + 32 * i))[0] = c0;
+  ((uint4*)(calc_hash + 32 * i))[1] = c1;
+  const bool match = e0.x == c0.x && e0.y == c0.y && e0.z == c0.z && e0.w == c0.w && e1.x == c1.x &&
+                     e1.y == c1.y && e1.z == c1.z && e1.w == c1.w;
+  uint8_t r = 0;
+  if (kes_bits[i] & (PRAOS_BIT_KES_MERKLE | PRAOS_BIT_KES_LEAF | PRAOS_BIT_INPUT)) r |= PRAOS_BLK_KES;
+  if (!match) r |= PRAOS_BLK_BODY_HASH;
+  result[i] = r;
+}
+
+}  // namespace
+
+// ---- host launchers (kernels are only launchable from their own module)
+void launch_block_split(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
+                        uint64_t arena_len, uint64_t* off_io, uint32_t* len_io, uint64_t* seg_off, uint32_t* seg_len,
+                        uint8_t* nseg, uint8_t* status) {
+  hipLaunchKernelGGL(k_block_split, grid, block, 0, stream, n, arena, arena_len, off_io, len_io, seg_off, seg_len,
+                     nseg, status);
+}
+
+void launch_seg_hash(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
+                     const uint64_t* seg_off, const uint32_t* seg_len, const uint8_t* nseg, uint8_t* seg_hash) {
+  hipLaunchKernelGGL(k_seg_hash, grid, block, 0, stream, n, arena, seg_off, seg_len, nseg, seg_hash);
+}
+
+void launch_block_join(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* nseg,
+                       const uint8_t* split_status, const uint16_t* dec_status, const uint16_t* kes_bits,
+                       const uint8_t* seg_hash, const uint8_t* body_hash, uint8_t* result, uint8_t* calc_hash) {
+  hipLaunchKernelGGL(k_block_join, grid, block, 0, stream, n, nseg, split_status, dec_status, kes_bits, seg_hash,
+                     body_hash, result, calc_hash);
+}

@@ -62,3 +62,11 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
                          uint8_t* header_hash, uint16_t* status);
+void launch_block_split(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
+                        uint64_t arena_len, uint64_t* off_io, uint32_t* len_io, uint64_t* seg_off, uint32_t* seg_len,
+                        uint8_t* nseg, uint8_t* status);
+void launch_seg_hash(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
+                     const uint64_t* seg_off, const uint32_t* seg_len, const uint8_t* nseg, uint8_t* seg_hash);
+void launch_block_join(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* nseg,
+                       const uint8_t* split_status, const uint16_t* dec_status, const uint16_t* kes_bits,
+                       const uint8_t* seg_hash, const uint8_t* body_hash, uint8_t* result, uint8_t* calc_hash);

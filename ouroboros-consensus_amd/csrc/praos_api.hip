@@ -73,6 +73,12 @@ struct praos_batch {
   uint32_t *hlen = nullptr, *body_size = nullptr;
   uint8_t *prev_hash = nullptr, *prev_genesis = nullptr, *body_hash = nullptr, *header_hash = nullptr;
   uint16_t* dec_status = nullptr;
+  // block-integrity batches (k_block.hip): stored block spans, segment spans
+  // (segment-major [k][i]), per-segment hashes, results
+  bool is_block = false;
+  uint64_t *blk_off = nullptr, *seg_off = nullptr;
+  uint32_t *blk_len = nullptr, *seg_len = nullptr;
+  uint8_t *nseg = nullptr, *split_status = nullptr, *seg_hash = nullptr, *blk_result = nullptr, *blk_hash = nullptr;
   std::vector<void*> owned;
 };
 
@@ -453,6 +459,87 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   HIPCHK(c, hipGetLastError());
   return PRAOS_OK;
+}
+
+// ---- block-integrity batch (k_block.hip + k_decode + k_kes header mode)
+praos_batch* praos_block_batch_upload(praos_ctx* c, const praos_header_bytes* blocks) {
+  praos_batch* b = praos_batch_upload_bytes(c, blocks);
+  if (!b) return nullptr;
+  const size_t n = b->n;
+  b->is_block = true;
+  bool ok = dalloc(b, &b->blk_off, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->blk_len, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->seg_off, 8 * 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->seg_len, 4 * 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->nseg, n) == hipSuccess;
+  ok &= dalloc(b, &b->split_status, n) == hipSuccess;
+  ok &= dalloc(b, &b->seg_hash, 32 * 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->blk_result, n) == hipSuccess;
+  ok &= dalloc(b, &b->blk_hash, 32 * n) == hipSuccess;
+  if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
+  // the uploaded spans are whole blocks; k_block_split rewrites hoff/hlen to the header spans
+  if (n) {
+    ok &= hipMemcpyAsync(b->blk_off, b->hoff, 8 * n, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
+    ok &= hipMemcpyAsync(b->blk_len, b->hlen, 4 * n, hipMemcpyDeviceToDevice, c->stream) == hipSuccess;
+  }
+  ok &= hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) { c->err = "upload failed"; praos_batch_free(c, b); return nullptr; }
+  return b;
+}
+
+int praos_block_batch_run(praos_ctx* c, praos_batch* b, uint64_t slots_per_kes_period) {
+  if (!c || !b || !b->is_block || slots_per_kes_period == 0) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = b->n;
+  if (n == 0) return PRAOS_OK;
+  const dim3 g(nblocks(n, NT)), blk(NT);
+  uint16_t* bk = b->bits3 + n;
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, hipMemcpyAsync(b->hoff, b->blk_off, 8 * n, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(b->hlen, b->blk_len, 4 * n, hipMemcpyDeviceToDevice, c->stream));
+  launch_block_split(g, blk, c->stream, n, b->arena, b->arena_len, b->hoff, b->hlen, b->seg_off, b->seg_len, b->nseg,
+                     b->split_status);
+  const int rd = batch_decode(c, b);
+  if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
+  HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+  // segment hashes on a side stream, concurrent with the KES verify
+  HIPCHK(c, hipStreamWaitEvent(c->side[0], c->ev[1], 0));
+  launch_seg_hash(dim3(nblocks(4 * n, NT)), blk, c->side[0], n, b->arena, b->seg_off, b->seg_len, b->nseg,
+                  b->seg_hash);
+  HIPCHK(c, hipEventRecord(c->side_ev[0], c->side[0]));
+  launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
+             b->body_bytes_len, b->slot, b->ocert_c0, slots_per_kes_period, (const uint32_t*)nullptr, bk,
+             (uint8_t*)nullptr);
+  HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[0], 0));
+  launch_block_join(g, blk, c->stream, n, b->nseg, b->split_status, b->dec_status, bk, b->seg_hash, b->body_hash,
+                    b->blk_result, b->blk_hash);
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  HIPCHK(c, hipGetLastError());
+  return PRAOS_OK;
+}
+
+int praos_block_batch_download(praos_ctx* c, praos_batch* b, uint8_t* result, uint8_t* body_hash) {
+  if (!c || !b || !b->is_block || (b->n && !result)) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (b->n == 0) return PRAOS_OK;
+  HIPCHK(c, hipMemcpy(result, b->blk_result, b->n, hipMemcpyDeviceToHost));
+  if (body_hash) HIPCHK(c, hipMemcpy(body_hash, b->blk_hash, 32 * b->n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_verify_block_integrity(praos_ctx* c, const praos_header_bytes* blocks, uint64_t slots_per_kes_period,
+                                 uint8_t* result, uint8_t* body_hash) {
+  if (!c || !blocks || (blocks->n && !result) || slots_per_kes_period == 0) return PRAOS_E_ARG;
+  if (c->device < 0) { c->err = "host-only context: no HIP device"; return PRAOS_E_STATE; }
+  if (blocks->n == 0) return PRAOS_OK;
+  praos_batch* b = praos_block_batch_upload(c, blocks);
+  if (!b) return PRAOS_E_OOM;
+  int r = praos_block_batch_run(c, b, slots_per_kes_period);
+  if (r == PRAOS_OK) r = praos_block_batch_download(c, b, result, body_hash);
+  praos_batch_free(c, b);
+  return r;
 }
 
 int praos_batch_stats(praos_ctx* c, praos_batch* b, uint32_t out[6]) {

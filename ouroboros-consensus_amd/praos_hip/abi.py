@@ -22,6 +22,9 @@ u64p = ctypes.POINTER(ctypes.c_uint64)
 i32p = ctypes.POINTER(ctypes.c_int32)
 
 # bits (PRAOS_BIT_*)
+BLK_DECODE = 0x01      # block-integrity result bits (praos_verify_block_integrity)
+BLK_KES = 0x02
+BLK_BODY_HASH = 0x04
 BIT_KES_BEFORE_START = 0x0001
 BIT_KES_AFTER_END = 0x0002
 BIT_OCERT_SIG = 0x0004
@@ -169,6 +172,11 @@ SIGNATURES = {
                                                  ctypes.POINTER(Decoded)]),
     "praos_batch_upload_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
     "praos_batch_download_decoded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Decoded)]),
+    "praos_verify_block_integrity": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.c_uint64,
+                                                    u8p, u8p]),
+    "praos_block_batch_upload": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
+    "praos_block_batch_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "praos_block_batch_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u8p, u8p]),
     "praos_debug_fe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, u8p, u8p, u8p]),
     "praos_debug_sha512": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u64p, u32p, u8p, ctypes.c_size_t,
                                           u8p]),
@@ -395,6 +403,36 @@ class Context:
         self.check(self.L.praos_verify_header_bytes(self.h, ctypes.byref(hb), ctypes.byref(os_),
                                                     ctypes.byref(d) if d is not None else None))
         return (o, D) if decoded else o
+
+    # ---- stored blocks: verifyBlockIntegrity (k_block.hip) ----
+    def verify_block_integrity(self, arena, off, length, slots_per_kes_period):
+        """Integrity.hs:14-20 over blocks arena[off[i]:off[i]+len[i]]; returns (result u8[n] of
+        PRAOS_BLK_* bits, computed hashTxSeq u8[n,32])."""
+        arena, off, length = self._chunk(arena, off, length)
+        n = len(off)
+        hb = self.header_bytes_struct(arena, off, length)
+        res = np.zeros(n, np.uint8)
+        bh = np.zeros((n, 32), np.uint8)
+        self.check(self.L.praos_verify_block_integrity(self.h, ctypes.byref(hb), slots_per_kes_period, ptr(res),
+                                                       ptr(bh)))
+        return res, bh
+
+    def upload_blocks(self, arena, off, length):
+        arena, off, length = self._chunk(arena, off, length)
+        hb = self.header_bytes_struct(arena, off, length)
+        b = self.L.praos_block_batch_upload(self.h, ctypes.byref(hb))
+        if not b:
+            raise RuntimeError("praos_block_batch_upload: " + self.L.praos_last_error(self.h).decode())
+        return b
+
+    def run_blocks(self, b, slots_per_kes_period):
+        self.check(self.L.praos_block_batch_run(self.h, b, slots_per_kes_period))
+
+    def download_blocks(self, b, n):
+        res = np.zeros(n, np.uint8)
+        bh = np.zeros((n, 32), np.uint8)
+        self.check(self.L.praos_block_batch_download(self.h, b, ptr(res), ptr(bh)))
+        return res, bh
 
     def upload_bytes(self, arena, off, length):
         arena, off, length = self._chunk(arena, off, length)

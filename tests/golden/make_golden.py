@@ -18,6 +18,8 @@ Expected values and where they come from:
     BHBody is valid; the two VRF certs (eta, leader) verify for
     alpha = Blake2b256(0x00) / Blake2b256(0x01) (the example's dummy seeds),
     and the stored 64-B outputs equal proof_to_hash.
+  * Every block matches its header (blockMatchesHeader): the header body hash
+    is the reference's hashTxSeq of the stored block segments.
   * Praos blocks (Babbage, Conway): Examples.hs:173-192 coerce the TPraos KES
     signature into the Praos header, so the Merkle path is valid but the leaf
     signature does NOT verify over the 10-field Praos body (a natural
@@ -69,7 +71,10 @@ def main():
         body = body_it.raw(buf)
         rec = {"era": era, "file": "ouroboros-consensus-cardano/golden/" + rel,
                "header_cbor": h.raw(buf).hex(), "body_cbor": body.hex(),
-               "kes_sig": sig_it.value.hex()}
+               "kes_sig": sig_it.value.hex(),
+               # the whole stored block (HardForkBlock [eraTag, block] or a bare Shelley block):
+               # the block-integrity batch (Integrity.hs:14-20) hashes its segments
+               "block_cbor": buf.hex()}
         if len(f) == 15:  # TPraos BHBody (cardano-protocol-tpraos BHeader)
             rec.update(kind="tpraos", block_no=f[0].value, slot=f[1].value,
                        cold_vk=f[3].value.hex(), vrf_vk=f[4].value.hex(),
@@ -99,6 +104,9 @@ def main():
             recon_body = reconstruct(shelley_body, bytes.fromhex(rec["body_hash"]))
             rec["kes_recon_body"] = recon_body.hex()
             rec["expect"]["kes_result_recon_body"] = 0
+        # blockMatchesHeader (Shelley/Ledger/Block.hs:150-158): the stored header's body hash
+        # is the reference's hashTxSeq of these segments -- every golden block matches
+        rec["expect"]["block_matches_header"] = True
         kats.append(rec)
     out = os.path.join(HERE, "reference_kats.json")
     with open(out, "w") as fh:
