@@ -382,6 +382,8 @@ typedef struct {
   uint32_t corrupt_per_10000;     /* seeded corruptions (Corruption.hs model: +1 at a byte) */
   uint32_t nkes;                  /* distinct Sum6KES keys (0 = one per pool); header of pool p uses key p mod nkes */
   uint8_t seed[32];
+  const uint8_t* body_hash;       /* n*32 hbBodyHash of each CBOR body (e.g. hashTxSeq of the block's
+                                     segments, for stored-block corpora); NULL = pseudo-random */
 } praos_synth_params;
 
 /* Fills caller buffers (same layout as praos_headers; body_off/body_len/body_bytes

@@ -47,27 +47,40 @@ __device__ __forceinline__ void b2b_compress(uint64_t h[8], const uint64_t m[16]
   for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
 }
 
-// Blake2b-256 of p[pos, pos + len)
-__device__ __forceinline__ void b2b256_range(uint32_t out[8], const uint8_t* __restrict__ p, uint64_t pos, uint64_t len) {
+// one 128-byte message block of p[pos, pos + len) starting at byte `base` (zero padded)
+__device__ __forceinline__ void b2b_load_block(uint64_t m[16], const uint8_t* __restrict__ p, uint64_t pos,
+                                               uint64_t len, uint64_t base) {
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint64_t o = base + 8 * k;
+    uint64_t w = o < len ? ld64u(p, pos + o) : 0;
+    if (o < len && len - o < 8) w &= (1ull << (8 * (len - o))) - 1;
+    m[k] = w;
+  }
+}
+
+// Blake2b-256 of p[pos, pos + len).  Register double buffering: block b + 1 is
+// loaded before block b is compressed, so its (uncoalesced, per-lane) loads are
+// in flight during ~2k VALU instructions -- latency hidden even at one wave per
+// SIMD, which is what a batch of long block segments gives.
+__device__ __forceinline__ void b2b256_range(uint32_t out[8], const uint8_t* __restrict__ p, uint64_t pos,
+                                             uint64_t len) {
   uint64_t h[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) h[i] = B2B_IV[i];
   h[0] ^= 0x01010000ULL ^ 32u;
   const uint64_t nblk = len == 0 ? 1 : (len + 127) / 128;
+  uint64_t nxt[16];
+  b2b_load_block(nxt, p, pos, len, 0);
   for (uint64_t b = 0; b < nblk; b++) {
     uint64_t m[16];
-    const uint64_t base = 128 * b;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const uint64_t o = base + 8 * k;
-      uint64_t w = o < len ? ld64u(p, pos + o) : 0;
-      if (o < len && len - o < 8) w &= (1ull << (8 * (len - o))) - 1;
-      m[k] = w;
-    }
+    for (int k = 0; k < 16; k++) m[k] = nxt[k];
+    const uint64_t base = 128 * b;
+    if (b + 1 < nblk) b2b_load_block(nxt, p, pos, len, base + 128);
     const bool last = b + 1 == nblk;
     b2b_compress(h, m, last ? len : base + 128, last);
   }
 #pragma unroll
   for (int i = 0; i < 4; i++) { out[2 * i] = (uint32_t)h[i]; out[2 * i + 1] = (uint32_t)(h[i] >> 32); }
 }
-

@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk,
     uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
     uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos,
-    uint8_t* l_out, uint8_t* l_proof) {
+    uint8_t* l_out, uint8_t* l_proof, const uint8_t* __restrict__ body_hash_in) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
   const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
@@ -226,8 +226,12 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     sw_bytes(w, vrf_proof + 80 * i, 80);
     st = mix64(st + 17);
     sw_head(w, 0, st & 0xffffu);                                // bodySize
-    sw_head(w, 2, 32);                                          // bodyHash (pseudo-random)
-    for (int k = 0; k < 4; k++) { st = mix64(st + k); for (int b = 0; b < 8; b++) sw_byte(w, (uint32_t)(st >> (8 * b))); }
+    sw_head(w, 2, 32);                                          // bodyHash (caller's, else pseudo-random)
+    for (int k = 0; k < 4; k++) {
+      st = mix64(st + k);
+      for (int b = 0; b < 8; b++)
+        sw_byte(w, body_hash_in ? (uint32_t)body_hash_in[32 * i + 8 * k + b] : (uint32_t)(st >> (8 * b)));
+    }
     sw_head(w, 4, 4);
     sw_bytes(w, hot_vk + 32 * i, 32);
     sw_head(w, 0, nn);
@@ -339,11 +343,13 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
                           uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out,
                           uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len,
-                          uint8_t* body_bytes, int tpraos, uint8_t* l_out, uint8_t* l_proof) {
+                          uint8_t* body_bytes, int tpraos, uint8_t* l_out, uint8_t* l_proof,
+                          const uint8_t* body_hash_in) {
   hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, nkes, first_slot, slot_stride,
                      slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk,
                      leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
-                     ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, tpraos, l_out, l_proof);
+                     ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, tpraos, l_out, l_proof,
+                     body_hash_in);
 }
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt,
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out,

@@ -497,8 +497,10 @@ int praos_block_batch_run(praos_ctx* c, praos_batch* b, uint64_t slots_per_kes_p
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   HIPCHK(c, hipMemcpyAsync(b->hoff, b->blk_off, 8 * n, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(b->hlen, b->blk_len, 4 * n, hipMemcpyDeviceToDevice, c->stream));
+  (void)hipGetLastError();   // clear a stale error of an earlier, already-reported runtime call
   launch_block_split(g, blk, c->stream, n, b->arena, b->arena_len, b->hoff, b->hlen, b->seg_off, b->seg_len, b->nseg,
                      b->split_status);
+  HIPCHK(c, hipGetLastError());
   const int rd = batch_decode(c, b);
   if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -1021,6 +1023,7 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
   auto dcor = s.zeros<uint8_t>(n);
   auto dlout = s.zeros<uint8_t>(tpraos ? 64 * n : 16);
   auto dlproof = s.zeros<uint8_t>(tpraos ? 80 * n : 16);
+  const uint8_t* dbh = sp->body_hash ? s.up(sp->body_hash, 32 * n) : nullptr;   // caller's hbBodyHash values
   if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
   uint64_t salt = 0;
   std::memcpy(&salt, sp->seed, 8);
@@ -1033,7 +1036,8 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
     launch_synth_headers(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, (uint32_t)np,
                        (uint32_t)nk, sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
-                       dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof);
+                       dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof,
+                       sp->body_len == 0 && !tpraos ? dbh : nullptr);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
                        salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
                        sp->body_len == 0 ? 1 : 0);

@@ -102,7 +102,8 @@ class Counters(ctypes.Structure):
 class SynthParams(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("npools", ctypes.c_uint32), ("first_slot", ctypes.c_uint64),
                 ("slot_stride", ctypes.c_uint64), ("body_len", ctypes.c_uint32),
-                ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32)]
+                ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32),
+                ("body_hash", u8p)]
 
 
 class HeaderBytes(ctypes.Structure):
@@ -549,8 +550,11 @@ class Context:
         return res
 
     def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
-                   body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False):
+                   body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False, body_hash=None):
         sp = SynthParams()
+        if body_hash is not None:   # n*32 hbBodyHash values for the CBOR bodies (body_len=0)
+            body_hash = np.ascontiguousarray(body_hash, dtype=np.uint8).reshape(n, 32)
+            sp.body_hash = ptr(body_hash)
         sp.n = n
         sp.npools = npools
         sp.first_slot = first_slot

@@ -49,3 +49,41 @@ def pack_chunk(H):
     off = (start + HEADER_OFFSET).astype(np.uint64)
     length = (bl + OVERHEAD - len(BLOCK_PREFIX) - len(BLOCK_SUFFIX)).astype(np.uint32)
     return arena, off, length
+
+
+SEG_FIXED = (bytes([0x80]), bytes([0xA0]), bytes([0x80]))   # witnesses [], aux {}, invalid txs []
+
+
+def tx_segment(payload: bytes) -> bytes:
+    """Synthetic tx-bodies segment: [payload] as one byte string (4-byte length head)."""
+    return bytes([0x81, 0x5A]) + len(payload).to_bytes(4, "big") + payload
+
+
+def hash_tx_seq(segments):
+    """hashTxSeq of a segregated-witness TxSeq: Blake2b-256 over the Blake2b-256 of each
+    stored segment (cardano-ledger; pinned against the reference's golden blocks in
+    tests/test_block_oracle.py)."""
+    import hashlib
+
+    def b2b(m):
+        return hashlib.blake2b(m, digest_size=32).digest()
+    return b2b(b"".join(b2b(s) for s in segments))
+
+
+def pack_blocks(H, payloads):
+    """Whole stored Babbage blocks [6, [header, [payload], [], {}, []]] from synthesize()
+    output with CBOR bodies whose hbBodyHash is hash_tx_seq of these segments.
+    Returns (arena u8[], off u64[n], len u32[n]) of the BLOCKS (what
+    praos_verify_block_integrity takes)."""
+    n = len(H["slot"])
+    parts, off, ln, pos = [], np.zeros(n, np.uint64), np.zeros(n, np.uint32), 0
+    body = H["body_bytes"]
+    for i in range(n):
+        bo, bl = int(H["body_off"][i]), int(H["body_len"][i])
+        blk = b"".join([BLOCK_PREFIX, HEADER_PREFIX, body[bo:bo + bl].tobytes(), SIG_HEAD,
+                        H["kes_sig"][i].tobytes(), tx_segment(payloads[i]), *SEG_FIXED])
+        parts.append(blk)
+        off[i] = pos
+        ln[i] = len(blk)
+        pos += len(blk)
+    return np.frombuffer(b"".join(parts), np.uint8), off, ln

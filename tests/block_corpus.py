@@ -46,9 +46,14 @@ def rand_item(r, depth=0):
     return H(4, n) + b"".join(rand_item(r, depth + 1) for _ in range(n))
 
 
-def rand_segments(r, big=False):
-    """[tx bodies, witnesses, auxiliary data, invalid txs] (Alonzo+ TxSeq)."""
+def rand_segments(r, big=False, pad=0):
+    """[tx bodies, witnesses, auxiliary data, invalid txs] (Alonzo+ TxSeq); pad > 0 adds one
+    tx body carrying a pad-byte string (mainnet-sized blocks for the bench)."""
     ntx = r.randrange(8 if not big else 60)
+    if pad:
+        return [H(4, ntx + 1) + H(5, 1) + H(0, 0) + H(2, pad) + rbytes(r, pad) + b"".join(
+                    H(5, 1) + H(0, 0) + rand_item(r) for _ in range(ntx)),
+                H(4, 1) + H(2, 100) + rbytes(r, 100), H(5, 0), H(4, 0)]
     bodies = H(4, ntx) + b"".join(H(5, 2) + H(0, 0) + rand_item(r) + H(0, 2) + H(0, r.getrandbits(20))
                                   for _ in range(ntx))
     wits = H(4, ntx) + b"".join(rand_item(r) for _ in range(ntx))
@@ -57,9 +62,9 @@ def rand_segments(r, big=False):
     return [bodies, wits, aux, inval]
 
 
-def make_block(r, spkp, era=6, slot=None, c0=None, big=False, wrapped=True):
+def make_block(r, spkp, era=6, slot=None, c0=None, big=False, wrapped=True, pad=0):
     """-> (block bytes, header fields, KES seed)."""
-    segs = rand_segments(r, big)
+    segs = rand_segments(r, big, pad)
     bh = bi._b2b(b"".join(bi._b2b(s) for s in segs))
     seed = rbytes(r, 32)
     slot = r.getrandbits(24) if slot is None else slot
