@@ -8,9 +8,10 @@
 //                   (eraTag 6/7) or a bare [header, s1..s3|s4]; every segment must be one
 //                   well-formed CBOR item.  Emits the header span (k_decode's input) and
 //                   the segment spans, segment-major ([k][i]).
-//   k_seg_hash      one lane per (segment k, block i), segment-major so a wave hashes the
-//                   same segment kind of 64 neighbouring blocks (similar lengths, little
-//                   divergence): Blake2b-256 of the stored segment bytes.
+//   k_seg_hash      one lane per (segment k, block i), segment-major so a workgroup hashes
+//                   the same segment kind of 256 neighbouring blocks (similar lengths):
+//                   Blake2b-256 of the stored segment bytes, message blocks staged through
+//                   LDS by coalesced cooperative loads.
 //   k_block_join    one lane per block: hashTxSeq = Blake2b-256 of the concatenated segment
 //                   hashes (one 96/128-byte compression), compared with hbBodyHash
 //                   (blockMatchesHeader, Shelley/Ledger/Block.hs:150-158); folds the KES
@@ -158,17 +159,81 @@ __global__ void __launch_bounds__(NT) k_block_split(size_t n, const uint8_t* __r
   status[i] = 0;
 }
 
+// Segment hashes with the message blocks staged through LDS: a lane streaming
+// its own segment with per-lane 8-byte loads touches 64 different cache lines
+// per instruction and the L1 thrashes (each 128-byte line is re-fetched from L2
+// for every word).  Here the workgroup loads the next 128-byte block of all 256
+// segments cooperatively -- 8 lanes x 16 bytes per block, whole lines per
+// instruction -- into LDS (stride 17 words: 2-way bank conflicts at most), and
+// each lane compresses its own block from LDS.  The loop runs to the
+// workgroup's longest segment; segment-major order keeps neighbours similar.
+constexpr uint32_t SEG_STRIDE = 17;   // u64 words per staged block (16 + 1 pad)
+
 __global__ void __launch_bounds__(NT) k_seg_hash(size_t n, const uint8_t* __restrict__ arena,
                                                  const uint64_t* __restrict__ seg_off,
                                                  const uint32_t* __restrict__ seg_len, const uint8_t* __restrict__ nseg,
                                                  uint8_t* __restrict__ seg_hash) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 4 * n) return;
-  const size_t k = j / n, i = j - k * n;
-  if (k >= nseg[i]) return;
-  uint32_t h[8];
-  b2b256_range(h, arena, seg_off[j], seg_len[j]);
-  store_words(seg_hash + 32 * j, h, 8);
+  __shared__ uint64_t sm[NT * SEG_STRIDE];
+  __shared__ uint64_t s_pos[NT];
+  __shared__ uint32_t s_len[NT];
+  __shared__ uint32_t s_max;
+  const uint32_t t = threadIdx.x;
+  const size_t j = (size_t)blockIdx.x * NT + t;
+  bool act = false;
+  uint64_t pos = 0;
+  uint32_t len = 0;
+  if (j < 4 * n) {
+    const size_t k = j / n, i = j - k * n;
+    if (k < nseg[i]) { act = true; pos = seg_off[j]; len = seg_len[j]; }
+  }
+  const uint32_t nblk = act ? (len == 0 ? 1u : (len + 127u) / 128u) : 0u;
+  s_pos[t] = pos;
+  s_len[t] = len;
+  if (t == 0) s_max = 0;
+  __syncthreads();
+  if (nblk) atomicMax(&s_max, nblk);
+  __syncthreads();
+  const uint32_t nb = s_max;
+  uint64_t h[8];
+#pragma unroll
+  for (int w = 0; w < 8; w++) h[w] = B2B_IV[w];
+  h[0] ^= 0x01010000ULL ^ 32u;
+  for (uint32_t b = 0; b < nb; b++) {
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) {
+      const uint32_t c = r * NT + t, owner = c >> 3, part = c & 7u;
+      const uint32_t olen = s_len[owner];
+      const uint64_t o = (uint64_t)b * 128 + 16 * part;
+      uint64_t w0 = 0, w1 = 0;
+      if (o < olen) {
+        const uint64_t opos = s_pos[owner];
+        w0 = ld64u(arena, opos + o);
+        if (o + 8 < olen) w1 = ld64u(arena, opos + o + 8);
+      }
+      sm[owner * SEG_STRIDE + 2 * part] = w0;
+      sm[owner * SEG_STRIDE + 2 * part + 1] = w1;
+    }
+    __syncthreads();
+    if (b < nblk) {
+      uint64_t m[16];
+      const uint64_t base = (uint64_t)b * 128;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const uint64_t o = base + 8 * k;
+        uint64_t w = o < len ? sm[t * SEG_STRIDE + k] : 0;
+        if (o < len && len - o < 8) w &= (1ull << (8 * (len - o))) - 1;
+        m[k] = w;
+      }
+      const bool last = b + 1 == nblk;
+      b2b_compress(h, m, last ? (uint64_t)len : base + 128, last);
+    }
+    __syncthreads();
+  }
+  if (!act) return;
+  uint32_t out[8];
+#pragma unroll
+  for (int w = 0; w < 4; w++) { out[2 * w] = (uint32_t)h[w]; out[2 * w + 1] = (uint32_t)(h[w] >> 32); }
+  store_words(seg_hash + 32 * j, out, 8);
 }
 
 __global__ void __launch_bounds__(NT) k_block_join(size_t n, const uint8_t* __restrict__ nseg,

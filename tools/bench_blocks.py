@@ -31,7 +31,7 @@ SPKP = 129600
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--blocks", type=int, default=65536)
+    ap.add_argument("--blocks", type=int, default=262144)
     ap.add_argument("--payload", type=int, default=16384, help="tx-segment payload bytes per block")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
