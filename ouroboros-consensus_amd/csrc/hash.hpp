@@ -11,7 +11,16 @@
 
 #define H_INLINE __device__ __forceinline__
 
-H_INLINE uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate right by a constant as two v_alignbit_b32 (funnel shifts of the
+// 32-bit halves) instead of two 64-bit shifts + two ORs; n = 32 is a half swap.
+H_INLINE uint64_t ror64(uint64_t x, int n) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n == 32) return ((uint64_t)lo << 32) | hi;
+  if (n < 32)
+    return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+  const int m = n - 32;
+  return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, m) << 32) | __builtin_amdgcn_alignbit(lo, hi, m);
+}
 H_INLINE uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
 __device__ __constant__ static const uint64_t SHA512_K[80] = {
