@@ -208,7 +208,8 @@ typedef struct {
 #define PRAOS_DEC_UNSUPPORTED  0x08u /* indefinite-length item or tag (never emitted by the reference) */
 #define PRAOS_DEC_TRAILING     0x10u /* bytes after the header item within len */
 #define PRAOS_DEC_NONCANONICAL 0x20u /* informational: stored body not canonical; signed bytes re-encoded */
-#define PRAOS_DEC_OVERFLOW     0x40u /* integer out of range (bodySize > Word32) */
+#define PRAOS_DEC_OVERFLOW     0x40u /* integer out of range (bodySize > Word32, ProtVer major > maxVersion) */
+#define PRAOS_MAX_PROT_MAJOR   9     /* cardano-ledger-binary maxVersion at the reference's CHaP index-state */
 #define PRAOS_DEC_FAILED       0x5Fu /* mask of the failure bits */
 #define PRAOS_SIGNED_STRIDE    448   /* bytes per header in praos_decoded.signed_body */
 

@@ -34,6 +34,9 @@ DEC_UNSUPPORTED = 0x08
 DEC_TRAILING = 0x10
 DEC_NONCANONICAL = 0x20
 DEC_OVERFLOW = 0x40
+# DecCBOR Version (cardano-ledger-binary, not vendored) rejects a ProtVer major above
+# maxVersion; 9 (Conway) at the CHaP index-state of the reference -- parity unpinned.
+MAX_PROT_MAJOR = 9
 DEC_FAIL = 0x5F               # every bit but NONCANONICAL
 
 SIGNED_STRIDE = 448           # max canonical body = 447 bytes
@@ -173,7 +176,7 @@ def decode_header(arena, off, length):
         f["c0"] = r.uint()
         f["ocert_sig"] = r.bytes_fixed(64)
         r.array(2)
-        f["prot_major"] = r.uint()
+        f["prot_major"] = r.uint(MAX_PROT_MAJOR)
         f["prot_minor"] = r.uint()
         canon = r.canon
         body_end = r.pos

@@ -75,11 +75,20 @@ def apply_batch(hk, bits, ocert_n, known, counters):
     return out, (len(bits) if stop is None else stop), cm
 
 
+def _copy(st):
+    return {k: (dict(v) if isinstance(v, dict) else v) for k, v in st.items()}
+
+
 def fold(st, hk, slots, bits, ocert_n, nonces, prev_hash, known, eta0, base_slot, base_no, length, window):
     """st: dict(last_slot (None = Origin), counters, evolving, candidate, epoch_nonce, lab, leb).
-    Returns (verdicts, chain_stop, processed); st is updated in place."""
+    Returns (verdicts, chain_stop, processed).  st is updated in place to the state the
+    reference chain reaches: after the last valid header before the first invalid one
+    (the reference stops the chain there).  Verdicts of later headers are would-be
+    verdicts, judged against a working copy that skips the invalid headers."""
     def epoch(s):
         return base_no + (s - base_slot) // length
+    w = _copy(st)
+    frozen = None
     out, stop = [], None
     i = 0
     for i in range(len(slots) + 1):
@@ -87,25 +96,28 @@ def fold(st, hk, slots, bits, ocert_n, nonces, prev_hash, known, eta0, base_slot
             break
         s = int(slots[i])
         e_new = epoch(s)
-        e_old = 0 if st["last_slot"] is None else epoch(st["last_slot"])
-        t_epoch, t_leb = st["epoch_nonce"], st["leb"]
+        e_old = 0 if w["last_slot"] is None else epoch(w["last_slot"])
+        t_epoch, t_leb = w["epoch_nonce"], w["leb"]
         if e_new > e_old:
-            t_epoch, t_leb = combine(st["candidate"], st["leb"]), st["lab"]
+            t_epoch, t_leb = combine(w["candidate"], w["leb"]), w["lab"]
         if t_epoch != eta0:
             break
-        m = st["counters"].get(hk[i], 0 if hk[i] in known else None)
+        m = w["counters"].get(hk[i], 0 if hk[i] in known else None)
         v = verdict(int(bits[i]), m, int(ocert_n[i]))
         out.append(v)
         if v != V_OK:
             if stop is None:
                 stop = i
+                frozen = _copy(w)
             continue
-        st["epoch_nonce"], st["leb"] = t_epoch, t_leb
-        st["last_slot"] = s
-        st["lab"] = prev_hash[i]
-        st["evolving"] = combine(st["evolving"], bytes(nonces[i]))
+        w["epoch_nonce"], w["leb"] = t_epoch, t_leb
+        w["last_slot"] = s
+        w["lab"] = prev_hash[i]
+        w["evolving"] = combine(w["evolving"], bytes(nonces[i]))
         if s + window < base_slot + (e_new - base_no + 1) * length:
-            st["candidate"] = st["evolving"]
-        st["counters"][hk[i]] = int(ocert_n[i])
+            w["candidate"] = w["evolving"]
+        w["counters"][hk[i]] = int(ocert_n[i])
     processed = i
+    st.clear()
+    st.update(frozen if frozen is not None else w)
     return out, min(len(slots) if stop is None else stop, processed), processed

@@ -91,7 +91,10 @@ inline void ceil_div_256_128(uint8_t q_le[16], const u256& x, unsigned __int128 
   std::memcpy(q_le, q.w, 16);
 }
 
-// x_raw = -floor(sigma_fp * c_raw / R) = ceil(sigma_fp * |c| / R) for c_raw <= 0
+// x_raw = -floor(sigma_fp * c_raw / R) = ceil(sigma_fp * |c| / R) for c_raw <= 0.
+// Rejected above X_MAX = 16 R: the device Taylor loop (leader.hpp) keeps err * x in
+// 256 bits, and err_n <= R e^X, so err * x <= R^2 X e^X < 2^226 * 2^28 for X <= 16
+// (sigma |ln(1-f)| <= 16 covers every f <= 1 - e^-16).
 inline bool leader_x_raw(uint8_t x_le[16], const uint8_t sigma_fp[16], const uint8_t c_raw[16]) {
   unsigned __int128 c;
   std::memcpy(&c, c_raw, 16);
@@ -108,7 +111,10 @@ inline bool leader_x_raw(uint8_t x_le[16], const uint8_t sigma_fp[16], const uin
   for (int i = 0; i < 34; i++) R *= 10;
   bool of = false;
   ceil_div_256_128(x_le, p, R, &of);
-  return !of;
+  if (of) return false;
+  unsigned __int128 x;
+  std::memcpy(&x, x_le, 16);
+  return x <= 16 * R;
 }
 
 }  // namespace praos_host

@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
   const uint64_t occ0 = rd_uint(r, ~0ull);
   rd_bytes<64>(r, o.ocert_sig + 64 * i);
   rd_array(r, 2);
-  const uint64_t pmaj = rd_uint(r, ~0ull);
+  const uint64_t pmaj = rd_uint(r, PRAOS_MAX_PROT_MAJOR);   // DecCBOR Version: <= maxVersion
   const uint64_t pmin = rd_uint(r, ~0ull);
   const bool canon = r.canon;
   const uint64_t body_end = r.pos;

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restri
                                                int f_is_one, int leader_words, const uint16_t* __restrict__ b_ocert,
                                                const uint16_t* __restrict__ b_kes, const uint16_t* __restrict__ b_vrf,
                                                uint16_t* __restrict__ bits, uint8_t* __restrict__ is_leader,
-                                               int32_t* __restrict__ iters) {
+                                               int32_t* __restrict__ iters, const uint16_t* __restrict__ dec_status) {
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
   uint32_t x[4];
@@ -62,6 +62,8 @@ __global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restri
     for (int k = 0; k < 4; k++) x[k] = x_item[4 * i + k];
   } else {
     b = b_ocert[i] | b_kes[i] | b_vrf[i];      // the three crypto kernels' bits
+    // a stored header that did not decode is malformed input whatever kernels ran
+    if (dec_status && (dec_status[i] & PRAOS_DEC_FAILED)) b |= PRAOS_BIT_INPUT;
     const int32_t s = pool_sorted_idx[i];
     skip = s < 0;                              // VRFKeyUnknown precedes the leader check
 #pragma unroll
@@ -214,8 +216,8 @@ void launch_debug_h2c(dim3 grid, dim3 block, hipStream_t stream, size_t n, const
 void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in,
                    const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one,
                    int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits,
-                   uint8_t* is_leader, int32_t* iters) {
+                   uint8_t* is_leader, int32_t* iters, const uint16_t* dec_status) {
   hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one,
                      leader_words, b_ocert,
-                     b_kes, b_vrf, bits, is_leader, iters);
+                     b_kes, b_vrf, bits, is_leader, iters, dec_status);
 }

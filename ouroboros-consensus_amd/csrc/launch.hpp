@@ -41,7 +41,7 @@ void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, 
                            uint32_t* kinfo);
 void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result);
 void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab);
-void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in, const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one, int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits, uint8_t* is_leader, int32_t* iters);
+void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in, const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one, int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits, uint8_t* is_leader, int32_t* iters, const uint16_t* dec_status);
 void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);
 void launch_debug_sha512(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* prefix, const uint64_t* off, const uint32_t* len, const uint8_t* msg, uint8_t* out);
 void launch_debug_blake2b(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* in, uint8_t* out);

@@ -167,17 +167,9 @@ void praos_close(praos_ctx* c) {
 int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
                     const praos_params* params) {
   if (!c || !params || (npools && !pools) || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
-  if (c->device >= 0) {
-    HIPCHK(c, hipSetDevice(c->device));
-    free_epoch(c);
-  }
-  c->params = *params;
-  c->eta0_neutral = eta0 == nullptr;
-  std::memset(c->eta0, 0, 32);
-  if (eta0) std::memcpy(c->eta0, eta0, 32);
-  c->npools = npools;
-  c->pools.assign(pools, pools + npools);
-  c->pool_by_hash.clear();
+  // Validate and build every table into locals first; the context is only
+  // touched once all of it succeeded (a failed call leaves NO epoch: runs
+  // return PRAOS_E_STATE until the next successful praos_set_epoch).
   std::vector<int32_t> order(npools);
   for (uint32_t i = 0; i < npools; i++) order[i] = (int32_t)i;
   std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
@@ -185,32 +177,57 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
   });
   std::vector<uint32_t> h(7 * (size_t)std::max(1u, npools)), v(8 * (size_t)std::max(1u, npools)),
       x(4 * (size_t)std::max(1u, npools));
+  std::map<std::string, int32_t> by_hash;
+  bool bad = false;
   for (uint32_t s = 0; s < npools; s++) {
     const praos_pool& p = pools[order[s]];
     std::memcpy(&h[7 * s], p.hash28, 28);
     std::memcpy(&v[8 * s], p.vrf_hash32, 32);
     uint8_t xr[16];
-    if (!praos_host::leader_x_raw(xr, p.sigma_fp, params->c_raw)) {
-      c->err = "sigma * activeSlotLog out of range";
-      return PRAOS_E_ARG;
-    }
+    if (!praos_host::leader_x_raw(xr, p.sigma_fp, params->c_raw)) bad = true;
     std::memcpy(&x[4 * s], xr, 16);
-    c->pool_by_hash[std::string((const char*)p.hash28, 28)] = order[s];
+    by_hash[std::string((const char*)p.hash28, 28)] = order[s];
   }
-  if (c->device < 0) {          // host-only context: the sequential part needs no tables
-    c->have_epoch = true;
-    return PRAOS_OK;
+  if (c->device >= 0) {
+    HIPCHK(c, hipSetDevice(c->device));
+    (void)hipStreamSynchronize(c->stream);      // no run in flight reads the old tables
+    free_epoch(c);
   }
-  HIPCHK(c, hipMalloc(&c->d_pool_hash, h.size() * 4));
-  HIPCHK(c, hipMalloc(&c->d_pool_vrf, v.size() * 4));
-  HIPCHK(c, hipMalloc(&c->d_pool_x, x.size() * 4));
-  HIPCHK(c, hipMalloc(&c->d_pool_map, std::max<size_t>(1, npools) * 4));
-  HIPCHK(c, hipMalloc(&c->d_eta0, 32));
-  HIPCHK(c, hipMemcpy(c->d_pool_hash, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_pool_vrf, v.data(), v.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_pool_x, x.data(), x.size() * 4, hipMemcpyHostToDevice));
-  if (npools) HIPCHK(c, hipMemcpy(c->d_pool_map, order.data(), npools * 4, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(c->d_eta0, c->eta0, 32, hipMemcpyHostToDevice));
+  c->have_epoch = false;
+  c->npools = 0;
+  c->pools.clear();
+  c->pool_by_hash.clear();
+  if (bad) {
+    c->err = "sigma * activeSlotLog out of range (x_raw > 16 * 10^34)";
+    return PRAOS_E_ARG;
+  }
+  if (c->device >= 0) {
+    uint32_t *dh = nullptr, *dv = nullptr, *dx = nullptr, *de = nullptr;
+    int32_t* dm = nullptr;
+    bool ok = hipMalloc(&dh, h.size() * 4) == hipSuccess && hipMalloc(&dv, v.size() * 4) == hipSuccess &&
+              hipMalloc(&dx, x.size() * 4) == hipSuccess &&
+              hipMalloc(&dm, std::max<size_t>(1, npools) * 4) == hipSuccess && hipMalloc(&de, 32) == hipSuccess;
+    uint32_t e0[8] = {0};
+    if (eta0) std::memcpy(e0, eta0, 32);
+    ok = ok && hipMemcpy(dh, h.data(), h.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(dv, v.data(), v.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(dx, x.data(), x.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         (!npools || hipMemcpy(dm, order.data(), npools * 4, hipMemcpyHostToDevice) == hipSuccess) &&
+         hipMemcpy(de, e0, 32, hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {
+      (void)hipFree(dh); (void)hipFree(dv); (void)hipFree(dx); (void)hipFree(dm); (void)hipFree(de);
+      c->err = "praos_set_epoch: device allocation / copy failed";
+      return PRAOS_E_OOM;
+    }
+    c->d_pool_hash = dh; c->d_pool_vrf = dv; c->d_pool_x = dx; c->d_pool_map = dm; c->d_eta0 = de;
+  }
+  c->params = *params;
+  c->eta0_neutral = eta0 == nullptr;
+  std::memset(c->eta0, 0, 32);
+  if (eta0) std::memcpy(c->eta0, eta0, 32);
+  c->npools = npools;
+  c->pools.assign(pools, pools + npools);
+  c->pool_by_hash.swap(by_hash);
   c->have_epoch = true;
   return PRAOS_OK;
 }
@@ -455,7 +472,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
   launch_leader(g, blk, c->stream, n, b->leader, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
-                (int)P.f_is_one, 8, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr);
+                (int)P.f_is_one, 8, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
+                b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   HIPCHK(c, hipGetLastError());
   return PRAOS_OK;
@@ -817,7 +835,7 @@ int praos_check_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr,
                 (const uint32_t*)nullptr, dx, (int)params->f_is_one, 8, (const uint16_t*)nullptr,
-                (const uint16_t*)nullptr, (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, (int32_t*)nullptr);
+                (const uint16_t*)nullptr, (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, (int32_t*)nullptr, (const uint16_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -922,8 +940,30 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
     *ok = s >= ei->epoch_base_slot;
     return ei->epoch_base_no + (*ok ? (s - ei->epoch_base_slot) / ei->epoch_length : 0);
   };
-  std::map<std::string, size_t> where;
-  for (size_t k = 0; k < st->m; k++) where[std::string((const char*)st->counter_hash28 + 28 * k, 28)] = k;
+  // Working state W (the fold) and the returned state: the reference stops the
+  // chain at the first invalid header, so *st is the state after the last valid
+  // header before chain_stop.  Later headers keep being judged (would-be
+  // verdicts) against W, which carries on as if the failing header were absent.
+  struct Work {
+    int32_t origin;
+    uint64_t last_slot;
+    std::vector<std::string> keys;
+    std::vector<uint64_t> ctr;
+    std::map<std::string, size_t> where;
+    praos_nonce evolving, candidate, epoch_nonce, lab, leb;
+  };
+  Work W;
+  W.origin = st->last_slot_origin;
+  W.last_slot = st->last_slot;
+  for (size_t k = 0; k < st->m; k++) {
+    W.keys.emplace_back((const char*)st->counter_hash28 + 28 * k, 28);
+    W.ctr.push_back(st->counter[k]);
+    W.where[W.keys.back()] = k;
+  }
+  W.evolving = st->evolving; W.candidate = st->candidate; W.epoch_nonce = st->epoch_nonce;
+  W.lab = st->lab; W.leb = st->last_epoch_block;
+  bool frozen = false;
+  Work F;                                            // state at the chain stop
   size_t stop = h->n, i = 0;
   for (; i < h->n; i++) {
     const uint64_t slot = h->slot[i];
@@ -931,46 +971,56 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
     const uint64_t e_new = epoch_of(slot, &ok);
     if (!ok) { c->err = "slot before the epoch base"; return PRAOS_E_ARG; }
     // tickChainDepState (Praos.hs:407-431) with isNewEpoch (Ledger/Util.hs:27-40)
-    const uint64_t e_old = st->last_slot_origin ? 0 : epoch_of(st->last_slot, &ok);
-    praos_nonce tick_epoch = st->epoch_nonce, tick_leb = st->last_epoch_block;
+    const uint64_t e_old = W.origin ? 0 : epoch_of(W.last_slot, &ok);
+    praos_nonce tick_epoch = W.epoch_nonce, tick_leb = W.leb;
     if (e_new > e_old) {
-      tick_epoch = nonce_combine(st->candidate, st->last_epoch_block);
-      tick_leb = st->lab;
+      tick_epoch = nonce_combine(W.candidate, W.leb);
+      tick_leb = W.lab;
     }
     if (!nonce_eq(tick_epoch, eta0)) break;        // crypto outputs were computed for another epoch nonce
     const std::string hk = issuer_hash(c, h, crypto, i);
     const uint64_t n = h->ocert_n[i];
-    auto it = where.find(hk);
-    const bool have = it != where.end() || c->pool_by_hash.count(hk);
-    const uint8_t v = header_verdict(crypto->bits[i], have, it != where.end() ? st->counter[it->second] : 0, n);
+    auto it = W.where.find(hk);
+    const bool have = it != W.where.end() || c->pool_by_hash.count(hk);
+    const uint8_t v = header_verdict(crypto->bits[i], have, it != W.where.end() ? W.ctr[it->second] : 0, n);
     verdict[i] = v;
     if (v != PRAOS_V_OK) {
-      if (stop == h->n) stop = i;
+      if (!frozen) { F = W; frozen = true; stop = i; }
       continue;
     }
     // reupdateChainDepState (Praos.hs:468-502)
-    st->epoch_nonce = tick_epoch;
-    st->last_epoch_block = tick_leb;
-    st->last_slot_origin = 0;
-    st->last_slot = slot;
-    st->lab.neutral = prev_is_genesis && prev_is_genesis[i];
-    std::memset(st->lab.hash, 0, 32);
-    if (!st->lab.neutral) std::memcpy(st->lab.hash, prev_hash + 32 * i, 32);
+    W.epoch_nonce = tick_epoch;
+    W.leb = tick_leb;
+    W.origin = 0;
+    W.last_slot = slot;
+    W.lab.neutral = prev_is_genesis && prev_is_genesis[i];
+    std::memset(W.lab.hash, 0, 32);
+    if (!W.lab.neutral) std::memcpy(W.lab.hash, prev_hash + 32 * i, 32);
     praos_nonce eta{};
     std::memcpy(eta.hash, crypto->nonce + 32 * i, 32);
     eta.neutral = 0;
-    st->evolving = nonce_combine(st->evolving, eta);
+    W.evolving = nonce_combine(W.evolving, eta);
     const uint64_t first_next = ei->epoch_base_slot + (e_new - ei->epoch_base_no + 1) * ei->epoch_length;
-    if (slot + ei->stability_window < first_next) st->candidate = st->evolving;
-    if (it != where.end()) {
-      st->counter[it->second] = n;
+    if (slot + ei->stability_window < first_next) W.candidate = W.evolving;
+    if (it != W.where.end()) {
+      W.ctr[it->second] = n;
     } else {
-      if (st->m >= st->cap) { c->err = "counter map capacity exceeded"; return PRAOS_E_ARG; }
-      std::memcpy(st->counter_hash28 + 28 * st->m, hk.data(), 28);
-      st->counter[st->m] = n;
-      where[hk] = st->m++;
+      W.where[hk] = W.keys.size();
+      W.keys.push_back(hk);
+      W.ctr.push_back(n);
     }
   }
+  const Work& R = frozen ? F : W;
+  if (R.keys.size() > st->cap) { c->err = "counter map capacity exceeded"; return PRAOS_E_ARG; }
+  st->last_slot_origin = R.origin;
+  st->last_slot = R.last_slot;
+  for (size_t k = 0; k < R.keys.size(); k++) {
+    std::memcpy(st->counter_hash28 + 28 * k, R.keys[k].data(), 28);
+    st->counter[k] = R.ctr[k];
+  }
+  st->m = R.keys.size();
+  st->evolving = R.evolving; st->candidate = R.candidate; st->epoch_nonce = R.epoch_nonce;
+  st->lab = R.lab; st->last_epoch_block = R.leb;
   if (chain_stop) *chain_stop = std::min(stop, i);
   if (processed) *processed = i;
   return PRAOS_OK;
@@ -1124,7 +1174,8 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
                   b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
                   (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce);
     launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
-                  (int)P.f_is_one, 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr);
+                  (int)P.f_is_one, 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
+                  (const uint16_t*)nullptr);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(out->bits, b->bits, 2 * n, hipMemcpyDeviceToHost));
@@ -1250,7 +1301,7 @@ int praos_debug_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   if (!s.ok) return PRAOS_E_OOM;
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr, (const uint32_t*)nullptr,
                 (const uint32_t*)dx, 0, 8, (const uint16_t*)nullptr, (const uint16_t*)nullptr,
-                (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, dit);
+                (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, dit, (const uint16_t*)nullptr);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(is_leader, dres, n, hipMemcpyDeviceToHost));

@@ -5,7 +5,7 @@ field dict, so the expected decode result is the oracle's decode of the same
 bytes.  Variants cover the decoder's edge cases: non-canonical heads (the
 signed bytes must then be RE-encoded, Header.hs:90-94), GenesisHash prev,
 truncation, trailing bytes, wrong fixed sizes, indefinite lengths, tags,
-Word32 overflow of bodySize, wrong major types and out-of-range slices."""
+Word32 overflow of bodySize, ProtVer major above maxVersion, wrong major types and out-of-range slices."""
 import cbor_header as ch
 from helpers import rbytes
 
@@ -33,6 +33,7 @@ def variants(f, kes_sig, k):
         ("neg_slot", lambda: _neg_slot(f, kes_sig)),
         ("body_len_11", lambda: h[:1] + b"\x8b" + h[2:]),
         ("empty", lambda: b""),
+        ("prot_major_over", lambda: ch.encode_header(dict(g, prot_major=ch.MAX_PROT_MAJOR + 1), kes_sig)),
     ]
     name, mk = kinds[k % len(kinds)]
     return mk(), name
@@ -54,7 +55,7 @@ def _neg_slot(f, kes_sig):
     return ch._head(4, 2) + body + ch._head(2, 448) + kes_sig
 
 
-N_KINDS = 17
+N_KINDS = 18
 
 
 def random_fields(r):
@@ -62,4 +63,4 @@ def random_fields(r):
             "prev_hash": rbytes(r, 32), "cold_vk": rbytes(r, 32), "vrf_vk": rbytes(r, 32), "vrf_out": rbytes(r, 64),
             "vrf_proof": rbytes(r, 80), "body_size": r.getrandbits(r.choice([4, 12, 32])), "body_hash": rbytes(r, 32),
             "hot_vk": rbytes(r, 32), "n": r.getrandbits(r.choice([1, 8, 33])), "c0": r.getrandbits(r.choice([2, 9])),
-            "ocert_sig": rbytes(r, 64), "prot_major": r.choice([7, 8, 9, 10, 300]), "prot_minor": r.getrandbits(3)}
+            "ocert_sig": rbytes(r, 64), "prot_major": r.choice([6, 7, 8, 9]), "prot_minor": r.getrandbits(3)}

@@ -69,14 +69,58 @@ def test_apply_batch_host_only(hctx):
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
+def test_chain_dep_state_stops_at_first_invalid(hctx, seed):
+    """A batch with invalid headers: the returned state is the state after the last
+    valid header before the first invalid one (the reference stops the chain there,
+    Praos.hs:441-459 in Except); later headers still get would-be verdicts."""
+    r = random.Random(100 + seed)
+    pools = _pools(r, 6)
+    base, length, window = 3000, 6000, 180
+    H, crypto, prev, hk = _batch(r, 200, pools, base + 40, 7)
+    eta = _b2b(b"epoch-a")
+    st = {"last_slot": None, "counters": {pools[2][0]: 0}, "evolving": _b2b(b"ev"), "candidate": _b2b(b"cand"),
+          "epoch_nonce": eta, "lab": None, "leb": _b2b(b"leb")}
+    ref = {k: (dict(v) if isinstance(v, dict) else v) for k, v in st.items()}
+    hctx.set_epoch(eta, pools, _params())
+    v, stop, done = hctx.update_chain_dep_state(H, crypto, prev, st, (base, 0, length, window))
+    wv, wstop, wdone = cs.fold(ref, hk, H["slot"], crypto["bits"], H["ocert_n"], crypto["nonce"],
+                               [bytes(p) for p in prev], {p[0] for p in pools}, eta, base, 0, length, window)
+    assert (done, stop) == (wdone, wstop) == (200, wstop)
+    assert stop < 200 and list(v) == wv
+    assert st == ref
+    assert st["last_slot"] == (int(H["slot"][stop - 1]) if stop > 0 else None)
+
+
+def test_failed_set_epoch_leaves_no_epoch(hctx):
+    """A praos_set_epoch that fails (here: x_raw out of range) must not leave the previous
+    epoch's tables behind: the next call needing an epoch returns PRAOS_E_STATE."""
+    from praos_hip import abi
+    r = random.Random(11)
+    pools = _pools(r, 3)
+    hctx.set_epoch(_b2b(b"ok"), pools, _params())
+    bad = [(h, v, 1 << 127) for h, v, _ in pools]        # sigma ~ 1.7e4: x_raw > 16 * 10^34
+    with pytest.raises(abi.PraosError):
+        hctx.set_epoch(_b2b(b"bad"), bad, _params())
+    H, crypto, prev, hk = _batch(r, 8, pools, 0, 5)
+    with pytest.raises(abi.PraosError, match="rc=-4"):
+        hctx.apply_batch(H, crypto, {})
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
 def test_chain_dep_state_fold_across_epochs(hctx, seed):
-    """Two epochs of 600 slots, stability window 180: the fold stops at the boundary
-    (the ticked epoch nonce differs from the context's), resumes after set_epoch with
-    the nonce the state computed, and matches the restatement step for step."""
+    """Two epochs of 600 slots, stability window 180, all headers valid: the fold stops
+    at the boundary (the ticked epoch nonce differs from the context's), resumes after
+    set_epoch with the nonce the state computed, and matches the restatement step for step."""
     r = random.Random(seed)
     pools = _pools(r, 6)
     base, length, window = 3000, 600, 180
     H, crypto, prev, hk = _batch(r, 160, pools, base + 40, 7)      # slots 3040 .. ~4160: epochs 0, 1
+    crypto["bits"][:] = 0
+    for i in range(160):                                             # known issuers, valid counters
+        H["ocert_n"][i] = 0
+        if crypto["pool_idx"][i] < 0:
+            crypto["pool_idx"][i] = 0
+            hk[i] = pools[0][0]
     genesis = np.zeros(160, np.uint8)
     genesis[0] = 1
     eta_a = _b2b(b"epoch-a")

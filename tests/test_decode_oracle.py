@@ -57,7 +57,7 @@ def test_mutation_corpus_statuses():
     assert seen["short_vrf_vk"] == ch.DEC_SIZE and seen["long_proof"] == ch.DEC_SIZE
     assert seen["short_kes"] == ch.DEC_SIZE
     assert seen["indef_body"] == ch.DEC_UNSUPPORTED and seen["tag_slot"] == ch.DEC_UNSUPPORTED
-    assert seen["body_size_overflow"] == ch.DEC_OVERFLOW
+    assert seen["body_size_overflow"] == ch.DEC_OVERFLOW and seen["prot_major_over"] == ch.DEC_OVERFLOW
     assert seen["neg_slot"] == ch.DEC_SYNTAX and seen["body_len_11"] == ch.DEC_SYNTAX and seen["empty"] == ch.DEC_SYNTAX
     assert ch.decode_header(b"\x00" * 10, 8, 5)["status"] == ch.DEC_RANGE
 
