@@ -2,34 +2,36 @@
 """bench.py -- Praos header-crypto validation throughput on MI355X.
 
 Metric (BASELINE.json): Praos headers validated/sec (VRF + KES + OCert + leader).
-Default workload (no flags) = configs[4], a mainnet-shaped epoch replay:
-432,000 Praos (Babbage) headers per GPU, 3000-pool stake distribution
-(sigma_i ~ 1/(i+10), exact rationals), one epoch nonce, f = 1/20,
-slotsPerKESPeriod 129600, maxKESEvo 62, 397-byte signed bodies, 1% of headers
-corrupted with the consensus-testlib +1-byte model.  The chain is synthesised
-on the GPU by the library's generator (real Ed25519 / Sum6KES / ECVRF-draft03
-signatures; db-synthesizer analogue) and is resident in HBM before the timed
-region.  One step = one full validation pass (all kernels) over the GPU's
-shard.  Multi-GPU: one process per GPU; each rank owns a contiguous slot range
-of its own 432k headers (weak scaling, no collective on the data path; only
-the timing max-reduce).
+Default workload (no flags) = configs[4], a mainnet-shaped epoch replay: the first
+432,000 blocks of a leader-valid Praos (Babbage) chain -- 3000 pools with stake
+sigma_i ~ 1/(i+10) (exact rationals), f = 1/20, one epoch nonce, slotsPerKESPeriod
+129600, maxKESEvo 62 -- forged first-leader-wins exactly as db-synthesizer does
+(Forging.hs:139-148; schedule shipped in praos_hip/data/c5_schedule.npz, see
+praos_hip/chains.py), with canonical HeaderBody CBOR bodies as KES messages and 1 %
+of the headers corrupted by the consensus-testlib +1-byte model.  The headers are
+signed on the GPU (real Ed25519 / Sum6KES / ECVRF-draft03) and resident in HBM
+before the timed region.  One step = one full validation pass (all kernels) over
+the GPU's shard.  Multi-GPU: one process per GPU, no collective on the data path
+(only the timing max-reduce); weak scaling -- each rank validates a full 432k-block
+shard (the one shipped schedule, so ranks > 0 replay the same blocks).
 
 --config c2|c3|c4 measure the single-primitive configs (1M OCert verifies with
 distinct keys, 1M VRF verifies + leader checks, 1M Sum6KES verifies), c1 the
-10k-header / 100-pool CPU config (GPU and oracle side by side).
+10k-block / 100-pool chain of configs[0] (GPU and CPU side by side).
 
-CPU baseline: the C oracle (oracle/, a port of the reference semantics; the
-Haskell reference cannot run here) timed on the host over a bounded sample of
-the same inputs with a process pool, cores stated; it also cross-checks the
-GPU result on that sample.
+CPU baseline (rank 0, N = 1): the C oracle (oracle/, a restatement of the reference
+semantics; the Haskell reference cannot run here) timed over a bounded sample of
+the same headers on the host cores this job may use, plus a single-core rate and an
+OpenSSL Ed25519 verify rate as an independent third-party point; the same sample
+cross-checks the GPU result bit for bit.
 """
 import argparse
 import json
 import multiprocessing as mp
 import os
+import platform
 import sys
 import time
-from fractions import Fraction
 
 import numpy as np
 
@@ -41,26 +43,27 @@ sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  # noqa: E402
                        W_KEY_COLD, W_KEY_VRF)
-W_HEADER = W_OCERT + W_KES + W_VRF + W_LEADER
-PEAK_INT32 = 256 * 64 * 2.4e9      # VOP3 integer issue: 64 lane-ops/clk/CU (tools/microbench)
+# gfx950 VALU peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
+# cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
+PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
 
 CONFIGS = {
-    "c1": dict(headers=10_000, pools=100, kernels=7, nkes=0, metric="Praos headers validated/sec (CPU config C1)",
-               workload="configs[0]: 10k-header Praos (Babbage) chain, 100 pools (GPU and oracle side by side)"),
-    "c2": dict(headers=1_000_000, pools=None, kernels=1, nkes=64, metric="OCert Ed25519 verifications/sec",
+    "c1": dict(items=10_000, kernels=7, metric="Praos headers validated/sec (CPU config C1)",
+               workload="configs[0]: the first 10,000 blocks of a first-leader-wins Praos (Babbage) chain, "
+                        "100 pools, tools-test genesis (GPU and CPU side by side)"),
+    "c2": dict(items=1_000_000, pools=None, kernels=1, nkes=64, metric="OCert Ed25519 verifications/sec",
                workload="configs[1]: 1M OCert Ed25519 verifications, distinct cold keys, 1% corrupted"),
-    "c3": dict(headers=1_000_000, pools=3000, kernels=4, nkes=0,
-               metric="ECVRF-draft03 verifies + leader checks/sec",
+    "c3": dict(items=1_000_000, pools=3000, kernels=4, nkes=0, metric="ECVRF-draft03 verifies + leader checks/sec",
                workload="configs[2]: 1M ECVRF-ED25519-SHA512-Elligator2 verifies + leader checks, single eta0, "
                         "3000 pools, 1% corrupted"),
-    "c4": dict(headers=1_000_000, pools=3000, kernels=2, nkes=0, metric="Sum6KES verifications/sec",
+    "c4": dict(items=1_000_000, pools=3000, kernels=2, nkes=0, metric="Sum6KES verifications/sec",
                workload="configs[3]: 1M Sum6KES verifies (depth-6 Blake2b-256 Merkle path + Ed25519 leaf), "
                         "397-byte messages, 1% corrupted"),
-    "c5": dict(headers=432_000, pools=3000, kernels=7, nkes=0,
-               metric="Praos headers validated/sec (VRF+KES+OCert+leader)",
-               workload="configs[4]: mainnet-shaped epoch replay, 432k Praos headers per GPU, 3000-pool stake "
-                        "distribution, single eta0, 1% corrupted"),
+    "c5": dict(items=432_000, kernels=7, metric="Praos headers validated/sec (VRF+KES+OCert+leader)",
+               workload="configs[4]: mainnet-shaped epoch replay, the first 432k blocks of a first-leader-wins "
+                        "Praos chain per GPU, 3000-pool stake distribution, single eta0, 1% corrupted"),
 }
 
 
@@ -68,11 +71,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def stake(npools):
-    from praos_hip import fixed
-    w = [Fraction(1, i + 10) for i in range(npools)]
-    tot = sum(w)
-    return [fixed.from_rational(x / tot) for x in w]
+def host_cores():
+    """CPUs this job may use (affinity), the machine's count, and the CPU model."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or 1, model
 
 
 def _hdr_dict(H, i):
@@ -88,10 +101,10 @@ def _oracle_worker(payload):
     """Checks one chunk with the oracle; returns (result bits, busy seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    kind, eta0, c_raw, pools, items = payload
+    kind, eta0, c_raw, spkp, maxevo, pools, items = payload
     out = []
     if kind == "header":
-        ep = oracle.make_epoch(eta0, 129600, 62, c_raw, pools)
+        ep = oracle.make_epoch(eta0, spkp, maxevo, c_raw, pools)
         t0 = time.perf_counter()
         out = [oracle.praos_header(ep, h)["bits"] for h in items]
     elif kind == "ocert":
@@ -102,7 +115,7 @@ def _oracle_worker(payload):
     elif kind == "kes":
         t0 = time.perf_counter()
         for h in items:
-            t = h["slot"] // 129600 - h["c0"]
+            t = h["slot"] // spkp - h["c0"]
             r = oracle.kes_verify(h["hot_vk"], max(t, 0), h["body"], h["kes_sig"])
             out.append({0: 0, 1: 0x0008, 2: 0x0010}[r])
     else:
@@ -110,15 +123,54 @@ def _oracle_worker(payload):
     return out, time.perf_counter() - t0
 
 
-def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, pool_list, seconds, workers, per_item, mask):
+def openssl_ed25519_rate(seconds=2.0):
+    """Ed25519 verifies/s on one core with OpenSSL's libcrypto (third-party point), or None."""
+    import ctypes
+    import ctypes.util
+    name = ctypes.util.find_library("crypto")
+    if not name:
+        return None
+    try:
+        C = ctypes.CDLL(name)
+        C.EVP_PKEY_new_raw_public_key.restype = ctypes.c_void_p
+        C.EVP_PKEY_new_raw_public_key.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+        C.EVP_MD_CTX_new.restype = ctypes.c_void_p
+        C.EVP_DigestVerifyInit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+        C.EVP_DigestVerify.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                       ctypes.c_size_t]
+        C.EVP_MD_CTX_free.argtypes = [ctypes.c_void_p]
+        C.EVP_PKEY_free.argtypes = [ctypes.c_void_p]
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        seed, msg = b"\x07" * 32, b"\x01" * 48
+        pk, sig = oracle.ed25519_pk(seed), oracle.ed25519_sign(seed, msg)
+        key = C.EVP_PKEY_new_raw_public_key(1087, None, pk, 32)          # EVP_PKEY_ED25519
+        n, t0 = 0, time.perf_counter()
+        ok = True
+        while time.perf_counter() - t0 < seconds:
+            for _ in range(100):
+                md = C.EVP_MD_CTX_new()
+                C.EVP_DigestVerifyInit(md, None, None, None, key)
+                ok &= C.EVP_DigestVerify(md, sig, 64, msg, 48) == 1
+                C.EVP_MD_CTX_free(md)
+            n += 100
+        C.EVP_PKEY_free(key)
+        return round(n / (time.perf_counter() - t0), 1) if ok else None
+    except (OSError, AttributeError):
+        return None
+
+
+def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, spkp, maxevo, pool_list, seconds, workers, per_item, mask,
+                 whole=False):
     n_total = len(H["slot"])
-    n_sample = int(min(n_total, max(workers * 8, seconds * workers / per_item)))
+    n_sample = n_total if whole else int(min(n_total, max(workers * 8, seconds * workers / per_item)))
     idx = np.linspace(0, n_total - 1, n_sample).astype(np.int64)
     items = [_hdr_dict(H, i) for i in idx]
     chunks = [items[k::workers] for k in range(workers)]
     t0 = time.perf_counter()
     with mp.get_context("spawn").Pool(workers) as pool:
-        res = pool.map(_oracle_worker, [(kind, eta0, c_raw, pool_list, c) for c in chunks])
+        res = pool.map(_oracle_worker, [(kind, eta0, c_raw, spkp, maxevo, pool_list, c) for c in chunks])
     wall = time.perf_counter() - t0
     busy = max(r[1] for r in res)
     bits = [None] * n_sample
@@ -126,11 +178,60 @@ def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, pool_list, seconds, workers, pe
         for j, v in enumerate(b):
             bits[k + j * workers] = v
     agree = sum(1 for j, i in enumerate(idx) if (int(gpu_bits[i]) & mask) == (bits[j] & mask))
+    # one core: a short run of the same items in this process
+    one = items[: max(8, int(min(len(items), 3.0 / per_item)))]
+    _, t1 = _oracle_worker((kind, eta0, c_raw, spkp, maxevo, pool_list, one))
+    usable, nproc, model = host_cores()
     return {"value": round(n_sample / busy, 1), "unit": "items/s" if kind != "header" else "headers/s",
             "cores": workers, "kind": "port",
             "sample": f"{n_sample} items evenly spaced over the benchmark input, C oracle (oracle/) in "
                       f"{workers} processes; busy {busy:.1f}s, wall {wall:.1f}s",
+            "single_core": round(len(one) / t1, 1), "host": {"cpu_model": model, "nproc": nproc,
+                                                             "usable_cores": usable},
             "parity_sample": {"n": n_sample, "bit_exact": agree}}
+
+
+def load_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (FETCH_SIZE
+    x2 gfx950 read correction + WRITE_SIZE, separate --pmc passes, tools/pmc_traffic.py)."""
+    try:
+        t = json.load(open(TRAFFIC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    k = t.get("kernels", {}).get(kernel)
+    if not k or t.get("workload") != workload:
+        return None, None
+    return k.get("bytes_per_launch"), os.path.relpath(TRAFFIC_FILE, ROOT)
+
+
+def make_input(ctx, args, cfg, rank):
+    """Returns (H, pool_list, corrupted, params, eta0, c_raw, spkp, maxevo)."""
+    from praos_hip import abi, chains, fixed
+    import hashlib
+    if args.config in ("c1", "c5"):
+        ccfg = chains.CONFIGS[args.config]
+        if args.config == "c5":
+            sched = chains.load_schedule("c5")
+        else:
+            sched = chains.search_schedule(ctx, ccfg, ccfg["blocks"])
+        n = args.items or cfg["items"]
+        assert n <= len(sched[0]), "the shipped schedule has fewer blocks"
+        H, pool_list, corrupted, p = chains.make_chain(ctx, ccfg, sched, n=n,
+                                                       corrupt_per_10000=args.corrupt_per_10000)
+        return (H, pool_list, corrupted, p, ccfg["eta0"], fixed.active_slot_log(ccfg["f"]),
+                ccfg["slots_per_kes_period"], ccfg["max_kes_evo"])
+    # single-primitive configs: evenly spaced slots, pools by hash (not a leader-valid chain)
+    n = args.items or cfg["items"]
+    npools = cfg["pools"] or n
+    from fractions import Fraction
+    c_raw = fixed.active_slot_log(Fraction(1, 20))
+    p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw, vrf_check_output=True)
+    eta0 = hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest()
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, (b"\x5a" * 27) + bytes([int(args.config[1])]) +
+                                         rank.to_bytes(4, "little"), first_slot=rank * n * 20, slot_stride=20,
+                                         body_len=397, corrupt_per_10000=args.corrupt_per_10000, nkes=cfg["nkes"])
+    pool_list = [] if cfg["pools"] is None else [(h, v, s) for (h, v), s in zip(pools, chains.stake(npools, 10))]
+    return H, pool_list, corrupted, p, eta0, c_raw, 129600, 62
 
 
 def main():
@@ -139,12 +240,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c5", choices=sorted(CONFIGS))
-    ap.add_argument("--headers", type=int, default=None, help="items per GPU (default: the config's)")
-    ap.add_argument("--pools", type=int, default=None)
+    ap.add_argument("--items", type=int, default=None, help="items per GPU (default: the config's)")
     ap.add_argument("--corrupt-per-10000", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
     ap.add_argument("--keycache", type=int, default=2,
                     help="min uses of a public key for the per-batch key cache (0 = off)")
@@ -163,28 +264,15 @@ def main():
     import torch
 
     import praos_hip
-    from praos_hip import abi, fixed
+    from praos_hip import abi
 
     ctx = praos_hip.Context(local)
-    ctx.set_option(1, args.concurrent)
-    ctx.set_option(2, cfg["kernels"])
+    ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
+    ctx.set_option(abi.OPT_KERNELS, cfg["kernels"])
     ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
-    n = args.headers or cfg["headers"]
-    npools = args.pools or cfg["pools"] or n           # c2: one distinct cold key per item
-    stride = 20                                        # one header per ~1/f slots
-    c_raw = fixed.active_slot_log(Fraction(1, 20))
-    p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw, vrf_check_output=True)
-    import hashlib
-    eta0 = hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest()
     t0 = time.perf_counter()
-    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, (b"\x5a" * 27) + bytes([int(args.config[1])]) +
-                                         rank.to_bytes(4, "little"), first_slot=rank * n * stride,
-                                         slot_stride=stride, body_len=397, corrupt_per_10000=args.corrupt_per_10000,
-                                         nkes=cfg["nkes"])
-    if cfg["pools"] is None:
-        pool_list = []                                 # OCert-only config: no stake distribution needed
-    else:
-        pool_list = [(h, v, s) for (h, v), s in zip(pools, stake(npools))]
+    H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank)
+    n = len(H["slot"])
     ctx.set_epoch(eta0, pool_list, p)
     b = ctx.upload(H)
     log(f"[rank {rank}] {args.config}: synthesised + uploaded {n} items in {time.perf_counter() - t0:.1f}s")
@@ -211,21 +299,32 @@ def main():
         dt = float(t.item())
     # per-kernel durations for the roofline: serial launches (HIP events on the
     # launch stream), untimed, after the timed region
-    ctx.set_option(1, 0)
+    ctx.set_option(abi.OPT_CONCURRENT, 0)
     kser = np.zeros(5)
     for _ in range(3):
         ctx.run(b)
         ctx.sync()
         kser += [ctx.kernel_ms(k) for k in range(5)]
     kser /= 3
-    ctx.set_option(1, args.concurrent)
+    ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
     kst = ctx.batch_stats(b)
     out = ctx.download(b, n)
     ctx.free(b)
+    # end to end through the blocking entry point: host SoA in, H2D, all kernels,
+    # D2H of bits/beta/leader/nonce (never the headline value)
+    e2e = None
+    if not args.no_e2e and rank == 0:
+        ctx.verify_headers(H)                          # warm (allocator)
+        te = time.perf_counter()
+        oe = ctx.verify_headers(H)
+        te = time.perf_counter() - te
+        e2e = {"value": round(n / te, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
+               "ms": round(te * 1e3, 2), "bit_exact_vs_resident": bool((oe["bits"] == out["bits"]).all()),
+               "path": "praos_verify_headers: host SoA -> H2D -> kernels -> D2H (pageable host memory)"}
 
     # self-check on the whole shard: clean items must pass every check that ran
     clean = corrupted == 0
-    crypto_bits = out["bits"] & ~np.uint16(0x1000)
+    crypto_bits = out["bits"] & ~np.uint16(0x1000) if args.config not in ("c1", "c5") else out["bits"]
     clean_ok = int((crypto_bits[clean] == 0).sum())
     corrupt_caught = int((crypto_bits[~clean] != 0).sum())
     # corruptions that land in a field the config does not check cannot be caught
@@ -253,34 +352,44 @@ def main():
     dom_achieved = work[dominant] / (per_kernel[dominant] * 1e-3)
     w_pipe = (sum(work[k] for k in ran) + (n * W_LEADER if "vrf" in ran else 0)) / n
     pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
+    traffic, traffic_src = load_traffic(f"k_{dominant}", cfg["workload"])
     line = {
         "metric": cfg["metric"],
         "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
         "n_gpus": world, "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32 (GF(2^255-19) radix-2^32 limbs; Fixed E34 bignum)", "data": "synthetic",
-        "config": {"workload": cfg["workload"], "items_per_gpu": n, "pools": npools if cfg["pools"] else None,
-                   "active_slot_coeff": "1/20", "body_bytes": 397, "parallelism": f"shard-by-slot-range x{world}"},
+        "dtype": "u32 (GF(2^255-19) radix-2^32 limbs; Fixed E34 bignum)",
+        "data": "synthetic: GPU-signed chain" + (" from the shipped first-leader-wins schedule"
+                                                  if args.config in ("c1", "c5") else ""),
+        "config": {"workload": cfg["workload"], "items_per_gpu": n, "pools": len(pool_list) or None,
+                   "active_slot_coeff": "1/20",
+                   "signed_body": "canonical HeaderBody CBOR" if args.config in ("c1", "c5") else "397 random bytes",
+                   "parallelism": f"shard-by-slot-range x{world}"},
         "roofline": {"bound": "valu-int32", "kernel": f"k_{dominant}",
                      "achieved": round(dom_achieved / 1e12, 3), "peak": round(PEAK_INT32 / 1e12, 2),
-                     "unit": "T int32-ops/s", "frac": round(dom_achieved / PEAK_INT32, 4), "traffic": None,
+                     "unit": "T int32-ops/s", "frac": round(dom_achieved / PEAK_INT32, 4), "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": traffic_src,
                      "work_per_unit": round(wk), "pipeline_achieved": round(pipe_achieved / 1e12, 3),
                      "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": round(w_pipe),
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},
-                     "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent)},
+                     "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent),
+                     "peak_basis": "128 int32 lane-ops/clk/CU x 256 CU x 2.4 GHz (VALU issue, MI355X_MICROARCH.md)"},
         "keycache": dict(kst, min_uses=args.keycache),
         "self_check": {"clean": int(clean.sum()), "clean_ok": clean_ok, "corrupted": int((~clean).sum()),
                        "corrupted_rejected": corrupt_caught, "corrupted_in_checked_fields": int(rel.sum()),
                        "corrupted_in_checked_fields_rejected": corrupt_caught_rel,
                        "leader_pass": int(((out["bits"] & 0x1000) == 0).sum()) if cfg["kernels"] & 4 else None},
     }
+    if e2e:
+        line["e2e"] = e2e
     if world == 1 and not args.no_cpu:
-        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+        usable, _, _ = host_cores()
+        workers = max(1, min(args.cpu_workers, usable))
         kind, per_item, mask = {7: ("header", 1.4e-3, 0x1F1F), 1: ("ocert", 0.3e-3, 0x0004),
                                 2: ("kes", 0.35e-3, 0x0018), 4: ("header", 1.4e-3, 0x1F00)}[cfg["kernels"]]
-        seconds = args.cpu_seconds if args.config != "c1" else 1e9      # c1: the whole chain on CPU
-        line["cpu_baseline"] = cpu_baseline(kind, H, out["bits"], eta0, c_raw, pool_list, seconds, workers,
-                                            per_item, mask)
+        line["cpu_baseline"] = cpu_baseline(kind, H, out["bits"], eta0, c_raw, spkp, maxevo, pool_list,
+                                            args.cpu_seconds, workers, per_item, mask, whole=args.config == "c1")
+        line["cpu_baseline"]["openssl_ed25519_verify_per_s_1core"] = openssl_ed25519_rate()
         line["gpu_vs_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     print(json.dumps(line), flush=True)
     ctx.close()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 4
+#define PRAOS_ABI_VERSION 5
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -385,6 +385,13 @@ typedef struct {
   uint8_t seed[32];
   const uint8_t* body_hash;       /* n*32 hbBodyHash of each CBOR body (e.g. hashTxSeq of the block's
                                      segments, for stored-block corpora); NULL = pseudo-random */
+  /* Leader schedule (from praos_leader_schedule): header i is forged in slot
+   * sched_slot[i] by pool sched_pool[i], blockNo = block_no0 + i.  NULL: slot of
+   * header i = first_slot + i * slot_stride and pools assigned by hash -- such a
+   * chain is NOT leader-valid (most headers fail VRFLeaderValueTooBig). */
+  const uint64_t* sched_slot;
+  const uint32_t* sched_pool;
+  uint64_t block_no0;
 } praos_synth_params;
 
 /* Fills caller buffers (same layout as praos_headers; body_off/body_len/body_bytes
@@ -396,6 +403,19 @@ int praos_synthesize(praos_ctx* ctx, const praos_synth_params* sp, const praos_p
                      uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n,
                      uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off,
                      uint32_t* body_len, uint8_t* body_bytes, uint8_t* corrupted);
+
+/* Leader schedule of the generator's pools (db-synthesizer, Forging.hs:139-148):
+ * the pools derived from `seed` (as praos_synthesize derives them, npools of them,
+ * stake sigma_fp[p], Fixed E34 raw uint128 LE) are the forgers, tried in index
+ * order.  For every slot s in [first_slot, first_slot + nslots): leader[s -
+ * first_slot] = the first pool p for which checkIsLeader holds (Praos.hs:375-397:
+ * meetsLeaderThreshold, :505-526, on evalCertified (mkInputVRF s eta0) under p's
+ * VRF key), or -1 (no block in that slot).  tpraos = 1: the TPraos leader cert
+ * (mkSeed seedL, 64-byte output, bound 2^512).  Cost: one VRF evaluation per
+ * (slot, pool) pair up to the slot's leader, i.e. ~npools per empty slot. */
+int praos_leader_schedule(praos_ctx* ctx, const uint8_t seed[32], uint32_t npools, const uint8_t* sigma_fp,
+                          const praos_params* params, const uint8_t eta0[32], uint64_t first_slot, uint64_t nslots,
+                          int tpraos, int32_t* leader);
 
 /* TPraos variant of the generator: the VRF cert pair uses mkSeed alphas;
  * leader_out/leader_proof receive the leader cert (n*64, n*80). */
@@ -423,6 +443,9 @@ int praos_debug_scalarmult_base(praos_ctx* ctx, size_t n, const uint8_t* s, uint
 /* leader check with explicit x_raw per item (4 words LE); is_leader, iters out */
 int praos_debug_leader(praos_ctx* ctx, size_t n, const uint8_t* leader, const uint8_t* x_raw16, uint8_t* is_leader,
                        int32_t* iters);
+/* the same for the TPraos form: 64-byte big-endian leader values, bound 2^512 */
+int praos_debug_leader512(praos_ctx* ctx, size_t n, const uint8_t* leader64, const uint8_t* x_raw16,
+                          uint8_t* is_leader, int32_t* iters);
 /* Elligator2 hash-to-curve of the VRF suite: h(pk, alpha); out n*32 */
 int praos_debug_hash_to_curve(praos_ctx* ctx, size_t n, const uint8_t* pk, const uint8_t* alpha, uint8_t* out);
 

@@ -271,3 +271,39 @@ def tpraos_header(ep, h: dict) -> dict:
     lib().orc_tpraos_header(ctypes.byref(ep), ctypes.byref(T), ctypes.byref(R))
     return {"bits": R.bits, "pool_idx": R.pool_idx, "beta_eta": bytes(R.beta_eta),
             "beta_leader": bytes(R.beta_leader), "nonce": bytes(R.nonce)}
+
+
+# ---- generator restatement (db-synthesizer first-leader-wins, Forging.hs:139-148) ----
+def mk_input_vrf(slot: int, eta0) -> bytes:
+    """mkInputVRF (Praos/VRF.hs:55-69): Blake2b-256(BE64 slot || eta0), eta0 omitted when Neutral."""
+    return blake2b(slot.to_bytes(8, "big") + (bytes(eta0) if eta0 is not None else b""))
+
+
+def synth_seed(master: bytes, tag: int, i: int) -> bytes:
+    """Key seeds of the GPU generator's pool i: Blake2b-256(tag || master || BE32 i);
+    tag 1 = cold key, 2 = VRF key, 3 = KES key (k_synth.hip derive_seed)."""
+    return blake2b(bytes([tag]) + bytes(master) + i.to_bytes(4, "big"))
+
+
+def is_leader_at(vrf_seed: bytes, slot: int, eta0, sigma_fp: int, c_raw: int, f_is_one=False, tpraos=False):
+    """checkIsLeader (Praos.hs:375-397) of one pool: evalCertified on mkInputVRF, then
+    meetsLeaderThreshold (:505-526) -- or the TPraos leader cert (mkSeed seedL, 2^512)."""
+    if tpraos:
+        beta = vrf_proof_to_hash(vrf_prove(vrf_seed, tpraos_seed(slot, eta0, 1)))
+        return check_leader512(beta, sigma_fp, c_raw, f_is_one)[0]
+    beta = vrf_proof_to_hash(vrf_prove(vrf_seed, mk_input_vrf(slot, eta0)))
+    return check_leader(blake2b(b"L" + beta), sigma_fp, c_raw, f_is_one)[0]
+
+
+def leader_schedule(master: bytes, sigmas, c_raw: int, eta0, slots, f_is_one=False, tpraos=False):
+    """Forger of each slot: the first pool (index order = forger order) that leads, else -1."""
+    seeds = [synth_seed(master, 2, p) for p in range(len(sigmas))]
+    out = []
+    for s in slots:
+        lead = -1
+        for p, sg in enumerate(sigmas):
+            if is_leader_at(seeds[p], int(s), eta0, sg, c_raw, f_is_one, tpraos):
+                lead = p
+                break
+        out.append(lead)
+    return out

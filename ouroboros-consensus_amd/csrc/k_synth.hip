@@ -117,6 +117,76 @@ __global__ void k_synth_kes_tree(uint32_t npools, uint32_t* tree) {
   }
 }
 
+// ------------------------------------------------------------------ leader schedule
+// VRF secret scalar x = (clamped SHA-512(seed))[0..32) mod L per pool (the scalar
+// vrf_prove_core uses), so Gamma = x H and beta = proof_to_hash exactly as the proof.
+__global__ void k_synth_vrf_scalar(uint32_t npools, const uint32_t* __restrict__ vrf_seed, uint32_t* __restrict__ vrf_x) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npools) return;
+  uint32_t seed[8], az[16], x[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) seed[k] = vrf_seed[8 * p + k];
+  ed25519_expand(az, seed);
+  sc_reduce256(x, az);
+#pragma unroll
+  for (int k = 0; k < 8; k++) vrf_x[8 * p + k] = x[k];
+}
+
+// db-synthesizer slot loop (Forging.hs:139-148): per slot, the forgers are tried in
+// order and the first whose checkShouldForge says ShouldForge forges.  Here one
+// lane = one (slot, pool) of the pools [p0, p0 + pn): checkIsLeader (Praos.hs:375-397)
+// = meetsLeaderThreshold (:505-526) on evalCertified (mkInputVRF slot eta0); the
+// minimum leading pool index per slot is kept with a vector atomicMin (first
+// leader wins).  Pools are processed in increasing chunks, so a lane whose slot
+// already has a leader from an earlier chunk returns at once.
+// TPraos (tpraos = 1): the leader cert of the pair, mkSeed seedL, and the raw
+// 64-byte output as the natural (bound 2^512, cardano-protocol-tpraos checkLeaderValue).
+__global__ void __launch_bounds__(NT) k_synth_leader_search(uint64_t first_slot, uint64_t nslots, uint32_t p0,
+                                                            uint32_t pn, const uint32_t* __restrict__ vrf_x,
+                                                            const uint32_t* __restrict__ vrf_pk,
+                                                            const uint32_t* __restrict__ pool_thr,
+                                                            const uint32_t* __restrict__ eta0, int eta0_neutral,
+                                                            int f_is_one, int tpraos, int32_t* __restrict__ leader) {
+  const uint64_t g = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  const uint64_t si = g / pn;
+  const uint32_t p = p0 + (uint32_t)(g % pn);
+  if (si >= nslots) return;
+  if (leader[si] < (int32_t)p) return;                 // an earlier forger already leads this slot
+  const uint64_t s = first_slot + si;
+  uint32_t e0[8], alpha[8], ys[8], x[8], thr[4];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { e0[k] = eta0[k]; ys[k] = vrf_pk[8 * p + k]; x[k] = vrf_x[8 * p + k]; }
+#pragma unroll
+  for (int k = 0; k < 4; k++) thr[k] = pool_thr[4 * p + k];
+  if (tpraos) tpraos_seed(alpha, s, e0, eta0_neutral != 0, 1ull);
+  else mk_input_vrf(alpha, s, e0, eta0_neutral != 0);
+  ge_p3 H, G, G2, G4, G8;
+  vrf_hash_to_curve(H, ys, alpha);
+  ge_scalarmult_var(G, x, H);
+  ge_p3_dbl_to_p3(G2, G);
+  ge_p3_dbl_to_p3(G4, G2);
+  ge_p3_dbl_to_p3(G8, G4);
+  uint32_t g8s[8], beta[16];
+  ge_tobytes(g8s, G8.X, G8.Y, G8.Z);
+  vrf_beta(beta, g8s);
+  bool lead = true;
+  if (!f_is_one) {
+    if (tpraos) {
+      uint32_t l[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) l[k] = __builtin_bswap32(beta[15 - k]);
+      lead = leader_check_t<16>(l, thr, nullptr);
+    } else {
+      uint32_t lv[8], l[8];
+      blake2b256_tag64(lv, 'L', beta);                   // vrfLeaderValue, Praos/VRF.hs:103-112
+#pragma unroll
+      for (int k = 0; k < 8; k++) l[k] = __builtin_bswap32(lv[7 - k]);
+      lead = leader_check(l, thr, nullptr);
+    }
+  }
+  if (lead) atomicMin(&leader[si], (int32_t)p);
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
   return x;
@@ -147,13 +217,16 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk,
     uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
     uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos,
-    uint8_t* l_out, uint8_t* l_proof, const uint8_t* __restrict__ body_hash_in) {
+    uint8_t* l_out, uint8_t* l_proof, const uint8_t* __restrict__ body_hash_in,
+    const uint64_t* __restrict__ sched_slot, const uint32_t* __restrict__ sched_pool, uint64_t block_no0) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
   const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
   if (i >= n) return;
-  const uint32_t p = (uint32_t)(mix64(i ^ salt) % npools);
-  const uint64_t s = first_slot + i * slot_stride;
+  // a leader schedule (praos_leader_schedule) gives slot and forging pool per
+  // header; without one, slots are evenly spaced and pools hashed (not leader-valid)
+  const uint32_t p = sched_pool ? sched_pool[i] : (uint32_t)(mix64(i ^ salt) % npools);
+  const uint64_t s = sched_slot ? sched_slot[i] : first_slot + i * slot_stride;
   const uint64_t kp = s / slots_per_kes_period;
   const uint64_t c0 = kp - (kp % 60u);          // OCert issued at a period boundary <= kp
   const uint64_t t = kp - c0;                   // < 60 <= maxKESEvo (62)
@@ -215,7 +288,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   } else {
     SynthWr w{body_bytes + boff, 0};
     sw_head(w, 4, 10);
-    sw_head(w, 0, first_slot / slot_stride + i);                // blockNo
+    sw_head(w, 0, sched_slot ? block_no0 + i : first_slot / slot_stride + i);   // blockNo
     sw_head(w, 0, s);                                           // slotNo
     sw_head(w, 2, 32);                                          // prevHash (pseudo-random)
     for (int k = 0; k < 4; k++) { st = mix64(st + k); for (int b = 0; b < 8; b++) sw_byte(w, (uint32_t)(st >> (8 * b))); }
@@ -344,12 +417,24 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
                           uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len,
                           uint8_t* body_bytes, int tpraos, uint8_t* l_out, uint8_t* l_proof,
-                          const uint8_t* body_hash_in) {
+                          const uint8_t* body_hash_in, const uint64_t* sched_slot, const uint32_t* sched_pool,
+                          uint64_t block_no0) {
   hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, nkes, first_slot, slot_stride,
                      slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk,
                      leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
                      ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, tpraos, l_out, l_proof,
-                     body_hash_in);
+                     body_hash_in, sched_slot, sched_pool, block_no0);
+}
+void launch_synth_vrf_scalar(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const uint32_t* vrf_seed,
+                             uint32_t* vrf_x) {
+  hipLaunchKernelGGL(k_synth_vrf_scalar, grid, block, 0, stream, npools, vrf_seed, vrf_x);
+}
+void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint64_t first_slot, uint64_t nslots,
+                                uint32_t p0, uint32_t pn, const uint32_t* vrf_x, const uint32_t* vrf_pk,
+                                const uint32_t* pool_thr, const uint32_t* eta0, int eta0_neutral, int f_is_one,
+                                int tpraos, int32_t* leader) {
+  hipLaunchKernelGGL(k_synth_leader_search, grid, block, 0, stream, first_slot, nslots, p0, pn, vrf_x, vrf_pk,
+                     pool_thr, eta0, eta0_neutral, f_is_one, tpraos, leader);
 }
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt,
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out,

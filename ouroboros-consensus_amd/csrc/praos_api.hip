@@ -1074,6 +1074,12 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
   auto dlout = s.zeros<uint8_t>(tpraos ? 64 * n : 16);
   auto dlproof = s.zeros<uint8_t>(tpraos ? 80 * n : 16);
   const uint8_t* dbh = sp->body_hash ? s.up(sp->body_hash, 32 * n) : nullptr;   // caller's hbBodyHash values
+  if ((sp->sched_slot == nullptr) != (sp->sched_pool == nullptr)) return PRAOS_E_ARG;
+  if (sp->sched_pool)
+    for (size_t i = 0; i < n; i++)
+      if (sp->sched_pool[i] >= np) { c->err = "sched_pool out of range"; return PRAOS_E_ARG; }
+  const uint64_t* dss = sp->sched_slot ? s.up(sp->sched_slot, 8 * n) : nullptr;
+  const uint32_t* dsp = sp->sched_pool ? s.up(sp->sched_pool, 4 * n) : nullptr;
   if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
   uint64_t salt = 0;
   std::memcpy(&salt, sp->seed, 8);
@@ -1087,7 +1093,7 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
                        (uint32_t)nk, sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
                        dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof,
-                       sp->body_len == 0 && !tpraos ? dbh : nullptr);
+                       sp->body_len == 0 && !tpraos ? dbh : nullptr, dss, dsp, sp->block_no0);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
                        salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
                        sp->body_len == 0 ? 1 : 0);
@@ -1139,6 +1145,58 @@ int praos_synthesize_tpraos(praos_ctx* c, const praos_synth_params* sp, const pr
   return synthesize_impl(c, sp, params, eta0, pools_out, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
                          ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, corrupted, 1, leader_out,
                          leader_proof);
+}
+
+int praos_leader_schedule(praos_ctx* c, const uint8_t seed[32], uint32_t npools, const uint8_t* sigma_fp,
+                          const praos_params* params, const uint8_t eta0[32], uint64_t first_slot, uint64_t nslots,
+                          int tpraos, int32_t* leader) {
+  if (!c || !seed || npools == 0 || !sigma_fp || !params || (nslots && !leader)) return PRAOS_E_ARG;
+  if (nslots > (1ull << 32)) { c->err = "nslots > 2^32: split the range"; return PRAOS_E_ARG; }
+  HIPCHK(c, hipSetDevice(c->device));
+  if (nslots == 0) return PRAOS_OK;
+  std::vector<uint32_t> thr(4 * (size_t)npools);
+  for (uint32_t p = 0; p < npools; p++)
+    if (!praos_host::leader_x_raw((uint8_t*)&thr[4 * p], sigma_fp + 16 * (size_t)p, params->c_raw)) {
+      c->err = "sigma * activeSlotLog out of range";
+      return PRAOS_E_ARG;
+    }
+  Scratch s(c);
+  uint32_t master[8], e0[8] = {0};
+  std::memcpy(master, seed, 32);
+  if (eta0) std::memcpy(e0, eta0, 32);
+  const size_t np = npools;
+  auto dmaster = s.up(master, 32);
+  auto de0 = s.up(e0, 32);
+  auto cold_seed = s.zeros<uint32_t>(32 * np);
+  auto cold_pk = s.zeros<uint32_t>(32 * np);
+  auto vrf_seed = s.zeros<uint32_t>(32 * np);
+  auto vrf_pk = s.zeros<uint32_t>(32 * np);
+  auto kes_seed = s.zeros<uint32_t>(32 * np);
+  auto vrf_x = s.zeros<uint32_t>(32 * np);
+  auto ph = s.zeros<uint8_t>(28 * np);
+  auto pv = s.zeros<uint8_t>(32 * np);
+  auto dthr = s.up(thr.data(), 16 * np);
+  auto dlead = s.up<int32_t>(nullptr, 4 * nslots);
+  if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
+  launch_synth_pools(dim3(nblocks(np, NT)), dim3(NT), c->stream, (uint32_t)np, c->btab, dmaster, cold_seed, cold_pk,
+                     vrf_seed, vrf_pk, kes_seed, ph, pv);
+  launch_synth_vrf_scalar(dim3(nblocks(np, 64)), dim3(64), c->stream, (uint32_t)np, vrf_seed, vrf_x);
+  HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)dlead, 0x7fffffff, nslots, c->stream));
+  // pool chunks in forger order; a slot led by an earlier chunk is skipped by later ones
+  constexpr uint32_t CH = 32;
+  for (uint32_t p0 = 0; p0 < npools; p0 += CH) {
+    const uint32_t pn = std::min(CH, npools - p0);
+    const uint64_t lanes = nslots * pn;
+    if (lanes / NT + 1 > 0x7fffffffull) { c->err = "range too large"; return PRAOS_E_ARG; }
+    launch_synth_leader_search(dim3((unsigned)((lanes + NT - 1) / NT)), dim3(NT), c->stream, first_slot, nslots, p0,
+                               pn, vrf_x, vrf_pk, dthr, de0, eta0 ? 0 : 1, (int)params->f_is_one, tpraos, dlead);
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(leader, dlead, 4 * nslots, hipMemcpyDeviceToHost));
+  for (uint64_t k = 0; k < nslots; k++)
+    if (leader[k] == 0x7fffffff) leader[k] = -1;
+  return PRAOS_OK;
 }
 
 // TPraos batch: OCert + KES kernels are shared with Praos; VRF checks use the
@@ -1301,6 +1359,26 @@ int praos_debug_leader(praos_ctx* c, size_t n, const uint8_t* leader, const uint
   if (!s.ok) return PRAOS_E_OOM;
   launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr, (const uint32_t*)nullptr,
                 (const uint32_t*)dx, 0, 8, (const uint16_t*)nullptr, (const uint16_t*)nullptr,
+                (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, dit, (const uint16_t*)nullptr);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(is_leader, dres, n, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(iters, dit, 4 * n, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
+int praos_debug_leader512(praos_ctx* c, size_t n, const uint8_t* leader64, const uint8_t* x_raw16, uint8_t* is_leader,
+                          int32_t* iters) {
+  if (!c) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  Scratch s(c);
+  auto dl = s.up(leader64, 64 * n);
+  auto dx = s.up(x_raw16, 16 * n);
+  auto dres = s.zeros<uint8_t>(n);
+  auto dit = s.zeros<int32_t>(4 * n);
+  if (!s.ok) return PRAOS_E_OOM;
+  launch_leader(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, dl, (const int32_t*)nullptr, (const uint32_t*)nullptr,
+                (const uint32_t*)dx, 0, 16, (const uint16_t*)nullptr, (const uint16_t*)nullptr,
                 (const uint16_t*)nullptr, (uint16_t*)nullptr, dres, dit, (const uint16_t*)nullptr);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -103,7 +103,7 @@ class SynthParams(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("npools", ctypes.c_uint32), ("first_slot", ctypes.c_uint64),
                 ("slot_stride", ctypes.c_uint64), ("body_len", ctypes.c_uint32),
                 ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32),
-                ("body_hash", u8p)]
+                ("body_hash", u8p), ("sched_slot", u64p), ("sched_pool", u32p), ("block_no0", ctypes.c_uint64)]
 
 
 class HeaderBytes(ctypes.Structure):
@@ -163,6 +163,8 @@ SIGNATURES = {
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
+    "praos_leader_schedule": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.c_uint32, u8p, ctypes.POINTER(Params), u8p,
+                                             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, i32p]),
     "praos_verify_tpraos_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders),
                                                    ctypes.POINTER(TPOut)]),
     "praos_synthesize_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params),
@@ -186,6 +188,7 @@ SIGNATURES = {
     "praos_debug_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p]),
     "praos_debug_scalarmult_base": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p]),
     "praos_debug_leader": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p, i32p]),
+    "praos_debug_leader512": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p, i32p]),
     "praos_debug_hash_to_curve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u8p]),
 }
 
@@ -549,12 +552,32 @@ class Context:
                                              ptr(res)))
         return res
 
+    def leader_schedule(self, seed: bytes, sigma_fp, params: Params, eta0, first_slot, nslots, tpraos=False):
+        """First-leader-wins forger per slot (praos_leader_schedule): int32[nslots], -1 = empty slot.
+        sigma_fp: per-pool Fixed E34 stake (ints), in forger order."""
+        npools = len(sigma_fp)
+        sig = np.frombuffer(b"".join(int(x).to_bytes(16, "little") for x in sigma_fp), np.uint8).copy()
+        sd = np.frombuffer(bytes(seed), np.uint8).copy()
+        e = None if eta0 is None else np.frombuffer(bytes(eta0), np.uint8).copy()
+        out = np.zeros(nslots, np.int32)
+        self.check(self.L.praos_leader_schedule(self.h, ptr(sd), npools, ptr(sig), ctypes.byref(params), ptr(e),
+                                                first_slot, nslots, int(bool(tpraos)), ptr(out, i32p)))
+        return out
+
     def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
-                   body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False, body_hash=None):
+                   body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False, body_hash=None, schedule=None,
+                   block_no0=0):
+        """schedule: (slots u64[n], pools u32[n]) from leader_schedule (a leader-valid chain), or None
+        (evenly spaced slots, pools by hash: not leader-valid)."""
         sp = SynthParams()
         if body_hash is not None:   # n*32 hbBodyHash values for the CBOR bodies (body_len=0)
             body_hash = np.ascontiguousarray(body_hash, dtype=np.uint8).reshape(n, 32)
             sp.body_hash = ptr(body_hash)
+        if schedule is not None:
+            ss = np.ascontiguousarray(schedule[0], dtype=np.uint64)
+            sq = np.ascontiguousarray(schedule[1], dtype=np.uint32)
+            assert len(ss) == n and len(sq) == n
+            sp.sched_slot, sp.sched_pool, sp.block_no0 = ptr(ss, u64p), ptr(sq, u32p), block_no0
         sp.n = n
         sp.npools = npools
         sp.first_slot = first_slot
@@ -638,6 +661,13 @@ class Context:
         res = np.zeros(n, np.uint8)
         it = np.zeros(n, np.int32)
         self.check(self.L.praos_debug_leader(self.h, n, ptr(leader_be), ptr(x_raw16), ptr(res), ptr(it, i32p)))
+        return res, it
+
+    def debug_leader512(self, leader_be64, x_raw16):
+        n = len(leader_be64)
+        res = np.zeros(n, np.uint8)
+        it = np.zeros(n, np.int32)
+        self.check(self.L.praos_debug_leader512(self.h, n, ptr(leader_be64), ptr(x_raw16), ptr(res), ptr(it, i32p)))
         return res, it
 
     def debug_hash_to_curve(self, pk, alpha):

@@ -226,3 +226,25 @@ def test_leader_f_is_one(ctx):
     from praos_hip import abi
     res = ctx.check_leader(arr([bytes([0xff] * 32)], 32), arr([bytes(16)], 16), abi.params(f_is_one=True))
     assert list(res) == [1]
+
+
+def test_leader_boundary_vectors(ctx):
+    """Bisected decision boundaries (tests/golden/leader_boundary.json): for each (sigma, f)
+    the leader values l*-2, l*-1 (leader) and l*, l*+1 (not leader), 256-bit (Praos) and
+    512-bit (TPraos) forms; decisions and Taylor iteration counts bit-exact."""
+    import json
+    import os
+    R = 10 ** 34
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "leader_boundary.json")))["cases"]
+    for bits in (256, 512):
+        ls, xs, want, want_it = [], [], [], []
+        for c in (c for c in cases if c["bits"] == bits):
+            x = -((int(c["sigma_fp"]) * int(c["c_raw"])) // R)
+            for v in c["vectors"]:
+                ls.append(int(v["leader_value"], 16).to_bytes(bits // 8, "big"))
+                xs.append(x.to_bytes(16, "little"))
+                want.append(int(v["is_leader"]))
+                want_it.append(v["iterations"])
+        fn = ctx.debug_leader if bits == 256 else ctx.debug_leader512
+        res, it = fn(arr(ls, bits // 8), arr(xs, 16))
+        assert list(res) == want and list(it) == want_it

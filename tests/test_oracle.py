@@ -177,3 +177,22 @@ def test_active_slot_log_value():
     c = fixed.active_slot_log(Fraction(1, 20))
     assert abs(c / 10 ** 34 - math.log(0.95)) < 1e-15 and c < 0
     assert fixed.from_rational(Fraction(1, 3)) == 10 ** 34 // 3
+
+
+def test_leader_boundary_fixture():
+    """The bisected boundary vectors reproduce on the C oracle and on the pure-Python
+    restatement of checkLeaderNatValue (tests/golden/make_leader_boundary.py)."""
+    import json
+    import os
+    import oracle
+    from golden.make_leader_boundary import leader_python
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "leader_boundary.json")))["cases"]
+    assert len(cases) == 16
+    for c in cases:
+        bits, s_fp, c_raw = c["bits"], int(c["sigma_fp"]), int(c["c_raw"])
+        check = oracle.check_leader if bits == 256 else oracle.check_leader512
+        for v in c["vectors"]:
+            l = int(v["leader_value"], 16)
+            assert check(l.to_bytes(bits // 8, "big"), s_fp, c_raw) == (v["is_leader"], v["iterations"])
+            assert leader_python(l, bits, s_fp, c_raw) == (v["is_leader"], v["iterations"])
+        assert int(c["boundary"], 16) == int(c["vectors"][2]["leader_value"], 16)
