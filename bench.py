@@ -19,11 +19,12 @@ shard (the one shipped schedule, so ranks > 0 replay the same blocks).
 distinct keys, 1M VRF verifies + leader checks, 1M Sum6KES verifies), c1 the
 10k-block / 100-pool chain of configs[0] (GPU and CPU side by side).
 
-CPU baseline (rank 0, N = 1): the C oracle (oracle/, a restatement of the reference
-semantics; the Haskell reference cannot run here) timed over a bounded sample of
-the same headers on the host cores this job may use, plus a single-core rate and an
-OpenSSL Ed25519 verify rate as an independent third-party point; the same sample
-cross-checks the GPU result bit for bit.
+CPU baseline (rank 0, N = 1): the CPU twin libpraos_cpu.so (C++ restatement of the
+reference semantics with the same C ABI; the Haskell reference cannot run here)
+timed over a bounded sample of the same headers on the host cores this job may use,
+plus its single-core rate and an OpenSSL Ed25519 verify rate as an independent
+third-party point; the twin's bits are compared with the GPU's on the whole sample
+and the oracle (oracle/) checks both on a sub-sample.
 """
 import argparse
 import json
@@ -47,7 +48,7 @@ from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  #
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")   # tools/profile.sh r02
 
 CONFIGS = {
     "c1": dict(items=10_000, kernels=7, metric="Praos headers validated/sec (CPU config C1)",
@@ -161,34 +162,98 @@ def openssl_ed25519_rate(seconds=2.0):
         return None
 
 
-def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, spkp, maxevo, pool_list, seconds, workers, per_item, mask,
+def _sample(H, idx):
+    """Sub-batch of the SoA header dict H at indices idx (bodies repacked)."""
+    S = {k: np.ascontiguousarray(H[k][idx]) for k in H if k not in ("body_bytes", "body_off", "body_len")}
+    lens = H["body_len"][idx].astype(np.uint64)
+    offs = H["body_off"][idx]
+    S["body_len"] = np.ascontiguousarray(H["body_len"][idx])
+    S["body_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    S["body_bytes"] = np.concatenate([H["body_bytes"][int(o):int(o) + int(ln)] for o, ln in zip(offs, lens)] +
+                                     [np.zeros(8, np.uint8)])
+    return S
+
+
+def _twin_run(ctx, kind, S, eta0, pool_list, p, spkp):
+    """One CPU-twin pass over the sample S; returns the per-item result bits."""
+    import hashlib
+    n = len(S["slot"])
+    if kind == "header":
+        return ctx.verify_headers(S)["bits"]
+    if kind == "ocert":
+        ok = ctx.verify_ocert(S["cold_vk"], S["hot_vk"], S["ocert_n"], S["ocert_c0"], S["ocert_sig"])
+        return np.where(ok == 1, 0, 0x0004).astype(np.uint16)
+    if kind == "kes":
+        t = np.maximum(S["slot"].astype(np.int64) // spkp - S["ocert_c0"].astype(np.int64), 0).astype(np.uint32)
+        msgs = [bytes(S["body_bytes"][int(o):int(o) + int(ln)]) for o, ln in zip(S["body_off"], S["body_len"])]
+        r = ctx.verify_kes(S["hot_vk"], t, S["kes_sig"], msgs)
+        return np.array([{0: 0, 1: 0x0008, 2: 0x0010}[int(x)] for x in r], np.uint16)
+    # vrf + leader (configs[2]): alpha = mkInputVRF, leader value of the certified output
+    alpha = np.frombuffer(b"".join(hashlib.blake2b(int(s).to_bytes(8, "big") + eta0, digest_size=32).digest()
+                                   for s in S["slot"]), np.uint8).reshape(n, 32).copy()
+    ok, beta = ctx.verify_vrf(S["vrf_vk"], S["vrf_proof"], alpha)
+    lv = np.frombuffer(b"".join(hashlib.blake2b(b"L" + bytes(o), digest_size=32).digest() for o in S["vrf_out"]),
+                       np.uint8).reshape(n, 32).copy()
+    by_hash = {h: s for h, _, s in pool_list}
+    hk = [hashlib.blake2b(bytes(c), digest_size=28).digest() for c in S["cold_vk"]]
+    known = np.array([h in by_hash for h in hk])
+    sig = np.frombuffer(b"".join(int(by_hash.get(h, 0)).to_bytes(16, "little") for h in hk),
+                        np.uint8).reshape(n, 16).copy()
+    lead = ctx.check_leader(lv, sig, p) | ~known          # VRFKeyUnknown precedes the leader test
+    bits = np.where(ok == 1, 0, 0x0400) | np.where((beta == S["vrf_out"]).all(axis=1), 0, 0x0800)
+    return (bits | np.where(lead == 1, 0, 0x1000)).astype(np.uint16)
+
+
+def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, seconds, threads, per_item, mask,
                  whole=False):
+    """The CPU twin (libpraos_cpu.so, same ABI, `threads` worker threads) timed over a
+    bounded sample of the benchmark input, its single-core rate, and the oracle as
+    the checker of both implementations on a sub-sample."""
+    from praos_hip import cpu as C
     n_total = len(H["slot"])
-    n_sample = n_total if whole else int(min(n_total, max(workers * 8, seconds * workers / per_item)))
+    n_sample = n_total if whole else int(min(n_total, max(threads * 64, seconds * threads / per_item)))
     idx = np.linspace(0, n_total - 1, n_sample).astype(np.int64)
-    items = [_hdr_dict(H, i) for i in idx]
-    chunks = [items[k::workers] for k in range(workers)]
+    S = _sample(H, idx)
+    twin = C.CpuContext(threads)
+    twin.set_epoch(eta0, pool_list, p)
+    _twin_run(twin, kind, _sample(H, idx[:64]), eta0, pool_list, p, spkp)       # warm
     t0 = time.perf_counter()
+    bits = _twin_run(twin, kind, S, eta0, pool_list, p, spkp)
+    busy = time.perf_counter() - t0
+    agree = int(((gpu_bits[idx] & mask) == (bits & mask)).sum())
+    # one core: the first part of the same sample on one thread
+    n1 = max(16, min(n_sample, int(3.0 / per_item)))
+    twin.set_option(C.OPT_THREADS, 1)
+    t1 = time.perf_counter()
+    _twin_run(twin, kind, _sample(H, idx[:n1]), eta0, pool_list, p, spkp)
+    t1 = time.perf_counter() - t1
+    twin.close()
+    # the oracle (checker) on a sub-sample, in a process pool
+    sub = idx[:: max(1, n_sample // 2000)]
+    items = [_hdr_dict(H, i) for i in sub]
+    workers = max(1, min(threads, 16))
+    chunks = [items[k::workers] for k in range(workers)]
     with mp.get_context("spawn").Pool(workers) as pool:
-        res = pool.map(_oracle_worker, [(kind, eta0, c_raw, spkp, maxevo, pool_list, c) for c in chunks])
-    wall = time.perf_counter() - t0
-    busy = max(r[1] for r in res)
-    bits = [None] * n_sample
+        res = pool.map(_oracle_worker, [(kind if kind != "vrf" else "header", eta0, c_raw, spkp, maxevo, pool_list, c)
+                                        for c in chunks])
+    obits = [None] * len(sub)
     for k, (b, _) in enumerate(res):
         for j, v in enumerate(b):
-            bits[k + j * workers] = v
-    agree = sum(1 for j, i in enumerate(idx) if (int(gpu_bits[i]) & mask) == (bits[j] & mask))
-    # one core: a short run of the same items in this process
-    one = items[: max(8, int(min(len(items), 3.0 / per_item)))]
-    _, t1 = _oracle_worker((kind, eta0, c_raw, spkp, maxevo, pool_list, one))
+            obits[k + j * workers] = v
+    omask = mask if kind != "vrf" else 0x1F00
+    oracle_agree = sum(1 for j, i in enumerate(sub) if (int(gpu_bits[i]) & omask) == (obits[j] & omask))
     usable, nproc, model = host_cores()
+    single = len(range(n1)) / t1
     return {"value": round(n_sample / busy, 1), "unit": "items/s" if kind != "header" else "headers/s",
-            "cores": workers, "kind": "port",
-            "sample": f"{n_sample} items evenly spaced over the benchmark input, C oracle (oracle/) in "
-                      f"{workers} processes; busy {busy:.1f}s, wall {wall:.1f}s",
-            "single_core": round(len(one) / t1, 1), "host": {"cpu_model": model, "nproc": nproc,
-                                                             "usable_cores": usable},
-            "parity_sample": {"n": n_sample, "bit_exact": agree}}
+            "cores": threads, "kind": "port",
+            "sample": f"{n_sample} items evenly spaced over the benchmark input; CPU twin libpraos_cpu.so "
+                      f"(C++, radix-2^51, sliding-window Straus, same ABI) on {threads} threads, {busy:.2f}s",
+            "single_core": round(single, 1),
+            "all_cores_linear_estimate": round(single * nproc, 1),
+            "host": {"cpu_model": model, "nproc": nproc, "usable_cores": usable,
+                     "threads_used": threads, "note": "threads capped at the box's CPU share (16 per GPU)"},
+            "parity_sample": {"n": n_sample, "bit_exact_twin_vs_gpu": agree,
+                              "oracle_checked": len(sub), "bit_exact_oracle_vs_gpu": oracle_agree}}
 
 
 def load_traffic(kernel, workload):
@@ -243,7 +308,7 @@ def main():
     ap.add_argument("--items", type=int, default=None, help="items per GPU (default: the config's)")
     ap.add_argument("--corrupt-per-10000", type=int, default=100)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=16, help="CPU-twin threads (the box's share: 16)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
@@ -384,11 +449,11 @@ def main():
         line["e2e"] = e2e
     if world == 1 and not args.no_cpu:
         usable, _, _ = host_cores()
-        workers = max(1, min(args.cpu_workers, usable))
-        kind, per_item, mask = {7: ("header", 1.4e-3, 0x1F1F), 1: ("ocert", 0.3e-3, 0x0004),
-                                2: ("kes", 0.35e-3, 0x0018), 4: ("header", 1.4e-3, 0x1F00)}[cfg["kernels"]]
-        line["cpu_baseline"] = cpu_baseline(kind, H, out["bits"], eta0, c_raw, spkp, maxevo, pool_list,
-                                            args.cpu_seconds, workers, per_item, mask, whole=args.config == "c1")
+        threads = max(1, min(args.cpu_workers, usable))
+        kind, per_item, mask = {7: ("header", 2.5e-4, 0x1F1F), 1: ("ocert", 5e-5, 0x0004),
+                                2: ("kes", 6e-5, 0x0018), 4: ("vrf", 1.5e-4, 0x1C00)}[cfg["kernels"]]
+        line["cpu_baseline"] = cpu_baseline(kind, H, out["bits"], eta0, c_raw, p, spkp, maxevo, pool_list,
+                                            args.cpu_seconds, threads, per_item, mask, whole=args.config == "c1")
         line["cpu_baseline"]["openssl_ed25519_verify_per_s_1core"] = openssl_ed25519_rate()
         line["gpu_vs_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     print(json.dumps(line), flush=True)

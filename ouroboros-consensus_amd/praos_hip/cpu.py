@@ -1,0 +1,42 @@
+"""ctypes binding of libpraos_cpu.so, the multi-threaded CPU twin of libpraos_hip
+(ouroboros-consensus_amd/cpu/praos_cpu.cpp): the same C ABI for the header-crypto
+entry points, run on host cores.  It is the CPU baseline bench.py times; the GPU
+path never falls back to it (Context below is a separate object)."""
+import ctypes
+import os
+
+from . import abi
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libpraos_cpu.so")
+OPT_THREADS = 4
+EXPORTS = ("praos_abi_version", "praos_open", "praos_close", "praos_last_error", "praos_set_option",
+           "praos_set_epoch", "praos_verify_headers", "praos_verify_ocert", "praos_verify_kes", "praos_verify_vrf",
+           "praos_check_leader")
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with __graft_entry__.build() "
+                               "(make -C ouroboros-consensus_amd/cpu)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name in EXPORTS:
+            res, args = abi.SIGNATURES[name]
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+class CpuContext(abi.Context):
+    """The CPU twin behind the Context API (only the EXPORTS entry points exist)."""
+
+    def __init__(self, threads=0):
+        self.L = load()
+        self.h = self.L.praos_open(0)
+        if not self.h:
+            raise abi.PraosError("praos_open failed (CPU twin)")
+        self._keep = []
+        self.set_option(OPT_THREADS, threads)

@@ -75,7 +75,7 @@ def main():
                            "lds": int(r["LDS_Block_Size"])}
     out = {}
     if acc:
-        lines.append("== PMC (one counter group per pass; bench.py --no-cpu --headers 131072 --steps 1) ==")
+        lines.append("== PMC (one counter group per pass; bench.py <args> --no-cpu --steps 1 --warmup 0) ==")
         lines.append("per dispatch (mean over dispatches), and per lane = per header / signature")
         for k in KERNELS:
             if k not in acc:
@@ -99,7 +99,27 @@ def main():
                 lines.append(f"   VALU wave-instructions per wave (one item per lane): "
                              f"{o['SQ_INSTS_VALU']['per_lane'] * 64:.0f}")
             out[k] = o
+    # per-launch HBM traffic for bench.py's roofline.traffic (FETCH x2 gfx950 read correction)
+    workload = None
+    if os.path.exists(bench):
+        try:
+            workload = json.loads(open(bench).read().strip().splitlines()[-1])["config"]["workload"]
+        except (ValueError, KeyError, IndexError):
+            workload = None
+    traffic = {}
+    for k, o in out.items():
+        if "FETCH_SIZE" in o and "WRITE_SIZE" in o:
+            rd = 2 * 1024 * o["FETCH_SIZE"]["per_dispatch"]
+            wr = 1024 * o["WRITE_SIZE"]["per_dispatch"]
+            traffic[k] = {"bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                          "items_per_launch": o["FETCH_SIZE"]["grid"], "bytes_per_item": (rd + wr) / o["FETCH_SIZE"]["grid"]}
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
+    if traffic and workload:
+        with open(os.path.join(root, "profiles", f"{tag}_traffic.json"), "w") as f:
+            json.dump({"workload": workload, "source": f"profiles/{tag}_rocprof.txt (tools/profile.sh)",
+                       "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                                 "bytes = 2 x FETCH_SIZE KiB x 1024 (gfx950 half-count correction) + WRITE_SIZE KiB x 1024",
+                       "kernels": traffic}, f, indent=1)
     with open(os.path.join(root, "profiles", f"{tag}_rocprof.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
     if out:
