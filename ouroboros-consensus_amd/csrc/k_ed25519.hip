@@ -16,6 +16,7 @@ struct OcertIn {
   uint64_t slots_per_kes_period, max_kes_evo;
   uint16_t* __restrict__ bits;
   uint8_t* __restrict__ ok_out;
+  ge_cached* __restrict__ tabs;          // per-lane tables (LT_ED entries per item)
 };
 
 __device__ __forceinline__ void ocert_store(const OcertIn& a, size_t i, bool ok) {
@@ -52,7 +53,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_ocert(size_t n, const uint32_t* _
   const size_t i = list ? list[t] : t;
   uint32_t pk[8], sg[16], hram[16];
   ocert_load(a, i, sg, hram, pk);
-  ocert_store(a, i, ed25519_verify_core(pk, sg, sg + 8, hram, btab));
+  ocert_store(a, i, ed25519_verify_core(pk, sg, sg + 8, hram, btab, lane_tab(a.tabs, i, LT_ED)));
 }
 
 __global__ void __launch_bounds__(NT, LB_ED) k_ocert_ck(const uint32_t* __restrict__ list,
@@ -83,7 +84,8 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
                                             const uint8_t* __restrict__ body, size_t body_bytes_len,
                                             const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0,
                                             uint64_t slots_per_kes_period, const uint32_t* __restrict__ period,
-                                            uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {
+                                            uint16_t* __restrict__ bits, uint8_t* __restrict__ result,
+                                            ge_cached* __restrict__ tabs) {
   if ((size_t)blockIdx.x * NT >= n) return;
   __shared__ ge_niels sbtab[BTAB_N];
   const ge_niels* btab = stage_btab<1>(gbtab, sbtab);
@@ -109,7 +111,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
 #pragma unroll
   for (int k = 0; k < 8; k++) { pre[k] = sg[k]; pre[8 + k] = leaf[k]; }
   sha512_stream(hram, pre, 64, body + off, len);
-  const bool leaf_ok = ed25519_verify_core(leaf, sg, sg + 8, hram, btab);
+  const bool leaf_ok = ed25519_verify_core(leaf, sg, sg + 8, hram, btab, lane_tab(tabs, i, LT_ED));
   if (result) {
     result[i] = !in_range ? 3 : (!merkle_ok ? 1 : (leaf_ok ? 0 : 2));
     return;
@@ -126,8 +128,8 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const ge_niels* __r
 void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                   const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
                   const uint64_t* ocert_c0, const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period,
-                  uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out) {
-  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out};
+                  uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out, ge_cached* tabs) {
+  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out, tabs};
   hipLaunchKernelGGL(k_ocert, grid, block, 0, stream, n, list, count, gbtab, a);
 }
 void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
@@ -135,10 +137,10 @@ void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* 
                      const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
                      const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo,
                      uint16_t* bits, uint8_t* ok_out) {
-  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out};
+  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out, nullptr};
   hipLaunchKernelGGL(k_ocert_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }
 
-void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result) {
-  hipLaunchKernelGGL(k_kes, grid, block, 0, stream, n, gbtab, hot_vk, kes_sig, body_off, body_len, body, body_bytes_len, slot, ocert_c0, slots_per_kes_period, period, bits, result);
+void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result, ge_cached* tabs) {
+  hipLaunchKernelGGL(k_kes, grid, block, 0, stream, n, gbtab, hot_vk, kes_sig, body_off, body_len, body, body_bytes_len, slot, ocert_c0, slots_per_kes_period, period, bits, result, tabs);
 }

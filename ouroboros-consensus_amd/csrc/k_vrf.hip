@@ -28,6 +28,7 @@ struct VrfIn {
   uint8_t* __restrict__ leader_out;
   uint8_t* __restrict__ nonce_out;
   uint8_t* __restrict__ ok_out;
+  ge_cached* __restrict__ tabs;          // per-lane tables (LT_VRF entries per item)
 };
 
 // issuer pool: hashKey (Blake2b-224 of the cold vk, Praos.hs:552) -> sorted index or -1
@@ -81,7 +82,8 @@ __device__ __forceinline__ void vrf_item(const VrfIn& a, size_t i, const ge_niel
   uint32_t beta[16];
   bool gamma_ok;
   const bool proof_ok =
-      vrf_verify_core<CACHED>(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab, ktab, kinfo);
+      vrf_verify_core<CACHED>(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab, lane_tab(a.tabs, i, LT_VRF),
+                              ktab, kinfo);
   if (!gamma_ok) {
 #pragma unroll
     for (int k = 0; k < 16; k++) beta[k] = 0;
@@ -153,7 +155,8 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     const uint32_t* __restrict__ eta0, int eta0_neutral, const uint32_t* __restrict__ pool_hash,
     const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map, uint32_t npools, int check_output,
     uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx, int32_t* __restrict__ pool_sorted_idx,
-    uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_l, uint8_t* __restrict__ nonce_out) {
+    uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_l, uint8_t* __restrict__ nonce_out,
+    ge_cached* __restrict__ tabs) {
   if ((size_t)blockIdx.x * NT >= n) return;
   __shared__ ge_niels sbtab[2 * BTAB_N];
   const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
@@ -185,7 +188,8 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     load_words(out, (cert ? l_out : eta_out) + 64 * i, 16);
     tpraos_seed(alpha, s, e0, eta0_neutral != 0, (uint64_t)cert);
     bool gamma_ok;
-    const bool ok = vrf_verify_core<false>(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab);
+    const bool ok = vrf_verify_core<false>(beta, gamma_ok, pk, pr, pr + 8, pr + 12, alpha, btab,
+                                           lane_tab(tabs, i, LT_VRF));
     if (!gamma_ok) {
 #pragma unroll
       for (int k = 0; k < 16; k++) beta[k] = 0;
@@ -213,9 +217,9 @@ void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint3
                 const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
                 const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
                 int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out) {
+                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs) {
   VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools,
-          check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out};
+          check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out, tabs};
   hipLaunchKernelGGL(k_vrf, grid, block, 0, stream, n, list, count, gbtab, a);
 }
 void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
@@ -224,9 +228,9 @@ void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash,
                    const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                    const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out) {
+                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs) {
   VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools,
-          check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out};
+          check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out, tabs};
   hipLaunchKernelGGL(k_vrf_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk,
@@ -234,8 +238,8 @@ void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge
                    const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
                    const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
                    int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta,
-                   uint8_t* beta_l, uint8_t* nonce_out) {
+                   uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs) {
   hipLaunchKernelGGL(k_vrf_tp, grid, block, 0, stream, n, gbtab, cold_vk, vrf_vk, eta_out, eta_proof, l_out, l_proof,
                      slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools, check_output, bits, pool_idx,
-                     pool_sorted_idx, beta_eta, beta_l, nonce_out);
+                     pool_sorted_idx, beta_eta, beta_l, nonce_out, tabs);
 }

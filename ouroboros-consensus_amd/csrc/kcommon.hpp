@@ -24,6 +24,15 @@
 #define LB_VRF 3
 #endif
 
+// Per-lane point tables in global memory (praos_api.hip allocates them per batch):
+// item i owns `entries` cached points, 128 contiguous bytes each, at arena + i *
+// entries -- 8 for an Ed25519 verify (KES leaf, OCert), 16 for a VRF verify.
+#define LT_ED 8
+#define LT_VRF 16
+__device__ __forceinline__ ge_cached* lane_tab(ge_cached* __restrict__ arena, size_t i, int entries) {
+  return arena + i * (size_t)entries;
+}
+
 __device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* p, int nwords) {
   const uint4* q = (const uint4*)p;
   for (int i = 0; i < nwords / 4; i++) {

@@ -9,7 +9,7 @@ struct ge_cached;
 void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                   const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
                   const uint64_t* ocert_c0, const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period,
-                  uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out);
+                  uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out, ge_cached* tabs);
 void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
                      const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                      const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
@@ -20,14 +20,14 @@ void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint3
                 const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
                 const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
                 int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out);
+                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs);
 void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                    const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
                    const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash,
                    const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                    const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out);
+                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs);
 void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* keys, uint32_t mask,
                        uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot);
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
@@ -39,7 +39,7 @@ void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
                            uint32_t* kinfo);
-void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result);
+void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result, ge_cached* tabs);
 void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab);
 void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in, const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one, int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits, uint8_t* is_leader, int32_t* iters, const uint16_t* dec_status);
 void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);
@@ -60,7 +60,7 @@ void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint6
                                 const uint32_t* pool_thr, const uint32_t* eta0, int eta0_neutral, int f_is_one,
                                 int tpraos, int32_t* leader);
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body);
-void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out);
+void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs);
 void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena, uint64_t arena_len,
                          const uint64_t* hoff, const uint32_t* hlen, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk,
                          uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint8_t* ocert_sig, uint8_t* kes_sig,

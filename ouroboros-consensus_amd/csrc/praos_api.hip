@@ -8,6 +8,8 @@
 static constexpr size_t NT = 256;                  // threads per block of the crypto kernels
 static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
 static constexpr size_t BTAB_N = 128;              // entries per fixed-base table (scalarmult.hpp)
+static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
+static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
 
 #include <algorithm>
 #include <cstdio>
@@ -55,6 +57,8 @@ struct praos_batch {
   uint16_t* bits3 = nullptr;   // per-kernel bits: ocert | kes | vrf
   int32_t *pool_idx = nullptr, *pool_sorted = nullptr;
   uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
+  // per-lane point tables of the three crypto kernels (kcommon.hpp lane_tab)
+  ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys
   struct KeyCache {
     uint32_t cap = 0, max_entries = 0;
@@ -262,6 +266,9 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   ok &= dalloc(b, &b->beta, 64 * n) == hipSuccess;
   ok &= dalloc(b, &b->leader, 32 * n) == hipSuccess;
   ok &= dalloc(b, &b->nonce, 32 * n) == hipSuccess;
+  ok &= dalloc(b, (uint8_t**)&b->tab_ocert, LT_ED_B * n) == hipSuccess;
+  ok &= dalloc(b, (uint8_t**)&b->tab_kes, LT_ED_B * n) == hipSuccess;
+  ok &= dalloc(b, (uint8_t**)&b->tab_vrf, LT_VRF_B * n) == hipSuccess;
   for (auto& k : b->kc) {
     k.cap = 256;
     while (k.cap < 2 * n) k.cap <<= 1;
@@ -427,11 +434,11 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, (uint8_t*)nullptr);
       launch_ocert(g, blk, so, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
     } else {
       launch_ocert(g, blk, so, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk,
                    b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo,
-                   bo, (uint8_t*)nullptr);
+                   bo, (uint8_t*)nullptr, b->tab_ocert);
     }
   } else {
     HIPCHK(c, hipMemsetAsync(bo, 0, 2 * n, so));
@@ -439,7 +446,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
   if (c->kernels & 2)
     launch_kes(g, blk, sk, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body, b->body_bytes_len,
-               b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr);
+               b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr,
+               b->tab_kes);
   else
     HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
@@ -452,16 +460,16 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk, b->vrf_vk,
                     b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
                     c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
-                    b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr);
+                    b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
       launch_vrf(g, blk, sv, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
                  b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
                  (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
-                 b->leader, b->nonce, (uint8_t*)nullptr);
+                 b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
     } else {
       launch_vrf(g, blk, sv, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk, b->vrf_vk,
                  b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
                  c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
-                 b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr);
+                 b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
     }
   }
   else {
@@ -529,7 +537,7 @@ int praos_block_batch_run(praos_ctx* c, praos_batch* b, uint64_t slots_per_kes_p
   HIPCHK(c, hipEventRecord(c->side_ev[0], c->side[0]));
   launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
              b->body_bytes_len, b->slot, b->ocert_c0, slots_per_kes_period, (const uint32_t*)nullptr, bk,
-             (uint8_t*)nullptr);
+             (uint8_t*)nullptr, b->tab_kes);
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[0], 0));
   launch_block_join(g, blk, c->stream, n, b->nseg, b->split_status, b->dec_status, bk, b->seg_hash, b->body_hash,
@@ -740,10 +748,11 @@ int praos_verify_ocert(praos_ctx* c, size_t n, const uint8_t* cold_vk, const uin
   auto dc = s.up(ocert_c0, 8 * n);
   auto ds = s.up(sig, 64 * n);
   auto dok = s.zeros<uint8_t>(n);
+  auto dtab = s.up<ge_cached>(nullptr, LT_ED_B * n);
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_ocert(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, nullptr, nullptr, c->btab, dv, dh, dn, dc, ds,
-                     (const uint64_t*)nullptr, (uint64_t)1, (uint64_t)0, (uint16_t*)nullptr, dok);
+                     (const uint64_t*)nullptr, (uint64_t)1, (uint64_t)0, (uint16_t*)nullptr, dok, dtab);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -776,11 +785,12 @@ int praos_verify_kes(praos_ctx* c, size_t n, const uint8_t* vk, const uint32_t* 
   auto dlen = s.up(len.data(), 4 * n);
   auto dmsg = s.up(arena.data(), arena.size());
   auto dres = s.zeros<uint8_t>(n);
+  auto dtab = s.up<ge_cached>(nullptr, LT_ED_B * n);
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_kes(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, dvk, dsig, doff, dlen, dmsg,
                      total, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)1, dp, (uint16_t*)nullptr,
-                     dres);
+                     dres, dtab);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -800,13 +810,14 @@ int praos_verify_vrf(praos_ctx* c, size_t n, const uint8_t* vk, const uint8_t* p
   auto dal = s.up(alpha, 32 * n);
   auto dok = s.zeros<uint8_t>(n);
   auto dbeta = s.zeros<uint8_t>(64 * n);
+  auto dtab = s.up<ge_cached>(nullptr, LT_VRF_B * n);
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, nullptr, nullptr, c->btab, (const uint8_t*)nullptr, dvk,
                      (const uint8_t*)nullptr, dpr, (const uint64_t*)nullptr, (const uint32_t*)nullptr, 1,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const int32_t*)nullptr, 0u, 0, dal,
                      (uint16_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, dbeta, (uint8_t*)nullptr,
-                     (uint8_t*)nullptr, dok);
+                     (uint8_t*)nullptr, dok, dtab);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1224,13 +1235,13 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
     HIPCHK(c, hipMemcpy(dlout, th->leader_out, 64 * n, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
     launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
-                 P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr);
+                 P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
     launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
                b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk,
-               (uint8_t*)nullptr);
+               (uint8_t*)nullptr, b->tab_kes);
     launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
                   b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
-                  (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce);
+                  (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce, b->tab_vrf);
     launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
                   (int)P.f_is_one, 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
                   (const uint16_t*)nullptr);

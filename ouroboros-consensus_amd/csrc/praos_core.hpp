@@ -83,8 +83,14 @@ FE_INLINE void sha512_stream(uint32_t out[16], const uint32_t prefix[16], uint32
 // ------------------------------------------------------------------ Ed25519
 // hram: SHA-512(R || A || M) digest words.  Checks in libsodium order; all
 // lanes do the full computation (rejections are folded in at the end).
+// tab: the lane's 8-entry table of -A ({1..8}(-A), cached form).  Kernels pass a
+// per-lane region of a global arena (kcommon.hpp lane_tab): each entry is 128
+// contiguous bytes of the lane's own, so a digit-indexed select reads whole
+// cache lines.  (A private array would live in swizzled scratch, where a
+// lane-divergent index touches one dword per 128-byte line.)
 FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], const uint32_t S[8],
-                                   const uint32_t hram[16], const ge_niels* __restrict__ btab) {
+                                   const uint32_t hram[16], const ge_niels* __restrict__ btab,
+                                   ge_cached* __restrict__ tab) {
   bool ok = sc_is_canonical(S) && !ge_has_small_order(R) && ge_is_canonical(pk) && !ge_has_small_order(pk);
   ge_p3 A;
   ok = ge_frombytes(A, pk, /*negate=*/true) && ok;
@@ -92,7 +98,6 @@ FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], co
   sc_reduce512(h, hram);
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;      // keep the recoding in range (S < L)
-  ge_cached tab[8];
   build_cached_table(tab, A);
   uint32_t hw[8], sw[8];
   sc_recode16(hw, h);
@@ -312,10 +317,13 @@ FE_INLINE void vrf_hash_points(uint32_t c[4], const uint32_t h[8], const uint32_
 // CACHED: the VRF key comes from k_keys.hip (kinfo[0] bit 0 = key valid,
 // kinfo[1..8] = canonical encoding of Y, ktab = tables of -Y at 2^0, 2^64,
 // 2^128) and U runs on a 16-window chain over the four fixed-base tables.
+// vt: the lane's 16-entry table region (see ed25519_verify_core): {1..8}H, {1..8}(-Gamma)
+// and, uncached, {1..8}(-Y) in its first half before H's table replaces it.
 template <bool CACHED>
 FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t pk[8], const uint32_t gamma[8],
                                const uint32_t c4[4], const uint32_t s8[8], const uint32_t alpha[8],
-                               const ge_niels* __restrict__ btab, const ge_cached* __restrict__ ktab = nullptr,
+                               const ge_niels* __restrict__ btab, ge_cached* __restrict__ vt,
+                               const ge_cached* __restrict__ ktab = nullptr,
                                const uint32_t* __restrict__ kinfo = nullptr) {
   // vrf_validate_key: small order -> reject; ge25519_frombytes must succeed
   bool ok;
@@ -353,7 +361,7 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
     ge_p3 nY = Y;
     fe_neg(nY.X, Y.X);
     fe_neg(nY.T, Y.T);
-    ge_cached ty[8];
+    ge_cached* ty = vt;
     build_cached_table(ty, nY);
     uint32_t cw[8], sw[8];
     sc_recode16(cw, c);
@@ -366,7 +374,8 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
     ge_p3 nG = G;
     fe_neg(nG.X, G.X);
     fe_neg(nG.T, G.T);
-    ge_cached th[8], tg[8];
+    ge_cached* th = vt;
+    ge_cached* tg = vt + 8;
     build_cached_table(th, H);
     build_cached_table(tg, nG);
     uint32_t sw[8], cw[8];

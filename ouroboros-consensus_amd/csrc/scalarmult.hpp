@@ -56,7 +56,7 @@ FE_INLINE void shl_const(uint32_t w[NW]) {          // w <<= BITS (compile-time)
 }
 
 // table[k] = (k+1) * P in cached form
-FE_INLINE void build_cached_table(ge_cached tab[8], const ge_p3& P) {
+FE_INLINE void build_cached_table(ge_cached* __restrict__ tab, const ge_p3& P) {
   ge_p3 acc, P2;
   ge_p1p1 t;
   ge_p3_to_cached(tab[0], P);
