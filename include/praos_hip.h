@@ -83,7 +83,14 @@ enum praos_verdict {
   PRAOS_V_VRF_KEY_WRONG = 9,
   PRAOS_V_VRF_BAD_PROOF = 10,
   PRAOS_V_LEADER_TOO_BIG = 11,
-  PRAOS_V_INPUT = 12
+  PRAOS_V_INPUT = 12,
+  /* envelope (praos_validate_headers only): HeaderEnvelopeError, then PraosEnvelopeError */
+  PRAOS_V_ENV_BLOCK_NO = 13,      /* UnexpectedBlockNo expected actual */
+  PRAOS_V_ENV_SLOT_NO = 14,       /* UnexpectedSlotNo expected actual */
+  PRAOS_V_ENV_PREV_HASH = 15,     /* UnexpectedPrevHash oldTip actual */
+  PRAOS_V_ENV_OBSOLETE_NODE = 16, /* ObsoleteNode lvProtVerMajor maxMajorPV */
+  PRAOS_V_ENV_HEADER_SIZE = 17,   /* HeaderSizeTooLarge size max */
+  PRAOS_V_ENV_BLOCK_SIZE = 18     /* BlockSizeTooLarge size max */
 };
 
 typedef struct praos_ctx praos_ctx;
@@ -367,6 +374,35 @@ int praos_update_chain_dep_state(praos_ctx* ctx, const praos_headers* h, const u
                                  const uint8_t* prev_is_genesis, const praos_out* crypto,
                                  const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict,
                                  size_t* chain_stop, size_t* processed);
+
+/* ---- validateHeader over a batch (HeaderValidation.hs:413-432) ----
+ * The envelope first -- validateEnvelope (:297-344: block number = tip + 1 (0 after
+ * Origin), slot >= tip slot + 1 (>= 0 after Origin), prev hash = tip hash (GenesisHash
+ * after Origin)) and the Praos additionalEnvelopeChecks (Shelley/Protocol/Praos.hs:66-80:
+ * ObsoleteNode, HeaderSizeTooLarge, BlockSizeTooLarge) -- then updateChainDepState as
+ * praos_update_chain_dep_state does.  The tip advances with every valid header; on
+ * return env's tip (like st) is the one at chain_stop.  Per-header inputs come from
+ * the decoder (praos_decoded: block_no, header_hash, body_size; header_size = the
+ * stored header length). */
+typedef struct {
+  const uint64_t* block_no;       /* n: hbBlockNo */
+  const uint8_t* header_hash;     /* n*32: headerHash (Blake2b-256 of the header bytes) */
+  const uint32_t* header_size;    /* n: bhviewHSize, bytes of the serialised header */
+  const uint32_t* body_size;      /* n: bhviewBSize = hbBodySize */
+  int32_t tip_is_origin;          /* HeaderState tip before the batch (in / out) */
+  uint64_t tip_slot;
+  uint64_t tip_block_no;
+  uint8_t tip_hash[32];
+  uint64_t max_major_pv;          /* praosMaxMajorPV */
+  uint64_t lv_prot_major;         /* pvMajor (lvProtocolVersion lv) */
+  uint64_t max_header_size;       /* lvMaxHeaderSize */
+  uint64_t max_body_size;         /* lvMaxBodySize */
+} praos_envelope;
+
+int praos_validate_headers(praos_ctx* ctx, const praos_headers* h, const uint8_t* prev_hash,
+                           const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
+                           const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict, size_t* chain_stop,
+                           size_t* processed);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

@@ -19,7 +19,9 @@ BIT_KES_MERKLE, BIT_KES_LEAF = 0x8, 0x10
 BIT_VRF_KEY_UNKNOWN, BIT_VRF_KEY_WRONG, BIT_VRF_PROOF, BIT_VRF_OUTPUT, BIT_LEADER = 0x100, 0x200, 0x400, 0x800, 0x1000
 BIT_INPUT = 0x8000
 (V_OK, V_KES_BEFORE_START, V_KES_AFTER_END, V_OCERT_SIG, V_KES_SIG, V_COUNTER_MISSING, V_COUNTER_TOO_SMALL,
- V_COUNTER_OVER_INC, V_VRF_KEY_UNKNOWN, V_VRF_KEY_WRONG, V_VRF_BAD_PROOF, V_LEADER_TOO_BIG, V_INPUT) = range(13)
+ V_COUNTER_OVER_INC, V_VRF_KEY_UNKNOWN, V_VRF_KEY_WRONG, V_VRF_BAD_PROOF, V_LEADER_TOO_BIG, V_INPUT,
+ V_ENV_BLOCK_NO, V_ENV_SLOT_NO, V_ENV_PREV_HASH, V_ENV_OBSOLETE_NODE, V_ENV_HEADER_SIZE,
+ V_ENV_BLOCK_SIZE) = range(19)
 
 
 def verdict(b, m, n):
@@ -51,6 +53,24 @@ def verdict(b, m, n):
     return V_OK
 
 
+def envelope_verdict(env, tip, i, slot, prev_hash):
+    """validateEnvelope (HeaderValidation.hs:297-344) + Praos envelopeChecks
+    (Shelley/Protocol/Praos.hs:66-80); tip = None (Origin) or (slot, block_no, hash)."""
+    if env["block_no"][i] != (0 if tip is None else tip[1] + 1):
+        return V_ENV_BLOCK_NO
+    if not slot >= (0 if tip is None else tip[0] + 1):
+        return V_ENV_SLOT_NO
+    if not ((prev_hash is None) if tip is None else (prev_hash is not None and bytes(prev_hash) == tip[2])):
+        return V_ENV_PREV_HASH
+    if not env["lv_prot_major"] <= env["max_major_pv"]:
+        return V_ENV_OBSOLETE_NODE
+    if not env["header_size"][i] <= env["max_header_size"]:
+        return V_ENV_HEADER_SIZE
+    if not env["body_size"][i] <= env["max_body_size"]:
+        return V_ENV_BLOCK_SIZE
+    return V_OK
+
+
 def combine(a, b):
     """Nonce semigroup (⭒)."""
     if a is None:
@@ -79,15 +99,20 @@ def _copy(st):
     return {k: (dict(v) if isinstance(v, dict) else v) for k, v in st.items()}
 
 
-def fold(st, hk, slots, bits, ocert_n, nonces, prev_hash, known, eta0, base_slot, base_no, length, window):
+def fold(st, hk, slots, bits, ocert_n, nonces, prev_hash, known, eta0, base_slot, base_no, length, window,
+         env=None):
     """st: dict(last_slot (None = Origin), counters, evolving, candidate, epoch_nonce, lab, leb).
     Returns (verdicts, chain_stop, processed).  st is updated in place to the state the
     reference chain reaches: after the last valid header before the first invalid one
     (the reference stops the chain there).  Verdicts of later headers are would-be
-    verdicts, judged against a working copy that skips the invalid headers."""
+    verdicts, judged against a working copy that skips the invalid headers.  env (optional):
+    validateHeader's envelope checks first (envelope_verdict); env["tip"] is the chain tip,
+    updated like st."""
     def epoch(s):
         return base_no + (s - base_slot) // length
     w = _copy(st)
+    if env is not None:
+        w["tip"] = env["tip"]
     frozen = None
     out, stop = [], None
     i = 0
@@ -104,6 +129,9 @@ def fold(st, hk, slots, bits, ocert_n, nonces, prev_hash, known, eta0, base_slot
             break
         m = w["counters"].get(hk[i], 0 if hk[i] in known else None)
         v = verdict(int(bits[i]), m, int(ocert_n[i]))
+        if env is not None and v != V_INPUT:
+            ve = envelope_verdict(env, w["tip"], i, s, prev_hash[i])
+            v = ve if ve != V_OK else v
         out.append(v)
         if v != V_OK:
             if stop is None:
@@ -117,7 +145,12 @@ def fold(st, hk, slots, bits, ocert_n, nonces, prev_hash, known, eta0, base_slot
         if s + window < base_slot + (e_new - base_no + 1) * length:
             w["candidate"] = w["evolving"]
         w["counters"][hk[i]] = int(ocert_n[i])
+        if env is not None:
+            w["tip"] = (s, int(env["block_no"][i]), bytes(env["header_hash"][i]))
     processed = i
+    res = frozen if frozen is not None else w
+    if env is not None:
+        env["tip"] = res.pop("tip")
     st.clear()
-    st.update(frozen if frozen is not None else w)
+    st.update(res)
     return out, min(len(slots) if stop is None else stop, processed), processed

@@ -936,12 +936,38 @@ int praos_apply_batch(praos_ctx* c, const praos_headers* h, const praos_out* cry
   return PRAOS_OK;
 }
 
-int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash,
-                                 const uint8_t* prev_is_genesis, const praos_out* crypto,
-                                 const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict,
-                                 size_t* chain_stop, size_t* processed) {
+}  // extern "C"
+
+// validateEnvelope (HeaderValidation.hs:297-344) with the Praos additionalEnvelopeChecks
+// (envelopeChecks, Shelley/Protocol/Praos.hs:66-80), against the tip the chain has
+// reached (AnnTip: slot, block number, header hash).  First failure in that order.
+struct EnvTip {
+  int32_t origin;
+  uint64_t slot, block_no;
+  uint8_t hash[32];
+};
+static uint8_t envelope_verdict(const praos_envelope* e, const EnvTip& tip, const praos_headers* h,
+                                const uint8_t* prev_hash, const uint8_t* prev_is_genesis, size_t i) {
+  const uint64_t expected_block = tip.origin ? 0 : tip.block_no + 1;     // expectedFirstBlockNo / succ
+  if (e->block_no[i] != expected_block) return PRAOS_V_ENV_BLOCK_NO;
+  const uint64_t min_slot = tip.origin ? 0 : tip.slot + 1;                // minimumPossibleSlotNo / succ
+  if (!(h->slot[i] >= min_slot)) return PRAOS_V_ENV_SLOT_NO;
+  const bool genesis = prev_is_genesis && prev_is_genesis[i];
+  const bool prev_ok = tip.origin ? genesis : (!genesis && std::memcmp(prev_hash + 32 * i, tip.hash, 32) == 0);
+  if (!prev_ok) return PRAOS_V_ENV_PREV_HASH;                             // checkPrevHash'
+  if (!(e->lv_prot_major <= e->max_major_pv)) return PRAOS_V_ENV_OBSOLETE_NODE;
+  if (!((uint64_t)e->header_size[i] <= e->max_header_size)) return PRAOS_V_ENV_HEADER_SIZE;
+  if (!((uint64_t)e->body_size[i] <= e->max_body_size)) return PRAOS_V_ENV_BLOCK_SIZE;
+  return PRAOS_V_OK;
+}
+
+static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
+                     const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei,
+                     praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed) {
   if (!c || !h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash ||
       ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter)))
+    return PRAOS_E_ARG;
+  if (env && h->n && (!env->block_no || !env->header_hash || !env->header_size || !env->body_size))
     return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
   praos_nonce eta0{};
@@ -962,8 +988,15 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
     std::vector<uint64_t> ctr;
     std::map<std::string, size_t> where;
     praos_nonce evolving, candidate, epoch_nonce, lab, leb;
+    EnvTip tip;
   };
   Work W;
+  if (env) {
+    W.tip.origin = env->tip_is_origin;
+    W.tip.slot = env->tip_slot;
+    W.tip.block_no = env->tip_block_no;
+    std::memcpy(W.tip.hash, env->tip_hash, 32);
+  }
   W.origin = st->last_slot_origin;
   W.last_slot = st->last_slot;
   for (size_t k = 0; k < st->m; k++) {
@@ -993,7 +1026,12 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
     const uint64_t n = h->ocert_n[i];
     auto it = W.where.find(hk);
     const bool have = it != W.where.end() || c->pool_by_hash.count(hk);
-    const uint8_t v = header_verdict(crypto->bits[i], have, it != W.where.end() ? W.ctr[it->second] : 0, n);
+    uint8_t v = header_verdict(crypto->bits[i], have, it != W.where.end() ? W.ctr[it->second] : 0, n);
+    // validateHeader (HeaderValidation.hs:419-428): the envelope before the protocol checks
+    if (env && v != PRAOS_V_INPUT) {
+      const uint8_t ve = envelope_verdict(env, W.tip, h, prev_hash, prev_is_genesis, i);
+      if (ve != PRAOS_V_OK) v = ve;
+    }
     verdict[i] = v;
     if (v != PRAOS_V_OK) {
       if (!frozen) { F = W; frozen = true; stop = i; }
@@ -1020,6 +1058,12 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
       W.keys.push_back(hk);
       W.ctr.push_back(n);
     }
+    if (env) {                                       // HeaderState tip := getAnnTip hdr
+      W.tip.origin = 0;
+      W.tip.slot = slot;
+      W.tip.block_no = env->block_no[i];
+      std::memcpy(W.tip.hash, env->header_hash + 32 * i, 32);
+    }
   }
   const Work& R = frozen ? F : W;
   if (R.keys.size() > st->cap) { c->err = "counter map capacity exceeded"; return PRAOS_E_ARG; }
@@ -1032,10 +1076,35 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
   st->m = R.keys.size();
   st->evolving = R.evolving; st->candidate = R.candidate; st->epoch_nonce = R.epoch_nonce;
   st->lab = R.lab; st->last_epoch_block = R.leb;
+  if (env) {
+    env->tip_is_origin = R.tip.origin;
+    env->tip_slot = R.tip.slot;
+    env->tip_block_no = R.tip.block_no;
+    std::memcpy(env->tip_hash, R.tip.hash, 32);
+  }
   if (chain_stop) *chain_stop = std::min(stop, i);
   if (processed) *processed = i;
   return PRAOS_OK;
 }
+
+extern "C" {
+
+int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash,
+                                 const uint8_t* prev_is_genesis, const praos_out* crypto,
+                                 const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict,
+                                 size_t* chain_stop, size_t* processed) {
+  return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, nullptr, ei, st, verdict, chain_stop, processed);
+}
+
+int praos_validate_headers(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash,
+                           const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
+                           const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict, size_t* chain_stop,
+                           size_t* processed) {
+  if (!env) return PRAOS_E_ARG;
+  return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, env, ei, st, verdict, chain_stop, processed);
+}
+
+
 
 // ---------------------------------------------------------------- generator
 }  // extern "C"

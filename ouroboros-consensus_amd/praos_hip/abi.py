@@ -46,7 +46,8 @@ BIT_TP_VRF_LEADER = 0x0800
 # verdicts (enum praos_verdict)
 V_OK, V_KES_BEFORE_START, V_KES_AFTER_END, V_OCERT_SIG, V_KES_SIG, V_COUNTER_MISSING, \
     V_COUNTER_TOO_SMALL, V_COUNTER_OVER_INC, V_VRF_KEY_UNKNOWN, V_VRF_KEY_WRONG, V_VRF_BAD_PROOF, \
-    V_LEADER_TOO_BIG, V_INPUT = range(13)
+    V_LEADER_TOO_BIG, V_INPUT, V_ENV_BLOCK_NO, V_ENV_SLOT_NO, V_ENV_PREV_HASH, V_ENV_OBSOLETE_NODE, \
+    V_ENV_HEADER_SIZE, V_ENV_BLOCK_SIZE = range(19)
 
 
 class Params(ctypes.Structure):
@@ -93,6 +94,14 @@ class ChainState(ctypes.Structure):
 class EpochInfo(ctypes.Structure):
     _fields_ = [("epoch_base_slot", ctypes.c_uint64), ("epoch_base_no", ctypes.c_uint64),
                 ("epoch_length", ctypes.c_uint64), ("stability_window", ctypes.c_uint64)]
+
+
+class Envelope(ctypes.Structure):
+    _fields_ = [("block_no", u64p), ("header_hash", u8p), ("header_size", u32p), ("body_size", u32p),
+                ("tip_is_origin", ctypes.c_int32), ("tip_slot", ctypes.c_uint64), ("tip_block_no", ctypes.c_uint64),
+                ("tip_hash", ctypes.c_uint8 * 32), ("max_major_pv", ctypes.c_uint64),
+                ("lv_prot_major", ctypes.c_uint64), ("max_header_size", ctypes.c_uint64),
+                ("max_body_size", ctypes.c_uint64)]
 
 
 class Counters(ctypes.Structure):
@@ -160,6 +169,10 @@ SIGNATURES = {
                                                     ctypes.POINTER(Out), ctypes.POINTER(EpochInfo),
                                                     ctypes.POINTER(ChainState), u8p, ctypes.POINTER(ctypes.c_size_t),
                                                     ctypes.POINTER(ctypes.c_size_t)]),
+    "praos_validate_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), u8p, u8p, ctypes.POINTER(Out),
+                                              ctypes.POINTER(Envelope), ctypes.POINTER(EpochInfo),
+                                              ctypes.POINTER(ChainState), u8p, ctypes.POINTER(ctypes.c_size_t),
+                                              ctypes.POINTER(ctypes.c_size_t)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -451,10 +464,14 @@ class Context:
         self.check(self.L.praos_batch_download_decoded(self.h, b, ctypes.byref(d)))
         return D
 
-    def update_chain_dep_state(self, H, crypto, prev_hash, state: dict, epoch_info, prev_is_genesis=None):
+    def update_chain_dep_state(self, H, crypto, prev_hash, state: dict, epoch_info, prev_is_genesis=None,
+                               envelope=None):
         """state: dict(last_slot (None = Origin), counters {hash28: n}, evolving, candidate, epoch_nonce,
         lab, leb) with nonces None (Neutral) or 32 bytes; updated in place.  epoch_info: (base_slot,
-        base_no, length, stability_window).  Returns (verdict u8[n], chain_stop, processed)."""
+        base_no, length, stability_window).  envelope (praos_validate_headers): dict(block_no u64[n],
+        header_hash u8[n,32], header_size u32[n], body_size u32[n], tip (None = Origin, or (slot,
+        block_no, hash32)), max_major_pv, lv_prot_major, max_header_size, max_body_size); its "tip" is
+        updated in place.  Returns (verdict u8[n], chain_stop, processed)."""
         n = len(H["slot"])
         hs = self.headers_struct(H)
         os_ = self.out_struct(crypto)
@@ -485,10 +502,30 @@ class Context:
         pg = None if prev_is_genesis is None else np.ascontiguousarray(prev_is_genesis, dtype=np.uint8)
         verdict = np.zeros(n, np.uint8)
         stop, done = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        self.check(self.L.praos_update_chain_dep_state(self.h, ctypes.byref(hs), ptr(ph),
-                                                       ptr(pg) if pg is not None else None, ctypes.byref(os_),
-                                                       ctypes.byref(ei), ctypes.byref(st), ptr(verdict),
-                                                       ctypes.byref(stop), ctypes.byref(done)))
+        if envelope is None:
+            self.check(self.L.praos_update_chain_dep_state(self.h, ctypes.byref(hs), ptr(ph),
+                                                           ptr(pg) if pg is not None else None, ctypes.byref(os_),
+                                                           ctypes.byref(ei), ctypes.byref(st), ptr(verdict),
+                                                           ctypes.byref(stop), ctypes.byref(done)))
+        else:
+            E = Envelope()
+            arrs = {k: np.ascontiguousarray(envelope[k], dtype=dt) for k, dt in
+                    (("block_no", np.uint64), ("header_hash", np.uint8), ("header_size", np.uint32),
+                     ("body_size", np.uint32))}
+            E.block_no, E.header_hash = ptr(arrs["block_no"], u64p), ptr(arrs["header_hash"])
+            E.header_size, E.body_size = ptr(arrs["header_size"], u32p), ptr(arrs["body_size"], u32p)
+            tip = envelope["tip"]
+            E.tip_is_origin = int(tip is None)
+            if tip is not None:
+                E.tip_slot, E.tip_block_no = tip[0], tip[1]
+                ctypes.memmove(E.tip_hash, bytes(tip[2]), 32)
+            for k in ("max_major_pv", "lv_prot_major", "max_header_size", "max_body_size"):
+                setattr(E, k, envelope[k])
+            self.check(self.L.praos_validate_headers(self.h, ctypes.byref(hs), ptr(ph),
+                                                     ptr(pg) if pg is not None else None, ctypes.byref(os_),
+                                                     ctypes.byref(E), ctypes.byref(ei), ctypes.byref(st),
+                                                     ptr(verdict), ctypes.byref(stop), ctypes.byref(done)))
+            envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no), bytes(E.tip_hash))
         state["last_slot"] = None if st.last_slot_origin else int(st.last_slot)
         state["counters"] = {bytes(hk[28 * k:28 * k + 28]): int(cv[k]) for k in range(st.m)}
         for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),

@@ -162,3 +162,82 @@ def test_host_only_refuses_gpu_calls(hctx):
     H, crypto, prev, hk = _batch(r, 4, pools, 0, 5)
     with pytest.raises(abi.PraosError):
         hctx.verify_headers(H)
+
+
+def _envelope_chain(r, n, first_slot, tip, kind, at):
+    """Block numbers / slots / header hashes of a linked chain after `tip`; header `at`
+    mutated by `kind` (every later header then fails too: the tip stays before it)."""
+    bn0 = 0 if tip is None else tip[1] + 1
+    block_no = np.array([bn0 + i for i in range(n)], np.uint64)
+    slots = np.array([first_slot + 3 * i + r.randrange(3) for i in range(n)], np.uint64)
+    hh = [_b2b(b"hdr" + bytes([i % 256, i // 256])) for i in range(n)]
+    prev = [tip[2] if tip is not None else None] + hh[:-1]
+    hsize = np.array([r.choice([600, 849, 1100]) for _ in range(n)], np.uint32)
+    bsize = np.array([r.randrange(0, 90_000) for _ in range(n)], np.uint32)
+    if kind == "block_no":
+        block_no[at] += r.choice([1, 2])
+    elif kind == "slot":
+        slots[at] = slots[at - 1]
+    elif kind == "prev":
+        prev[at] = _b2b(b"fork")
+    elif kind == "genesis":
+        prev[at] = None
+    elif kind == "hsize":
+        hsize[at] = 1101
+    elif kind == "bsize":
+        bsize[at] = 90_113
+    return block_no, slots, hh, prev, hsize, bsize
+
+
+ENV_KINDS = {"ok": 0, "block_no": 13, "slot": 14, "prev": 15, "genesis": 15, "hsize": 17, "bsize": 18}
+
+
+@pytest.mark.parametrize("origin", [True, False])
+@pytest.mark.parametrize("kind", sorted(ENV_KINDS))
+def test_validate_headers_envelope(hctx, kind, origin):
+    """praos_validate_headers = validateEnvelope + Praos envelopeChecks, then the protocol
+    verdicts (HeaderValidation.hs:413-432), against the oracle restatement: verdicts,
+    the chain state and the tip at the chain stop."""
+    r = random.Random(sum(map(ord, kind)) * 2 + origin)
+    pools = _pools(r, 5)
+    n, at = 60, 25
+    tip = None if origin else (4000, 77, _b2b(b"tip"))
+    H, crypto, _, hk = _batch(r, n, pools, 4100, 7)
+    block_no, slots, hh, prev, hsize, bsize = _envelope_chain(r, n, 4100, tip, kind, at)
+    H["slot"] = slots
+    crypto["bits"][:] = 0
+    crypto["bits"][40] = cs.BIT_VRF_PROOF             # a protocol failure after the envelope one
+    for i in range(n):
+        H["ocert_n"][i] = 0
+        if crypto["pool_idx"][i] < 0:
+            crypto["pool_idx"][i] = 0
+            hk[i] = pools[0][0]
+    prev_arr = np.array([list(p) if p is not None else [0] * 32 for p in prev], np.uint8)
+    genesis = np.array([p is None for p in prev], np.uint8)
+    eta = _b2b(b"epoch-env")
+    st = {"last_slot": None, "counters": {}, "evolving": eta, "candidate": eta, "epoch_nonce": eta, "lab": None,
+          "leb": None}
+    ref = {k: (dict(v) if isinstance(v, dict) else v) for k, v in st.items()}
+    env = {"block_no": block_no, "header_hash": np.array([list(x) for x in hh], np.uint8), "header_size": hsize,
+           "body_size": bsize, "tip": tip, "max_major_pv": 9, "lv_prot_major": 8, "max_header_size": 1100,
+           "max_body_size": 90_112}
+    renv = dict(env)
+    hctx.set_epoch(eta, pools, _params())
+    v, stop, done = hctx.update_chain_dep_state(H, crypto, prev_arr, st, (0, 0, 1_000_000, 129_600),
+                                                prev_is_genesis=genesis, envelope=env)
+    wv, wstop, wdone = cs.fold(ref, hk, slots, crypto["bits"], H["ocert_n"], crypto["nonce"], prev,
+                               {p[0] for p in pools}, eta, 0, 0, 1_000_000, 129_600, env=renv)
+    assert (done, stop) == (wdone, wstop) and list(v) == wv
+    assert st == ref and env["tip"] == renv["tip"]
+    want_stop = at if kind != "ok" else 40
+    assert stop == want_stop and wv[want_stop] == (ENV_KINDS[kind] if kind != "ok" else cs.V_VRF_BAD_PROOF)
+    assert all(x == cs.V_OK for x in wv[:want_stop])
+    assert env["tip"] == (int(slots[want_stop - 1]), int(block_no[want_stop - 1]), hh[want_stop - 1])
+    if kind == "ok":
+        # ObsoleteNode: the ledger view's protocol version above the node's maximum fails every header
+        env2 = dict(env, tip=tip, lv_prot_major=10)
+        st2 = {"last_slot": None, "counters": {}, "evolving": eta, "candidate": eta, "epoch_nonce": eta,
+               "lab": None, "leb": None}
+        v2, stop2, _ = hctx.update_chain_dep_state(H, crypto, prev_arr, st2, (0, 0, 1_000_000, 129_600),
+                                                   prev_is_genesis=genesis, envelope=env2)
+        assert stop2 == 0 and env2["tip"] == tip and v2[0] == cs.V_ENV_OBSOLETE_NODE
