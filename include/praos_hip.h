@@ -428,6 +428,14 @@ typedef struct {
   const uint64_t* sched_slot;
   const uint32_t* sched_pool;
   uint64_t block_no0;
+  /* Chain linking (CBOR bodies, Praos): link_prev = 1 makes hbPrev of header i the
+   * headerHash of header i-1 -- header 0 gets prev0, or GenesisHash when prev0 is NULL --
+   * re-signing each KES signature in order (sequential on the device: ~0.1 ms per
+   * header).  header_hash (optional, n*32) receives the header hashes (before any
+   * seeded corruption). */
+  int32_t link_prev;
+  const uint8_t* prev0;
+  uint8_t* header_hash;
 } praos_synth_params;
 
 /* Fills caller buffers (same layout as praos_headers; body_off/body_len/body_bytes

@@ -1,5 +1,6 @@
 // k_synth.hip -- synthetic chain generator kernels (db-synthesizer analogue).
 #include "kcommon.hpp"
+#include "arena.hpp"
 
 // ------------------------------------------------------------------ synthetic chain generator
 // seeds: Blake2b-256(tag || master seed(32) || BE32(i))
@@ -218,7 +219,8 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0,
     uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos,
     uint8_t* l_out, uint8_t* l_proof, const uint8_t* __restrict__ body_hash_in,
-    const uint64_t* __restrict__ sched_slot, const uint32_t* __restrict__ sched_pool, uint64_t block_no0) {
+    const uint64_t* __restrict__ sched_slot, const uint32_t* __restrict__ sched_pool, uint64_t block_no0,
+    uint32_t* __restrict__ leaf_of) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
   const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
@@ -320,6 +322,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   body_len[i] = bl;
   // KES: leaf t signs the body; path pairs from the tree (leaf level first)
   const uint32_t leaf = (uint32_t)t;
+  if (leaf_of) leaf_of[i] = kk * 64u + leaf;      // for k_synth_link
   uint32_t lpk[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[(8 * (size_t)kk * 64) + 8 * leaf + k]; lpk[k] = T[(64 + leaf) * 8 + k]; }
@@ -333,6 +336,70 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     store_words(ks + 64 * d, T + (2 * parent) * 8, 8);
     store_words(ks + 64 * d + 32, T + (2 * parent + 1) * 8, 8);
     node = parent;
+  }
+}
+
+// Chain linking (one lane, sequential): prevHash of header i := headerHash of header i-1
+// (HeaderValidation.hs:308-309 checks exactly that), so every KES signature has to be
+// redone in order -- the body, and with it the header hash, changes.  Header 0 gets
+// prev0, or GenesisHash (CBOR null, the body shrinks by 33 bytes) when prev0 is null.
+// headerHash = Blake2b-256 of the stored header [body, kesSig] (Praos/Header.hs:147-151).
+__global__ void __launch_bounds__(64) k_synth_link(size_t n, const ge_niels* gbtab, const uint8_t* __restrict__ prev0,
+                                                   const uint32_t* __restrict__ leaf_seed,
+                                                   const uint32_t* __restrict__ tree, const uint32_t* __restrict__ leaf_of,
+                                                   uint8_t* __restrict__ body_bytes, const uint64_t* __restrict__ body_off,
+                                                   uint32_t* __restrict__ body_len, uint8_t* __restrict__ kes_sig,
+                                                   uint8_t* __restrict__ hdr_scratch, uint8_t* __restrict__ header_hash) {
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
+  if (threadIdx.x != 0) return;
+  uint32_t prev[8];
+  bool genesis = prev0 == nullptr;
+  if (!genesis) load_words(prev, prev0, 8);
+  auto ulen = [](uint32_t ib) -> uint32_t {
+    const uint32_t ai = ib & 31u;
+    return ai < 24 ? 1u : ai == 24 ? 2u : ai == 25 ? 3u : ai == 26 ? 5u : 9u;
+  };
+  for (size_t i = 0; i < n; i++) {
+    uint8_t* b = body_bytes + body_off[i];
+    uint32_t bl = body_len[i];
+    uint32_t q = 1;
+    q += ulen(b[q]);                              // blockNo
+    q += ulen(b[q]);                              // slotNo; b[q] = 0x58 (bytes(32)) or 0xf6 (null)
+    if (genesis) {
+      if (b[q] == 0x58) {                         // bytes(32) -> null: shift the tail left by 33
+        for (uint32_t k = q + 1; k + 33 < bl; k++) b[k] = b[k + 33];
+        b[q] = 0xf6;
+        bl -= 33;
+        for (uint32_t k = bl; k < ((bl + 7) & ~7u) + 8 && k < 448; k++) b[k] = 0;
+        body_len[i] = bl;
+      }
+    } else {
+      if (b[q] != 0x58) return;                   // not produced by k_synth_headers
+      for (int k = 0; k < 32; k++) b[q + 2 + k] = (uint8_t)(prev[k / 4] >> (8 * (k % 4)));
+    }
+    // KES leaf signature over the new body (the Merkle path of the signature is unchanged)
+    const uint32_t li = leaf_of[i];
+    const uint32_t* T = tree + (size_t)(li / 64u) * 128 * 8;
+    uint32_t seed[8], lpk[8], az[16], sig[16];
+#pragma unroll
+    for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[8 * (size_t)li + k]; lpk[k] = T[(64 + li % 64u) * 8 + k]; }
+    ed25519_expand(az, seed);
+    ed25519_sign_core(sig, az, lpk, b, bl, btab);
+    uint8_t* ks = kes_sig + 448 * i;
+    store_words(ks, sig, 16);
+    // header bytes [body, kesSig] -> Blake2b-256
+    uint8_t* h = hdr_scratch;
+    h[0] = 0x82;
+    for (uint32_t k = 0; k < bl; k++) h[1 + k] = b[k];
+    h[1 + bl] = 0x59; h[2 + bl] = 0x01; h[3 + bl] = 0xc0;
+    for (uint32_t k = 0; k < 448; k++) h[4 + bl + k] = ks[k];
+    uint32_t hh[8];
+    b2b256_range(hh, h, 0, 4 + bl + 448);
+    if (header_hash) store_words(header_hash + 32 * i, hh, 8);
+#pragma unroll
+    for (int k = 0; k < 8; k++) prev[k] = hh[k];
+    genesis = false;
   }
 }
 
@@ -356,7 +423,7 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
     int32_t q = 1;
     q += ulen(b[q]);                       // blockNo
     q += ulen(b[q]);                       // slotNo
-    q += 34 + 34 + 34 + 1;                 // prevHash, vk, vrfVk, [ of the cert
+    q += (b[q] == 0xf6 ? 1 : 34) + 34 + 34 + 1;   // prevHash (or GenesisHash null), vk, vrfVk, [ of the cert
     at_vrf_out = q + 2;
     q += 66;
     at_vrf_proof = q + 2;
@@ -418,12 +485,19 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len,
                           uint8_t* body_bytes, int tpraos, uint8_t* l_out, uint8_t* l_proof,
                           const uint8_t* body_hash_in, const uint64_t* sched_slot, const uint32_t* sched_pool,
-                          uint64_t block_no0) {
+                          uint64_t block_no0, uint32_t* leaf_of) {
   hipLaunchKernelGGL(k_synth_headers, grid, block, 0, stream, n, gbtab, npools, nkes, first_slot, slot_stride,
                      slots_per_kes_period, blen, salt, eta0, eta0_neutral, cold_seed, cold_pk, vrf_seed, vrf_pk,
                      leaf_seed, tree, msg_scratch, slot, cold_vk, vrf_vk, vrf_out, vrf_proof, hot_vk, ocert_n,
                      ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, tpraos, l_out, l_proof,
-                     body_hash_in, sched_slot, sched_pool, block_no0);
+                     body_hash_in, sched_slot, sched_pool, block_no0, leaf_of);
+}
+void launch_synth_link(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
+                       const uint32_t* leaf_seed, const uint32_t* tree, const uint32_t* leaf_of, uint8_t* body_bytes,
+                       const uint64_t* body_off, uint32_t* body_len, uint8_t* kes_sig, uint8_t* hdr_scratch,
+                       uint8_t* header_hash) {
+  hipLaunchKernelGGL(k_synth_link, grid, block, 0, stream, n, gbtab, prev0, leaf_seed, tree, leaf_of, body_bytes,
+                     body_off, body_len, kes_sig, hdr_scratch, header_hash);
 }
 void launch_synth_vrf_scalar(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const uint32_t* vrf_seed,
                              uint32_t* vrf_x) {

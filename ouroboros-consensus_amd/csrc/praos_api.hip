@@ -1160,6 +1160,12 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
       if (sp->sched_pool[i] >= np) { c->err = "sched_pool out of range"; return PRAOS_E_ARG; }
   const uint64_t* dss = sp->sched_slot ? s.up(sp->sched_slot, 8 * n) : nullptr;
   const uint32_t* dsp = sp->sched_pool ? s.up(sp->sched_pool, 4 * n) : nullptr;
+  const bool link = sp->link_prev != 0;
+  if (link && (sp->body_len != 0 || tpraos)) { c->err = "link_prev needs CBOR Praos bodies (body_len 0)"; return PRAOS_E_ARG; }
+  auto dleaf = s.zeros<uint32_t>(4 * n);
+  auto dprev0 = link && sp->prev0 ? s.up(sp->prev0, 32) : nullptr;
+  auto dhscr = s.zeros<uint8_t>(link ? 1024 + 16 : 16);
+  auto dhh = s.zeros<uint8_t>(link ? 32 * n : 16);
   if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
   uint64_t salt = 0;
   std::memcpy(&salt, sp->seed, 8);
@@ -1173,7 +1179,10 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
                        (uint32_t)nk, sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
                        dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof,
-                       sp->body_len == 0 && !tpraos ? dbh : nullptr, dss, dsp, sp->block_no0);
+                       sp->body_len == 0 && !tpraos ? dbh : nullptr, dss, dsp, sp->block_no0, dleaf);
+    if (link)
+      launch_synth_link(dim3(1), dim3(64), c->stream, n, c->btab, dprev0, leaf_seed, tree, dleaf, dbody, doff, dlen,
+                        dksig, dhscr, dhh);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
                        salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
                        sp->body_len == 0 ? 1 : 0);
@@ -1200,6 +1209,7 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
     r |= dn2h(kes_sig, dksig, 448 * n); r |= dn2h(body_off, doff, 8 * n); r |= dn2h(body_len, dlen, 4 * n);
     r |= dn2h(body_bytes, dbody, bstride * n + 8); r |= dn2h(corrupted, dcor, n);
     if (tpraos) { r |= dn2h(leader_out, dlout, 64 * n); r |= dn2h(leader_proof, dlproof, 80 * n); }
+    if (link) r |= dn2h(sp->header_hash, dhh, 32 * n);
     if (r != PRAOS_OK) return PRAOS_E_HIP;
   }
   return PRAOS_OK;

@@ -112,7 +112,8 @@ class SynthParams(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("npools", ctypes.c_uint32), ("first_slot", ctypes.c_uint64),
                 ("slot_stride", ctypes.c_uint64), ("body_len", ctypes.c_uint32),
                 ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32),
-                ("body_hash", u8p), ("sched_slot", u64p), ("sched_pool", u32p), ("block_no0", ctypes.c_uint64)]
+                ("body_hash", u8p), ("sched_slot", u64p), ("sched_pool", u32p), ("block_no0", ctypes.c_uint64),
+                ("link_prev", ctypes.c_int32), ("prev0", u8p), ("header_hash", u8p)]
 
 
 class HeaderBytes(ctypes.Structure):
@@ -603,10 +604,18 @@ class Context:
 
     def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
                    body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False, body_hash=None, schedule=None,
-                   block_no0=0):
+                   block_no0=0, link=False, prev0=None):
         """schedule: (slots u64[n], pools u32[n]) from leader_schedule (a leader-valid chain), or None
-        (evenly spaced slots, pools by hash: not leader-valid)."""
+        (evenly spaced slots, pools by hash: not leader-valid).  link=True chains the headers
+        (prevHash = headerHash of the previous header; header 0: prev0, None = GenesisHash) and
+        returns the header hashes in H["header_hash"]."""
         sp = SynthParams()
+        if link:
+            hh_out = np.zeros((n, 32), np.uint8)
+            sp.link_prev, sp.header_hash = 1, ptr(hh_out)
+            if prev0 is not None:
+                p0 = np.frombuffer(bytes(prev0), np.uint8).copy()
+                sp.prev0 = ptr(p0)
         if body_hash is not None:   # n*32 hbBodyHash values for the CBOR bodies (body_len=0)
             body_hash = np.ascontiguousarray(body_hash, dtype=np.uint8).reshape(n, 32)
             sp.body_hash = ptr(body_hash)
@@ -649,6 +658,8 @@ class Context:
         else:
             self.check(self.L.praos_synthesize(*common, ptr(corrupted)))
         H["body_bytes"] = H["body_bytes"][:bstride * n]
+        if link:
+            H["header_hash"] = hh_out
         pool_list = [(bytes(p.hash28), bytes(p.vrf_hash32)) for p in pools]
         return H, pool_list, corrupted
 

@@ -83,16 +83,19 @@ def load_schedule(name="c5"):
     return slots, z["pool"].astype(np.uint32)
 
 
-def make_chain(ctx, cfg, schedule, n=None, corrupt_per_10000=0, cbor_bodies=True, body_len=397, nkes=0):
+def make_chain(ctx, cfg, schedule, n=None, corrupt_per_10000=0, cbor_bodies=True, body_len=397, nkes=0, link=False,
+               prev0=None):
     """Sign the first n blocks of a schedule.  Returns (H, pool_list, corrupted, params)
-    with pool_list = [(hash28, vrf_hash32, sigma_fp)] in forger order."""
+    with pool_list = [(hash28, vrf_hash32, sigma_fp)] in forger order.  link=True: a real
+    chain, hbPrev = headerHash of the previous block (block 0: prev0, None = GenesisHash),
+    H["header_hash"] holds the header hashes (sequential re-signing, ~0.1 ms per block)."""
     slots, pools = schedule
     n = len(slots) if n is None else n
     p = params(cfg)
     H, keys, corrupted = ctx.synthesize(n, cfg["npools"], p, cfg["eta0"], cfg["seed"],
                                         body_len=0 if cbor_bodies else body_len,
                                         corrupt_per_10000=corrupt_per_10000, nkes=nkes,
-                                        schedule=(slots[:n], pools[:n]))
+                                        schedule=(slots[:n], pools[:n]), link=link, prev0=prev0)
     sig = stake(cfg["npools"], cfg["stake_offset"])
     pool_list = [(h, v, s) for (h, v), s in zip(keys, sig)]
     return H, pool_list, corrupted, p

@@ -154,3 +154,78 @@ def test_c5_shaped_batch(ctx, oracle):
         assert bytes(o["nonce"][i]) == r["nonce"]
         assert int(o["pool_idx"][i]) == hash_of.get(r["issuer_hash"], -1)
     assert abi.BIT_LEADER not in {int(x) & abi.BIT_LEADER for x in o["bits"][clean]}
+
+
+def _validate_from_bytes(ctx, cfg, H, tip=None):
+    """Stored headers -> GPU decode + crypto -> praos_validate_headers (envelope + protocol)."""
+    import hashlib
+    from praos_hip.chunk import pack_chunk
+    arena, off, ln = pack_chunk(H)
+    o, D = ctx.verify_header_bytes(arena, off, ln, decoded=True)
+    n = len(off)
+    eta = cfg["eta0"]
+    st = {"last_slot": None, "counters": {}, "evolving": eta, "candidate": eta, "epoch_nonce": eta, "lab": None,
+          "leb": None}
+    env = {"block_no": D["block_no"], "header_hash": D["header_hash"], "header_size": ln,
+           "body_size": D["body_size"], "tip": tip, "max_major_pv": 9, "lv_prot_major": 8, "max_header_size": 1100,
+           "max_body_size": 90_112}
+    Hs = dict(H, slot=D["slot"], ocert_n=D["ocert_n"])
+    ref_in = (dict(st), dict(env))
+    v, stop, done = ctx.update_chain_dep_state(Hs, o, D["prev_hash"], st, (0, 0, cfg["epoch_length"], 129_600),
+                                               prev_is_genesis=D["prev_is_genesis"], envelope=env)
+    return o, D, v, stop, done, st, env, ref_in, ln
+
+
+def test_linked_chain_validate_headers(ctx, oracle):
+    """A real chain (hbPrev = headerHash of the previous block, GenesisHash first) of the
+    configs[0] pools: stored bytes -> GPU decode + crypto -> validateHeader over the batch
+    (envelope + updateChainDepState): every header valid, the tip is the last header; the
+    same with seeded corruptions stops exactly at the first corrupted header, verdicts and
+    state equal to the oracle's fold."""
+    import chainstate as cs
+    from praos_hip import chains
+    cfg = chains.CONFIGS["c1"]
+    sched = chains.search_schedule(ctx, cfg, 1500, window=40_000)
+    H, pool_list, corrupted, p = chains.make_chain(ctx, cfg, sched, link=True)
+    ctx.set_epoch(cfg["eta0"], pool_list, p)
+    o, D, v, stop, done, st, env, _, ln = _validate_from_bytes(ctx, cfg, H)
+    n = len(sched[0])
+    assert (D["status"] & 0x5F == 0).all() and D["prev_is_genesis"][0] == 1 and D["prev_is_genesis"][1:].sum() == 0
+    assert (D["header_hash"] == H["header_hash"]).all()
+    assert (D["prev_hash"][1:] == D["header_hash"][:-1]).all()
+    assert int((o["bits"] != 0).sum()) == 0
+    assert (done, stop) == (n, n) and int((v != 0).sum()) == 0
+    assert env["tip"] == (int(sched[0][-1]), n - 1, bytes(D["header_hash"][-1]))
+    # corrupted copy: the chain stops at the first corrupted header
+    H2, _, corrupted2, _ = chains.make_chain(ctx, cfg, sched, link=True, corrupt_per_10000=150)
+    o2, D2, v2, stop2, done2, st2, env2, (ref_st, ref_env), _ = _validate_from_bytes(ctx, cfg, H2)
+    first_bad = int(np.nonzero(corrupted2)[0][0])
+    assert stop2 == first_bad and v2[first_bad] != 0 and int((v2[:first_bad] != 0).sum()) == 0
+    hk = [oracle.blake2b(bytes(c), 28) for c in D2["cold_vk"]]
+    prev = [None if D2["prev_is_genesis"][i] else bytes(D2["prev_hash"][i]) for i in range(n)]
+    wv, wstop, wdone = cs.fold(ref_st, hk, D2["slot"], o2["bits"], D2["ocert_n"], o2["nonce"], prev,
+                               {h for h, _, _ in pool_list}, cfg["eta0"], 0, 0, cfg["epoch_length"], 129_600,
+                               env=ref_env)
+    assert (wdone, wstop) == (done2, stop2) and list(v2) == wv
+    assert st2 == ref_st and env2["tip"] == ref_env["tip"]
+
+
+def test_decode_failure_is_input_with_kernel_mask(ctx):
+    """A stored header that does not decode reports PRAOS_BIT_INPUT even when the KES
+    kernel (which used to carry that bit) is masked out (praos_set_option KERNELS)."""
+    from praos_hip import abi, chains
+    from praos_hip.chunk import pack_chunk
+    cfg = chains.CONFIGS["c1"]
+    sched = chains.search_schedule(ctx, cfg, 40, window=2_000)
+    H, pool_list, _, p = chains.make_chain(ctx, cfg, sched)
+    arena, off, ln = pack_chunk(H)
+    ln = ln.copy()
+    ln[7] -= 5                                      # truncated: DEC_SYNTAX
+    ctx.set_epoch(cfg["eta0"], pool_list, p)
+    try:
+        for mask in (1, 4, 5):
+            ctx.set_option(abi.OPT_KERNELS, mask)
+            o = ctx.verify_header_bytes(arena, off, ln)
+            assert o["bits"][7] & abi.BIT_INPUT and int((o["bits"][:7] & abi.BIT_INPUT).sum()) == 0
+    finally:
+        ctx.set_option(abi.OPT_KERNELS, 7)
