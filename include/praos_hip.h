@@ -375,6 +375,14 @@ int praos_update_chain_dep_state(praos_ctx* ctx, const praos_headers* h, const u
                                  const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict,
                                  size_t* chain_stop, size_t* processed);
 
+/* ---- PraosState CBOR (checkpoint / resume of a replay) ----
+ * Serialise (PraosState c), Praos.hs:274-310: [0, [lastSlot, ocertCounters, evolving,
+ * candidate, epoch, lab, lastEpochBlock]].  encode: *len gets the size; PRAOS_E_ARG
+ * if cap is too small (call with cap 0 to size).  decode: counters into the caller's
+ * arrays (st->cap entries). */
+int praos_state_encode(const praos_chain_state* st, uint8_t* out, size_t cap, size_t* len);
+int praos_state_decode(const uint8_t* in, size_t len, praos_chain_state* st);
+
 /* ---- validateHeader over a batch (HeaderValidation.hs:413-432) ----
  * The envelope first -- validateEnvelope (:297-344: block number = tip + 1 (0 after
  * Origin), slot >= tip slot + 1 (>= 0 after Origin), prev hash = tip hash (GenesisHash

@@ -1106,6 +1106,114 @@ int praos_validate_headers(praos_ctx* c, const praos_headers* h, const uint8_t* 
 
 
 
+// ---------------------------------------------------------------- PraosState CBOR
+// Serialise (PraosState c) (Praos.hs:274-310): encodeVersion 0 [lastSlot, counters,
+// evolving, candidate, epoch, lab, lastEpochBlock]; WithOrigin: Origin = [0], At s =
+// [1, s]; Nonce: NeutralNonce = [0], Nonce h = [1, bytes(32)]; counters = CBOR map
+// KeyHash (bytes 28) -> Word64 in ascending key order (Data.Map).  Shortest-form heads.
+namespace {
+struct CborW {
+  uint8_t* out;
+  size_t cap, n;
+  void byte(uint32_t b) { if (n < cap) out[n] = (uint8_t)b; n++; }
+  void head(uint32_t mt, uint64_t v) {
+    if (v < 24) { byte((mt << 5) | (uint32_t)v); return; }
+    const int nb = v < 256 ? 1 : v < 65536 ? 2 : v < (1ull << 32) ? 4 : 8;
+    byte((mt << 5) | (nb == 1 ? 24u : nb == 2 ? 25u : nb == 4 ? 26u : 27u));
+    for (int k = nb - 1; k >= 0; k--) byte((uint32_t)(v >> (8 * k)));
+  }
+  void bytes(const uint8_t* p, size_t len) { head(2, len); for (size_t k = 0; k < len; k++) byte(p[k]); }
+  void nonce(const praos_nonce& x) {
+    if (x.neutral) { head(4, 1); head(0, 0); }
+    else { head(4, 2); head(0, 1); bytes(x.hash, 32); }
+  }
+};
+struct CborR {
+  const uint8_t* p;
+  size_t len, pos;
+  bool ok = true;
+  bool head(uint32_t want_mt, uint64_t* v) {
+    if (!ok || pos >= len) return ok = false;
+    const uint32_t ib = p[pos++], mt = ib >> 5, ai = ib & 31;
+    if (mt != want_mt) return ok = false;
+    if (ai < 24) { *v = ai; return true; }
+    if (ai > 27) return ok = false;
+    const int nb = 1 << (ai - 24);
+    if (pos + nb > len) return ok = false;
+    uint64_t x = 0;
+    for (int k = 0; k < nb; k++) x = (x << 8) | p[pos++];
+    *v = x;
+    return true;
+  }
+  bool expect(uint32_t mt, uint64_t want) { uint64_t v; return head(mt, &v) && (v == want || (ok = false)); }
+  bool bytes(uint8_t* dst, size_t n) {
+    uint64_t l;
+    if (!head(2, &l) || l != n || pos + n > len) return ok = false;
+    std::memcpy(dst, p + pos, n);
+    pos += n;
+    return true;
+  }
+  bool nonce(praos_nonce& x) {
+    uint64_t l, tag;
+    if (!head(4, &l) || !head(0, &tag)) return false;
+    std::memset(&x, 0, sizeof x);
+    if (l == 1 && tag == 0) { x.neutral = 1; return true; }
+    if (l == 2 && tag == 1) { x.neutral = 0; return bytes(x.hash, 32); }
+    return ok = false;
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int praos_state_encode(const praos_chain_state* st, uint8_t* out, size_t cap, size_t* len) {
+  if (!st || !len || (cap && !out) || (st->m && (!st->counter_hash28 || !st->counter))) return PRAOS_E_ARG;
+  std::vector<size_t> order(st->m);
+  for (size_t k = 0; k < st->m; k++) order[k] = k;
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    return std::memcmp(st->counter_hash28 + 28 * a, st->counter_hash28 + 28 * b, 28) < 0;
+  });
+  for (size_t k = 1; k < order.size(); k++)
+    if (!std::memcmp(st->counter_hash28 + 28 * order[k - 1], st->counter_hash28 + 28 * order[k], 28))
+      return PRAOS_E_ARG;                                   // duplicate key: not a Map
+  CborW w{out, cap, 0};
+  w.head(4, 2); w.head(0, 0);                               // encodeVersion 0
+  w.head(4, 7);
+  if (st->last_slot_origin) { w.head(4, 1); w.head(0, 0); }
+  else { w.head(4, 2); w.head(0, 1); w.head(0, st->last_slot); }
+  w.head(5, st->m);
+  for (size_t k : order) { w.bytes(st->counter_hash28 + 28 * k, 28); w.head(0, st->counter[k]); }
+  w.nonce(st->evolving); w.nonce(st->candidate); w.nonce(st->epoch_nonce); w.nonce(st->lab);
+  w.nonce(st->last_epoch_block);
+  *len = w.n;
+  return w.n <= cap ? PRAOS_OK : PRAOS_E_ARG;
+}
+
+int praos_state_decode(const uint8_t* in, size_t len, praos_chain_state* st) {
+  if (!in || !st || (st->cap && (!st->counter_hash28 || !st->counter))) return PRAOS_E_ARG;
+  CborR r{in, len, 0};
+  uint64_t v, tag, m;
+  r.expect(4, 2); r.expect(0, 0); r.expect(4, 7);
+  if (!r.ok) return PRAOS_E_ARG;
+  if (!r.head(4, &v) || !r.head(0, &tag)) return PRAOS_E_ARG;
+  if (v == 1 && tag == 0) { st->last_slot_origin = 1; st->last_slot = 0; }
+  else if (v == 2 && tag == 1 && r.head(0, &st->last_slot)) st->last_slot_origin = 0;
+  else return PRAOS_E_ARG;
+  if (!r.head(5, &m) || m > st->cap) return PRAOS_E_ARG;
+  for (size_t k = 0; k < m; k++) {
+    if (!r.bytes(st->counter_hash28 + 28 * k, 28) || !r.head(0, &st->counter[k])) return PRAOS_E_ARG;
+    if (k && std::memcmp(st->counter_hash28 + 28 * (k - 1), st->counter_hash28 + 28 * k, 28) >= 0)
+      return PRAOS_E_ARG;                                   // Data.Map decoding wants ascending keys
+  }
+  st->m = m;
+  if (!r.nonce(st->evolving) || !r.nonce(st->candidate) || !r.nonce(st->epoch_nonce) || !r.nonce(st->lab) ||
+      !r.nonce(st->last_epoch_block))
+    return PRAOS_E_ARG;
+  return r.pos == len ? PRAOS_OK : PRAOS_E_ARG;
+}
+
+}  // extern "C"
+
 // ---------------------------------------------------------------- generator
 }  // extern "C"
 static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const praos_params* params,

@@ -174,6 +174,9 @@ SIGNATURES = {
                                               ctypes.POINTER(Envelope), ctypes.POINTER(EpochInfo),
                                               ctypes.POINTER(ChainState), u8p, ctypes.POINTER(ctypes.c_size_t),
                                               ctypes.POINTER(ctypes.c_size_t)]),
+    "praos_state_encode": (ctypes.c_int, [ctypes.POINTER(ChainState), u8p, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t)]),
+    "praos_state_decode": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.POINTER(ChainState)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -722,6 +725,56 @@ class Context:
         out = np.zeros((len(pk), 32), np.uint8)
         self.check(self.L.praos_debug_hash_to_curve(self.h, len(pk), ptr(pk), ptr(alpha), ptr(out)))
         return out
+
+
+def _state_struct(state, cap):
+    st = ChainState()
+    keys = list(state.get("counters", {}).keys())
+    hk = np.zeros(28 * max(cap, 1), np.uint8)
+    cv = np.zeros(max(cap, 1), np.uint64)
+    for k, key in enumerate(keys):
+        hk[28 * k:28 * k + 28] = np.frombuffer(key, np.uint8)
+        cv[k] = state["counters"][key]
+    st.last_slot_origin = int(state.get("last_slot") is None)
+    st.last_slot = state.get("last_slot") or 0
+    st.counter_hash28, st.counter, st.m, st.cap = ptr(hk), ptr(cv, u64p), len(keys), cap
+    for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),
+                 ("lab", "lab"), ("last_epoch_block", "leb")):
+        v = state.get(b)
+        getattr(st, a).neutral = int(v is None)
+        if v is not None:
+            ctypes.memmove(getattr(st, a).hash, v, 32)
+    return st, hk, cv
+
+
+def state_encode(state):
+    """PraosState CBOR (praos_state_encode, Praos.hs:274-310) of a state dict (the form
+    Context.update_chain_dep_state uses)."""
+    L = load()
+    st, hk, cv = _state_struct(state, len(state.get("counters", {})))
+    n = ctypes.c_size_t(0)
+    L.praos_state_encode(ctypes.byref(st), None, 0, ctypes.byref(n))
+    out = np.zeros(max(n.value, 1), np.uint8)
+    rc = L.praos_state_encode(ctypes.byref(st), ptr(out), n.value, ctypes.byref(n))
+    if rc != 0:
+        raise PraosError(f"praos_state_encode rc={rc}")
+    return bytes(out[:n.value])
+
+
+def state_decode(data: bytes, cap=1 << 16):
+    L = load()
+    st, hk, cv = _state_struct({}, cap)
+    buf = np.frombuffer(bytes(data), np.uint8).copy()
+    rc = L.praos_state_decode(ptr(buf), len(buf), ctypes.byref(st))
+    if rc != 0:
+        raise PraosError(f"praos_state_decode rc={rc}")
+    state = {"last_slot": None if st.last_slot_origin else int(st.last_slot),
+             "counters": {bytes(hk[28 * k:28 * k + 28]): int(cv[k]) for k in range(st.m)}}
+    for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),
+                 ("lab", "lab"), ("last_epoch_block", "leb")):
+        x = getattr(st, a)
+        state[b] = None if x.neutral else bytes(x.hash)
+    return state
 
 
 def params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=0, f_is_one=False, vrf_check_output=True):
