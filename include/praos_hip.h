@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 5
+#define PRAOS_ABI_VERSION 6
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -411,6 +411,39 @@ int praos_validate_headers(praos_ctx* ctx, const praos_headers* h, const uint8_t
                            const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
                            const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict, size_t* chain_stop,
                            size_t* processed);
+
+/* ---- chain replay from an ImmutableDB directory (db-analyser) ----
+ * Replaces the per-block loop of DBAnalyser/Analysis.hs:815-847 (processAllImmutableDB
+ * driving benchmarkLedgerOps / validateHeader, :479-607) for the header-validation
+ * pass.  Reads dir/NNNNN.chunk + dir/NNNNN.secondary (56-byte Entry per block,
+ * Storage/ImmutableDB/Impl/Index/Secondary.hs:93-128) from chunk 0 up, batches of at
+ * most batch_max headers that never cross an epoch, installs each epoch's nonce (ticked
+ * from *st) with praos_set_epoch(pools, params), verifies on the device and folds with
+ * praos_validate_headers.  Ends at the first invalid header (stop_index, stop_verdict)
+ * or at the end of the database (stop_index = headers).  *st and env's tip are the
+ * state and tip after the last valid header; verdicts[i] (i < verdicts_cap, may be
+ * NULL with cap 0) for every header up to and including the stop.  Resume: when env's
+ * tip is not Origin (a checkpointed state, praos_state_decode), the blocks up to and
+ * including the tip (matched by slot and header hash in the secondary index) are
+ * skipped; indices count from the first block after it. */
+typedef struct {
+  uint64_t skipped;               /* blocks up to the resume tip, not replayed */
+  uint64_t headers;               /* headers read and judged (through the stop) */
+  uint64_t validated;             /* valid headers folded into *st */
+  uint64_t stop_index;            /* first invalid header, or headers when none */
+  uint32_t stop_verdict;          /* its PRAOS_V_* (0 when none) */
+  uint32_t epochs;                /* praos_set_epoch calls (epoch nonces installed) */
+  uint32_t batches;               /* device passes */
+  uint32_t chunks;                /* chunk files read */
+  double ms_io;                   /* reading chunks + secondary indexes, building batches */
+  double ms_device;               /* upload + decode + crypto + download */
+  double ms_fold;                 /* envelope + updateChainDepState on the host */
+} praos_replay_stats;
+
+int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
+                           const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                           praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
+                           praos_replay_stats* stats);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

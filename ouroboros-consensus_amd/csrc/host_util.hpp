@@ -8,50 +8,63 @@
 #include <cstdint>
 #include <cstring>
 
+#include "praos_hip.h"
+
 namespace praos_host {
 
 inline uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 
+// BLAKE2b (RFC 7693), unkeyed.  The 16 working words live in locals and the 12
+// rounds are unrolled with compile-time message schedules, so the compiler keeps the
+// whole compression in registers (~3x faster than an indexed v[16] array; the
+// sequential evolving-nonce chain of the fold is one compression per header).
+#define PH_G(a, b, c, d, x, y)               \
+  a = a + b + (x); d = ror64(d ^ a, 32);     \
+  c = c + d;       b = ror64(b ^ c, 24);     \
+  a = a + b + (y); d = ror64(d ^ a, 16);     \
+  c = c + d;       b = ror64(b ^ c, 63);
+#define PH_ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  PH_G(v0, v4, v8, v12, M[s0], M[s1]) PH_G(v1, v5, v9, v13, M[s2], M[s3])          \
+  PH_G(v2, v6, v10, v14, M[s4], M[s5]) PH_G(v3, v7, v11, v15, M[s6], M[s7])        \
+  PH_G(v0, v5, v10, v15, M[s8], M[s9]) PH_G(v1, v6, v11, v12, M[s10], M[s11])      \
+  PH_G(v2, v7, v8, v13, M[s12], M[s13]) PH_G(v3, v4, v9, v14, M[s14], M[s15])
+
+inline void blake2b_compress(uint64_t h[8], const uint8_t blk[128], uint64_t t, bool last) {
+  static constexpr uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                                     0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                     0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  uint64_t M[16];
+  std::memcpy(M, blk, 128);                          // little-endian host
+  uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3], v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+  uint64_t v8 = IV[0], v9 = IV[1], v10 = IV[2], v11 = IV[3], v12 = IV[4] ^ t, v13 = IV[5];
+  uint64_t v14 = last ? ~IV[6] : IV[6], v15 = IV[7];
+  PH_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  PH_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
+  PH_ROUND(11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4)
+  PH_ROUND(7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8)
+  PH_ROUND(9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13)
+  PH_ROUND(2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9)
+  PH_ROUND(12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11)
+  PH_ROUND(13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10)
+  PH_ROUND(6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5)
+  PH_ROUND(10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0)
+  PH_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
+  PH_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
+  h[0] ^= v0 ^ v8; h[1] ^= v1 ^ v9; h[2] ^= v2 ^ v10; h[3] ^= v3 ^ v11;
+  h[4] ^= v4 ^ v12; h[5] ^= v5 ^ v13; h[6] ^= v6 ^ v14; h[7] ^= v7 ^ v15;
+}
+#undef PH_ROUND
+#undef PH_G
+
 inline void blake2b(uint8_t* out, size_t outlen, const uint8_t* m, size_t n) {
-  static const uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
-                                 0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
-                                 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
-  static const uint8_t S[12][16] = {
-      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
-      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
-      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
-      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
-      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
-      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
-  uint64_t h[8];
-  for (int i = 0; i < 8; i++) h[i] = IV[i];
+  uint64_t h[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                   0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
   h[0] ^= 0x01010000ULL ^ (uint64_t)outlen;
   size_t off = 0;
-  auto compress = [&](const uint8_t* blk, uint64_t t, bool last) {
-    uint64_t mm[16], v[16];
-    for (int i = 0; i < 16; i++) { uint64_t w; std::memcpy(&w, blk + 8 * i, 8); mm[i] = w; }
-    for (int i = 0; i < 8; i++) { v[i] = h[i]; v[i + 8] = IV[i]; }
-    v[12] ^= t;
-    if (last) v[14] = ~v[14];
-    auto G = [&](int a, int b, int c, int d, uint64_t x, uint64_t y) {
-      v[a] = v[a] + v[b] + x; v[d] = ror64(v[d] ^ v[a], 32);
-      v[c] = v[c] + v[d]; v[b] = ror64(v[b] ^ v[c], 24);
-      v[a] = v[a] + v[b] + y; v[d] = ror64(v[d] ^ v[a], 16);
-      v[c] = v[c] + v[d]; v[b] = ror64(v[b] ^ v[c], 63);
-    };
-    for (int r = 0; r < 12; r++) {
-      const uint8_t* s = S[r];
-      G(0, 4, 8, 12, mm[s[0]], mm[s[1]]); G(1, 5, 9, 13, mm[s[2]], mm[s[3]]);
-      G(2, 6, 10, 14, mm[s[4]], mm[s[5]]); G(3, 7, 11, 15, mm[s[6]], mm[s[7]]);
-      G(0, 5, 10, 15, mm[s[8]], mm[s[9]]); G(1, 6, 11, 12, mm[s[10]], mm[s[11]]);
-      G(2, 7, 8, 13, mm[s[12]], mm[s[13]]); G(3, 4, 9, 14, mm[s[14]], mm[s[15]]);
-    }
-    for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
-  };
-  while (n - off > 128) { off += 128; compress(m + off - 128, off, false); }
+  while (n - off > 128) { off += 128; blake2b_compress(h, m + off - 128, off, false); }
   uint8_t blk[128] = {0};
   std::memcpy(blk, m + off, n - off);
-  compress(blk, n, true);
+  blake2b_compress(h, blk, n, true);
   for (size_t i = 0; i < outlen; i++) out[i] = (uint8_t)(h[i / 8] >> (8 * (i % 8)));
 }
 
@@ -115,6 +128,24 @@ inline bool leader_x_raw(uint8_t x_le[16], const uint8_t sigma_fp[16], const uin
   unsigned __int128 x;
   std::memcpy(&x, x_le, 16);
   return x <= 16 * R;
+}
+
+// a ⭒ b (Nonce semigroup): Neutral is the identity, else Blake2b-256(a || b).
+inline praos_nonce nonce_combine(const praos_nonce& a, const praos_nonce& b) {
+  if (a.neutral) return b;
+  if (b.neutral) return a;
+  uint8_t m[64];
+  std::memcpy(m, a.hash, 32);
+  std::memcpy(m + 32, b.hash, 32);
+  praos_nonce r{};
+  blake2b(r.hash, 32, m, 64);
+  r.neutral = 0;
+  return r;
+}
+
+inline bool nonce_eq(const praos_nonce& a, const praos_nonce& b) {
+  if (a.neutral || b.neutral) return a.neutral && b.neutral;
+  return std::memcmp(a.hash, b.hash, 32) == 0;
 }
 
 }  // namespace praos_host

@@ -890,23 +890,11 @@ static std::string issuer_hash(const praos_ctx* c, const praos_headers* h, const
   return std::string((const char*)hh, 28);
 }
 
-// a ⭒ b (Nonce semigroup): Neutral is the identity, else Blake2b-256(a || b).
-static praos_nonce nonce_combine(const praos_nonce& a, const praos_nonce& b) {
-  if (a.neutral) return b;
-  if (b.neutral) return a;
-  uint8_t m[64];
-  std::memcpy(m, a.hash, 32);
-  std::memcpy(m + 32, b.hash, 32);
-  praos_nonce r{};
-  praos_host::blake2b(r.hash, 32, m, 64);
-  r.neutral = 0;
-  return r;
-}
+using praos_host::nonce_combine;
+using praos_host::nonce_eq;
 
-static bool nonce_eq(const praos_nonce& a, const praos_nonce& b) {
-  if (a.neutral || b.neutral) return a.neutral && b.neutral;
-  return std::memcmp(a.hash, b.hash, 32) == 0;
-}
+// error text for the other host modules of the library (praos_replay.hip)
+void praos_set_error_(praos_ctx* c, const std::string& m) { if (c) c->err = m; }
 
 extern "C" {
 
@@ -961,6 +949,31 @@ static uint8_t envelope_verdict(const praos_envelope* e, const EnvTip& tip, cons
   return PRAOS_V_OK;
 }
 
+// OCert counters of the fold, indexed densely: slot k < npools is pool k of the epoch's
+// distribution (caller order, found through the device's pool_idx), slots >= npools
+// hold issuers outside it (keys from the incoming state, or headers whose issuer the
+// distribution lacks).  has[k] = the praosStateOCertCounters map has the key.
+struct CounterTab {
+  std::vector<uint64_t> ctr;
+  std::vector<uint8_t> has;
+  std::vector<std::string> extra_keys;
+  std::map<std::string, uint32_t> extra;
+};
+
+static uint32_t counter_slot(const praos_ctx* c, CounterTab& T, const uint8_t* hash28) {
+  const std::string k((const char*)hash28, 28);
+  auto p = c->pool_by_hash.find(k);
+  if (p != c->pool_by_hash.end()) return (uint32_t)p->second;
+  auto e = T.extra.find(k);
+  if (e != T.extra.end()) return e->second;
+  const uint32_t slot = (uint32_t)T.ctr.size();
+  T.extra.emplace(k, slot);
+  T.extra_keys.push_back(k);
+  T.ctr.push_back(0);
+  T.has.push_back(0);
+  return slot;
+}
+
 static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
                      const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei,
                      praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed) {
@@ -984,12 +997,18 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
   struct Work {
     int32_t origin;
     uint64_t last_slot;
-    std::vector<std::string> keys;
-    std::vector<uint64_t> ctr;
-    std::map<std::string, size_t> where;
     praos_nonce evolving, candidate, epoch_nonce, lab, leb;
     EnvTip tip;
   };
+  const uint32_t np = c->npools;
+  CounterTab T;
+  T.ctr.assign(np, 0);
+  T.has.assign(np, 0);
+  for (size_t k = 0; k < st->m; k++) {
+    const uint32_t slot = counter_slot(c, T, st->counter_hash28 + 28 * k);
+    T.ctr[slot] = st->counter[k];
+    T.has[slot] = 1;
+  }
   Work W;
   if (env) {
     W.tip.origin = env->tip_is_origin;
@@ -999,15 +1018,12 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
   }
   W.origin = st->last_slot_origin;
   W.last_slot = st->last_slot;
-  for (size_t k = 0; k < st->m; k++) {
-    W.keys.emplace_back((const char*)st->counter_hash28 + 28 * k, 28);
-    W.ctr.push_back(st->counter[k]);
-    W.where[W.keys.back()] = k;
-  }
   W.evolving = st->evolving; W.candidate = st->candidate; W.epoch_nonce = st->epoch_nonce;
   W.lab = st->lab; W.leb = st->last_epoch_block;
   bool frozen = false;
   Work F;                                            // state at the chain stop
+  std::vector<uint64_t> Fctr;                        // and its counters (T is W's)
+  std::vector<uint8_t> Fhas;
   size_t stop = h->n, i = 0;
   for (; i < h->n; i++) {
     const uint64_t slot = h->slot[i];
@@ -1022,11 +1038,19 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
       tick_leb = W.lab;
     }
     if (!nonce_eq(tick_epoch, eta0)) break;        // crypto outputs were computed for another epoch nonce
-    const std::string hk = issuer_hash(c, h, crypto, i);
+    // the issuer's counter slot (hashKey of the cold key, Praos.hs:595-606)
+    const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
+    uint32_t k;
+    if (pidx >= 0 && (uint32_t)pidx < np) {
+      k = (uint32_t)pidx;
+    } else {
+      uint8_t hh[28];
+      praos_host::blake2b(hh, 28, h->cold_vk + 32 * i, 32);
+      k = counter_slot(c, T, hh);
+    }
     const uint64_t n = h->ocert_n[i];
-    auto it = W.where.find(hk);
-    const bool have = it != W.where.end() || c->pool_by_hash.count(hk);
-    uint8_t v = header_verdict(crypto->bits[i], have, it != W.where.end() ? W.ctr[it->second] : 0, n);
+    const bool has = T.has[k];
+    uint8_t v = header_verdict(crypto->bits[i], has || k < np, has ? T.ctr[k] : 0, n);
     // validateHeader (HeaderValidation.hs:419-428): the envelope before the protocol checks
     if (env && v != PRAOS_V_INPUT) {
       const uint8_t ve = envelope_verdict(env, W.tip, h, prev_hash, prev_is_genesis, i);
@@ -1034,7 +1058,13 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     }
     verdict[i] = v;
     if (v != PRAOS_V_OK) {
-      if (!frozen) { F = W; frozen = true; stop = i; }
+      if (!frozen) {
+        F = W;
+        Fctr = T.ctr;
+        Fhas = T.has;
+        frozen = true;
+        stop = i;
+      }
       continue;
     }
     // reupdateChainDepState (Praos.hs:468-502)
@@ -1051,13 +1081,8 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     W.evolving = nonce_combine(W.evolving, eta);
     const uint64_t first_next = ei->epoch_base_slot + (e_new - ei->epoch_base_no + 1) * ei->epoch_length;
     if (slot + ei->stability_window < first_next) W.candidate = W.evolving;
-    if (it != W.where.end()) {
-      W.ctr[it->second] = n;
-    } else {
-      W.where[hk] = W.keys.size();
-      W.keys.push_back(hk);
-      W.ctr.push_back(n);
-    }
+    T.ctr[k] = n;
+    T.has[k] = 1;
     if (env) {                                       // HeaderState tip := getAnnTip hdr
       W.tip.origin = 0;
       W.tip.slot = slot;
@@ -1066,14 +1091,21 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     }
   }
   const Work& R = frozen ? F : W;
-  if (R.keys.size() > st->cap) { c->err = "counter map capacity exceeded"; return PRAOS_E_ARG; }
+  const std::vector<uint64_t>& Rctr = frozen ? Fctr : T.ctr;
+  const std::vector<uint8_t>& Rhas = frozen ? Fhas : T.has;
+  size_t m = 0;
+  for (size_t k = 0; k < Rhas.size(); k++) m += Rhas[k];
+  if (m > st->cap) { c->err = "counter map capacity exceeded"; return PRAOS_E_ARG; }
+  size_t j = 0;
+  for (size_t k = 0; k < Rhas.size(); k++) {
+    if (!Rhas[k]) continue;
+    const uint8_t* key = k < np ? c->pools[k].hash28 : (const uint8_t*)T.extra_keys[k - np].data();
+    std::memcpy(st->counter_hash28 + 28 * j, key, 28);
+    st->counter[j++] = Rctr[k];
+  }
+  st->m = m;
   st->last_slot_origin = R.origin;
   st->last_slot = R.last_slot;
-  for (size_t k = 0; k < R.keys.size(); k++) {
-    std::memcpy(st->counter_hash28 + 28 * k, R.keys[k].data(), 28);
-    st->counter[k] = R.ctr[k];
-  }
-  st->m = R.keys.size();
   st->evolving = R.evolving; st->candidate = R.candidate; st->epoch_nonce = R.epoch_nonce;
   st->lab = R.lab; st->last_epoch_block = R.leb;
   if (env) {

@@ -104,6 +104,13 @@ class Envelope(ctypes.Structure):
                 ("max_body_size", ctypes.c_uint64)]
 
 
+class ReplayStats(ctypes.Structure):
+    _fields_ = [("skipped", ctypes.c_uint64), ("headers", ctypes.c_uint64), ("validated", ctypes.c_uint64), ("stop_index", ctypes.c_uint64),
+                ("stop_verdict", ctypes.c_uint32), ("epochs", ctypes.c_uint32), ("batches", ctypes.c_uint32),
+                ("chunks", ctypes.c_uint32), ("ms_io", ctypes.c_double), ("ms_device", ctypes.c_double),
+                ("ms_fold", ctypes.c_double)]
+
+
 class Counters(ctypes.Structure):
     _fields_ = [("hash28", u8p), ("counter", u64p), ("m", ctypes.c_size_t)]
 
@@ -177,6 +184,10 @@ SIGNATURES = {
     "praos_state_encode": (ctypes.c_int, [ctypes.POINTER(ChainState), u8p, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_size_t)]),
     "praos_state_decode": (ctypes.c_int, [u8p, ctypes.c_size_t, ctypes.POINTER(ChainState)]),
+    "praos_replay_immutable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(Pool), ctypes.c_uint32,
+                                              ctypes.POINTER(Params), ctypes.POINTER(EpochInfo),
+                                              ctypes.POINTER(Envelope), ctypes.POINTER(ChainState), ctypes.c_size_t,
+                                              u8p, ctypes.c_size_t, ctypes.POINTER(ReplayStats)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -269,13 +280,19 @@ class Context:
             raise PraosError(f"praos rc={rc}: {msg.decode() if msg else ''}")
 
     # ---- epoch ----
-    def set_epoch(self, eta0, pools, params: Params):
+    @staticmethod
+    def pool_array(pools):
         """pools: list of (hash28: bytes, vrf_hash32: bytes, sigma_fp: int)."""
         arr = (Pool * max(1, len(pools)))()
         for i, (h, v, s) in enumerate(pools):
             ctypes.memmove(arr[i].hash28, h, 28)
             ctypes.memmove(arr[i].vrf_hash32, v, 32)
             ctypes.memmove(arr[i].sigma_fp, int(s).to_bytes(16, "little"), 16)
+        return arr
+
+    def set_epoch(self, eta0, pools, params: Params):
+        """pools: list of (hash28: bytes, vrf_hash32: bytes, sigma_fp: int)."""
+        arr = self.pool_array(pools)
         e = None
         if eta0 is not None:
             eb = np.frombuffer(bytes(eta0), dtype=np.uint8).copy()
@@ -537,6 +554,33 @@ class Context:
             state[b] = getn(getattr(st, a))
         return verdict, stop.value, done.value
 
+    def replay_immutable(self, path, pools, params: Params, epoch_info, state: dict, envelope: dict,
+                         batch_max=1 << 16, verdicts_cap=0, counter_cap=1 << 16):
+        """praos_replay_immutable over an ImmutableDB directory.  state (chain state dict, as
+        update_chain_dep_state) and envelope (limits + "tip") are updated in place.
+        Returns (stats dict, verdict u8[verdicts_cap])."""
+        arr = self.pool_array(pools)
+        st, hk, cv = _state_struct(state, counter_cap)
+        E = Envelope()
+        tip = envelope.get("tip")
+        E.tip_is_origin = int(tip is None)
+        if tip is not None:
+            E.tip_slot, E.tip_block_no = tip[0], tip[1]
+            ctypes.memmove(E.tip_hash, bytes(tip[2]), 32)
+        for k in ("max_major_pv", "lv_prot_major", "max_header_size", "max_body_size"):
+            setattr(E, k, envelope[k])
+        ei = EpochInfo(*epoch_info)
+        verdict = np.zeros(max(verdicts_cap, 1), np.uint8)
+        S = ReplayStats()
+        self.check(self.L.praos_replay_immutable(self.h, os.fsencode(str(path)), arr, len(pools),
+                                                 ctypes.byref(params), ctypes.byref(ei), ctypes.byref(E),
+                                                 ctypes.byref(st), batch_max, ptr(verdict), verdicts_cap,
+                                                 ctypes.byref(S)))
+        envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no), bytes(E.tip_hash))
+        state.update(_state_from_struct(st, hk, cv))
+        stats = {name: getattr(S, name) for name, _ in ReplayStats._fields_}
+        return stats, verdict[:verdicts_cap]
+
     def apply_batch(self, H, crypto, counters=None):
         """counters: dict hash28 -> int.  Returns (verdict u8[n], chain_stop, counters_out)."""
         n = len(H["slot"])
@@ -761,13 +805,7 @@ def state_encode(state):
     return bytes(out[:n.value])
 
 
-def state_decode(data: bytes, cap=1 << 16):
-    L = load()
-    st, hk, cv = _state_struct({}, cap)
-    buf = np.frombuffer(bytes(data), np.uint8).copy()
-    rc = L.praos_state_decode(ptr(buf), len(buf), ctypes.byref(st))
-    if rc != 0:
-        raise PraosError(f"praos_state_decode rc={rc}")
+def _state_from_struct(st, hk, cv):
     state = {"last_slot": None if st.last_slot_origin else int(st.last_slot),
              "counters": {bytes(hk[28 * k:28 * k + 28]): int(cv[k]) for k in range(st.m)}}
     for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),
@@ -775,6 +813,16 @@ def state_decode(data: bytes, cap=1 << 16):
         x = getattr(st, a)
         state[b] = None if x.neutral else bytes(x.hash)
     return state
+
+
+def state_decode(data: bytes, cap=1 << 16):
+    L = load()
+    st, hk, cv = _state_struct({}, cap)
+    buf = np.frombuffer(bytes(data), np.uint8).copy()
+    rc = L.praos_state_decode(ptr(buf), len(buf), ctypes.byref(st))
+    if rc != 0:
+        raise PraosError(f"praos_state_decode rc={rc}")
+    return _state_from_struct(st, hk, cv)
 
 
 def params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=0, f_is_one=False, vrf_check_output=True):

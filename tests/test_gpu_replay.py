@@ -1,0 +1,200 @@
+"""Chain replay from an ImmutableDB directory (praos_replay_immutable, SURVEY.md sec. 8
+N3; db-analyser's processAllImmutableDB + validateHeader, Analysis.hs:479-607, 815-847).
+
+A linked multi-epoch chain (first-leader-wins under each epoch's own nonce) is written
+as chunk + secondary + primary files whose chunk boundaries do not line up with the
+epochs, then replayed through the library.  Checked against the oracle's fold run epoch
+by epoch (tickChainDepState nonces evolved by the oracle, crypto from the GPU):
+every header valid, the final PraosState and tip identical; a corrupted KES signature,
+a broken prev-hash link and a damaged secondary index each stop (or fail) where the
+reference would; resume from a checkpointed state (CBOR) reaches the same end state."""
+import os
+import shutil
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from helpers import b2b
+
+pytestmark = pytest.mark.gpu
+
+EPOCHS, EPOCH_LEN, WINDOW, CHUNK_SLOTS = 4, 600, 200, 250
+ENV = {"max_major_pv": 9, "lv_prot_major": 8, "max_header_size": 1100, "max_body_size": 90_112}
+
+
+@pytest.fixture(scope="module")
+def chain(ctx, tmp_path_factory):
+    from praos_hip import immutable
+    cfg = dict(npools=20, stake_offset=1, f=Fraction(1, 2), slots_per_kes_period=129600, max_kes_evo=62,
+               eta0=b2b(b"replay-genesis"), seed=b"\x2a" * 32)
+    data = immutable.make_multi_epoch_chain(ctx, cfg, EPOCHS, EPOCH_LEN, WINDOW)
+    path = str(tmp_path_factory.mktemp("immdb") / "immutable")
+    nchunks = immutable.write_immutable(path, data["arena"], data["off"], data["len"], data["slots"],
+                                        data["header_hash"], CHUNK_SLOTS)
+    data.update(cfg=cfg, path=path, nchunks=nchunks)
+    return data
+
+
+def _genesis_state(eta0):
+    return {"last_slot": None, "counters": {}, "evolving": eta0, "candidate": eta0, "epoch_nonce": eta0,
+            "lab": None, "leb": None}
+
+
+def _replay(ctx, data, path=None, state=None, tip=None, batch_max=1 << 16, cap=None):
+    st = state if state is not None else _genesis_state(data["cfg"]["eta0"])
+    env = dict(ENV, tip=tip)
+    n = len(data["off"])
+    stats, v = ctx.replay_immutable(path or data["path"], data["pools"], data["params"], data["epoch_info"], st, env,
+                                    batch_max=batch_max, verdicts_cap=n if cap is None else cap)
+    return stats, v, st, env
+
+
+def _oracle_fold(ctx, data, upto):
+    """The oracle's fold (oracle/chainstate.py) over headers [0, upto), epoch by epoch:
+    nonces evolved by the oracle, the crypto of each epoch from the GPU under that nonce."""
+    import chainstate as cs
+    cfg, arena, off, ln = data["cfg"], data["arena"], data["off"], data["len"]
+    st = _genesis_state(cfg["eta0"])
+    env = {"tip": None}
+    known = {h for h, _, _ in data["pools"]}
+    epoch = (data["slots"][:upto] // EPOCH_LEN).astype(int)
+    verdicts, etas = [], []
+    for e in range(EPOCHS):
+        rows = np.nonzero(epoch == e)[0]
+        if len(rows) == 0:
+            break
+        eta = st["epoch_nonce"] if e == 0 else cs.combine(st["candidate"], st["leb"])
+        etas.append(eta)
+        ctx.set_epoch(eta, data["pools"], data["params"])
+        o, D = ctx.verify_header_bytes(arena, off[rows], ln[rows], decoded=True)
+        m = len(rows)
+        env.update(block_no=D["block_no"], header_hash=D["header_hash"], header_size=ln[rows],
+                   body_size=D["body_size"], **ENV)
+        hk = [b2b(bytes(c), 28) for c in D["cold_vk"]]
+        prev = [None if D["prev_is_genesis"][i] else bytes(D["prev_hash"][i]) for i in range(m)]
+        v, stop, done = cs.fold(st, hk, D["slot"], o["bits"], D["ocert_n"], o["nonce"], prev, known, eta, 0, 0,
+                                EPOCH_LEN, WINDOW, env=env)
+        verdicts += v
+        assert done == m
+        if stop < m:
+            return verdicts, st, env["tip"], etas, int(rows[stop])
+    return verdicts, st, env["tip"], etas, upto
+
+
+def test_immutable_files(chain):
+    """The files follow the on-disk layout: secondary entries point at the headers."""
+    from praos_hip import immutable
+    n = len(chain["off"])
+    assert chain["nchunks"] == (int(chain["slots"][-1]) // CHUNK_SLOTS) + 1
+    entries = [e for c in range(chain["nchunks"]) for e in immutable.read_secondary(chain["path"], c)]
+    assert len(entries) == n
+    assert [e["slot"] for e in entries] == [int(s) for s in chain["slots"]]
+    assert all(e["header_hash"] == bytes(h) for e, h in zip(entries, chain["header_hash"]))
+    e = entries[-1]
+    raw = open(os.path.join(chain["path"], f"{chain['nchunks'] - 1:05d}.chunk"), "rb").read()
+    hdr = raw[e["block_offset"] + e["header_offset"]:][:e["header_size"]]
+    assert b2b(hdr) == e["header_hash"]
+    prim = open(os.path.join(chain["path"], "00000.primary"), "rb").read()
+    assert prim[0] == 1 and len(prim) == 1 + 4 * (CHUNK_SLOTS + 2)
+
+
+@pytest.mark.parametrize("batch_max", [1 << 16, 97])
+def test_replay_all_valid(ctx, chain, batch_max):
+    """Every header valid over 4 epochs; final state and tip = the oracle's; one epoch
+    nonce installed per epoch, equal to the ones the chain was forged under."""
+    n = len(chain["off"])
+    stats, v, st, env = _replay(ctx, chain, batch_max=batch_max)
+    assert (stats["headers"], stats["validated"], stats["stop_index"], stats["stop_verdict"]) == (n, n, n, 0)
+    assert int((v != 0).sum()) == 0
+    assert stats["epochs"] == EPOCHS and stats["chunks"] == chain["nchunks"]
+    assert stats["batches"] >= (EPOCHS if batch_max > n else n // batch_max)
+    assert st == chain["state"]
+    assert env["tip"] == (int(chain["slots"][-1]), n - 1, bytes(chain["header_hash"][-1]))
+    ov, ost, otip, etas, ostop = _oracle_fold(ctx, chain, n)
+    assert ostop == n and etas == chain["nonces"] and len(set(etas)) == EPOCHS
+    assert st == ost and env["tip"] == otip
+
+
+def _copy_db(chain, tmp_path, name):
+    dst = str(tmp_path / name)
+    shutil.copytree(chain["path"], dst)
+    return dst
+
+
+def _locate(chain, i):
+    """(chunk file, byte offset of header i in it) via the secondary index."""
+    from praos_hip import immutable
+    c = int(chain["slots"][i]) // CHUNK_SLOTS
+    ents = immutable.read_secondary(chain["path"], c)
+    e = next(e for e in ents if e["slot"] == int(chain["slots"][i]))
+    return f"{c:05d}.chunk", e["block_offset"] + e["header_offset"]
+
+
+@pytest.mark.parametrize("where", ["kes_sig", "prev_hash"])
+def test_replay_stops_at_corruption(ctx, chain, tmp_path, where):
+    """A header damaged on disk in epoch 2: the replay stops exactly there with the
+    reference's first error (a KES signature byte -> InvalidKesSignatureOCERT; the
+    prev-hash field -> UnexpectedPrevHash, the envelope judged first), state and tip =
+    the oracle's after the header before."""
+    from praos_hip import abi
+    n = len(chain["off"])
+    k = int(np.nonzero(chain["slots"] >= 2 * EPOCH_LEN)[0][5])
+    db = _copy_db(chain, tmp_path, where)
+    fname, pos = _locate(chain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    hdr = bytes(raw[pos:pos + int(chain["len"][k])])
+    if where == "kes_sig":
+        at = pos + len(hdr) - 100
+    else:
+        at = pos + hdr.index(bytes(chain["header_hash"][k - 1])) + 7
+    raw[at] ^= 0x40
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    stats, v, st, env = _replay(ctx, chain, path=db)
+    want = abi.V_KES_SIG if where == "kes_sig" else abi.V_ENV_PREV_HASH
+    assert (stats["stop_index"], stats["stop_verdict"], stats["validated"]) == (k, want, k)
+    assert int((v[:k] != 0).sum()) == 0 and v[k] == want
+    # the oracle, over the first k headers, reaches the same state
+    _, ost, otip, _, ostop = _oracle_fold(ctx, chain, k)
+    assert ostop == k and st == ost and env["tip"] == otip
+    assert n > k
+
+
+def test_replay_bad_secondary(ctx, chain, tmp_path):
+    """A secondary index whose size is not a whole number of entries, and one whose entry
+    points past its chunk, are reported as errors (no silent partial replay)."""
+    from praos_hip import abi
+    db = _copy_db(chain, tmp_path, "badsec")
+    sec = os.path.join(db, "00001.secondary")
+    raw = open(sec, "rb").read()
+    open(sec, "wb").write(raw[:-3])
+    with pytest.raises(abi.PraosError, match="secondary"):
+        _replay(ctx, chain, path=db)
+    bad = bytearray(raw)
+    bad[0:8] = (1 << 40).to_bytes(8, "big")
+    open(sec, "wb").write(bytes(bad))
+    with pytest.raises(abi.PraosError, match="outside its chunk"):
+        _replay(ctx, chain, path=db)
+
+
+def test_replay_resume_from_checkpoint(ctx, chain, tmp_path):
+    """Checkpoint/resume: replay a database holding the first m blocks, serialise the
+    PraosState (CBOR) and the tip, decode it and resume over the full database -- the
+    end state equals the one-pass replay."""
+    from praos_hip import abi, immutable
+    n = len(chain["off"])
+    m = int(np.nonzero(chain["slots"] >= EPOCH_LEN + 350)[0][0])      # mid-epoch 1, past the window
+    part = str(tmp_path / "part")
+    immutable.write_immutable(part, chain["arena"], chain["off"][:m], chain["len"][:m], chain["slots"][:m],
+                              chain["header_hash"][:m], CHUNK_SLOTS)
+    stats, _, st, env = _replay(ctx, chain, path=part)
+    assert stats["validated"] == m
+    blob = abi.state_encode(st)
+    st2 = abi.state_decode(blob)
+    assert st2 == st
+    stats2, v2, st2, env2 = _replay(ctx, chain, state=st2, tip=env["tip"])
+    assert stats2["skipped"] == m and stats2["validated"] == n - m and stats2["stop_index"] == n - m
+    assert int((v2[:n - m] != 0).sum()) == 0
+    assert st2 == chain["state"] and env2["tip"][2] == bytes(chain["header_hash"][-1])
+    with pytest.raises(abi.PraosError, match="tip is not a block"):
+        _replay(ctx, chain, state=dict(st), tip=(env["tip"][0], env["tip"][1], b"\x00" * 32))
