@@ -407,6 +407,13 @@ typedef struct {
   uint64_t max_body_size;         /* lvMaxBodySize */
 } praos_envelope;
 
+/* The epoch nonce tickChainDepState (Praos.hs:407-431) gives the state at `slot`:
+ * candidate ⭒ lastEpochBlock when the slot is in a later epoch than the state's last
+ * slot (isNewEpoch), else the current epoch nonce.  What praos_set_epoch needs before
+ * validating headers of that slot's epoch.  Pure: st is not changed. */
+int praos_ticked_epoch_nonce(const praos_chain_state* st, const praos_epoch_info* ei, uint64_t slot,
+                             praos_nonce* out);
+
 int praos_validate_headers(praos_ctx* ctx, const praos_headers* h, const uint8_t* prev_hash,
                            const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
                            const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict, size_t* chain_stop,
@@ -444,6 +451,27 @@ int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* po
                            const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                            praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
                            praos_replay_stats* stats);
+
+/* ---- several GPUs from one process ----
+ * A group = one context per entry of devices[] (a device may repeat: several
+ * contexts on one GPU), each driven by its own host thread.  Batch calls split the
+ * n headers into contiguous shards (member k: [n*k/m, n*(k+1)/m)), run them
+ * concurrently and write every output in place, so the caller's arrays look exactly
+ * as after the single-context call.  The fold (praos_validate_headers) then runs
+ * over the gathered outputs on praos_group_ctx(g, 0).  No exchange between devices
+ * (headers of one epoch are independent, Praos.hs:441-459). */
+typedef struct praos_group praos_group;
+praos_group* praos_group_open(const int* devices, int ndev);     /* NULL on failure */
+void praos_group_close(praos_group* g);
+int praos_group_size(praos_group* g);
+praos_ctx* praos_group_ctx(praos_group* g, int k);               /* member k's context */
+const char* praos_group_last_error(praos_group* g);
+int praos_group_set_option(praos_group* g, int opt, int value);
+int praos_group_set_epoch(praos_group* g, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
+                          const praos_params* params);
+int praos_group_verify_headers(praos_group* g, const praos_headers* h, praos_out* out);
+int praos_group_verify_header_bytes(praos_group* g, const praos_header_bytes* in, praos_out* out,
+                                    praos_decoded* dec);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

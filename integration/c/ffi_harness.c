@@ -1,0 +1,339 @@
+/* ffi_harness.c -- replays, from C, the foreign-call sequence of the Haskell binding
+ * (integration/haskell/Ouroboros/Consensus/Protocol/Praos/Batch.hs) against
+ * libpraos_hip.so, plus the multi-threaded uses the ABI allows.  Driven by
+ * tests/test_gpu_ffi.py, which builds the ImmutableDB and the epoch file and compares
+ * the JSON this prints with its own results.
+ *
+ *   ffi_harness <immutable dir> <epoch file> <threads>
+ *
+ * epoch file (text, one record per line):
+ *   eta0 <64 hex>                      genesis epoch nonce
+ *   params <spkp> <maxevo> <f_is_one> <vrf_check_output> <c_raw 32 hex, LE>
+ *   epoch <base_slot> <base_no> <length> <stability_window>
+ *   env <max_major_pv> <lv_prot_major> <max_header_size> <max_body_size>
+ *   pool <hash28 56 hex> <vrf_hash32 64 hex> <sigma_fp 32 hex, LE>
+ *
+ * Output: one JSON object per phase.
+ *   "binding":  praosReplayEpochs as the Haskell module runs it (stream the chunk files,
+ *               cut at epoch boundaries, praos_ticked_epoch_nonce -> praos_set_epoch ->
+ *               praos_verify_header_bytes -> praos_validate_headers, stop at the first
+ *               invalid header) and the PraosState CBOR (praos_state_encode) it ends in;
+ *   "replay":   praos_replay_immutable over the same directory (must agree);
+ *   "threads":  the first epoch's headers split over <threads> POSIX threads, each with
+ *               its own praos_ctx on device 0, and the same through praos_group_open
+ *               with <threads> members: bits / pool_idx / nonce equal to one context's.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "praos_hip.h"
+
+#define DIE(...) do { fprintf(stderr, __VA_ARGS__); fputc('\n', stderr); exit(2); } while (0)
+#define CK(ctx, x) do { int rc_ = (x); if (rc_ != PRAOS_OK) DIE("%s -> %d: %s", #x, rc_, praos_last_error(ctx)); } while (0)
+
+static void hex_in(const char* s, uint8_t* out, size_t n) {
+  if (strlen(s) != 2 * n) DIE("hex field of %zu bytes expected: %s", n, s);
+  for (size_t i = 0; i < n; i++) {
+    unsigned v;
+    if (sscanf(s + 2 * i, "%2x", &v) != 1) DIE("bad hex %s", s);
+    out[i] = (uint8_t)v;
+  }
+}
+
+static void hex_out(const uint8_t* p, size_t n) {
+  for (size_t i = 0; i < n; i++) printf("%02x", p[i]);
+}
+
+static uint64_t be(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int k = 0; k < n; k++) v = (v << 8) | p[k];
+  return v;
+}
+
+static uint8_t* slurp(const char* path, size_t* len) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return NULL;
+  fseek(f, 0, SEEK_END);
+  long sz = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t* p = malloc(sz > 0 ? (size_t)sz : 1);
+  if (sz > 0 && fread(p, 1, (size_t)sz, f) != (size_t)sz) DIE("read %s", path);
+  fclose(f);
+  *len = (size_t)(sz > 0 ? sz : 0);
+  return p;
+}
+
+/* ---- inputs ---- */
+static uint8_t g_eta0[32];
+static praos_params g_params;
+static praos_epoch_info g_ei;
+static praos_envelope g_env0;
+static praos_pool* g_pools;
+static uint32_t g_npools;
+
+static void read_epoch_file(const char* path) {
+  FILE* f = fopen(path, "r");
+  if (!f) DIE("open %s", path);
+  char line[512], a[128], b[128], c[128];
+  uint32_t cap = 0;
+  while (fgets(line, sizeof line, f)) {
+    unsigned long long x, y, z, w;
+    if (sscanf(line, "eta0 %127s", a) == 1) {
+      hex_in(a, g_eta0, 32);
+    } else if (sscanf(line, "params %llu %llu %llu %llu %127s", &x, &y, &z, &w, a) == 5) {
+      g_params.slots_per_kes_period = x;
+      g_params.max_kes_evo = y;
+      g_params.f_is_one = (int32_t)z;
+      g_params.vrf_check_output = (int32_t)w;
+      hex_in(a, g_params.c_raw, 16);
+    } else if (sscanf(line, "epoch %llu %llu %llu %llu", &x, &y, &z, &w) == 4) {
+      g_ei.epoch_base_slot = x; g_ei.epoch_base_no = y; g_ei.epoch_length = z; g_ei.stability_window = w;
+    } else if (sscanf(line, "env %llu %llu %llu %llu", &x, &y, &z, &w) == 4) {
+      g_env0.max_major_pv = x; g_env0.lv_prot_major = y; g_env0.max_header_size = z; g_env0.max_body_size = w;
+    } else if (sscanf(line, "pool %127s %127s %127s", a, b, c) == 3) {
+      if (g_npools == cap) {
+        cap = cap ? 2 * cap : 64;
+        g_pools = realloc(g_pools, cap * sizeof *g_pools);
+      }
+      hex_in(a, g_pools[g_npools].hash28, 28);
+      hex_in(b, g_pools[g_npools].vrf_hash32, 32);
+      hex_in(c, g_pools[g_npools].sigma_fp, 16);
+      g_npools++;
+    }
+  }
+  fclose(f);
+  g_env0.tip_is_origin = 1;
+}
+
+/* the stored headers, in chain order, through the secondary indexes */
+typedef struct {
+  uint8_t* bytes;   /* all headers back to back */
+  size_t len, n, cap;
+  uint64_t* off;
+  uint32_t* hlen;
+  uint64_t* slot;
+} chain_t;
+
+static void read_chain(const char* dir, chain_t* ch) {
+  memset(ch, 0, sizeof *ch);
+  for (int c = 0;; c++) {
+    char p[4096];
+    size_t dl, sl;
+    snprintf(p, sizeof p, "%s/%05d.chunk", dir, c);
+    uint8_t* data = slurp(p, &dl);
+    if (!data) break;
+    snprintf(p, sizeof p, "%s/%05d.secondary", dir, c);
+    uint8_t* sec = slurp(p, &sl);
+    if (!sec || sl % 56) DIE("secondary %d", c);
+    for (size_t e = 0; e < sl / 56; e++) {
+      const uint8_t* r = sec + 56 * e;
+      const uint64_t boff = be(r, 8), hoff = be(r + 8, 2), hsz = be(r + 10, 2);
+      if (boff + hoff + hsz > dl) DIE("entry outside chunk");
+      if (ch->n == ch->cap) {
+        ch->cap = ch->cap ? 2 * ch->cap : 1024;
+        ch->off = realloc(ch->off, ch->cap * 8);
+        ch->hlen = realloc(ch->hlen, ch->cap * 4);
+        ch->slot = realloc(ch->slot, ch->cap * 8);
+      }
+      ch->bytes = realloc(ch->bytes, ch->len + hsz);
+      memcpy(ch->bytes + ch->len, data + boff + hoff, hsz);
+      ch->off[ch->n] = ch->len;
+      ch->hlen[ch->n] = (uint32_t)hsz;
+      ch->slot[ch->n] = be(r + 48, 8);
+      ch->len += hsz;
+      ch->n++;
+    }
+    free(data);
+    free(sec);
+  }
+}
+
+/* ---- chain state storage ---- */
+enum { CAP = 1 << 16 };
+typedef struct {
+  praos_chain_state st;
+  uint8_t hk[28 * CAP];
+  uint64_t ctr[CAP];
+} state_buf;
+
+static void genesis_state(state_buf* s) {
+  memset(s, 0, sizeof *s);
+  s->st.last_slot_origin = 1;
+  s->st.counter_hash28 = s->hk;
+  s->st.counter = s->ctr;
+  s->st.cap = CAP;
+  memcpy(s->st.evolving.hash, g_eta0, 32);
+  memcpy(s->st.candidate.hash, g_eta0, 32);
+  memcpy(s->st.epoch_nonce.hash, g_eta0, 32);
+  s->st.lab.neutral = 1;
+  s->st.last_epoch_block.neutral = 1;
+}
+
+static void print_state(const char* phase, const state_buf* s, const praos_envelope* env, uint64_t validated,
+                        uint64_t stop, int stop_verdict, uint64_t epochs) {
+  size_t len = 0;
+  static uint8_t buf[64 + 48 * CAP];
+  if (praos_state_encode(&s->st, buf, sizeof buf, &len) != PRAOS_OK) DIE("state_encode");
+  printf("{\"phase\": \"%s\", \"validated\": %llu, \"stop_index\": %llu, \"stop_verdict\": %d, \"epochs\": %llu, "
+         "\"tip_slot\": %llu, \"tip_block_no\": %llu, \"tip_hash\": \"", phase, (unsigned long long)validated,
+         (unsigned long long)stop, stop_verdict, (unsigned long long)epochs, (unsigned long long)env->tip_slot,
+         (unsigned long long)env->tip_block_no);
+  hex_out(env->tip_hash, 32);
+  printf("\", \"state_cbor\": \"");
+  hex_out(buf, len);
+  printf("\"}\n");
+  fflush(stdout);
+}
+
+/* ---- phase 1: the Haskell binding's call sequence (Batch.hs praosReplayEpochs) ---- */
+static void phase_binding(const chain_t* ch) {
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) DIE("praos_open(0)");
+  static state_buf S;
+  genesis_state(&S);
+  praos_envelope env = g_env0;
+  uint64_t validated = 0, stop_index = ch->n, epochs = 0;
+  int stop_verdict = 0;
+  size_t i = 0;
+  while (i < ch->n) {
+    /* one epoch's headers */
+    const uint64_t e = (ch->slot[i] - g_ei.epoch_base_slot) / g_ei.epoch_length;
+    size_t j = i;
+    while (j < ch->n && (ch->slot[j] - g_ei.epoch_base_slot) / g_ei.epoch_length == e) j++;
+    const size_t n = j - i;
+    praos_nonce eta;
+    CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
+    CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
+    epochs++;
+    uint64_t* off = malloc(8 * n);
+    for (size_t k = 0; k < n; k++) off[k] = ch->off[i + k];
+    praos_header_bytes hb = {n, ch->bytes, ch->len, off, ch->hlen + i};
+    uint16_t* bits = calloc(n, 2);
+    int32_t* pidx = calloc(n, 4);
+    uint8_t* nonce = calloc(n, 32);
+    praos_out out = {bits, pidx, NULL, NULL, nonce};
+    praos_decoded dec;
+    memset(&dec, 0, sizeof dec);
+    uint64_t *slot = calloc(n, 8), *bno = calloc(n, 8), *ocn = calloc(n, 8);
+    uint8_t *prev = calloc(n, 32), *gen = calloc(n, 1), *cold = calloc(n, 32), *hh = calloc(n, 32);
+    uint32_t* bsz = calloc(n, 4);
+    dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;
+    dec.cold_vk = cold; dec.header_hash = hh; dec.body_size = bsz;
+    CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
+    praos_headers h;
+    memset(&h, 0, sizeof h);
+    h.n = n; h.slot = slot; h.cold_vk = cold; h.ocert_n = ocn;
+    env.block_no = bno; env.header_hash = hh; env.header_size = ch->hlen + i; env.body_size = bsz;
+    uint8_t* verdict = calloc(n, 1);
+    size_t stop = 0, done = 0;
+    CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
+    if (done != n) DIE("an epoch batch did not fold through (%zu of %zu)", done, n);
+    const int stopped = stop < n;
+    if (stopped) { stop_index = i + stop; stop_verdict = verdict[stop]; validated += stop; }
+    else validated += n;
+    free(off); free(bits); free(pidx); free(nonce); free(slot); free(bno); free(ocn); free(prev); free(gen);
+    free(cold); free(hh); free(bsz); free(verdict);
+    if (stopped) break;
+    i = j;
+  }
+  print_state("binding", &S, &env, validated, stop_index, stop_verdict, epochs);
+  praos_close(ctx);
+}
+
+/* ---- phase 2: the library's own driver ---- */
+static void phase_replay(const char* dir) {
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) DIE("praos_open(0)");
+  static state_buf S;
+  genesis_state(&S);
+  praos_envelope env = g_env0;
+  praos_replay_stats rs;
+  CK(ctx, praos_replay_immutable(ctx, dir, g_pools, g_npools, &g_params, &g_ei, &env, &S.st, 1 << 16, NULL, 0, &rs));
+  print_state("replay", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs);
+  praos_close(ctx);
+}
+
+/* ---- phase 3: several threads, one context each; and a group ---- */
+typedef struct {
+  const chain_t* ch;
+  size_t i0, i1;
+  uint16_t* bits;
+  int32_t* pidx;
+  uint8_t* nonce;
+  int rc;
+} job_t;
+
+static void* worker(void* arg) {
+  job_t* j = arg;
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) { j->rc = -100; return NULL; }
+  j->rc = praos_set_epoch(ctx, g_eta0, g_pools, g_npools, &g_params);
+  const size_t n = j->i1 - j->i0;
+  if (j->rc == PRAOS_OK && n) {
+    praos_header_bytes hb = {n, j->ch->bytes, j->ch->len, j->ch->off + j->i0, j->ch->hlen + j->i0};
+    praos_out out = {j->bits + j->i0, j->pidx + j->i0, NULL, NULL, j->nonce + 32 * j->i0};
+    for (int rep = 0; rep < 3 && j->rc == PRAOS_OK; rep++)   /* repeated: contexts interleave on the device */
+      j->rc = praos_verify_header_bytes(ctx, &hb, &out, NULL);
+  }
+  praos_close(ctx);
+  return NULL;
+}
+
+static void phase_threads(const chain_t* ch, int T) {
+  size_t n = 0;   /* the first epoch: eta0 is the genesis nonce */
+  while (n < ch->n && (ch->slot[n] - g_ei.epoch_base_slot) / g_ei.epoch_length == 0) n++;
+  uint16_t *b1 = calloc(n, 2), *bt = calloc(n, 2), *bg = calloc(n, 2);
+  int32_t *p1 = calloc(n, 4), *pt = calloc(n, 4), *pg = calloc(n, 4);
+  uint8_t *n1 = calloc(n, 32), *nt = calloc(n, 32), *ng = calloc(n, 32);
+  /* one context */
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) DIE("praos_open(0)");
+  CK(ctx, praos_set_epoch(ctx, g_eta0, g_pools, g_npools, &g_params));
+  praos_header_bytes hb = {n, ch->bytes, ch->len, ch->off, ch->hlen};
+  praos_out o1 = {b1, p1, NULL, NULL, n1};
+  CK(ctx, praos_verify_header_bytes(ctx, &hb, &o1, NULL));
+  praos_close(ctx);
+  /* T threads x own context */
+  pthread_t* th = calloc((size_t)T, sizeof *th);
+  job_t* jobs = calloc((size_t)T, sizeof *jobs);
+  for (int k = 0; k < T; k++) {
+    jobs[k] = (job_t){ch, n * k / T, n * (k + 1) / T, bt, pt, nt, 0};
+    pthread_create(&th[k], NULL, worker, &jobs[k]);
+  }
+  int trc = 0;
+  for (int k = 0; k < T; k++) {
+    pthread_join(th[k], NULL);
+    if (jobs[k].rc) trc = jobs[k].rc;
+  }
+  /* a group of T members on device 0 */
+  int* devs = calloc((size_t)T, sizeof *devs);
+  praos_group* g = praos_group_open(devs, T);
+  if (!g) DIE("praos_group_open");
+  if (praos_group_set_epoch(g, g_eta0, g_pools, g_npools, &g_params) != PRAOS_OK) DIE("%s", praos_group_last_error(g));
+  praos_out og = {bg, pg, NULL, NULL, ng};
+  if (praos_group_verify_header_bytes(g, &hb, &og, NULL) != PRAOS_OK) DIE("%s", praos_group_last_error(g));
+  const int gsize = praos_group_size(g);
+  praos_group_close(g);
+  size_t valid = 0;
+  for (size_t i = 0; i < n; i++) valid += b1[i] == 0;
+  const int same_t = !trc && !memcmp(b1, bt, 2 * n) && !memcmp(p1, pt, 4 * n) && !memcmp(n1, nt, 32 * n);
+  const int same_g = !memcmp(b1, bg, 2 * n) && !memcmp(p1, pg, 4 * n) && !memcmp(n1, ng, 32 * n);
+  printf("{\"phase\": \"threads\", \"threads\": %d, \"group_size\": %d, \"headers\": %zu, \"valid\": %zu, "
+         "\"thread_rc\": %d, \"threads_equal\": %s, \"group_equal\": %s}\n", T, gsize, n, valid, trc,
+         same_t ? "true" : "false", same_g ? "true" : "false");
+  fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+  if (argc != 4) DIE("usage: %s <immutable dir> <epoch file> <threads>", argv[0]);
+  if (praos_abi_version() != PRAOS_ABI_VERSION) DIE("ABI version %d, header %d", praos_abi_version(), PRAOS_ABI_VERSION);
+  read_epoch_file(argv[2]);
+  chain_t ch;
+  read_chain(argv[1], &ch);
+  phase_binding(&ch);
+  phase_replay(argv[1]);
+  phase_threads(&ch, atoi(argv[3]));
+  return 0;
+}

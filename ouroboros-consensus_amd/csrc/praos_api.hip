@@ -1128,6 +1128,17 @@ int praos_update_chain_dep_state(praos_ctx* c, const praos_headers* h, const uin
   return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, nullptr, ei, st, verdict, chain_stop, processed);
 }
 
+int praos_ticked_epoch_nonce(const praos_chain_state* st, const praos_epoch_info* ei, uint64_t slot,
+                             praos_nonce* out) {
+  if (!st || !ei || !out || ei->epoch_length == 0 || slot < ei->epoch_base_slot) return PRAOS_E_ARG;
+  auto epoch_of = [&](uint64_t s) {
+    return ei->epoch_base_no + (s < ei->epoch_base_slot ? 0 : (s - ei->epoch_base_slot) / ei->epoch_length);
+  };
+  const uint64_t e_old = st->last_slot_origin ? 0 : epoch_of(st->last_slot);
+  *out = epoch_of(slot) > e_old ? nonce_combine(st->candidate, st->last_epoch_block) : st->epoch_nonce;
+  return PRAOS_OK;
+}
+
 int praos_validate_headers(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash,
                            const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
                            const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict, size_t* chain_stop,

@@ -1,0 +1,183 @@
+// praos_group.hip -- one process driving several GPUs (in-library
+// multi-device): a group holds one praos_ctx per member device and splits every batch
+// into contiguous shards, one per member, each run by its own host thread on its own
+// context (HIP device and stream), outputs written in place in the caller's arrays.
+// Headers of one epoch are independent (Praos.hs:441-459 checks one header against
+// the epoch's ledger view only), so the shards need no exchange; the sequential fold
+// (praos_validate_headers / praos_update_chain_dep_state) runs afterwards over the
+// gathered outputs in slot order on any member context.
+//
+// A device may appear several times (several contexts on one GPU: the multi-threaded
+// use the C ABI allows, one context per host thread).
+#include "praos_kernels.h"
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+struct praos_group {
+  std::vector<praos_ctx*> ctx;
+  std::string err;
+};
+
+namespace {
+
+// [i0, i1) of member k when n items are split over m members
+inline void shard(size_t n, size_t m, size_t k, size_t* i0, size_t* i1) {
+  *i0 = n * k / m;
+  *i1 = n * (k + 1) / m;
+}
+
+template <typename T>
+inline T* at(T* p, size_t i, size_t per) { return p ? p + i * per : nullptr; }
+
+praos_out out_at(const praos_out* o, size_t i) {
+  return {at(o->bits, i, 1), at(o->pool_idx, i, 1), at(o->beta, i, 64), at(o->leader, i, 32), at(o->nonce, i, 32)};
+}
+
+praos_decoded dec_at(const praos_decoded* d, size_t i) {
+  praos_decoded r;
+  r.status = at(d->status, i, 1);
+  r.block_no = at(d->block_no, i, 1);
+  r.slot = at(d->slot, i, 1);
+  r.prev_hash = at(d->prev_hash, i, 32);
+  r.prev_is_genesis = at(d->prev_is_genesis, i, 1);
+  r.cold_vk = at(d->cold_vk, i, 32);
+  r.vrf_vk = at(d->vrf_vk, i, 32);
+  r.vrf_out = at(d->vrf_out, i, 64);
+  r.vrf_proof = at(d->vrf_proof, i, 80);
+  r.body_size = at(d->body_size, i, 1);
+  r.body_hash = at(d->body_hash, i, 32);
+  r.hot_vk = at(d->hot_vk, i, 32);
+  r.ocert_n = at(d->ocert_n, i, 1);
+  r.ocert_c0 = at(d->ocert_c0, i, 1);
+  r.ocert_sig = at(d->ocert_sig, i, 64);
+  r.prot_major = at(d->prot_major, i, 1);
+  r.prot_minor = at(d->prot_minor, i, 1);
+  r.kes_sig = at(d->kes_sig, i, 448);
+  r.signed_len = at(d->signed_len, i, 1);
+  r.signed_body = at(d->signed_body, i, PRAOS_SIGNED_STRIDE);
+  r.header_hash = at(d->header_hash, i, 32);
+  return r;
+}
+
+// run f(k) for every member on its own thread; the first failing member's code wins
+template <typename F>
+int fan_out(praos_group* g, F f) {
+  const size_t m = g->ctx.size();
+  std::vector<int> rc(m, PRAOS_OK);
+  std::vector<std::thread> th;
+  th.reserve(m);
+  for (size_t k = 0; k < m; k++) th.emplace_back([&, k] { rc[k] = f(k); });
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < m; k++)
+    if (rc[k] != PRAOS_OK) {
+      g->err = "member " + std::to_string(k) + ": " + praos_last_error(g->ctx[k]);
+      return rc[k];
+    }
+  return PRAOS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+praos_group* praos_group_open(const int* devices, int ndev) {
+  if (!devices || ndev <= 0) return nullptr;
+  praos_group* g = new praos_group();
+  for (int k = 0; k < ndev; k++) {
+    praos_ctx* c = praos_open(devices[k]);
+    if (!c || devices[k] < 0) {
+      if (c) praos_close(c);
+      for (praos_ctx* o : g->ctx) praos_close(o);
+      delete g;
+      return nullptr;
+    }
+    g->ctx.push_back(c);
+  }
+  return g;
+}
+
+void praos_group_close(praos_group* g) {
+  if (!g) return;
+  for (praos_ctx* c : g->ctx) praos_close(c);
+  delete g;
+}
+
+int praos_group_size(praos_group* g) { return g ? (int)g->ctx.size() : 0; }
+
+praos_ctx* praos_group_ctx(praos_group* g, int k) {
+  return g && k >= 0 && k < (int)g->ctx.size() ? g->ctx[k] : nullptr;
+}
+
+const char* praos_group_last_error(praos_group* g) { return g ? g->err.c_str() : "no group"; }
+
+int praos_group_set_option(praos_group* g, int opt, int value) {
+  if (!g) return PRAOS_E_ARG;
+  for (praos_ctx* c : g->ctx) {
+    const int r = praos_set_option(c, opt, value);
+    if (r != PRAOS_OK) return r;
+  }
+  return PRAOS_OK;
+}
+
+int praos_group_set_epoch(praos_group* g, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
+                          const praos_params* params) {
+  if (!g) return PRAOS_E_ARG;
+  return fan_out(g, [&](size_t k) { return praos_set_epoch(g->ctx[k], eta0, pools, npools, params); });
+}
+
+int praos_group_verify_headers(praos_group* g, const praos_headers* h, praos_out* out) {
+  if (!g || !h || !out || !out->bits) return PRAOS_E_ARG;
+  const size_t m = g->ctx.size();
+  return fan_out(g, [&](size_t k) {
+    size_t i0, i1;
+    shard(h->n, m, k, &i0, &i1);
+    if (i1 == i0) return (int)PRAOS_OK;
+    praos_headers s = *h;   // body_off stays absolute into the shared body_bytes
+    s.n = i1 - i0;
+    s.slot = at(h->slot, i0, 1);
+    s.cold_vk = at(h->cold_vk, i0, 32);
+    s.vrf_vk = at(h->vrf_vk, i0, 32);
+    s.vrf_out = at(h->vrf_out, i0, 64);
+    s.vrf_proof = at(h->vrf_proof, i0, 80);
+    s.hot_vk = at(h->hot_vk, i0, 32);
+    s.ocert_n = at(h->ocert_n, i0, 1);
+    s.ocert_c0 = at(h->ocert_c0, i0, 1);
+    s.ocert_sig = at(h->ocert_sig, i0, 64);
+    s.kes_sig = at(h->kes_sig, i0, 448);
+    s.body_off = at(h->body_off, i0, 1);
+    s.body_len = at(h->body_len, i0, 1);
+    praos_out o = out_at(out, i0);
+    return praos_verify_headers(g->ctx[k], &s, &o);
+  });
+}
+
+int praos_group_verify_header_bytes(praos_group* g, const praos_header_bytes* in, praos_out* out,
+                                    praos_decoded* dec) {
+  if (!g || !in || !out || !out->bits || (in->n && (!in->off || !in->len))) return PRAOS_E_ARG;
+  const size_t m = g->ctx.size();
+  return fan_out(g, [&](size_t k) {
+    size_t i0, i1;
+    shard(in->n, m, k, &i0, &i1);
+    if (i1 == i0) return (int)PRAOS_OK;
+    // only the shard's window of the arena travels to this member's device
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (size_t i = i0; i < i1; i++) {
+      lo = std::min<uint64_t>(lo, in->off[i]);
+      hi = std::max<uint64_t>(hi, in->off[i] + in->len[i]);
+    }
+    if (hi > in->bytes_len) { lo = 0; hi = in->bytes_len; }   // out-of-range entries: the decoder flags them
+    lo = std::min<uint64_t>(lo, hi);
+    std::vector<uint64_t> off(in->off + i0, in->off + i1);
+    for (auto& o : off) o -= std::min<uint64_t>(o, lo);
+    praos_header_bytes s{i1 - i0, in->bytes + lo, (size_t)(hi - lo), off.data(), in->len + i0};
+    praos_out o = out_at(out, i0);
+    if (!dec) return praos_verify_header_bytes(g->ctx[k], &s, &o, nullptr);
+    praos_decoded d = dec_at(dec, i0);
+    return praos_verify_header_bytes(g->ctx[k], &s, &o, &d);
+  });
+}
+
+}  // extern "C"

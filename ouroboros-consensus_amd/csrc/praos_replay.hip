@@ -111,11 +111,6 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
   auto epoch_of = [&](uint64_t s) {
     return s < ei->epoch_base_slot ? ei->epoch_base_no : ei->epoch_base_no + (s - ei->epoch_base_slot) / ei->epoch_length;
   };
-  // the epoch nonce the state ticks to at `slot` (tickChainDepState with isNewEpoch)
-  auto ticked_eta = [&](uint64_t slot) {
-    const uint64_t e_old = st->last_slot_origin ? 0 : epoch_of(st->last_slot);
-    return epoch_of(slot) > e_old ? praos_host::nonce_combine(st->candidate, st->last_epoch_block) : st->epoch_nonce;
-  };
   // resume (db-analyser --analyse-from a snapshot): a tip that is not Origin must be a
   // block of the database; replay starts right after it
   if (!env->tip_is_origin) {
@@ -169,7 +164,11 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
     int idle = 0;               // folds in a row that made no progress
     while (first < off.size()) {
       const size_t n = off.size() - first;
-      const praos_nonce eta = ticked_eta(eta_slot);
+      praos_nonce eta{};
+      if (praos_ticked_epoch_nonce(st, ei, eta_slot, &eta) != PRAOS_OK) {
+        praos_set_error_(ctx, "replay: slot " + std::to_string(eta_slot) + " before the epoch base");
+        return PRAOS_E_ARG;
+      }
       if (!have_eta || !praos_host::nonce_eq(eta, cur)) {
         const int r = praos_set_epoch(ctx, eta.neutral ? nullptr : eta.hash, pools, npools, params);
         if (r != PRAOS_OK) return r;

@@ -188,6 +188,19 @@ SIGNATURES = {
                                               ctypes.POINTER(Params), ctypes.POINTER(EpochInfo),
                                               ctypes.POINTER(Envelope), ctypes.POINTER(ChainState), ctypes.c_size_t,
                                               u8p, ctypes.c_size_t, ctypes.POINTER(ReplayStats)]),
+    "praos_ticked_epoch_nonce": (ctypes.c_int, [ctypes.POINTER(ChainState), ctypes.POINTER(EpochInfo), ctypes.c_uint64,
+                                                ctypes.POINTER(Nonce)]),
+    "praos_group_open": (ctypes.c_void_p, [i32p, ctypes.c_int]),
+    "praos_group_close": (None, [ctypes.c_void_p]),
+    "praos_group_size": (ctypes.c_int, [ctypes.c_void_p]),
+    "praos_group_ctx": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+    "praos_group_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "praos_group_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "praos_group_set_epoch": (ctypes.c_int, [ctypes.c_void_p, u8p, ctypes.POINTER(Pool), ctypes.c_uint32,
+                                             ctypes.POINTER(Params)]),
+    "praos_group_verify_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), ctypes.POINTER(Out)]),
+    "praos_group_verify_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
+                                                       ctypes.POINTER(Out), ctypes.POINTER(Decoded)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -771,6 +784,71 @@ class Context:
         return out
 
 
+class Group:
+    """praos_group: one context per listed device (repeats allowed), batches split into
+    contiguous shards run concurrently, outputs gathered in place (include/praos_hip.h)."""
+
+    def __init__(self, devices):
+        self.L = load()
+        arr = np.ascontiguousarray(devices, dtype=np.int32)
+        self.g = self.L.praos_group_open(ptr(arr, i32p), len(arr))
+        if not self.g:
+            raise PraosError(f"praos_group_open({list(devices)}) failed")
+        self.size = self.L.praos_group_size(self.g)
+
+    def close(self):
+        if self.g:
+            self.L.praos_group_close(self.g)
+            self.g = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def check(self, rc):
+        if rc != 0:
+            msg = self.L.praos_group_last_error(self.g)
+            raise PraosError(f"praos group rc={rc}: {msg.decode() if msg else ''}")
+
+    def member(self, k):
+        """A Context view of member k (not owned: closing the group closes it)."""
+        c = Context.__new__(Context)
+        c.L, c.h, c._keep = self.L, self.L.praos_group_ctx(self.g, k), []
+        return c
+
+    def set_option(self, opt, value):
+        self.check(self.L.praos_group_set_option(self.g, opt, value))
+
+    def set_epoch(self, eta0, pools, params: Params):
+        arr = Context.pool_array(pools)
+        e = None
+        if eta0 is not None:
+            eb = np.frombuffer(bytes(eta0), dtype=np.uint8).copy()
+            e = ptr(eb)
+        self.check(self.L.praos_group_set_epoch(self.g, e, arr, len(pools), ctypes.byref(params)))
+
+    def verify_headers(self, H):
+        n = len(H["slot"])
+        hs = Context.headers_struct(H)
+        o = Context.alloc_out(n)
+        os_ = Context.out_struct(o)
+        self.check(self.L.praos_group_verify_headers(self.g, ctypes.byref(hs), ctypes.byref(os_)))
+        return o
+
+    def verify_header_bytes(self, arena, off, length, decoded=False):
+        arena, off, length = Context._chunk(arena, off, length)
+        n = len(off)
+        hb = Context.header_bytes_struct(arena, off, length)
+        o = Context.alloc_out(n)
+        os_ = Context.out_struct(o)
+        D, d = Context.alloc_decoded(n) if decoded else (None, None)
+        self.check(self.L.praos_group_verify_header_bytes(self.g, ctypes.byref(hb), ctypes.byref(os_),
+                                                          ctypes.byref(d) if decoded else None))
+        return (o, D) if decoded else o
+
+
 def _state_struct(state, cap):
     st = ChainState()
     keys = list(state.get("counters", {}).keys())
@@ -813,6 +891,17 @@ def _state_from_struct(st, hk, cv):
         x = getattr(st, a)
         state[b] = None if x.neutral else bytes(x.hash)
     return state
+
+
+def ticked_epoch_nonce(state, epoch_info, slot):
+    """praos_ticked_epoch_nonce: the epoch nonce at `slot` (None = NeutralNonce)."""
+    L = load()
+    st, hk, cv = _state_struct(state, len(state.get("counters", {})))
+    out = Nonce()
+    rc = L.praos_ticked_epoch_nonce(ctypes.byref(st), ctypes.byref(EpochInfo(*epoch_info)), slot, ctypes.byref(out))
+    if rc != 0:
+        raise PraosError(f"praos_ticked_epoch_nonce rc={rc}")
+    return None if out.neutral else bytes(out.hash)
 
 
 def state_decode(data: bytes, cap=1 << 16):

@@ -1,0 +1,88 @@
+"""The FFI call sequence of the Haskell binding, replayed from C (integration/c/
+ffi_harness.c against libpraos_hip.so; module integration/haskell/.../Praos/Batch.hs),
+and the multi-threaded uses of the C ABI (one context per POSIX thread; a praos_group
+of several members on one device).
+
+The harness streams a multi-epoch ImmutableDB the way the binding does (cut at epoch
+boundaries, praos_ticked_epoch_nonce -> praos_set_epoch -> praos_verify_header_bytes ->
+praos_validate_headers) and must end in the PraosState (CBOR) and tip that both the
+library's own driver (praos_replay_immutable) and the Python replay reach; on a copy
+with a corrupted header all three stop at the same header with the same verdict."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from test_gpu_replay import ENV, EPOCH_LEN, _genesis_state, _locate, chain  # noqa: F401  (fixture)
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "integration", "c", "ffi_harness")
+
+
+def _epoch_file(path, chain):
+    p = chain["params"]
+    lines = [f"eta0 {chain['cfg']['eta0'].hex()}",
+             f"params {p.slots_per_kes_period} {p.max_kes_evo} {p.f_is_one} {p.vrf_check_output} {bytes(p.c_raw).hex()}",
+             "epoch " + " ".join(str(x) for x in chain["epoch_info"]),
+             f"env {ENV['max_major_pv']} {ENV['lv_prot_major']} {ENV['max_header_size']} {ENV['max_body_size']}"]
+    lines += [f"pool {h.hex()} {v.hex()} {int(s).to_bytes(16, 'little').hex()}" for h, v, s in chain["pools"]]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def _run_harness(db, epoch_file, threads=4):
+    assert os.path.exists(HARNESS), "build it: make -C integration/c (done by __graft_entry__.build())"
+    r = subprocess.run([HARNESS, db, epoch_file, str(threads)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    return {d["phase"]: d for d in (json.loads(x) for x in r.stdout.splitlines() if x.strip())}
+
+
+def _python_replay(ctx, chain, db):
+    from praos_hip import abi
+    st, env = _genesis_state(chain["cfg"]["eta0"]), dict(ENV, tip=None)
+    stats, _ = ctx.replay_immutable(db, chain["pools"], chain["params"], chain["epoch_info"], st, env)
+    return stats, abi.state_encode(st).hex(), env["tip"]
+
+
+def _agree(out, stats, cbor, tip):
+    for phase in ("binding", "replay"):
+        o = out[phase]
+        assert (o["validated"], o["stop_index"], o["stop_verdict"]) == \
+            (stats["validated"], stats["stop_index"], stats["stop_verdict"]), phase
+        assert o["state_cbor"] == cbor, phase
+        assert (o["tip_slot"], o["tip_block_no"], bytes.fromhex(o["tip_hash"])) == tip, phase
+
+
+def test_ffi_sequence_matches_replay(ctx, chain, tmp_path):  # noqa: F811
+    ef = str(tmp_path / "epoch.txt")
+    _epoch_file(ef, chain)
+    out = _run_harness(chain["path"], ef)
+    stats, cbor, tip = _python_replay(ctx, chain, chain["path"])
+    n = len(chain["off"])
+    assert stats["validated"] == n and out["binding"]["epochs"] == stats["epochs"] == 4
+    _agree(out, stats, cbor, tip)
+    t = out["threads"]
+    assert t["threads_equal"] and t["group_equal"] and t["group_size"] == 4
+    assert t["valid"] == t["headers"] == int((chain["slots"] < EPOCH_LEN).sum())
+
+
+def test_ffi_sequence_stops_with_replay(ctx, chain, tmp_path):  # noqa: F811
+    from praos_hip import abi
+    k = int(np.nonzero(chain["slots"] >= EPOCH_LEN)[0][17])
+    db = str(tmp_path / "bad")
+    shutil.copytree(chain["path"], db)
+    fname, pos = _locate(chain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + int(chain["len"][k]) - 200] ^= 0x01              # inside the KES signature
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    ef = str(tmp_path / "epoch.txt")
+    _epoch_file(ef, chain)
+    out = _run_harness(db, ef, threads=2)
+    stats, cbor, tip = _python_replay(ctx, chain, db)
+    assert (stats["stop_index"], stats["stop_verdict"]) == (k, abi.V_KES_SIG)
+    _agree(out, stats, cbor, tip)
