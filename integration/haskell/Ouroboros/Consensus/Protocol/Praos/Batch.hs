@@ -1,0 +1,353 @@
+{-# LANGUAGE DataKinds                #-}
+{-# LANGUAGE ForeignFunctionInterface #-}
+{-# LANGUAGE ScopedTypeVariables      #-}
+
+-- | Batched Praos header validation on AMD MI355X GPUs (libpraos_hip.so).
+--
+-- The binding a maintainer adds beside
+-- @ouroboros-consensus-protocol/src/ouroboros-consensus-protocol/Ouroboros/Consensus/Protocol/Praos.hs@.
+-- It replaces, for the headers of one epoch at a time, the per-header crypto of
+-- 'updateChainDepState' (Praos.hs:441-459: validateKESSignature :558-606 and
+-- validateVRFSignature :528-556) and, for db-analyser's header revalidation
+-- (Cardano/Tools/DBAnalyser/Analysis.hs:479-607, streaming loop :815-847), the whole
+-- validateHeader fold (envelope + updateChainDepState) over stored header bytes.
+--
+-- GHC is not available where this repository is built, so this module is shipped as
+-- source.  Its exact foreign-call sequence is exercised from C by
+-- integration/c/ffi_harness.c (tests/test_gpu_ffi.py), and the struct layouts below
+-- are checked against the C header by tests/test_abi.py (the "-- struct" lines).
+--
+-- Link: @extra-libraries: praos_hip@ (and @amdhip64@), include-dirs: include/.
+module Ouroboros.Consensus.Protocol.Praos.Batch
+  ( -- * Context
+    PraosBatchCtx
+  , withPraosBatchCtx
+  , PraosBatchError (..)
+    -- * Per epoch
+  , praosSetEpoch
+  , praosTickedEpochNonce
+    -- * Headers from stored bytes
+  , BatchResult (..)
+  , praosValidateHeaderBytes
+    -- * Whole ImmutableDB replay (db-analyser)
+  , ReplayStats (..)
+  , praosReplayImmutable
+    -- * Error reconstruction
+  , verdictToError
+  ) where
+
+import           Control.Exception (Exception, bracket, throwIO)
+import           Control.Monad (forM_, when)
+import qualified Data.ByteString as BS
+import qualified Data.ByteString.Unsafe as BSU
+import           Data.Word (Word16, Word32, Word64, Word8)
+import           Foreign
+import           Foreign.C.String (CString, peekCString, withCString)
+import           Foreign.C.Types (CInt (..), CSize (..))
+
+-- ---------------------------------------------------------------- C ABI (include/praos_hip.h)
+
+data PraosCtx
+
+-- struct praos_params (40 bytes): slots_per_kes_period@0 max_kes_evo@8 f_is_one@16 vrf_check_output@20 c_raw@24
+-- struct praos_pool (76 bytes): hash28@0 vrf_hash32@28 sigma_fp@60
+-- struct praos_headers (120 bytes): n@0 slot@8 cold_vk@16 ocert_n@56 body_bytes_len@112
+-- struct praos_header_bytes (40 bytes): n@0 bytes@8 bytes_len@16 off@24 len@32
+-- struct praos_out (40 bytes): bits@0 pool_idx@8 beta@16 leader@24 nonce@32
+-- struct praos_nonce (36 bytes): hash@0 neutral@32
+-- struct praos_chain_state (232 bytes): last_slot_origin@0 last_slot@8 counter_hash28@16 counter@24 m@32 cap@40 evolving@48 candidate@84 epoch_nonce@120 lab@156 last_epoch_block@192
+-- struct praos_epoch_info (32 bytes): epoch_base_slot@0 epoch_base_no@8 epoch_length@16 stability_window@24
+-- struct praos_envelope (120 bytes): block_no@0 header_hash@8 header_size@16 body_size@24 tip_is_origin@32 tip_slot@40 tip_block_no@48 tip_hash@56 max_major_pv@88 lv_prot_major@96 max_header_size@104 max_body_size@112
+-- struct praos_replay_stats (72 bytes): skipped@0 headers@8 validated@16 stop_index@24 stop_verdict@32 epochs@36 batches@40 chunks@44 ms_io@48 ms_device@56 ms_fold@64
+-- struct praos_decoded (168 bytes): status@0 block_no@8 slot@16 prev_hash@24 prev_is_genesis@32 cold_vk@40 body_size@72 ocert_n@96 header_hash@160
+
+foreign import ccall safe "praos_open"        c_open        :: CInt -> IO (Ptr PraosCtx)
+foreign import ccall safe "praos_close"       c_close       :: Ptr PraosCtx -> IO ()
+foreign import ccall safe "praos_last_error"  c_last_error  :: Ptr PraosCtx -> IO CString
+foreign import ccall safe "praos_abi_version" c_abi_version :: IO CInt
+foreign import ccall safe "praos_set_epoch"   c_set_epoch
+  :: Ptr PraosCtx -> Ptr Word8 -> Ptr () -> Word32 -> Ptr () -> IO CInt
+foreign import ccall safe "praos_ticked_epoch_nonce" c_ticked_epoch_nonce
+  :: Ptr () -> Ptr () -> Word64 -> Ptr () -> IO CInt
+foreign import ccall safe "praos_verify_header_bytes" c_verify_header_bytes
+  :: Ptr PraosCtx -> Ptr () -> Ptr () -> Ptr () -> IO CInt
+foreign import ccall safe "praos_validate_headers" c_validate_headers
+  :: Ptr PraosCtx -> Ptr () -> Ptr Word8 -> Ptr Word8 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> Ptr Word8 -> Ptr CSize -> Ptr CSize -> IO CInt
+foreign import ccall safe "praos_state_encode" c_state_encode
+  :: Ptr () -> Ptr Word8 -> CSize -> Ptr CSize -> IO CInt
+foreign import ccall safe "praos_state_decode" c_state_decode
+  :: Ptr Word8 -> CSize -> Ptr () -> IO CInt
+foreign import ccall safe "praos_replay_immutable" c_replay_immutable
+  :: Ptr PraosCtx -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
+
+abiVersion :: CInt
+abiVersion = 6
+
+-- ---------------------------------------------------------------- context
+
+newtype PraosBatchCtx = PraosBatchCtx (Ptr PraosCtx)
+
+data PraosBatchError = PraosBatchError !Int !String
+  deriving Show
+instance Exception PraosBatchError
+
+-- | One context per GPU (device ordinal) and per Haskell thread that uses it; calls block
+-- (the foreign imports are @safe@, so other Haskell threads keep running).
+withPraosBatchCtx :: Int -> (PraosBatchCtx -> IO a) -> IO a
+withPraosBatchCtx dev k = do
+  v <- c_abi_version
+  when (v /= abiVersion) $ throwIO (PraosBatchError (-2) ("libpraos_hip ABI " ++ show v))
+  bracket (c_open (fromIntegral dev)) c_close $ \p -> do
+    when (p == nullPtr) $ throwIO (PraosBatchError (-1) ("praos_open " ++ show dev))
+    k (PraosBatchCtx p)
+
+check :: PraosBatchCtx -> IO CInt -> IO ()
+check (PraosBatchCtx p) act = do
+  rc <- act
+  when (rc /= 0) $ do
+    msg <- c_last_error p >>= peekCString
+    throwIO (PraosBatchError (fromIntegral rc) msg)
+
+-- ---------------------------------------------------------------- marshalling helpers
+
+-- | Little-endian bytes of a non-negative Integer (Fixed E34 raw values, int128 two's
+-- complement for activeSlotLog).
+pokeLE :: Ptr Word8 -> Int -> Integer -> IO ()
+pokeLE p n x = forM_ [0 .. n - 1] $ \i ->
+  pokeByteOff p i (fromIntegral ((x `mod` 2 ^ (128 :: Int)) `shiftR` (8 * i)) :: Word8)
+
+pokeBS :: Ptr a -> Int -> BS.ByteString -> IO ()
+pokeBS p off bs = BSU.unsafeUseAsCStringLen bs $ \(src, n) -> copyBytes (p `plusPtr` off) (castPtr src) n
+
+-- | PraosParams as the ABI wants them (praos_params): slotsPerKESPeriod, maxKESEvo,
+-- f == 1, and activeSlotLog f (unActiveSlotLog, Fixed E34 raw, <= 0).
+data PraosParamsC = PraosParamsC
+  { ppSlotsPerKESPeriod :: !Word64
+  , ppMaxKESEvo         :: !Word64
+  , ppFIsOne            :: !Bool
+  , ppActiveSlotLogRaw  :: !Integer
+  }
+
+withParams :: PraosParamsC -> (Ptr () -> IO a) -> IO a
+withParams pp k = allocaBytes 40 $ \p -> do
+  fillBytes p 0 40
+  pokeByteOff p 0 (ppSlotsPerKESPeriod pp)
+  pokeByteOff p 8 (ppMaxKESEvo pp)
+  pokeByteOff p 16 (if ppFIsOne pp then 1 else 0 :: Word32)
+  pokeByteOff p 20 (1 :: Word32)                       -- verifyCertified checks the output
+  pokeLE (p `plusPtr` 24) 16 (ppActiveSlotLogRaw pp)
+  k (castPtr p)
+
+-- | PoolDistr entries: (KeyHash 'StakePool bytes, VRF key hash bytes, sigma as
+-- Fixed E34 raw = floor (sigma * 10^34), i.e. fromRational individualPoolStake).
+withPools :: [(BS.ByteString, BS.ByteString, Integer)] -> (Ptr () -> Word32 -> IO a) -> IO a
+withPools pools k = allocaBytes (76 * max 1 (length pools)) $ \p -> do
+  forM_ (zip [0 ..] pools) $ \(i, (hk, vrf, sigma)) -> do
+    let q = p `plusPtr` (76 * i)
+    pokeBS q 0 hk
+    pokeBS q 28 vrf
+    pokeLE (q `plusPtr` 60) 16 sigma
+  k (castPtr p) (fromIntegral (length pools))
+
+-- | A nonce: Nothing = NeutralNonce.
+pokeNonce :: Ptr a -> Int -> Maybe BS.ByteString -> IO ()
+pokeNonce p off mn = case mn of
+  Nothing -> fillBytes (p `plusPtr` off) 0 32 >> pokeByteOff p (off + 32) (1 :: Word32)
+  Just h  -> pokeBS p off h >> pokeByteOff p (off + 32) (0 :: Word32)
+
+peekNonce :: Ptr a -> Int -> IO (Maybe BS.ByteString)
+peekNonce p off = do
+  neutral :: Word32 <- peekByteOff p (off + 32)
+  if neutral /= 0 then pure Nothing else Just <$> BS.packCStringLen (castPtr (p `plusPtr` off), 32)
+
+-- ---------------------------------------------------------------- per epoch
+
+-- | praos_set_epoch: the epoch nonce (tickChainDepState's, see 'praosTickedEpochNonce'),
+-- the PoolDistr of the ledger view and the protocol parameters.
+praosSetEpoch :: PraosBatchCtx -> Maybe BS.ByteString -> [(BS.ByteString, BS.ByteString, Integer)]
+              -> PraosParamsC -> IO ()
+praosSetEpoch ctx@(PraosBatchCtx p) eta0 pools pp =
+  withPools pools $ \pp' np -> withParams pp $ \par ->
+    case eta0 of
+      Nothing -> check ctx (c_set_epoch p nullPtr pp' np par)
+      Just e  -> BSU.unsafeUseAsCString e $ \ep -> check ctx (c_set_epoch p (castPtr ep) pp' np par)
+
+-- | The serialised PraosState (Praos.hs:274-310) the fold reads and writes; the ABI
+-- takes the same CBOR through praos_state_encode / praos_state_decode, so the Haskell
+-- side keeps its own PraosState and converts at batch boundaries.
+withChainState :: BS.ByteString -> Int -> (Ptr () -> IO a) -> IO a
+withChainState cbor cap k =
+  allocaBytes 232 $ \st -> allocaBytes (28 * cap) $ \hk -> allocaBytes (8 * cap) $ \ctr -> do
+    fillBytes st 0 232
+    pokeByteOff st 16 hk
+    pokeByteOff st 24 ctr
+    pokeByteOff st 40 (fromIntegral cap :: CSize)
+    BSU.unsafeUseAsCStringLen cbor $ \(src, n) -> do
+      rc <- c_state_decode (castPtr src) (fromIntegral n) (castPtr st)
+      when (rc /= 0) $ throwIO (PraosBatchError (fromIntegral rc) "praos_state_decode")
+    k (castPtr st)
+
+encodeChainState :: Ptr () -> IO BS.ByteString
+encodeChainState st = alloca $ \lenp -> do
+  _ <- c_state_encode st nullPtr 0 lenp
+  n <- peek lenp
+  allocaBytes (fromIntegral n) $ \buf -> do
+    rc <- c_state_encode st buf n lenp
+    when (rc /= 0) $ throwIO (PraosBatchError (fromIntegral rc) "praos_state_encode")
+    BS.packCStringLen (castPtr buf, fromIntegral n)
+
+withEpochInfo :: (Word64, Word64, Word64, Word64) -> (Ptr () -> IO a) -> IO a
+withEpochInfo (baseSlot, baseNo, len, window) k = allocaBytes 32 $ \p -> do
+  pokeByteOff p 0 baseSlot >> pokeByteOff p 8 baseNo >> pokeByteOff p 16 len >> pokeByteOff p 24 window
+  k (castPtr p)
+
+-- | tickChainDepState's epoch nonce at a slot (praos_ticked_epoch_nonce).
+praosTickedEpochNonce :: BS.ByteString -> (Word64, Word64, Word64, Word64) -> Word64 -> IO (Maybe BS.ByteString)
+praosTickedEpochNonce stateCbor ei slot =
+  withChainState stateCbor (1 + 65536) $ \st -> withEpochInfo ei $ \eip -> allocaBytes 36 $ \out -> do
+    rc <- c_ticked_epoch_nonce st eip slot (castPtr out)
+    when (rc /= 0) $ throwIO (PraosBatchError (fromIntegral rc) "praos_ticked_epoch_nonce")
+    peekNonce out 0
+
+-- ---------------------------------------------------------------- headers from stored bytes
+
+-- | One epoch's stored headers validated (validateHeader over the batch): per-header
+-- verdicts (PRAOS_V_*), check bits, the chain stop and the state / tip after it.
+data BatchResult = BatchResult
+  { brVerdicts  :: ![Word8]
+  , brBits      :: ![Word16]
+  , brChainStop :: !Int
+  , brState     :: !BS.ByteString          -- PraosState CBOR after the last valid header
+  , brTip       :: !(Maybe (Word64, Word64, BS.ByteString))
+  }
+
+-- | Envelope limits of the ledger view: (praosMaxMajorPV, pvMajor lvProtocolVersion,
+-- lvMaxHeaderSize, lvMaxBodySize).
+type EnvLimits = (Word64, Word64, Word64, Word64)
+
+-- | praos_verify_header_bytes (decode + all crypto on the GPU) then praos_validate_headers
+-- (envelope, updateChainDepState) for the stored headers of one epoch, in chain order.
+-- The epoch must have been installed with 'praosSetEpoch'.
+praosValidateHeaderBytes :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
+                         -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> [BS.ByteString]
+                         -> IO BatchResult
+praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor hdrs = do
+  let n = length hdrs
+      arena = BS.concat hdrs
+      lens = map BS.length hdrs
+      offs = take n (scanl (+) 0 lens)
+  BSU.unsafeUseAsCString arena $ \ap ->
+    withArray (map fromIntegral offs :: [Word64]) $ \offp ->
+    withArray (map fromIntegral lens :: [Word32]) $ \lenp ->
+    allocaBytes 40 $ \hb ->
+    allocaArray n $ \(bits :: Ptr Word16) -> allocaArray n $ \(pidx :: Ptr Int32) ->
+    allocaBytes (32 * n) $ \nonce ->
+    allocaArray n $ \(slot :: Ptr Word64) -> allocaArray n $ \(bno :: Ptr Word64) ->
+    allocaArray n $ \(ocn :: Ptr Word64) -> allocaArray n $ \(bsz :: Ptr Word32) ->
+    allocaBytes (32 * n) $ \prev -> allocaBytes n $ \gen -> allocaBytes (32 * n) $ \cold ->
+    allocaBytes (32 * n) $ \hh -> allocaBytes 168 $ \dec -> allocaBytes 40 $ \out ->
+    allocaBytes 120 $ \hv -> allocaBytes 120 $ \env -> allocaArray n $ \(verdict :: Ptr Word8) ->
+    alloca $ \stopp -> alloca $ \donep ->
+    withChainState stateCbor (n + 65536) $ \st -> withEpochInfo ei $ \eip -> do
+      pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
+      pokeByteOff hb 16 (fromIntegral (BS.length arena) :: CSize)
+      pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
+      fillBytes out 0 40 >> pokeByteOff out 0 bits >> pokeByteOff out 8 pidx >> pokeByteOff out 32 nonce
+      fillBytes dec 0 168
+      pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
+      pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
+      check ctx (c_verify_header_bytes p (castPtr hb) (castPtr out) (castPtr dec))
+      -- praos_headers: n, slot, cold_vk, ocert_n are what the fold reads
+      fillBytes hv 0 120
+      pokeByteOff hv 0 (fromIntegral n :: CSize) >> pokeByteOff hv 8 slot >> pokeByteOff hv 16 cold
+      pokeByteOff hv 56 ocn
+      fillBytes env 0 120
+      pokeByteOff env 0 bno >> pokeByteOff env 8 hh >> pokeByteOff env 16 lenp >> pokeByteOff env 24 bsz
+      case tip of
+        Nothing -> pokeByteOff env 32 (1 :: Int32)
+        Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+      pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
+      pokeByteOff env 112 maxBS
+      check ctx (c_validate_headers p (castPtr hv) prev gen (castPtr out) (castPtr env) eip st verdict stopp donep)
+      stop <- peek stopp
+      vs <- peekArray n verdict
+      bs <- peekArray n bits
+      st' <- encodeChainState st
+      origin :: Int32 <- peekByteOff env 32
+      tip' <- if origin /= 0 then pure Nothing else do
+        s <- peekByteOff env 40
+        b <- peekByteOff env 48
+        h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+        pure (Just (s, b, h))
+      pure (BatchResult vs bs (fromIntegral stop) st' tip')
+
+-- ---------------------------------------------------------------- ImmutableDB replay
+
+data ReplayStats = ReplayStats
+  { rsSkipped, rsHeaders, rsValidated, rsStopIndex :: !Word64
+  , rsStopVerdict, rsEpochs, rsBatches, rsChunks :: !Word32
+  , rsMsIO, rsMsDevice, rsMsFold :: !Double
+  } deriving Show
+
+-- | praos_replay_immutable: the header-validation pass of db-analyser over an ImmutableDB
+-- directory (chunk + secondary index files), from the given state and tip (Nothing =
+-- Origin; otherwise a block of the database to resume after).  Returns the statistics,
+-- the final PraosState CBOR and tip.
+praosReplayImmutable :: PraosBatchCtx -> FilePath -> [(BS.ByteString, BS.ByteString, Integer)] -> PraosParamsC
+                     -> (Word64, Word64, Word64, Word64) -> EnvLimits -> Maybe (Word64, Word64, BS.ByteString)
+                     -> BS.ByteString -> Int
+                     -> IO (ReplayStats, BS.ByteString, Maybe (Word64, Word64, BS.ByteString))
+praosReplayImmutable ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor batchMax =
+  withCString dir $ \cdir -> withPools pools $ \pp' np -> withParams pp $ \par ->
+  withEpochInfo ei $ \eip -> withChainState stateCbor 65536 $ \st ->
+  allocaBytes 120 $ \env -> allocaBytes 72 $ \rs -> do
+    fillBytes env 0 120
+    case tip of
+      Nothing -> pokeByteOff env 32 (1 :: Int32)
+      Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+    pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
+    pokeByteOff env 112 maxBS
+    check ctx (c_replay_immutable p cdir pp' np par eip (castPtr env) st (fromIntegral batchMax) nullPtr 0
+                                  (castPtr rs))
+    stats <- ReplayStats <$> peekByteOff rs 0 <*> peekByteOff rs 8 <*> peekByteOff rs 16 <*> peekByteOff rs 24
+                         <*> peekByteOff rs 32 <*> peekByteOff rs 36 <*> peekByteOff rs 40 <*> peekByteOff rs 44
+                         <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64
+    st' <- encodeChainState st
+    origin :: Int32 <- peekByteOff env 32
+    tip' <- if origin /= 0 then pure Nothing else do
+      s <- peekByteOff env 40
+      b <- peekByteOff env 48
+      h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+      pure (Just (s, b, h))
+    pure (stats, st', tip')
+
+-- ---------------------------------------------------------------- errors
+
+-- | The reference error a verdict stands for, as a constructor name plus the payload
+-- the caller fills from the header it holds (Praos.hs:319-356 / HeaderValidation.hs).
+-- The bits split KES failures into "Reject" (Merkle path, 0x08) and the Ed25519 leaf
+-- ("Verification failed", 0x10), as verifySignedKES reports them.
+verdictToError :: Word8 -> Word16 -> Maybe String
+verdictToError v bits = case v of
+  0  -> Nothing
+  1  -> Just "KESBeforeStartOCERT"
+  2  -> Just "KESAfterEndOCERT"
+  3  -> Just "InvalidSignatureOCERT"
+  4  -> Just ("InvalidKesSignatureOCERT " ++ if bits .&. 0x08 /= 0 then "Reject" else "Verification failed")
+  5  -> Just "NoCounterForKeyHashOCERT"
+  6  -> Just "CounterTooSmallOCERT"
+  7  -> Just "CounterOverIncrementedOCERT"
+  8  -> Just "VRFKeyUnknown"
+  9  -> Just "VRFKeyWrongVRFKey"
+  10 -> Just "VRFKeyBadProof"
+  11 -> Just "VRFLeaderValueTooBig"
+  12 -> Just "(undecodable header)"
+  13 -> Just "UnexpectedBlockNo"
+  14 -> Just "UnexpectedSlotNo"
+  15 -> Just "UnexpectedPrevHash"
+  16 -> Just "ObsoleteNode"
+  17 -> Just "HeaderSizeTooLarge"
+  18 -> Just "BlockSizeTooLarge"
+  _  -> Just ("unknown verdict " ++ show v)

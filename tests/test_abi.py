@@ -57,3 +57,65 @@ def test_no_silent_fallback_without_gpu():
     from praos_hip import abi
     with pytest.raises(abi.PraosError):
         abi.Context(0)
+
+
+# C struct -> (ctypes class name in praos_hip.abi)
+_STRUCTS = {"praos_params": "Params", "praos_pool": "Pool", "praos_headers": "Headers",
+            "praos_header_bytes": "HeaderBytes", "praos_out": "Out", "praos_nonce": "Nonce",
+            "praos_chain_state": "ChainState", "praos_epoch_info": "EpochInfo", "praos_envelope": "Envelope",
+            "praos_replay_stats": "ReplayStats", "praos_decoded": "Decoded", "praos_counters": "Counters",
+            "praos_synth_params": "SynthParams"}
+HASKELL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "haskell",
+                       "Ouroboros", "Consensus", "Protocol", "Praos", "Batch.hs")
+
+
+def _c_layout(tmp_path):
+    """sizeof / offsetof of every field, from the C compiler over include/praos_hip.h."""
+    import subprocess
+    from praos_hip import abi
+    lines = ["#include <stddef.h>", "#include <stdio.h>", '#include "praos_hip.h"', "int main(void) {"]
+    for cs, py in _STRUCTS.items():
+        S = getattr(abi, py)
+        lines.append(f'  printf("{cs} %zu", sizeof({cs}));')
+        for name, _ in S._fields_:
+            lines.append(f'  printf(" {name}@%zu", offsetof({cs}, {name}));')
+        lines.append('  printf("\\n");')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(abi.HEADER_PATH), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    lay = {}
+    for ln in out.splitlines():
+        parts = ln.split()
+        lay[parts[0]] = (int(parts[1]), {k: int(v) for k, v in (p.split("@") for p in parts[2:])})
+    return lay
+
+
+def test_ctypes_and_haskell_layouts_match_c(tmp_path):
+    """Every ctypes struct of the Python binding and every '-- struct' layout line of the
+    Haskell binding (the offsets its pokeByteOff calls use) equal the C compiler's."""
+    from praos_hip import abi
+    lay = _c_layout(tmp_path)
+    for cs, py in _STRUCTS.items():
+        S = getattr(abi, py)
+        size, offs = lay[cs]
+        assert ctypes.sizeof(S) == size, cs
+        assert {n: getattr(S, n).offset for n, _ in S._fields_} == offs, cs
+    hs = open(HASKELL).read()
+    seen = 0
+    for m in re.finditer(r"^-- struct (\w+) \((\d+) bytes\): (.*)$", hs, flags=re.M):
+        cs, size, fields = m.group(1), int(m.group(2)), m.group(3).split()
+        assert lay[cs][0] == size, cs
+        for f in fields:
+            name, off = f.split("@")
+            assert lay[cs][1][name] == int(off), (cs, name)
+        seen += 1
+    assert seen >= 10
+
+
+def test_haskell_imports_declared_symbols():
+    hs = open(HASKELL).read()
+    imported = set(re.findall(r'foreign import ccall safe "(praos_[a-z0-9_]+)"', hs))
+    assert imported and imported <= _declared()
