@@ -15,13 +15,19 @@ What it restates:
     Alonzo onward 4.  Pinned: the formula reproduces the body hash of every golden block
     (golden/cardano/disk/Block_{Shelley,Allegra,Mary,Alonzo,Babbage,Conway}, golden/shelley/disk/Block;
     tests/test_block_oracle.py).
+  * verifyHeaderIntegrity for TPraos (Shelley/Protocol/TPraos.hs:59-76): the same KES check
+    (t = kp - c0 when kp >= c0, else 0) over the 15-field BHBody.
   * The on-disk Cardano block is the HardForkBlock wrapper [eraTag, block] (golden files); the
-    Shelley-family block is [header, seg_1 .. seg_k].  Praos headers (Babbage = 6, Conway = 7)
-    are decoded by oracle/cbor_header.py (same rules as k_decode.hip).
+    Shelley-family block is [header, seg_1 .. seg_k].  Era tags: Shelley 2, Allegra 3, Mary 4
+    (3 segments, TPraos headers), Alonzo 5 (4 segments, TPraos), Babbage 6, Conway 7 (4
+    segments, Praos headers).  Headers are decoded by oracle/cbor_header.py (same rules as
+    k_decode.hip).
 
 Restated decode rules (parity unpinned beyond the golden blocks -- the real segment decoders
-are the ledger's): a block is either [eraTag, [header, s1, s2, s3, s4]] with eraTag in {6, 7},
-or an unwrapped [header, s1..s3] / [header, s1..s4]; every segment must be ONE well-formed CBOR
+are the ledger's): a block is either [eraTag, [header, s1..sk]] with eraTag in 2..7, k = 3 for
+tags 2-4 and 4 for tags 5-7, the header's body a 15-field BHBody for tags 2-5 and a 10-field
+HeaderBody for 6-7; or an unwrapped [header, s1..s3] / [header, s1..s4] with either header
+kind; every segment must be ONE well-formed CBOR
 item (definite or indefinite lengths, tags, simple values; indefinite strings made of definite
 chunks of the same major type; at most MAX_INDEF nested indefinite items); no bytes may follow
 the block item.  Anything else sets BLK_DECODE and nothing else.
@@ -39,6 +45,7 @@ BLK_KES = 0x02
 BLK_BODY_HASH = 0x04
 MAX_INDEF = 16
 PRAOS_ERAS = (6, 7)
+TPRAOS_ERAS = (2, 3, 4, 5)
 
 
 def _b2b(m):
@@ -119,6 +126,17 @@ def cbor_skip(buf, p, end):
     return p
 
 
+def _body_arity(buf, p, end):
+    """Arity of the header body at p (the header is [body, kesSig])."""
+    mt, _, arg, q = _head(buf, p, end)
+    if mt != 4 or arg != 2:
+        raise _Bad
+    mt, _, arg, _ = _head(buf, q, end)
+    if mt != 4 or arg is None:
+        raise _Bad
+    return arg
+
+
 def split_block(buf, off, length):
     """-> (ok, header_off, header_len, [(seg_off, seg_len)])."""
     if off > len(buf) or length > len(buf) - off:
@@ -128,18 +146,18 @@ def split_block(buf, off, length):
         mt, ai, arg, p = _head(buf, off, end)
         if mt != 4 or arg is None:
             raise _Bad
-        wrapped = False
+        arity = None
         if arg == 2:
             mt2, _, tag, q = _head(buf, p, end)
-            if mt2 != 0:
-                raise _Bad
-            if tag not in PRAOS_ERAS:
+            if mt2 != 0 or tag not in PRAOS_ERAS + TPRAOS_ERAS:
                 raise _Bad
             mt, ai, arg, p = _head(buf, q, end)
-            if mt != 4 or arg != 5:
+            if mt != 4 or arg != (4 if tag in (2, 3, 4) else 5):
                 raise _Bad
-            wrapped = True
-        if not wrapped and arg not in (4, 5):
+            arity = 15 if tag in TPRAOS_ERAS else 10
+        elif arg not in (4, 5):
+            raise _Bad
+        if arity is not None and _body_arity(buf, p, end) != arity:
             raise _Bad
         spans = []
         for _ in range(arg):
@@ -163,7 +181,7 @@ def verify_block_integrity(buf, off, length, spkp):
     ok, ho, hl, segs = split_block(buf, off, length)
     if not ok:
         return BLK_DECODE, bytes(32)
-    d = ch.decode_header(buf, ho, hl)
+    d = ch.decode_header(buf, ho, hl, allow_tpraos=True)
     if d["status"] & ch.DEC_FAIL:
         return BLK_DECODE, bytes(32)
     f = d["fields"]

@@ -18,6 +18,14 @@ protocol/Ouroboros/Consensus/Protocol/Praos/Header.hs):
     cborg's plain decoders accept non-shortest integer/length heads, so a
     stored body may be non-canonical; the signed bytes are then re-encoded.
 
+TPraos (Shelley..Alonzo) headers, for the block-integrity path: BHeader = [BHBody,
+kesSig] with the 15-field BHBody of cardano-protocol-tpraos (BHeader.hs encodeBHBody,
+not vendored -- restated from its published encoder and pinned by the golden
+Block_{Shelley,Allegra,Mary,Alonzo} files): [blockNo, slotNo, prevHash, vk, vrfVk,
+[etaOut, etaProof], [leaderOut, leaderProof], bodySize, bodyHash, hotVk, n, c0, sigma,
+protMajor, protMinor] (OCert and ProtVer inlined as groups).  Its KES message is the
+same canonical re-serialisation (SignableRepresentation BHBody = serialize').
+
 Status bits (first failure only; NONCANONICAL is informational and only set on
 success).  Restated edge rules, parity unpinned (the decoders live in
 cardano-binary / cardano-ledger-binary, not vendored): indefinite-length items
@@ -40,6 +48,7 @@ MAX_PROT_MAJOR = 9
 DEC_FAIL = 0x5F               # every bit but NONCANONICAL
 
 SIGNED_STRIDE = 448           # max canonical body = 447 bytes
+TP_SIGNED_STRIDE = 640        # max canonical TPraos BHBody = 598 bytes
 
 
 class _Fail(Exception):
@@ -136,16 +145,33 @@ def encode_body(f, wide=()):
         _head(4, 2, "pv" in wide), u("prot_major"), u("prot_minor")])
 
 
+def encode_tpraos_body(f, wide=()):
+    """Canonical encodeBHBody (15 fields; the OCert and ProtVer groups inlined)."""
+    def u(k):
+        return _head(0, f[k], k in wide)
+
+    def b(k):
+        return _head(2, len(f[k]), k in wide) + f[k]
+    prev = b"\xf6" if f["prev_hash"] is None else b("prev_hash")
+    return b"".join([
+        _head(4, 15, "body" in wide), u("block_no"), u("slot"), prev, b("cold_vk"), b("vrf_vk"),
+        _head(4, 2, "vrf" in wide), b("vrf_out"), b("vrf_proof"),
+        _head(4, 2, "leader" in wide), b("leader_out"), b("leader_proof"),
+        u("body_size"), b("body_hash"), b("hot_vk"), u("n"), u("c0"), b("ocert_sig"),
+        u("prot_major"), u("prot_minor")])
+
+
 def encode_header(f, kes_sig, wide=()):
     """EncCBOR HeaderRaw (Header.hs:201-210): [body, kesSig]."""
     return _head(4, 2) + encode_body(f, wide) + _head(2, len(kes_sig)) + kes_sig
 
 
-def decode_header(arena, off, length):
+def decode_header(arena, off, length, allow_tpraos=False):
     """Decode header bytes arena[off:off+length].  Returns a dict with 'status',
-    the fields (None on failure), 'signed' (canonical body bytes, b'' on failure)
-    and 'header_hash' (Blake2b-256 of the stored bytes; zeros on DEC_RANGE)."""
-    out = {"status": 0, "fields": None, "signed": b"", "header_hash": bytes(32)}
+    the fields (None on failure), 'signed' (canonical body bytes, b'' on failure),
+    'header_hash' (Blake2b-256 of the stored bytes; zeros on DEC_RANGE) and 'tpraos'
+    (the body had 15 fields; only accepted with allow_tpraos, the block path)."""
+    out = {"status": 0, "fields": None, "signed": b"", "header_hash": bytes(32), "tpraos": False}
     if off > len(arena) or length > len(arena) - off:
         out["status"] = DEC_RANGE
         return out
@@ -156,7 +182,10 @@ def decode_header(arena, off, length):
         r.array(2)
         body_start = r.pos
         r.canon = True
-        r.array(10)
+        arity = r.expect(4)
+        tp = allow_tpraos and arity == 15
+        if arity != (15 if tp else 10):
+            raise _Fail(DEC_SYNTAX)
         f = {"block_no": r.uint(), "slot": r.uint()}
         if r.pos < r.end and r.b[r.pos] == 0xF6:
             r.pos += 1
@@ -168,14 +197,20 @@ def decode_header(arena, off, length):
         r.array(2)
         f["vrf_out"] = r.bytes_fixed(64)
         f["vrf_proof"] = r.bytes_fixed(80)
+        if tp:
+            r.array(2)
+            f["leader_out"] = r.bytes_fixed(64)
+            f["leader_proof"] = r.bytes_fixed(80)
         f["body_size"] = r.uint((1 << 32) - 1)
         f["body_hash"] = r.bytes_fixed(32)
-        r.array(4)
+        if not tp:
+            r.array(4)
         f["hot_vk"] = r.bytes_fixed(32)
         f["n"] = r.uint()
         f["c0"] = r.uint()
         f["ocert_sig"] = r.bytes_fixed(64)
-        r.array(2)
+        if not tp:
+            r.array(2)
         f["prot_major"] = r.uint(MAX_PROT_MAJOR)
         f["prot_minor"] = r.uint()
         canon = r.canon
@@ -186,11 +221,12 @@ def decode_header(arena, off, length):
     except _Fail as e:
         out["status"] = e.bit
         return out
-    signed = encode_body(f)
+    signed = encode_tpraos_body(f) if tp else encode_body(f)
     assert (signed == raw[body_start:body_end]) == canon
     out["status"] = 0 if canon else DEC_NONCANONICAL
     out["fields"] = f
     out["signed"] = signed
+    out["tpraos"] = tp
     return out
 
 

@@ -2,10 +2,13 @@
 //
 // verifyBlockIntegrity spkp blk = verifyHeaderIntegrity spkp hdr && blockMatchesHeader hdr blk
 // (Shelley/Ledger/Integrity.hs:14-20).  The header half is k_kes in header mode
-// (t = max(0, kp - c0), Shelley/Protocol/Praos.hs:84-101) over the k_decode SoA;
+// (t = max(0, kp - c0), Shelley/Protocol/Praos.hs:84-101 and TPraos.hs:59-76) over the
+// k_decode SoA (Praos HeaderBody or TPraos BHBody);
 // this module supplies the block half:
-//   k_block_split   one lane per stored block: the era wrapper [eraTag, [header, s1..s4]]
-//                   (eraTag 6/7) or a bare [header, s1..s3|s4]; every segment must be one
+//   k_block_split   one lane per stored block: the era wrapper [eraTag, [header, s1..sk]]
+//                   -- Shelley 2, Allegra 3, Mary 4 (k = 3, TPraos header), Alonzo 5 (k = 4,
+//                   TPraos), Babbage 6, Conway 7 (k = 4, Praos header) -- or a bare
+//                   [header, s1..s3|s4] with either header kind; every segment must be one
 //                   well-formed CBOR item.  Emits the header span (k_decode's input) and
 //                   the segment spans, segment-major ([k][i]).
 //   k_seg_hash      one lane per (segment k, block i), segment-major so a workgroup hashes
@@ -124,13 +127,21 @@ __global__ void __launch_bounds__(NT) k_block_split(size_t n, const uint8_t* __r
     bool indef;
     ok = head(c, mt, ai, arg, indef) && mt == 4 && !indef;
     bool wrapped = false;
+    uint64_t arity = 0;   // header body arity the era tag demands (0: bare block, either)
     if (ok && arg == 2) {
       uint64_t tag;
-      ok = head(c, mt, ai, tag, indef) && mt == 0 && (tag == 6 || tag == 7);   // Babbage, Conway
-      ok = ok && head(c, mt, ai, arg, indef) && mt == 4 && !indef && arg == 5;
+      ok = head(c, mt, ai, tag, indef) && mt == 0 && tag >= 2 && tag <= 7;        // Shelley .. Conway
+      ok = ok && head(c, mt, ai, arg, indef) && mt == 4 && !indef && arg == (tag <= 4 ? 4u : 5u);
+      arity = tag <= 5 ? 15 : 10;                                                // TPraos / Praos header
       wrapped = true;
     }
     ok = ok && (wrapped || arg == 4 || arg == 5);
+    if (ok && arity) {   // the header is [body, kesSig]: peek at the body's arity
+      Cur h{arena, c.p, c.end, true};
+      uint64_t a2, ab;
+      ok = head(h, mt, ai, a2, indef) && mt == 4 && !indef && a2 == 2 && head(h, mt, ai, ab, indef) && mt == 4 &&
+           !indef && ab == arity;
+    }
     if (ok) {
       nitems = (uint32_t)arg;
       for (uint32_t k = 0; k < nitems && ok; k++) {

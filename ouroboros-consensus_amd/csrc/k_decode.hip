@@ -16,6 +16,14 @@
 // The CPU restatement is oracle/cbor_header.py (same status semantics: the
 // first failure wins; NONCANONICAL is informational).
 //
+// Block batches (k_block.hip) also accept TPraos headers (allow_tp): BHeader =
+// [BHBody, kesSig] with the 15-field BHBody of cardano-protocol-tpraos
+// (encodeBHBody: the eta and leader certificates as two [out, proof] pairs, OCert and
+// ProtVer inlined), the integrity check of Shelley/Protocol/TPraos.hs:59-76.  The eta
+// certificate goes to vrf_out/vrf_proof; the leader certificate is only needed to
+// re-encode a non-canonical body and is then read back from the arena.  Signed
+// bodies of block batches use a 640-byte stride (max canonical BHBody 598 bytes).
+//
 // Memory: every field load goes through ld64u (two aligned 8-byte loads and a
 // funnel shift), so a lane walks its ~850-byte header with 8-byte accesses;
 // the arena is padded by 16 bytes so the second load never leaves it.  The
@@ -26,7 +34,6 @@
 
 namespace {
 
-constexpr uint32_t SIGNED_STRIDE = 448;
 
 struct Rd {
   const uint8_t* __restrict__ p;
@@ -85,6 +92,18 @@ __device__ __forceinline__ uint64_t rd_uint(Rd& r, uint64_t limit) {
 }
 
 // fixed-length byte string -> aligned destination record (N multiple of 16)
+// fixed-length byte string that is only skipped; returns the payload offset
+template <int N>
+__device__ __forceinline__ uint64_t rd_skip(Rd& r) {
+  const uint64_t ln = rd_expect(r, 2);
+  if (!r.st && ln != (uint64_t)N) r.st = PRAOS_DEC_SIZE;
+  if (!r.st && r.pos + N > r.end) r.st = PRAOS_DEC_SYNTAX;
+  if (r.st) return 0;
+  const uint64_t at = r.pos;
+  r.pos += N;
+  return at;
+}
+
 template <int N>
 __device__ __forceinline__ void rd_bytes(Rd& r, uint8_t* __restrict__ dst) {
   const uint64_t ln = rd_expect(r, 2);
@@ -137,7 +156,8 @@ struct DecOut {
 
 __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                      const uint64_t* __restrict__ hoff,
-                                                     const uint32_t* __restrict__ hlen, DecOut o) {
+                                                     const uint32_t* __restrict__ hlen, DecOut o, int allow_tp,
+                                                     uint32_t stride) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t off = hoff[i], len = hlen[i];
@@ -150,7 +170,9 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
   rd_array(r, 2);
   const uint64_t body_start = r.pos;
   r.canon = true;
-  rd_array(r, 10);
+  const uint64_t arity = rd_expect(r, 4);
+  const bool tp = allow_tp && arity == 15;
+  if (!r.st && arity != (tp ? 15u : 10u)) r.st = PRAOS_DEC_SYNTAX;
   const uint64_t block_no = rd_uint(r, ~0ull);
   const uint64_t slot = rd_uint(r, ~0ull);
   uint8_t genesis = 0;
@@ -167,14 +189,20 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
   rd_array(r, 2);
   rd_bytes<64>(r, o.vrf_out + 64 * i);
   rd_bytes<80>(r, o.vrf_proof + 80 * i);
+  uint64_t lead_out = 0, lead_proof = 0;     // TPraos leader certificate (arena offsets)
+  if (tp) {
+    rd_array(r, 2);
+    lead_out = rd_skip<64>(r);
+    lead_proof = rd_skip<80>(r);
+  }
   const uint64_t body_size = rd_uint(r, 0xffffffffull);
   rd_bytes<32>(r, o.body_hash + 32 * i);
-  rd_array(r, 4);
+  if (!tp) rd_array(r, 4);
   rd_bytes<32>(r, o.hot_vk + 32 * i);
   const uint64_t ocn = rd_uint(r, ~0ull);
   const uint64_t occ0 = rd_uint(r, ~0ull);
   rd_bytes<64>(r, o.ocert_sig + 64 * i);
-  rd_array(r, 2);
+  if (!tp) rd_array(r, 2);
   const uint64_t pmaj = rd_uint(r, PRAOS_MAX_PROT_MAJOR);   // DecCBOR Version: <= maxVersion
   const uint64_t pmin = rd_uint(r, ~0ull);
   const bool canon = r.canon;
@@ -182,11 +210,12 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
   rd_bytes<448>(r, o.kes_sig + 448 * i);
   if (!r.st && r.pos != r.end) r.st = PRAOS_DEC_TRAILING;
 
-  uint8_t* sb = o.signed_body + (size_t)SIGNED_STRIDE * i;
+  uint8_t* sb = o.signed_body + (size_t)stride * i;
   uint32_t slen = 0xffffffffu;
   if (!r.st) {
     if (canon) {
-      // signed bytes = the stored slice (<= 447 bytes for a canonical body)
+      // signed bytes = the stored slice (<= 447 bytes for a canonical Praos body,
+      // <= 598 for TPraos)
       slen = (uint32_t)(body_end - body_start);
       uint64_t* d = (uint64_t*)sb;
       for (uint32_t k = 0; k < slen; k += 8) {
@@ -196,7 +225,7 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
       }
     } else {
       Wr w{sb, 0};
-      wr_head(w, 4, 10);
+      wr_head(w, 4, tp ? 15 : 10);
       wr_head(w, 0, block_no);
       wr_head(w, 0, slot);
       if (genesis) wr_byte(w, 0xF6);
@@ -206,14 +235,19 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
       wr_head(w, 4, 2);
       wr_bytes(w, o.vrf_out + 64 * i, 64);
       wr_bytes(w, o.vrf_proof + 80 * i, 80);
+      if (tp) {
+        wr_head(w, 4, 2);
+        wr_bytes(w, arena + lead_out, 64);
+        wr_bytes(w, arena + lead_proof, 80);
+      }
       wr_head(w, 0, body_size);
       wr_bytes(w, o.body_hash + 32 * i, 32);
-      wr_head(w, 4, 4);
+      if (!tp) wr_head(w, 4, 4);
       wr_bytes(w, o.hot_vk + 32 * i, 32);
       wr_head(w, 0, ocn);
       wr_head(w, 0, occ0);
       wr_bytes(w, o.ocert_sig + 64 * i, 64);
-      wr_head(w, 4, 2);
+      if (!tp) wr_head(w, 4, 2);
       wr_head(w, 0, pmaj);
       wr_head(w, 0, pmin);
       slen = w.n;
@@ -230,7 +264,7 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
   o.prot_major[i] = ok ? pmaj : 0;
   o.prot_minor[i] = ok ? pmin : 0;
   o.prev_genesis[i] = ok ? genesis : 0;
-  o.body_off[i] = (uint64_t)SIGNED_STRIDE * i;
+  o.body_off[i] = (uint64_t)stride * i;
   o.body_len[i] = slen;
   if (!ok) {
     // a header that does not decode has no fields: zero every record
@@ -254,9 +288,9 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint64_t* ocert_n, uint64_t* ocert_c0, uint64_t* body_off, uint32_t* body_len,
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
-                         uint8_t* header_hash, uint16_t* status) {
+                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride) {
   DecOut o{slot,     cold_vk,   vrf_vk,      vrf_out,  vrf_proof, hot_vk,       ocert_sig, kes_sig,
            ocert_n,  ocert_c0,  body_off,    body_len, signed_body, block_no,   prev_hash, prev_genesis,
            body_size, body_hash, prot_major, prot_minor, header_hash, status};
-  hipLaunchKernelGGL(k_decode_praos, grid, block, 0, stream, n, arena, arena_len, hoff, hlen, o);
+  hipLaunchKernelGGL(k_decode_praos, grid, block, 0, stream, n, arena, arena_len, hoff, hlen, o, allow_tp, stride);
 }

@@ -71,7 +71,7 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint64_t* ocert_n, uint64_t* ocert_c0, uint64_t* body_off, uint32_t* body_len,
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
-                         uint8_t* header_hash, uint16_t* status);
+                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride);
 void launch_block_split(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
                         uint64_t arena_len, uint64_t* off_io, uint32_t* len_io, uint64_t* seg_off, uint32_t* seg_len,
                         uint8_t* nseg, uint8_t* status);

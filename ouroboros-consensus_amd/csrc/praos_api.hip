@@ -10,6 +10,7 @@ static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
 static constexpr size_t BTAB_N = 128;              // entries per fixed-base table (scalarmult.hpp)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
 static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
+static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
 #include <algorithm>
 #include <cstdio>
@@ -71,6 +72,7 @@ struct praos_batch {
   // batches from stored bytes (praos_batch_upload_bytes): the arena and the
   // decoded HeaderBody fields beyond the SoA above (k_decode.hip)
   bool from_bytes = false;
+  uint32_t signed_stride = PRAOS_SIGNED_STRIDE;   // bytes per signed body (block batches: TP_SIGNED_STRIDE)
   uint8_t* arena = nullptr;
   size_t arena_len = 0;
   uint64_t *hoff = nullptr, *block_no = nullptr, *prot_major = nullptr, *prot_minor = nullptr;
@@ -379,7 +381,7 @@ static int batch_decode(praos_ctx* c, praos_batch* b) {
                       b->slot, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->hot_vk, b->ocert_sig, b->kes_sig,
                       b->ocert_n, b->ocert_c0, b->body_off, b->body_len, b->body, b->block_no, b->prev_hash,
                       b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor, b->header_hash,
-                      b->dec_status);
+                      b->dec_status, b->is_block ? 1 : 0, b->signed_stride);
   return hipGetLastError() == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
 }
 
@@ -502,6 +504,10 @@ praos_batch* praos_block_batch_upload(praos_ctx* c, const praos_header_bytes* bl
   ok &= dalloc(b, &b->seg_hash, 32 * 4 * n) == hipSuccess;
   ok &= dalloc(b, &b->blk_result, n) == hipSuccess;
   ok &= dalloc(b, &b->blk_hash, 32 * n) == hipSuccess;
+  // TPraos BHBody signed bodies are up to 598 bytes: a wider stride than header batches
+  b->signed_stride = TP_SIGNED_STRIDE;
+  b->body_bytes_len = (size_t)TP_SIGNED_STRIDE * n;
+  ok &= dalloc(b, &b->body, b->body_bytes_len + 16) == hipSuccess;
   if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
   // the uploaded spans are whole blocks; k_block_split rewrites hoff/hlen to the header spans
   if (n) {

@@ -63,8 +63,12 @@ def rand_segments(r, big=False, pad=0):
 
 
 def make_block(r, spkp, era=6, slot=None, c0=None, big=False, wrapped=True, pad=0):
-    """-> (block bytes, header fields, KES seed)."""
+    """-> (block bytes, header fields, KES seed).  era 2..5: a TPraos block (15-field
+    BHBody; 3 segments for Shelley/Allegra/Mary, 4 for Alonzo); 6/7: Praos."""
+    tp = era in bi.TPRAOS_ERAS
     segs = rand_segments(r, big, pad)
+    if era in (2, 3, 4):
+        segs = segs[:3]
     bh = bi._b2b(b"".join(bi._b2b(s) for s in segs))
     seed = rbytes(r, 32)
     slot = r.getrandbits(24) if slot is None else slot
@@ -75,9 +79,12 @@ def make_block(r, spkp, era=6, slot=None, c0=None, big=False, wrapped=True, pad=
     f = {"block_no": r.getrandbits(20), "slot": slot, "prev_hash": rbytes(r, 32), "cold_vk": rbytes(r, 32),
          "vrf_vk": rbytes(r, 32), "vrf_out": rbytes(r, 64), "vrf_proof": rbytes(r, 80),
          "body_size": sum(map(len, segs)), "body_hash": bh, "hot_vk": orc.kes_vk(seed), "n": r.getrandbits(8),
-         "c0": c0, "ocert_sig": rbytes(r, 64), "prot_major": 9, "prot_minor": 0}
-    kes = orc.kes_sign(seed, min(t, 63), ch.encode_body(f))  # t > 63: verification must reject
-    hdr = ch.encode_header(f, kes)
+         "c0": c0, "ocert_sig": rbytes(r, 64), "prot_major": 9 if not tp else 2 + (era - 2), "prot_minor": 0}
+    if tp:
+        f["leader_out"], f["leader_proof"] = rbytes(r, 64), rbytes(r, 80)
+    body = ch.encode_tpraos_body(f) if tp else ch.encode_body(f)
+    kes = orc.kes_sign(seed, min(t, 63), body)  # t > 63: verification must reject
+    hdr = H(4, 2) + body + H(2, len(kes)) + kes
     inner = H(4, 1 + len(segs)) + hdr + b"".join(segs)
     blk = (H(4, 2) + H(0, era) + inner) if wrapped else inner
     return blk, f, seed

@@ -46,8 +46,50 @@ def test_golden_praos_blocks_integrity_bits():
             assert k["expect"]["kes_result_praos_body"] == 2
             assert bits == bi.BLK_KES, k["era"]
             assert bh.hex() == k["body_hash"]
-        else:  # TPraos eras are outside the Praos block path
-            assert bits == bi.BLK_DECODE
+        else:  # TPraos eras: KES over the 15-field BHBody, body hash -- intact
+            assert k["expect"]["kes_result"] == 0
+            assert bits == 0, k["era"]
+            assert bh.hex() == k["body_hash"]
+
+
+def test_golden_tpraos_headers_decode():
+    """The 15-field BHBody decode reproduces every field the golden TPraos headers hold, and
+    its canonical re-encoding is the stored body (the KES message)."""
+    import cbor_header as ch
+    for k in KATS:
+        if k["kind"] != "tpraos":
+            continue
+        hdr = bytes.fromhex(k["header_cbor"])
+        d = ch.decode_header(hdr, 0, len(hdr), allow_tpraos=True)
+        assert d["status"] == 0 and d["tpraos"], k["era"]
+        f = d["fields"]
+        assert (f["block_no"], f["slot"], f["n"], f["c0"]) == (k["block_no"], k["slot"], k["n"], k["c0"])
+        for key, fk in (("cold_vk", "cold_vk"), ("vrf_vk", "vrf_vk"), ("vrf_out", "eta_out"),
+                        ("vrf_proof", "eta_proof"), ("leader_out", "leader_out"), ("leader_proof", "leader_proof"),
+                        ("body_hash", "body_hash"), ("hot_vk", "hot_vk"), ("ocert_sig", "ocert_sig"),
+                        ("kes_sig", "kes_sig")):
+            assert f[key].hex() == k[fk], (k["era"], key)
+        assert hdr[1:1 + len(d["signed"])] == d["signed"]
+        # a Praos-only decode rejects the 15-field body
+        assert ch.decode_header(hdr, 0, len(hdr))["status"] == ch.DEC_SYNTAX
+
+
+def test_era_tag_and_header_kind_must_agree():
+    """[tag, block]: a TPraos header under a Praos era tag (and vice versa) or a wrong
+    segment count for the era does not decode."""
+    by = {k["era"]: bytes.fromhex(k["block_cbor"]) for k in KATS}
+    shelley, babbage = by["Shelley"], by["Babbage"]
+    assert bi.verify_block_integrity(shelley, 0, len(shelley), SPKP)[0] == 0
+    for tag in (6, 7):
+        b = bytearray(shelley)
+        b[1] = tag
+        assert bi.verify_block_integrity(bytes(b), 0, len(b), SPKP)[0] == bi.BLK_DECODE
+    b = bytearray(shelley)
+    b[1] = 5                                   # Alonzo wants 4 segments
+    assert bi.verify_block_integrity(bytes(b), 0, len(b), SPKP)[0] == bi.BLK_DECODE
+    b = bytearray(babbage)
+    b[1] = 5                                   # Alonzo: TPraos header expected
+    assert bi.verify_block_integrity(bytes(b), 0, len(b), SPKP)[0] == bi.BLK_DECODE
 
 
 def test_cbor_skip_agrees_with_generic_decoder():
@@ -78,3 +120,18 @@ def test_kes_period_clamp():
     # verifies; verifyHeaderIntegrity has no maxKESEvo bound (unlike validateKESSignature)
     blk, f, _ = bc.make_block(r, SPKP, slot=70 * SPKP, c0=3)
     assert bi.verify_block_integrity(blk, 0, len(blk), SPKP)[0] == 0
+
+
+def test_synthetic_tpraos_blocks():
+    """Synthetic TPraos blocks of every TPraos era (and a bare one) are intact; the
+    mutation corpus on an Alonzo block gives the same kinds as on Praos blocks."""
+    r = random.Random(0x7A)
+    for era in (2, 3, 4, 5):
+        for wrapped in (True, False):
+            blk, _, _ = bc.make_block(r, SPKP, era=era, wrapped=wrapped)
+            assert bi.verify_block_integrity(blk, 0, len(blk), SPKP)[0] == 0, (era, wrapped)
+    blk, f, _ = bc.make_block(r, SPKP, era=5)
+    for kind in bc.MUTATIONS:
+        m = bc.mutate(blk, f, r, kind)
+        want = 0 if kind == "era_5" else bc.expected_kind(kind)     # already an Alonzo block
+        assert bi.verify_block_integrity(m, 0, len(m), SPKP)[0] == want, kind

@@ -45,18 +45,18 @@ def test_golden_blocks(ctx):
     res = _check(ctx, arena, off, ln)
     for k, r in zip(kats, res):
         # Praos blocks: body matches, KES leaf made over the TPraos body (Examples.hs:173-192);
-        # TPraos eras are outside this path (DECODE)
-        assert int(r) == (bi.BLK_KES if k["kind"] == "praos" else bi.BLK_DECODE), k["era"]
+        # TPraos blocks (Shelley..Alonzo, 15-field BHBody): intact
+        assert int(r) == (bi.BLK_KES if k["kind"] == "praos" else 0), k["era"]
 
 
 def test_mutation_corpus(ctx):
     r = random.Random(0xB10C5)
     blocks, want = [], []
     for j in range(3):
-        blk, f, _ = bc.make_block(r, SPKP, era=6 + j % 2)
+        blk, f, _ = bc.make_block(r, SPKP, era=5 + j)        # Alonzo (TPraos), Babbage, Conway
         for kind in bc.MUTATIONS:
             blocks.append(bc.mutate(blk, f, r, kind))
-            want.append(bc.expected_kind(kind))
+            want.append(0 if (kind == "era_5" and j == 0) else bc.expected_kind(kind))   # j = 0: Alonzo
     arena, off, ln = _pack(blocks, r)
     res = _check(ctx, arena, off, ln)
     assert [int(x) for x in res] == want
@@ -72,6 +72,10 @@ def test_random_blocks_and_clamp(ctx):
             blk, _, _ = bc.make_block(r, SPKP, big=True)                        # multi-KB segments
         elif j % 8 == 2:
             blk, _, _ = bc.make_block(r, SPKP, wrapped=False)                   # bare 5-item block
+        elif j % 8 == 3:
+            blk, _, _ = bc.make_block(r, SPKP, era=2 + (j // 8) % 4)             # TPraos eras
+        elif j % 8 == 4:
+            blk, _, _ = bc.make_block(r, SPKP, era=2, wrapped=False)            # bare Shelley block
         else:
             blk, _, _ = bc.make_block(r, SPKP)
         if j % 5 == 4:
