@@ -12,8 +12,9 @@ of the headers corrupted by the consensus-testlib +1-byte model.  The headers ar
 signed on the GPU (real Ed25519 / Sum6KES / ECVRF-draft03) and resident in HBM
 before the timed region.  One step = one full validation pass (all kernels) over
 the GPU's shard.  Multi-GPU: one process per GPU, no collective on the data path
-(only the timing max-reduce); weak scaling -- each rank validates a full 432k-block
-shard (the one shipped schedule, so ranks > 0 replay the same blocks).
+(only the timing max-reduce); weak scaling by default -- each rank validates a full
+432k-block shard (the one shipped schedule, so ranks > 0 replay the same blocks);
+--scaling strong splits the 432k blocks into contiguous slot ranges, one per rank.
 
 --config c2|c3|c4 measure the single-primitive configs (1M OCert verifies with
 distinct keys, 1M VRF verifies + leader checks, 1M Sum6KES verifies), c1 the
@@ -269,8 +270,9 @@ def load_traffic(kernel, workload):
     return k.get("bytes_per_launch"), os.path.relpath(TRAFFIC_FILE, ROOT)
 
 
-def make_input(ctx, args, cfg, rank):
-    """Returns (H, pool_list, corrupted, params, eta0, c_raw, spkp, maxevo)."""
+def make_input(ctx, args, cfg, rank, world=1):
+    """Returns (H, pool_list, corrupted, params, eta0, c_raw, spkp, maxevo).  Strong
+    scaling: rank r signs blocks [r*n/world, (r+1)*n/world) of the chain."""
     from praos_hip import abi, chains, fixed
     import hashlib
     if args.config in ("c1", "c5"):
@@ -281,6 +283,9 @@ def make_input(ctx, args, cfg, rank):
             sched = chains.search_schedule(ctx, ccfg, ccfg["blocks"])
         n = args.items or cfg["items"]
         assert n <= len(sched[0]), "the shipped schedule has fewer blocks"
+        if args.scaling == "strong":
+            a, b = n * rank // world, n * (rank + 1) // world
+            sched, n = (sched[0][a:b], sched[1][a:b]), b - a
         H, pool_list, corrupted, p = chains.make_chain(ctx, ccfg, sched, n=n,
                                                        corrupt_per_10000=args.corrupt_per_10000)
         return (H, pool_list, corrupted, p, ccfg["eta0"], fixed.active_slot_log(ccfg["f"]),
@@ -307,6 +312,9 @@ def main():
     ap.add_argument("--config", default="c5", choices=sorted(CONFIGS))
     ap.add_argument("--items", type=int, default=None, help="items per GPU (default: the config's)")
     ap.add_argument("--corrupt-per-10000", type=int, default=100)
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: every GPU validates a full shard (default); strong: the config's "
+                         "blocks split over the GPUs (c1/c5)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-workers", type=int, default=16, help="CPU-twin threads (the box's share: 16)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -316,6 +324,8 @@ def main():
                     help="min uses of a public key for the per-batch key cache (0 = off)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.scaling == "strong" and args.config not in ("c1", "c5"):
+        ap.error("--scaling strong applies to the chain configs (c1, c5)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -336,7 +346,7 @@ def main():
     ctx.set_option(abi.OPT_KERNELS, cfg["kernels"])
     ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
     t0 = time.perf_counter()
-    H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank)
+    H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank, world)
     n = len(H["slot"])
     ctx.set_epoch(eta0, pool_list, p)
     b = ctx.upload(H)
@@ -401,7 +411,8 @@ def main():
         return
     steps = args.steps
     ms_step = dt * 1e3 / steps
-    value = world * n * steps / dt
+    total = n * world if args.scaling == "weak" else (args.items or cfg["items"])
+    value = total * steps / dt
     kms /= steps
     per_kernel = {"ocert": kser[0], "kes": kser[1], "vrf": kser[2], "leader": kser[3]}
     ran = [k for k in ("ocert", "kes", "vrf") if cfg["kernels"] & MASK[k]]
@@ -422,11 +433,11 @@ def main():
         "metric": cfg["metric"],
         "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
         "n_gpus": world, "steps": steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
         "dtype": "u32 (GF(2^255-19) radix-2^32 limbs; Fixed E34 bignum)",
         "data": "synthetic: GPU-signed chain" + (" from the shipped first-leader-wins schedule"
                                                   if args.config in ("c1", "c5") else ""),
-        "config": {"workload": cfg["workload"], "items_per_gpu": n, "pools": len(pool_list) or None,
+        "config": {"workload": cfg["workload"], "items_per_gpu": n, "items_total": total, "pools": len(pool_list) or None,
                    "active_slot_coeff": "1/20",
                    "signed_body": "canonical HeaderBody CBOR" if args.config in ("c1", "c5") else "397 random bytes",
                    "parallelism": f"shard-by-slot-range x{world}"},

@@ -183,8 +183,9 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items
- * uncached; out[3..5] = the same for VRF keys.  Returns 0. */
-int praos_batch_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[6]);
+ * uncached; out[3..5] = the same for VRF keys; out[6..8] for the KES leaf keys
+ * (the Ed25519 key each Sum6KES signature ends on).  Returns 0. */
+int praos_batch_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[9]);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
  * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run, 5 = header
  * decode (batches from praos_batch_upload_bytes; 0 otherwise).  With concurrent

@@ -39,7 +39,19 @@ void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
                            uint32_t* kinfo);
-void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ hot_vk, const uint8_t* __restrict__ kes_sig, const uint64_t* __restrict__ body_off, const uint32_t* __restrict__ body_len, const uint8_t* __restrict__ body, size_t body_bytes_len, const uint64_t* __restrict__ slot, const uint64_t* __restrict__ ocert_c0, uint64_t slots_per_kes_period, const uint32_t* __restrict__ period, uint16_t* __restrict__ bits, uint8_t* __restrict__ result, ge_cached* tabs);
+void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                const ge_niels* gbtab, const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off,
+                const uint32_t* body_len, const uint8_t* body, size_t body_bytes_len, const uint64_t* slot,
+                const uint64_t* ocert_c0, uint64_t slots_per_kes_period, const uint32_t* period, uint16_t* bits,
+                uint8_t* result, ge_cached* tabs);
+void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                   const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                   const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off, const uint32_t* body_len,
+                   const uint8_t* body, size_t body_bytes_len, const uint64_t* slot, const uint64_t* ocert_c0,
+                   uint64_t slots_per_kes_period, uint16_t* bits);
+void launch_kes_leafkeys(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* kes_sig,
+                         const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
+                         uint8_t* keys);
 void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab);
 void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in, const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one, int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits, uint8_t* is_leader, int32_t* iters, const uint16_t* dec_status);
 void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);

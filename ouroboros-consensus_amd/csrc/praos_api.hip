@@ -60,14 +60,15 @@ struct praos_batch {
   uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
   // per-lane point tables of the three crypto kernels (kcommon.hpp lane_tab)
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
-  // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys
+  // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
     uint32_t cap = 0, max_entries = 0;
     uint32_t *slot_rep = nullptr, *slot_cnt = nullptr, *entry_rep = nullptr, *kinfo = nullptr;
     int32_t *slot_entry = nullptr, *item_slot = nullptr, *item_entry = nullptr;
     uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
     ge_cached* ktab = nullptr;
-  } kc[2];
+  } kc[3];                       // [2] KES leaf keys
+  uint8_t* kes_leaf = nullptr;   // n*32: the leaf key of each header's KES signature
   bool kc_used = false;
   // batches from stored bytes (praos_batch_upload_bytes): the arena and the
   // decoded HeaderBody fields beyond the SoA above (k_decode.hip)
@@ -271,6 +272,7 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   ok &= dalloc(b, (uint8_t**)&b->tab_ocert, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_kes, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_vrf, LT_VRF_B * n) == hipSuccess;
+  ok &= dalloc(b, &b->kes_leaf, 32 * n) == hipSuccess;
   for (auto& k : b->kc) {
     k.cap = 256;
     while (k.cap < 2 * n) k.cap <<= 1;
@@ -446,11 +448,26 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(bo, 0, 2 * n, so));
   }
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
-  if (c->kernels & 2)
-    launch_kes(g, blk, sk, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body, b->body_bytes_len,
-               b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr,
-               b->tab_kes);
-  else
+  if (c->kernels & 2) {
+    if (kc) {
+      // leaf-key cache: the Ed25519 key a Sum6KES signature ends on repeats for every
+      // header a pool signs in one KES period
+      praos_batch::KeyCache& k = b->kc[2];
+      launch_kes_leafkeys(g, blk, sk, n, b->kes_sig, b->slot, b->ocert_c0, P.slots_per_kes_period, b->kes_leaf);
+      int r = keycache_prepass(k, b->kes_leaf, 0, sk);
+      if (r != PRAOS_OK) return r;
+      launch_kes_ck(g, blk, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->hot_vk, b->kes_sig,
+                    b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
+                    P.slots_per_kes_period, bk);
+      launch_kes(g, blk, sk, n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
+                 b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
+                 bk, (uint8_t*)nullptr, b->tab_kes);
+    } else {
+      launch_kes(g, blk, sk, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
+                 b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
+                 (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
+    }
+  } else
     HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
   const bool do_vrf = (c->kernels & 4) != 0;
@@ -541,7 +558,7 @@ int praos_block_batch_run(praos_ctx* c, praos_batch* b, uint64_t slots_per_kes_p
   launch_seg_hash(dim3(nblocks(4 * n, NT)), blk, c->side[0], n, b->arena, b->seg_off, b->seg_len, b->nseg,
                   b->seg_hash);
   HIPCHK(c, hipEventRecord(c->side_ev[0], c->side[0]));
-  launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
+  launch_kes(g, blk, c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
              b->body_bytes_len, b->slot, b->ocert_c0, slots_per_kes_period, (const uint32_t*)nullptr, bk,
              (uint8_t*)nullptr, b->tab_kes);
   HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
@@ -576,13 +593,13 @@ int praos_verify_block_integrity(praos_ctx* c, const praos_header_bytes* blocks,
   return r;
 }
 
-int praos_batch_stats(praos_ctx* c, praos_batch* b, uint32_t out[6]) {
+int praos_batch_stats(praos_ctx* c, praos_batch* b, uint32_t out[9]) {
   if (!c || !b || !out) return PRAOS_E_ARG;
-  for (int k = 0; k < 6; k++) out[k] = 0;
+  for (int k = 0; k < 9; k++) out[k] = 0;
   if (!b->kc_used) return PRAOS_OK;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (int t = 0; t < 2; t++) {
+  for (int t = 0; t < 3; t++) {
     uint32_t cnt[4] = {0, 0, 0, 0};
     HIPCHK(c, hipMemcpy(cnt, b->kc[t].counters, 16, hipMemcpyDeviceToHost));
     out[3 * t] = std::min(cnt[0], b->kc[t].max_entries);
@@ -794,7 +811,8 @@ int praos_verify_kes(praos_ctx* c, size_t n, const uint8_t* vk, const uint32_t* 
   auto dtab = s.up<ge_cached>(nullptr, LT_ED_B * n);
   if (!s.ok) { c->err = "alloc/copy"; return PRAOS_E_OOM; }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  launch_kes(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, c->btab, dvk, dsig, doff, dlen, dmsg,
+  launch_kes(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+             c->btab, dvk, dsig, doff, dlen, dmsg,
                      total, (const uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t)1, dp, (uint16_t*)nullptr,
                      dres, dtab);
   HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
@@ -1472,7 +1490,7 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
     HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
     launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
                  P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
-    launch_kes(g, blk, c->stream, n, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
+    launch_kes(g, blk, c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
                b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk,
                (uint8_t*)nullptr, b->tab_kes);
     launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,

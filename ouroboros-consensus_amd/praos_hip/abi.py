@@ -392,11 +392,12 @@ class Context:
         self.check(self.L.praos_set_option(self.h, opt, value))
 
     def batch_stats(self, b):
-        """Key-cache statistics of the last run: dict of cold/vrf entries, hits, misses."""
-        out = np.zeros(6, np.uint32)
+        """Key-cache statistics of the last run: dict of cold/vrf/kes entries, hits, misses."""
+        out = np.zeros(9, np.uint32)
         self.check(self.L.praos_batch_stats(self.h, b, ptr(out, u32p)))
         return {"cold_keys": int(out[0]), "cold_hits": int(out[1]), "cold_misses": int(out[2]),
-                "vrf_keys": int(out[3]), "vrf_hits": int(out[4]), "vrf_misses": int(out[5])}
+                "vrf_keys": int(out[3]), "vrf_hits": int(out[4]), "vrf_misses": int(out[5]),
+                "kes_keys": int(out[6]), "kes_hits": int(out[7]), "kes_misses": int(out[8])}
 
     def kernel_ms(self, which):
         return float(self.L.praos_batch_kernel_ms(self.h, which))
