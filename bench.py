@@ -44,12 +44,12 @@ sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 # kernel schedules (tools/workmodel.py; DESIGN.md sec. 4 "Work model").
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  # noqa: E402
-                       W_KEY_COLD, W_KEY_VRF)
+                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES)
 # gfx950 VALU peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")   # tools/profile.sh r02
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02c_traffic.json")   # tools/profile.sh r02c
 
 CONFIGS = {
     "c1": dict(items=10_000, kernels=7, metric="Praos headers validated/sec (CPU config C1)",
@@ -419,16 +419,19 @@ def main():
     # algorithmic work of one run (tools/workmodel.py): headers on cached keys
     # run the short chains, plus the per-key precomputation
     work = {"ocert": kst["cold_hits"] * W_OCERT_CK + kst["cold_misses"] * W_OCERT + kst["cold_keys"] * W_KEY_COLD,
-            "kes": n * W_KES,
+            "kes": kst["kes_hits"] * W_KES_CK + kst["kes_misses"] * W_KES + kst["kes_keys"] * W_KEY_KES,
             "vrf": kst["vrf_hits"] * W_VRF_CK + kst["vrf_misses"] * W_VRF + kst["vrf_keys"] * W_KEY_VRF}
     if args.keycache == 0:
-        work["ocert"], work["vrf"] = n * W_OCERT, n * W_VRF
+        work["ocert"], work["vrf"], work["kes"] = n * W_OCERT, n * W_VRF, n * W_KES
     dominant = max(ran, key=lambda k: per_kernel[k])
     wk = work[dominant] / n
     dom_achieved = work[dominant] / (per_kernel[dominant] * 1e-3)
     w_pipe = (sum(work[k] for k in ran) + (n * W_LEADER if "vrf" in ran else 0)) / n
     pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
-    traffic, traffic_src = load_traffic(f"k_{dominant}", cfg["workload"])
+    # the dominant kernel as it runs: the key-cache variant when the cache is on
+    dom_kernel = f"k_{dominant}_ck" if (args.keycache and kst.get(f"{'cold' if dominant == 'ocert' else dominant}_hits")) \
+        else f"k_{dominant}"
+    traffic, traffic_src = load_traffic(dom_kernel, cfg["workload"])
     line = {
         "metric": cfg["metric"],
         "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
@@ -441,7 +444,7 @@ def main():
                    "active_slot_coeff": "1/20",
                    "signed_body": "canonical HeaderBody CBOR" if args.config in ("c1", "c5") else "397 random bytes",
                    "parallelism": f"shard-by-slot-range x{world}"},
-        "roofline": {"bound": "valu-int32", "kernel": f"k_{dominant}",
+        "roofline": {"bound": "valu-int32", "kernel": dom_kernel,
                      "achieved": round(dom_achieved / 1e12, 3), "peak": round(PEAK_INT32 / 1e12, 2),
                      "unit": "T int32-ops/s", "frac": round(dom_achieved / PEAK_INT32, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": traffic_src,

@@ -10,8 +10,12 @@
 // sees exactly the point, validity flags and encoding its own bytes give.
 //
 //   k_key_insert     per item: insert key into the hash set, count uses
-//   k_key_assign     per slot: keys used >= min_count get a cache entry
-//   k_key_partition  per item: entry id, hit list / miss list (wave-aggregated)
+//   k_key_assign     per slot: keys used >= min_count get a cache entry and a
+//                    contiguous range of the hit list (one atomic per entry)
+//   k_key_partition  per item: entry id; hits go to their entry's range, so the
+//                    hit list is grouped by key: the lanes of a wave mostly share
+//                    one key's tables (L1/L2-resident) instead of 64 different ones;
+//                    misses to the miss list in item order (wave-aggregated)
 //   k_key_precompute per entry: checks, decode, tables (and Y's encoding)
 #include "kcommon.hpp"
 
@@ -44,10 +48,10 @@ __global__ void k_key_insert(size_t n, const uint8_t* __restrict__ keys, uint32_
   item_slot[i] = (int32_t)h;
 }
 
-// counters: [0] entries, [1] hits, [2] misses
+// counters: [0] entries, [1] hits, [2] misses, [3] hit-list ranges handed out
 __global__ void k_key_assign(uint32_t cap, const uint32_t* __restrict__ slot_rep, const uint32_t* __restrict__ slot_cnt,
                              uint32_t min_count, uint32_t max_entries, int32_t* __restrict__ slot_entry,
-                             uint32_t* __restrict__ entry_rep, uint32_t* counters) {
+                             uint32_t* __restrict__ entry_rep, uint32_t* __restrict__ entry_pos, uint32_t* counters) {
   const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= cap) return;
   int32_t e = -1;
@@ -56,6 +60,7 @@ __global__ void k_key_assign(uint32_t cap, const uint32_t* __restrict__ slot_rep
     if (k < max_entries) {
       e = (int32_t)k;
       entry_rep[k] = slot_rep[h] - 1u;
+      entry_pos[k] = atomicAdd(&counters[3], slot_cnt[h]);   // this key's range of the hit list
     }
   }
   slot_entry[h] = e;
@@ -77,13 +82,17 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t*
 }
 
 __global__ void k_key_partition(size_t n, const int32_t* __restrict__ item_slot, const int32_t* __restrict__ slot_entry,
-                                int32_t* __restrict__ item_entry, uint32_t* __restrict__ hit_list,
-                                uint32_t* __restrict__ miss_list, uint32_t* counters) {
+                                int32_t* __restrict__ item_entry, uint32_t* __restrict__ entry_pos,
+                                uint32_t* __restrict__ hit_list, uint32_t* __restrict__ miss_list,
+                                uint32_t* counters) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = i < n;
   const int32_t e = in ? slot_entry[item_slot[i]] : -1;
   if (in) item_entry[i] = e;
-  wave_append(in && e >= 0, (uint32_t)i, &counters[1], hit_list);
+  if (in && e >= 0) hit_list[atomicAdd(&entry_pos[e], 1u)] = (uint32_t)i;
+  const uint64_t hits = __ballot(in && e >= 0);
+  if (hits && __lane_id() == (uint32_t)(__ffsll((unsigned long long)hits) - 1))
+    atomicAdd(&counters[1], (uint32_t)__popcll(hits));
   wave_append(in && e < 0, (uint32_t)i, &counters[2], miss_list);
 }
 
@@ -129,15 +138,15 @@ void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, cons
 }
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
-                       uint32_t* entry_rep, uint32_t* counters) {
+                       uint32_t* entry_rep, uint32_t* entry_pos, uint32_t* counters) {
   hipLaunchKernelGGL(k_key_assign, grid, block, 0, stream, cap, slot_rep, slot_cnt, min_count, max_entries, slot_entry,
-                     entry_rep, counters);
+                     entry_rep, entry_pos, counters);
 }
 void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const int32_t* item_slot,
-                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* hit_list, uint32_t* miss_list,
-                          uint32_t* counters) {
-  hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, item_slot, slot_entry, item_entry, hit_list,
-                     miss_list, counters);
+                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* entry_pos, uint32_t* hit_list,
+                          uint32_t* miss_list, uint32_t* counters) {
+  hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, item_slot, slot_entry, item_entry, entry_pos,
+                     hit_list, miss_list, counters);
 }
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,

@@ -32,10 +32,10 @@ void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, cons
                        uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot);
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
-                       uint32_t* entry_rep, uint32_t* counters);
+                       uint32_t* entry_rep, uint32_t* entry_pos, uint32_t* counters);
 void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const int32_t* item_slot,
-                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* hit_list, uint32_t* miss_list,
-                          uint32_t* counters);
+                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* entry_pos, uint32_t* hit_list,
+                          uint32_t* miss_list, uint32_t* counters);
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
                            uint32_t* kinfo);

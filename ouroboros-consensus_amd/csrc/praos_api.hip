@@ -63,7 +63,7 @@ struct praos_batch {
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
     uint32_t cap = 0, max_entries = 0;
-    uint32_t *slot_rep = nullptr, *slot_cnt = nullptr, *entry_rep = nullptr, *kinfo = nullptr;
+    uint32_t *slot_rep = nullptr, *slot_cnt = nullptr, *entry_rep = nullptr, *entry_pos = nullptr, *kinfo = nullptr;
     int32_t *slot_entry = nullptr, *item_slot = nullptr, *item_entry = nullptr;
     uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
     ge_cached* ktab = nullptr;
@@ -286,6 +286,7 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
     ok &= dalloc(b, &k.miss, 4 * n) == hipSuccess;
     ok &= dalloc(b, &k.counters, 16) == hipSuccess;
     ok &= dalloc(b, &k.entry_rep, 4 * (size_t)k.max_entries) == hipSuccess;
+    ok &= dalloc(b, &k.entry_pos, 4 * (size_t)k.max_entries) == hipSuccess;
     ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
     ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
   }
@@ -423,8 +424,9 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
     launch_key_insert(g, blk, st, n, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
     launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)c->keycache,
-                      k.max_entries, k.slot_entry, k.entry_rep, k.counters);
-    launch_key_partition(g, blk, st, n, k.item_slot, k.slot_entry, k.item_entry, k.hit, k.miss, k.counters);
+                      k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
+    launch_key_partition(g, blk, st, n, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit, k.miss,
+                         k.counters);
     launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries,
                           k.entry_rep, keys, k.ktab, k.kinfo);
     return PRAOS_OK;

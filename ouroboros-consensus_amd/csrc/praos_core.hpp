@@ -204,59 +204,82 @@ __device__ __constant__ static const uint32_t FE_CURVE_A[8] = {486662u, 0, 0, 0,
 // libsodium ge25519_from_uniform (the VRF caller has cleared r's sign bit),
 // restated without its two field inversions: returns H = 8 * P projective
 // (the encoding is deferred to the caller's batched inversion).
-//   w = 1 + 2 r^2, Montgomery x = -A / w, e = x^3 + A x^2 + x.
-//   chi(e) = chi(-A w Q) with Q = A^2 - A^2 w + w^2 (e = -A Q / w^3).
-//   u = x (chi(e) != -1) or -x - A = A (1 - w) / w (chi(e) = -1), and
-//   y = (u - 1) / (u + 1) = N / D:  N = -(A + w), D = w - A  resp.
-//                                   N = A - A w - w, D = A - A w + w.
-//   libsodium inverts u + 1 = 0 to 0 (y = 0): D = 0 gives N/D = 0/1.
-// P = ge25519_frombytes(y, sign 0): x = sqrt((y^2 - 1) / (d y^2 + 1)) computed
-// as sqrt((N^2 - D^2) / (d N^2 + D^2)) with the same root/parity rules, so P =
-// (x D : N : D : x N) is exactly libsodium's point.
+//   w = 1 + 2 r^2, Montgomery x1 = -A / w, x2 = -x1 - A; libsodium picks u = x1 when
+//   chi(x1^3 + A x1^2 + x1) != -1, else x2, and y = (u - 1) / (u + 1) = N / D with
+//     case 1: N1 = -(A + w),      D1 = w - A
+//     case 2: N2 = A - A w - w,   D2 = A - A w + w.
+//   P = ge25519_frombytes(y, sign 0): x = sqrt((N^2 - D^2) / (d N^2 + D^2)), x even.
+// ONE exponentiation instead of two (chi, then the square root): with
+// a1 = (N1^2 - D1^2) / (d N1^2 + D1^2) = -486664 x1^2 / g(x1), case 1 holds exactly
+// when a1 is a square, and the case-2 ratio is a2 = a1 (w - 1) (g(x2) = 2 r^2 g(x1),
+// x2 / x1 = w - 1).  The sqrt_ratio candidate s of a1 (s^2 (dN1^2 + D1^2) = a1-numerator
+// times a 4th root of unity) then gives both roots: case 1 s or s sqrt(-1); case 2
+// t = s 2^((p+3)/8) r or t sqrt(-1) (the same 4th-root argument, RFC 9380's Elligator 2
+// sqrt trick).  libsodium's D = 0 corner (u + 1 = 0) is unreachable: w = A and
+// w = A / (A - 1) need r^2 = (A - 1) / 2 resp. (A / (A - 1) - 1) / 2, both
+// non-residues (tests/test_oracle.py::test_elligator_corner_unreachable).
+__device__ __constant__ static const uint32_t FE_2_P38[8] = {   // 2^((p+3)/8) = 1 + sqrt(-1)
+    0x4a0ea0b1u, 0xc4ee1b27u, 0xad2fe478u, 0x2f431806u, 0x3dfbd7a7u, 0x2b4d0099u, 0x4fc1df0bu, 0x2b832480u};
+
 FE_INLINE void vrf_from_uniform(ge_p3& H, const uint32_t r[8]) {
-  fe A, one, w, t, q, e, A2;
+  fe A, one, rf, w, t, Aw;
   fe_const(A, FE_CURVE_A);
   fe_set(one, 1);
-  fe_frombytes32(w, r);
-  fe_sq(w, w);
+  fe_frombytes32(rf, r);
+  fe_sq(w, rf);
   fe_add(w, w, w);
   fe_add(w, w, one);                // w = 1 + 2 r^2 (never 0: -1/2 is a non-square)
-  fe_sq(A2, A);
-  fe Aw;
   fe_mul(Aw, A, w);
-  fe_mul(t, A2, w);
-  fe_sub(q, A2, t);
-  fe_sq(t, w);
-  fe_add(q, q, t);                  // Q
-  fe_mul(q, q, Aw);
-  fe_neg(e, q);                     // -A w Q
-  fe_chi(e, e);
-  fe ec;
-  fe_canon(ec, e);
-  const bool e_is_minus_1 = (ec.v[0] >> 8) & 1;   // libsodium: s[1] & 1 of the encoding
-  fe N, D, N2, D2;
-  fe_add(N, A, w);
-  fe_neg(N, N);
-  fe_sub(D, w, A);
+  fe N1, D1, N2, D2;
+  fe_add(N1, A, w);
+  fe_neg(N1, N1);
+  fe_sub(D1, w, A);
   fe_sub(t, A, Aw);
   fe_sub(N2, t, w);
   fe_add(D2, t, w);
-  fe_cmov(N, N2, e_is_minus_1);
-  fe_cmov(D, D2, e_is_minus_1);
-  const bool dz = fe_iszero(D);
-  fe zero;
-  fe_set(zero, 0);
-  fe_cmov(N, zero, dz);
-  fe_cmov(D, one, dz);
-  // x^2 = (N^2 - D^2) / (d N^2 + D^2)
-  fe nn, dd, u, v, d, x;
-  fe_sq(nn, N);
-  fe_sq(dd, D);
-  fe_sub(u, nn, dd);
+  // case-1 ratio U / V and its sqrt_ratio candidate s = U V^3 (U V^7)^((p-5)/8)
+  fe nn, dd, U, V, d, v3, s;
+  fe_sq(nn, N1);
+  fe_sq(dd, D1);
+  fe_sub(U, nn, dd);
   fe_const(d, FE_D);
-  fe_mul(v, nn, d);
-  fe_add(v, v, dd);
-  fe_sqrt_ratio(x, u, v);           // cannot fail: the point exists
+  fe_mul(V, nn, d);
+  fe_add(V, V, dd);
+  fe_sq(v3, V);
+  fe_mul(v3, v3, V);                // V^3
+  fe_sq(s, v3);
+  fe_mul(s, s, V);
+  fe_mul(s, s, U);                  // U V^7
+  fe_pow22523(s, s);
+  fe_mul(s, s, v3);
+  fe_mul(s, s, U);
+  fe sq1, chk, vss;
+  fe_const(sq1, FE_SQRTM1);
+  fe_sq(vss, s);
+  fe_mul(vss, vss, V);
+  fe_sub(chk, vss, U);
+  const bool m1 = fe_iszero(chk);
+  fe_add(chk, vss, U);
+  const bool case1 = m1 || fe_iszero(chk);
+  fe x1, x2, c;
+  fe_mul(x1, s, sq1);
+  fe_cmov(x1, s, m1);               // case 1: s or s sqrt(-1)
+  fe_const(c, FE_2_P38);
+  fe_mul(t, s, rf);
+  fe_mul(t, t, c);                  // case 2 candidate
+  fe U2, wm1;
+  fe_sub(wm1, w, one);
+  fe_mul(U2, U, wm1);
+  fe_sq(vss, t);
+  fe_mul(vss, vss, V);
+  fe_sub(chk, vss, U2);
+  const bool m2 = fe_iszero(chk);
+  fe_mul(x2, t, sq1);
+  fe_cmov(x2, t, m2);
+  fe x = x2, N = N2, D = D2;
+  fe_cmov(x, x1, case1);
+  fe_cmov(N, N1, case1);
+  fe_cmov(D, D1, case1);
   fe negx;
   fe_neg(negx, x);
   fe_cmov(x, negx, fe_isnegative(x));   // sign bit 0

@@ -196,3 +196,57 @@ def test_leader_boundary_fixture():
             assert check(l.to_bytes(bits // 8, "big"), s_fp, c_raw) == (v["is_leader"], v["iterations"])
             assert leader_python(l, bits, s_fp, c_raw) == (v["is_leader"], v["iterations"])
         assert int(c["boundary"], 16) == int(c["vectors"][2]["leader_value"], 16)
+
+
+def test_elligator_single_exponentiation():
+    """k_vrf's vrf_from_uniform (praos_core.hpp) takes libsodium's two exponentiations
+    (chi of g(x1), then the square root of the chosen ratio) as ONE: case 1 <=> the
+    case-1 ratio a1 is a square, and the case-2 root comes from the same candidate times
+    2^((p+3)/8) r.  Checked here against the two-exponentiation restatement on random and
+    edge inputs; libsodium's u + 1 = 0 corner (D = 0) is unreachable: both r^2 it needs
+    are non-residues."""
+    import random
+    p, A = 2 ** 255 - 19, 486662
+    d = (-121665 * pow(121666, p - 2, p)) % p
+    I = pow(2, (p - 1) // 4, p)
+    k = (p - 5) // 8
+
+    def root(u, v):                                  # libsodium-style sqrt_ratio candidate
+        v3 = v * v * v % p
+        return u * v3 * pow(u * v3 * v3 * v % p, k, p) % p
+
+    def fix(x, u, v):
+        return x if (v * x * x - u) % p == 0 else x * I % p
+
+    def even(x):
+        return (p - x) % p if x & 1 else x
+
+    def two_exp(r):
+        w = (1 + 2 * r * r) % p
+        e = (-A * w * (A * A - A * A * w + w * w)) % p
+        if pow(e, (p - 1) // 2, p) != p - 1:
+            N, D = (-(A + w)) % p, (w - A) % p
+        else:
+            N, D = (A - A * w - w) % p, (A - A * w + w) % p
+        if D == 0:
+            N, D = 0, 1
+        U, V = (N * N - D * D) % p, (d * N * N + D * D) % p
+        return N, D, even(fix(root(U, V), U, V))
+
+    def one_exp(r):
+        w = (1 + 2 * r * r) % p
+        N1, D1 = (-(A + w)) % p, (w - A) % p
+        U, V = (N1 * N1 - D1 * D1) % p, (d * N1 * N1 + D1 * D1) % p
+        s = root(U, V)
+        if (V * s * s - U) % p == 0 or (V * s * s + U) % p == 0:
+            return N1, D1, even(fix(s, U, V))
+        U2 = U * (w - 1) % p
+        t = s * pow(2, k + 1, p) % p * r % p
+        return (A - A * w - w) % p, (A - A * w + w) % p, even(fix(t, U2, V))
+
+    rng = random.Random(0xE11)
+    for r in [0, 1, 2, p - 1, (p - 1) // 2] + [rng.getrandbits(255) % p for _ in range(400)]:
+        assert one_exp(r) == two_exp(r), r
+    assert pow(2, k + 1, p) == (I + 1) % p                      # the constant FE_2_P38
+    for r2 in ((A - 1) * pow(2, p - 2, p) % p, (A * pow(A - 1, p - 2, p) - 1) * pow(2, p - 2, p) % p):
+        assert pow(r2, (p - 1) // 2, p) == p - 1                 # D1 = 0 / D2 = 0 unreachable

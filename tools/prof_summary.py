@@ -16,7 +16,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_ocert", "k_ocert_ck", "k_kes", "k_vrf", "k_vrf_ck", "k_vrf_tp", "k_leader", "k_key_precompute", "k_synth_headers")
+KERNELS = ("k_ocert", "k_ocert_ck", "k_kes", "k_kes_ck", "k_kes_leafkeys", "k_vrf", "k_vrf_ck", "k_vrf_tp", "k_leader",
+           "k_key_precompute", "k_synth_headers")
 
 
 def short(name):

@@ -52,8 +52,9 @@ def ed25519_verify(sha_blocks):
 def vrf_verify():
     w = 2 * DECODE                                   # Y, Gamma
     w += SHA                                         # hash_to_curve digest
-    w += X + 10 * M + 6 * S + 12 * A + CANON         # Elligator2 chi + numerators
-    w += DECODE - X + X                              # sqrt ratio of the point on N/D
+    w += 10 * M + 6 * S + 12 * A                     # Elligator2 numerators N1/D1, N2/D2, ratio
+    w += DECODE                                      # ONE sqrt-ratio exponentiation (chi merged)
+    w += 6 * M + 2 * S + 2 * A                       # case-2 candidate 2^((p+3)/8) r s and its check
     w += 3 * (DBL + TO_P3)                           # cofactor 8
     w += TABLE8 + straus(33, 33, 0, 32) + TO_P2      # U = [s]B - [c]Y (B, 2^128 B)
     w += 2 * TABLE8 + straus(64, 64, 33, 0) + TO_P2  # V = [s]H - [c]Gamma
@@ -83,7 +84,9 @@ W_LEADER = 3000
 # key-cache path (k_keys.hip): per header on a cached key, and per cached key
 W_OCERT_CK = W_OCERT - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_chunked(4, False)
 W_VRF_CK = W_VRF - DECODE - TABLE8 - straus(33, 33, 0, 32) + straus_chunked(2, True)
+W_KES_CK = W_KES - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_chunked(4, False)
 W_KEY_COLD = key_precompute(4)
+W_KEY_KES = key_precompute(4)                        # leaf keys: same tables as cold keys
 W_KEY_VRF = key_precompute(3) + CANON
 
 if __name__ == "__main__":
