@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 6
+#define PRAOS_ABI_VERSION 7
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -133,6 +133,12 @@ typedef struct {
   const uint8_t* body_bytes;
   size_t body_bytes_len;
 } praos_headers;
+
+/* A Nonce (Praos.hs): 32-byte hash, or NeutralNonce. */
+typedef struct {
+  uint8_t hash[32];
+  int32_t neutral;                /* 1 = NeutralNonce */
+} praos_nonce;
 
 /* Outputs (any pointer may be NULL except bits). */
 typedef struct {
@@ -256,6 +262,16 @@ int praos_verify_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, prao
  * copies the decoded fields of the last run. */
 praos_batch* praos_batch_upload_bytes(praos_ctx* ctx, const praos_header_bytes* in);
 int praos_batch_download_decoded(praos_ctx* ctx, praos_batch* b, praos_decoded* dec);
+/* Decode a from-bytes batch now (async on the ctx stream; praos_batch_run then skips
+ * the decode): lets the caller read the decoded fields -- e.g. slots and the certified
+ * VRF outputs that drive the epoch nonces -- before the crypto runs. */
+int praos_batch_decode(praos_ctx* ctx, praos_batch* b);
+/* Several epochs in one batch (same ledger view, consecutive epoch nonces): header i
+ * is verified under etas[eta_idx[i]] (k <= 256 entries) instead of the praos_set_epoch
+ * nonce, from the next praos_batch_run on.  mkInputVRF (Praos/VRF.hs:55-69) is the only
+ * nonce-dependent input.  Fold such outputs with praos_validate_headers_nonces. */
+int praos_batch_set_nonces(praos_ctx* ctx, praos_batch* b, const praos_nonce* etas, uint32_t k,
+                           const uint8_t* eta_idx);
 
 /* ---- ImmutableDB block-integrity batch ----
  * Replaces verifyBlockIntegrity spkp blk (Shelley/Ledger/Integrity.hs:14-20), the
@@ -344,10 +360,6 @@ int praos_apply_batch(praos_ctx* ctx, const praos_headers* h, const praos_out* c
  * reupdated: last_slot := slot, lab := prevHashToNonce prev_hash, evolving :=
  * evolving ⭒ vrfNonceValue, candidate := evolving' if slot + stability_window <
  * firstSlotNextEpoch, counters[hk] := n (new keys appended; PRAOS_E_ARG past cap). */
-typedef struct {
-  uint8_t hash[32];
-  int32_t neutral;                /* 1 = NeutralNonce */
-} praos_nonce;
 
 typedef struct {
   int32_t last_slot_origin;       /* praosStateLastSlot = Origin */
@@ -420,19 +432,31 @@ int praos_validate_headers(praos_ctx* ctx, const praos_headers* h, const uint8_t
                            const praos_epoch_info* ei, praos_chain_state* st, uint8_t* verdict, size_t* chain_stop,
                            size_t* processed);
 
+/* praos_validate_headers (env != NULL) / praos_update_chain_dep_state (env == NULL) over
+ * outputs verified under per-header nonces (praos_batch_set_nonces): the fold goes on
+ * while the nonce the state ticks to at header i equals etas[eta_idx[i]]. */
+int praos_validate_headers_nonces(praos_ctx* ctx, const praos_headers* h, const uint8_t* prev_hash,
+                                  const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
+                                  const praos_epoch_info* ei, praos_chain_state* st, const praos_nonce* etas,
+                                  uint32_t k, const uint8_t* eta_idx, uint8_t* verdict, size_t* chain_stop,
+                                  size_t* processed);
+
 /* ---- chain replay from an ImmutableDB directory (db-analyser) ----
  * Replaces the per-block loop of DBAnalyser/Analysis.hs:815-847 (processAllImmutableDB
  * driving benchmarkLedgerOps / validateHeader, :479-607) for the header-validation
  * pass.  Reads dir/NNNNN.chunk + dir/NNNNN.secondary (56-byte Entry per block,
- * Storage/ImmutableDB/Impl/Index/Secondary.hs:93-128) from chunk 0 up, batches of at
- * most batch_max headers that never cross an epoch, installs each epoch's nonce (ticked
- * from *st) with praos_set_epoch(pools, params), verifies on the device and folds with
- * praos_validate_headers.  Ends at the first invalid header (stop_index, stop_verdict)
- * or at the end of the database (stop_index = headers).  *st and env's tip are the
- * state and tip after the last valid header; verdicts[i] (i < verdicts_cap, may be
- * NULL with cap 0) for every header up to and including the stop.  Resume: when env's
- * tip is not Origin (a checkpointed state, praos_state_decode), the blocks up to and
- * including the tip (matched by slot and header hash in the secondary index) are
+ * Storage/ImmutableDB/Impl/Index/Secondary.hs:93-128) from chunk 0 up in batches of at
+ * most batch_max headers (spanning up to 256 epochs).  Each batch is decoded on the
+ * device, given per-header epoch nonces (tickChainDepState, Praos.hs:407-431, run ahead
+ * over the certified VRF outputs), verified under them (praos_batch_set_nonces) and
+ * folded with praos_validate_headers_nonces, which re-derives every nonce it relies on;
+ * the fold of batch k overlaps the device work of batch k+1.  One ledger view (pools,
+ * params) for the whole replay.  Ends at the first invalid header (stop_index,
+ * stop_verdict) or at the end of the database (stop_index = headers).  *st and env's
+ * tip are the state and tip after the last valid header; verdicts[i] (i < verdicts_cap,
+ * may be NULL with cap 0) for every header up to and including the stop.  Resume: when
+ * env's tip is not Origin (a checkpointed state, praos_state_decode), the blocks up to
+ * and including the tip (matched by slot and header hash in the secondary index) are
  * skipped; indices count from the first block after it. */
 typedef struct {
   uint64_t skipped;               /* blocks up to the resume tip, not replayed */
@@ -440,12 +464,13 @@ typedef struct {
   uint64_t validated;             /* valid headers folded into *st */
   uint64_t stop_index;            /* first invalid header, or headers when none */
   uint32_t stop_verdict;          /* its PRAOS_V_* (0 when none) */
-  uint32_t epochs;                /* praos_set_epoch calls (epoch nonces installed) */
+  uint32_t epochs;                /* distinct epoch nonces the headers were verified under */
   uint32_t batches;               /* device passes */
   uint32_t chunks;                /* chunk files read */
   double ms_io;                   /* reading chunks + secondary indexes, building batches */
   double ms_device;               /* upload + decode + crypto + download */
   double ms_fold;                 /* envelope + updateChainDepState on the host */
+  double ms_nonce;                /* epoch nonces ahead of the crypto (host) */
 } praos_replay_stats;
 
 int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,

@@ -58,7 +58,7 @@ data PraosCtx
 -- struct praos_chain_state (232 bytes): last_slot_origin@0 last_slot@8 counter_hash28@16 counter@24 m@32 cap@40 evolving@48 candidate@84 epoch_nonce@120 lab@156 last_epoch_block@192
 -- struct praos_epoch_info (32 bytes): epoch_base_slot@0 epoch_base_no@8 epoch_length@16 stability_window@24
 -- struct praos_envelope (120 bytes): block_no@0 header_hash@8 header_size@16 body_size@24 tip_is_origin@32 tip_slot@40 tip_block_no@48 tip_hash@56 max_major_pv@88 lv_prot_major@96 max_header_size@104 max_body_size@112
--- struct praos_replay_stats (72 bytes): skipped@0 headers@8 validated@16 stop_index@24 stop_verdict@32 epochs@36 batches@40 chunks@44 ms_io@48 ms_device@56 ms_fold@64
+-- struct praos_replay_stats (80 bytes): skipped@0 headers@8 validated@16 stop_index@24 stop_verdict@32 epochs@36 batches@40 chunks@44 ms_io@48 ms_device@56 ms_fold@64 ms_nonce@72
 -- struct praos_decoded (168 bytes): status@0 block_no@8 slot@16 prev_hash@24 prev_is_genesis@32 cold_vk@40 body_size@72 ocert_n@96 header_hash@160
 
 foreign import ccall safe "praos_open"        c_open        :: CInt -> IO (Ptr PraosCtx)
@@ -83,7 +83,7 @@ foreign import ccall safe "praos_replay_immutable" c_replay_immutable
   -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 6
+abiVersion = 7
 
 -- ---------------------------------------------------------------- context
 
@@ -288,7 +288,7 @@ praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
 data ReplayStats = ReplayStats
   { rsSkipped, rsHeaders, rsValidated, rsStopIndex :: !Word64
   , rsStopVerdict, rsEpochs, rsBatches, rsChunks :: !Word32
-  , rsMsIO, rsMsDevice, rsMsFold :: !Double
+  , rsMsIO, rsMsDevice, rsMsFold, rsMsNonce :: !Double
   } deriving Show
 
 -- | praos_replay_immutable: the header-validation pass of db-analyser over an ImmutableDB
@@ -302,7 +302,7 @@ praosReplayImmutable :: PraosBatchCtx -> FilePath -> [(BS.ByteString, BS.ByteStr
 praosReplayImmutable ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor batchMax =
   withCString dir $ \cdir -> withPools pools $ \pp' np -> withParams pp $ \par ->
   withEpochInfo ei $ \eip -> withChainState stateCbor 65536 $ \st ->
-  allocaBytes 120 $ \env -> allocaBytes 72 $ \rs -> do
+  allocaBytes 120 $ \env -> allocaBytes 80 $ \rs -> do
     fillBytes env 0 120
     case tip of
       Nothing -> pokeByteOff env 32 (1 :: Int32)
@@ -313,7 +313,7 @@ praosReplayImmutable ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxH
                                   (castPtr rs))
     stats <- ReplayStats <$> peekByteOff rs 0 <*> peekByteOff rs 8 <*> peekByteOff rs 16 <*> peekByteOff rs 24
                          <*> peekByteOff rs 32 <*> peekByteOff rs 36 <*> peekByteOff rs 40 <*> peekByteOff rs 44
-                         <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64
+                         <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64 <*> peekByteOff rs 72
     st' <- encodeChainState st
     origin :: Int32 <- peekByteOff env 32
     tip' <- if origin /= 0 then pure Nothing else do

@@ -13,8 +13,10 @@ struct VrfIn {
   const uint8_t* __restrict__ vrf_out;
   const uint8_t* __restrict__ vrf_proof;
   const uint64_t* __restrict__ slot;
-  const uint32_t* __restrict__ eta0;
+  const uint32_t* __restrict__ eta0;     // eta_idx == null: the epoch nonce (8 words)
   int eta0_neutral;
+  const uint8_t* __restrict__ eta_idx;   // several epochs per batch: header i uses entry eta_idx[i]
+                                         // of eta0 = table of 9-word entries (nonce, neutral flag)
   const uint32_t* __restrict__ pool_hash;
   const uint32_t* __restrict__ pool_vrf;
   const int32_t* __restrict__ pool_map;
@@ -61,9 +63,11 @@ __device__ __forceinline__ void vrf_item(const VrfIn& a, size_t i, const ge_niel
     load_words(alpha, a.alpha_in + 32 * i, 8);
   } else {
     uint32_t e0[8];
+    const uint32_t* ep = a.eta_idx ? a.eta0 + 9 * (uint32_t)a.eta_idx[i] : a.eta0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) e0[k] = a.eta0[k];
-    mk_input_vrf(alpha, a.slot[i], e0, a.eta0_neutral != 0);     // Praos/VRF.hs:55-69
+    for (int k = 0; k < 8; k++) e0[k] = ep[k];
+    const bool neutral = a.eta_idx ? ep[8] != 0 : a.eta0_neutral != 0;
+    mk_input_vrf(alpha, a.slot[i], e0, neutral);                  // Praos/VRF.hs:55-69
     uint32_t cv[8], hk[8];
     load_words(cv, a.cold_vk + 32 * i, 8);
     blake2b_32(hk, cv, 28);
@@ -215,21 +219,23 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
 void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                 const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
                 const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
-                const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
-                int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs) {
-  VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools,
+                const uint8_t* eta_idx, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map,
+                uint32_t npools, int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx,
+                int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out,
+                ge_cached* tabs) {
+  VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, eta_idx, pool_hash, pool_vrf, pool_map, npools,
           check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out, tabs};
   hipLaunchKernelGGL(k_vrf, grid, block, 0, stream, n, list, count, gbtab, a);
 }
 void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                    const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
-                   const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash,
-                   const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
-                   const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs) {
-  VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools,
+                   const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx,
+                   const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
+                   int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx,
+                   int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out,
+                   uint8_t* ok_out, ge_cached* tabs) {
+  VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, eta_idx, pool_hash, pool_vrf, pool_map, npools,
           check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out, tabs};
   hipLaunchKernelGGL(k_vrf_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }

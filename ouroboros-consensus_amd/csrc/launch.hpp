@@ -18,16 +18,18 @@ void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* 
 void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                 const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
                 const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
-                const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
-                int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs);
+                const uint8_t* eta_idx, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map,
+                uint32_t npools, int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx,
+                int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out,
+                ge_cached* tabs);
 void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                    const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
-                   const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash,
-                   const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
-                   const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx,
-                   uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out, uint8_t* ok_out, ge_cached* tabs);
+                   const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx,
+                   const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
+                   int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx,
+                   int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out,
+                   uint8_t* ok_out, ge_cached* tabs);
 void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* keys, uint32_t mask,
                        uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot);
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,

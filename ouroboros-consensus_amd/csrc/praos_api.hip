@@ -83,6 +83,11 @@ struct praos_batch {
   // block-integrity batches (k_block.hip): stored block spans, segment spans
   // (segment-major [k][i]), per-segment hashes, results
   bool is_block = false;
+  // several epoch nonces in one batch (praos_batch_set_nonces): device table of 9-word
+  // entries (nonce, neutral flag) and per-header index; host copies for the fold
+  uint32_t* eta_tab = nullptr;
+  uint8_t* eta_idx = nullptr;
+  bool decoded = false;          // praos_batch_decode ran: praos_batch_run skips the decode
   uint64_t *blk_off = nullptr, *seg_off = nullptr;
   uint32_t *blk_len = nullptr, *seg_len = nullptr;
   uint8_t *nseg = nullptr, *split_status = nullptr, *seg_hash = nullptr, *blk_result = nullptr, *blk_hash = nullptr;
@@ -409,8 +414,10 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (b->from_bytes) {
     // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
-    const int rd = batch_decode(c, b);
-    if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
+    if (!b->decoded) {
+      const int rd = batch_decode(c, b);
+      if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
+    }
   }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
@@ -479,16 +486,16 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       int r = keycache_prepass(k, b->vrf_vk, 1, sv);
       if (r != PRAOS_OK) return r;
       launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk, b->vrf_vk,
-                    b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                    b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
                     c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
                     b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
       launch_vrf(g, blk, sv, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
-                 b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
+                 b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
                  (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
                  b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
     } else {
       launch_vrf(g, blk, sv, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk, b->vrf_vk,
-                 b->vrf_out, b->vrf_proof, b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                 b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
                  c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
                  b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
     }
@@ -675,6 +682,37 @@ int praos_verify_headers(praos_ctx* c, const praos_headers* h, praos_out* out) {
   return r;
 }
 
+int praos_batch_decode(praos_ctx* c, praos_batch* b) {
+  if (!c || !b || !b->from_bytes) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int r = batch_decode(c, b);
+  if (r != PRAOS_OK) { c->err = "decode launch failed"; return r; }
+  b->decoded = true;
+  return PRAOS_OK;
+}
+
+int praos_batch_set_nonces(praos_ctx* c, praos_batch* b, const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx) {
+  if (!c || !b || (b->n && (!etas || !eta_idx)) || k == 0 || k > 256) return PRAOS_E_ARG;
+  for (size_t i = 0; i < b->n; i++)
+    if (eta_idx[i] >= k) { c->err = "eta_idx out of range"; return PRAOS_E_ARG; }
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint32_t> tab(9 * (size_t)k, 0);
+  for (uint32_t e = 0; e < k; e++) {
+    if (!etas[e].neutral) std::memcpy(&tab[9 * e], etas[e].hash, 32);
+    tab[9 * e + 8] = etas[e].neutral ? 1u : 0u;
+  }
+  if (!b->eta_tab) {
+    if (dalloc(b, &b->eta_tab, 9 * 4 * 256) != hipSuccess || dalloc(b, &b->eta_idx, std::max<size_t>(b->n, 1)) != hipSuccess) {
+      c->err = "device allocation failed";
+      return PRAOS_E_OOM;
+    }
+  }
+  HIPCHK(c, hipMemcpyAsync(b->eta_tab, tab.data(), 4 * tab.size(), hipMemcpyHostToDevice, c->stream));
+  if (b->n) HIPCHK(c, hipMemcpyAsync(b->eta_idx, eta_idx, b->n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PRAOS_OK;
+}
+
 int praos_batch_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d) {
   if (!c || !b || !d || !b->from_bytes) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
@@ -841,6 +879,7 @@ int praos_verify_vrf(praos_ctx* c, size_t n, const uint8_t* vk, const uint8_t* p
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   launch_vrf(dim3(nblocks(n, NT)), dim3(NT), c->stream, n, nullptr, nullptr, c->btab, (const uint8_t*)nullptr, dvk,
                      (const uint8_t*)nullptr, dpr, (const uint64_t*)nullptr, (const uint32_t*)nullptr, 1,
+                     (const uint8_t*)nullptr,
                      (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const int32_t*)nullptr, 0u, 0, dal,
                      (uint16_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, dbeta, (uint8_t*)nullptr,
                      (uint8_t*)nullptr, dok, dtab);
@@ -1002,13 +1041,15 @@ static uint32_t counter_slot(const praos_ctx* c, CounterTab& T, const uint8_t* h
 
 static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
                      const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei,
-                     praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed) {
+                     praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed,
+                     const praos_nonce* etas = nullptr, uint32_t netas = 0, const uint8_t* eta_idx = nullptr) {
   if (!c || !h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash ||
       ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter)))
     return PRAOS_E_ARG;
   if (env && h->n && (!env->block_no || !env->header_hash || !env->header_size || !env->body_size))
     return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
+  if (eta_idx && (!etas || netas == 0)) return PRAOS_E_ARG;
   praos_nonce eta0{};
   eta0.neutral = c->eta0_neutral;
   if (!c->eta0_neutral) std::memcpy(eta0.hash, c->eta0, 32);
@@ -1063,7 +1104,10 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
       tick_epoch = nonce_combine(W.candidate, W.leb);
       tick_leb = W.lab;
     }
-    if (!nonce_eq(tick_epoch, eta0)) break;        // crypto outputs were computed for another epoch nonce
+    // the crypto outputs of header i were computed for this nonce: a tick to another one
+    // ends the fold (the caller re-verifies from here under the right nonce)
+    if (eta_idx && eta_idx[i] >= netas) { c->err = "eta_idx out of range"; return PRAOS_E_ARG; }
+    if (!nonce_eq(tick_epoch, eta_idx ? etas[eta_idx[i]] : eta0)) break;
     // the issuer's counter slot (hashKey of the cold key, Praos.hs:595-606)
     const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
     uint32_t k;
@@ -1171,6 +1215,16 @@ int praos_validate_headers(praos_ctx* c, const praos_headers* h, const uint8_t* 
                            size_t* processed) {
   if (!env) return PRAOS_E_ARG;
   return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, env, ei, st, verdict, chain_stop, processed);
+}
+
+int praos_validate_headers_nonces(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash,
+                                  const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,
+                                  const praos_epoch_info* ei, praos_chain_state* st, const praos_nonce* etas,
+                                  uint32_t k, const uint8_t* eta_idx, uint8_t* verdict, size_t* chain_stop,
+                                  size_t* processed) {
+  if (!eta_idx || !etas || k == 0) return PRAOS_E_ARG;
+  return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, env, ei, st, verdict, chain_stop, processed, etas, k,
+                   eta_idx);
 }
 
 

@@ -4,13 +4,16 @@
 // Mirrors the reference's streaming loop (DBAnalyser/Analysis.hs:815-847,
 // processAllImmutableDB: ImmutableDB.streamAll, one iteratorNext per block) and its
 // header-validation pass (benchmarkLedgerOps, :479-607: tick, then validateHeader),
-// in batches: headers are read through the secondary index, cut into batches that
-// never cross an epoch boundary, decoded and crypto-checked on the device in one pass
-// (praos_batch_upload_bytes / praos_batch_run), then folded on the host with
-// praos_validate_headers (envelope, then updateChainDepState).  Before each epoch the
-// epoch nonce the state ticks to (tickChainDepState, Praos.hs:407-431) is installed
-// with praos_set_epoch (same pools and parameters: one ledger view for the replay).
-// Like the reference, the replay ends at the first invalid header.
+// in batches: headers are read through the secondary index into batches of up to
+// batch_max headers (any number of epochs, up to 256), decoded on the device
+// (praos_batch_decode), given their epoch nonces -- the nonce tickChainDepState
+// (Praos.hs:407-431) reaches at each header, computed on the host from the certified
+// VRF outputs as if every header were valid -- crypto-checked under those nonces
+// (praos_batch_set_nonces + praos_batch_run) and folded on the host with
+// praos_validate_headers_nonces (envelope, then updateChainDepState), which accepts a
+// header only if the nonce its crypto ran with is the one the real fold ticks to.  One
+// ledger view (pools, parameters) for the whole replay.  Like the reference, the
+// replay ends at the first invalid header.
 //
 // On-disk format (ImmutableDB, Storage/ImmutableDB/Impl): NNNNN.chunk holds the
 // stored blocks back to back; NNNNN.secondary one 56-byte Entry per block
@@ -26,6 +29,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 void praos_set_error_(praos_ctx* c, const std::string& m);   // praos_api.hip
@@ -128,119 +132,225 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
       return PRAOS_E_ARG;
     }
   }
-  praos_nonce cur{};
-  bool have_eta = false;
-  std::vector<uint8_t> arena;
-  std::vector<uint64_t> off, slot, block_no, ocn;
-  std::vector<uint32_t> len, bsize;
-  std::vector<uint8_t> prev, gen, cold, hh, nonce, v;
-  std::vector<uint16_t> dstat, bits;
-  std::vector<int32_t> pidx;
-  uint64_t index0 = 0;          // global index of the batch's first header
-  bool stopped = false;
-  while (!stopped) {
-    // ---- one batch: at most batch_max headers, all in the first header's epoch
+  // The ledger view (pools, parameters) is installed once; the epoch nonces travel
+  // with each batch (praos_batch_set_nonces), so a batch may span many epochs and stay
+  // large enough to fill the device even when epochs are short.
+  {
+    praos_nonce eta0{};
+    uint32_t l;
+    uint64_t s0 = 0;
+    const uint8_t* p;
+    if (rd.peek(&p, &l, &s0) && praos_ticked_epoch_nonce(st, ei, s0, &eta0) != PRAOS_OK) {
+      praos_set_error_(ctx, "replay: first slot before the epoch base");
+      return PRAOS_E_ARG;
+    }
+    if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); return PRAOS_E_ARG; }
+    const int r = praos_set_epoch(ctx, eta0.neutral ? nullptr : eta0.hash, pools, npools, params);
+    if (r != PRAOS_OK) return r;
+  }
+  // Two batches in flight: while the host folds batch k, the device verifies batch k+1
+  // (its nonces come from the speculative nonce chain, which runs ahead of the fold).
+  struct Stage {
+    praos_batch* b = nullptr;
+    size_t n = 0;
+    uint64_t index0 = 0;
+    std::vector<uint8_t> arena;
+    std::vector<uint64_t> off, slot, block_no, ocn;
+    std::vector<uint32_t> len, bsize;
+    std::vector<uint8_t> prev, gen, cold, hh, nonce, v, vout, eidx;
+    std::vector<uint16_t> dstat, bits;
+    std::vector<int32_t> pidx;
+    std::vector<praos_nonce> etas;
+  };
+  Stage stage[2];
+  // the speculative nonce state (tick + reupdate as if every header were valid)
+  struct Spec {
+    int32_t origin;
+    uint64_t last;
+    praos_nonce evolving, candidate, epoch_nonce, lab, leb;
+    bool dead;
+  } sp{st->last_slot_origin, st->last_slot, st->evolving, st->candidate, st->epoch_nonce, st->lab,
+       st->last_epoch_block, false};
+  praos_nonce last_eta{};
+  bool have_last = false;
+  uint64_t next_index = 0;
+  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // read, upload and decode the next batch, derive its nonces; false at the end
+  auto prepare = [&](Stage& S, int& rc) -> bool {
+    rc = PRAOS_OK;
     auto t_io = std::chrono::steady_clock::now();
-    arena.clear();
-    off.clear();
-    len.clear();
-    uint64_t first_slot = 0;
+    S.arena.clear();
+    S.off.clear();
+    S.len.clear();
     const uint8_t* p;
     uint32_t l;
-    uint64_t s;
-    while (off.size() < batch_max && rd.peek(&p, &l, &s)) {
-      if (off.empty()) first_slot = s;
-      else if (epoch_of(s) != epoch_of(first_slot)) break;
-      off.push_back(arena.size());
-      len.push_back(l);
-      arena.insert(arena.end(), p, p + l);
+    uint64_t s, e_prev = 0;
+    uint32_t nep = 0;
+    while (S.off.size() < batch_max && rd.peek(&p, &l, &s)) {
+      const uint64_t e = epoch_of(s);
+      if (S.off.empty() || e != e_prev) {
+        if (nep == 256) break;
+        nep++;
+        e_prev = e;
+      }
+      if (S.arena.capacity() < S.arena.size() + l) S.arena.reserve(2 * S.arena.size() + (size_t(1) << 20));
+      S.off.push_back(S.arena.size());
+      S.len.push_back(l);
+      S.arena.insert(S.arena.end(), p, p + l);
       rd.pop();
     }
     stats->ms_io += ms_since(t_io);
-    if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); return PRAOS_E_ARG; }
-    if (off.empty()) break;
-    size_t first = 0;           // first header of the batch not yet folded
-    uint64_t eta_slot = first_slot;
-    int idle = 0;               // folds in a row that made no progress
-    while (first < off.size()) {
-      const size_t n = off.size() - first;
-      praos_nonce eta{};
-      if (praos_ticked_epoch_nonce(st, ei, eta_slot, &eta) != PRAOS_OK) {
-        praos_set_error_(ctx, "replay: slot " + std::to_string(eta_slot) + " before the epoch base");
-        return PRAOS_E_ARG;
-      }
-      if (!have_eta || !praos_host::nonce_eq(eta, cur)) {
-        const int r = praos_set_epoch(ctx, eta.neutral ? nullptr : eta.hash, pools, npools, params);
-        if (r != PRAOS_OK) return r;
-        cur = eta;
-        have_eta = true;
-        stats->epochs++;
-      }
-      auto t_dev = std::chrono::steady_clock::now();
-      praos_header_bytes hb{n, arena.data(), arena.size(), off.data() + first, len.data() + first};
-      praos_batch* b = praos_batch_upload_bytes(ctx, &hb);
-      if (!b) return PRAOS_E_OOM;
-      dstat.resize(n); block_no.resize(n); slot.resize(n); ocn.resize(n); bsize.resize(n);
-      prev.resize(32 * n); gen.resize(n); cold.resize(32 * n); hh.resize(32 * n);
-      bits.resize(n); pidx.resize(n); nonce.resize(32 * n); v.resize(n);
-      praos_decoded dec{};
-      dec.status = dstat.data(); dec.block_no = block_no.data(); dec.slot = slot.data();
-      dec.prev_hash = prev.data(); dec.prev_is_genesis = gen.data(); dec.cold_vk = cold.data();
-      dec.body_size = bsize.data(); dec.ocert_n = ocn.data(); dec.header_hash = hh.data();
-      praos_out out{bits.data(), pidx.data(), nullptr, nullptr, nonce.data()};
-      int r = praos_batch_run(ctx, b);
-      if (r == PRAOS_OK) r = praos_batch_download(ctx, b, &out);
-      if (r == PRAOS_OK) r = praos_batch_download_decoded(ctx, b, &dec);
-      praos_batch_free(ctx, b);
-      if (r != PRAOS_OK) return r;
-      stats->ms_device += ms_since(t_dev);
-      stats->batches++;
-      // ---- validateHeader over the batch: envelope, then updateChainDepState
-      auto t_fold = std::chrono::steady_clock::now();
-      praos_headers h{};
-      h.n = n;
-      h.slot = slot.data();
-      h.cold_vk = cold.data();
-      h.ocert_n = ocn.data();
-      env->block_no = block_no.data();
-      env->header_hash = hh.data();
-      env->header_size = len.data() + first;
-      env->body_size = bsize.data();
-      size_t stop = 0, done = 0;
-      r = praos_validate_headers(ctx, &h, prev.data(), gen.data(), &out, env, ei, st, v.data(), &stop, &done);
-      env->block_no = nullptr;
-      env->header_hash = nullptr;
-      env->header_size = nullptr;
-      env->body_size = nullptr;
-      stats->ms_fold += ms_since(t_fold);
-      if (r != PRAOS_OK) return r;
-      const uint64_t g0 = index0 + first;
-      for (size_t k = 0; k < done && g0 + k < verdicts_cap; k++) verdicts[g0 + k] = v[k];
-      if (stop < done) {        // the chain stops at the first invalid header
-        stats->validated += stop;
-        stats->stop_index = g0 + stop;
-        stats->stop_verdict = v[stop];
-        stats->headers = g0 + stop + 1;
-        stopped = true;
-        break;
-      }
-      stats->validated += done;
-      first += done;
-      if (first < off.size()) {
-        // the fold met a header whose ticked nonce is not the installed one: only a
-        // secondary-index slot that disagrees with the header's own slot does that
-        // (batches never cross an epoch); re-tick from the decoded slot
-        eta_slot = slot[done];
-        if (done == 0 && ++idle > 1) {
-          praos_set_error_(ctx, "replay: the epoch nonce of header " + std::to_string(g0) + " cannot be reached");
-          return PRAOS_E_STATE;
-        }
-        if (done) idle = 0;
-      }
+    if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); rc = PRAOS_E_ARG; return false; }
+    if (S.off.empty()) return false;
+    const size_t n = S.n = S.off.size();
+    S.index0 = next_index;
+    next_index += n;
+    auto t_dev = std::chrono::steady_clock::now();
+    praos_header_bytes hb{n, S.arena.data(), S.arena.size(), S.off.data(), S.len.data()};
+    S.b = praos_batch_upload_bytes(ctx, &hb);
+    if (!S.b) { rc = PRAOS_E_OOM; return false; }
+    S.dstat.resize(n); S.block_no.resize(n); S.slot.resize(n); S.ocn.resize(n); S.bsize.resize(n);
+    S.prev.resize(32 * n); S.gen.resize(n); S.cold.resize(32 * n); S.hh.resize(32 * n); S.vout.resize(64 * n);
+    S.bits.resize(n); S.pidx.resize(n); S.nonce.resize(32 * n); S.v.resize(n); S.eidx.resize(n);
+    praos_decoded dec{};
+    dec.status = S.dstat.data(); dec.block_no = S.block_no.data(); dec.slot = S.slot.data();
+    dec.prev_hash = S.prev.data(); dec.prev_is_genesis = S.gen.data(); dec.cold_vk = S.cold.data();
+    dec.body_size = S.bsize.data(); dec.ocert_n = S.ocn.data(); dec.header_hash = S.hh.data();
+    dec.vrf_out = S.vout.data();
+    rc = praos_batch_decode(ctx, S.b);
+    if (rc == PRAOS_OK) rc = praos_batch_download_decoded(ctx, S.b, &dec);
+    if (rc != PRAOS_OK) return false;
+    stats->ms_device += ms_since(t_dev);
+    // vrfNonceValue of every CERTIFIED output (Praos/VRF.hs:88-131), in parallel; then the
+    // nonce chain in order (tick at epoch changes, evolving ⭒ eta, candidate freeze)
+    auto t_nonce = std::chrono::steady_clock::now();
+    std::vector<praos_nonce> eta_of(n);
+    {
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < nthreads; t++)
+        th.emplace_back([&, t] {
+          for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) {
+            uint8_t m[65], h1[32];
+            m[0] = 'N';
+            std::memcpy(m + 1, S.vout.data() + 64 * i, 64);
+            praos_host::blake2b(h1, 32, m, 65);
+            praos_host::blake2b(eta_of[i].hash, 32, h1, 32);
+            eta_of[i].neutral = 0;
+          }
+        });
+      for (auto& t : th) t.join();
     }
-    index0 += off.size();
-    if (!stopped) stats->headers = index0;
+    S.etas.clear();
+    for (size_t i = 0; i < n; i++) {
+      const uint64_t e_new = epoch_of(S.slot[i]);
+      if (!sp.dead && e_new > (sp.origin ? 0 : epoch_of(sp.last))) {
+        sp.epoch_nonce = praos_host::nonce_combine(sp.candidate, sp.leb);
+        sp.leb = sp.lab;
+      }
+      if (S.etas.empty() || !praos_host::nonce_eq(S.etas.back(), sp.epoch_nonce)) S.etas.push_back(sp.epoch_nonce);
+      S.eidx[i] = (uint8_t)(S.etas.size() - 1);
+      if (sp.dead || (S.dstat[i] & PRAOS_DEC_FAILED)) { sp.dead = true; continue; }   // the chain stops here
+      sp.origin = 0;
+      sp.last = S.slot[i];
+      sp.lab.neutral = S.gen[i] ? 1 : 0;
+      std::memset(sp.lab.hash, 0, 32);
+      if (!S.gen[i]) std::memcpy(sp.lab.hash, S.prev.data() + 32 * i, 32);
+      sp.evolving = praos_host::nonce_combine(sp.evolving, eta_of[i]);
+      const uint64_t first_next = ei->epoch_base_slot + (e_new - ei->epoch_base_no + 1) * ei->epoch_length;
+      if (S.slot[i] + ei->stability_window < first_next) sp.candidate = sp.evolving;
+    }
+    if (S.etas.size() > 256) { praos_set_error_(ctx, "replay: > 256 epochs in a batch"); rc = PRAOS_E_STATE; return false; }
+    for (const praos_nonce& e : S.etas)
+      if (!have_last || !praos_host::nonce_eq(e, last_eta)) { stats->epochs++; last_eta = e; have_last = true; }
+    stats->ms_nonce += ms_since(t_nonce);
+    rc = praos_batch_set_nonces(ctx, S.b, S.etas.data(), (uint32_t)S.etas.size(), S.eidx.data());
+    return rc == PRAOS_OK;
+  };
+  auto launch = [&](Stage& S) {
+    auto t = std::chrono::steady_clock::now();
+    const int r = praos_batch_run(ctx, S.b);   // async on the ctx stream
+    stats->ms_device += ms_since(t);
+    stats->batches++;
+    return r;
+  };
+  auto download = [&](Stage& S) {
+    auto t = std::chrono::steady_clock::now();
+    praos_out out{S.bits.data(), S.pidx.data(), nullptr, nullptr, S.nonce.data()};
+    const int r = praos_batch_download(ctx, S.b, &out);
+    stats->ms_device += ms_since(t);
+    return r;
+  };
+  // envelope + updateChainDepState over a verified batch; true when the chain stops
+  auto fold = [&](Stage& S, int& rc) -> bool {
+    auto t_fold = std::chrono::steady_clock::now();
+    const size_t n = S.n;
+    praos_out out{S.bits.data(), S.pidx.data(), nullptr, nullptr, S.nonce.data()};
+    praos_headers h{};
+    h.n = n;
+    h.slot = S.slot.data();
+    h.cold_vk = S.cold.data();
+    h.ocert_n = S.ocn.data();
+    env->block_no = S.block_no.data();
+    env->header_hash = S.hh.data();
+    env->header_size = S.len.data();
+    env->body_size = S.bsize.data();
+    size_t stop = 0, done = 0;
+    rc = praos_validate_headers_nonces(ctx, &h, S.prev.data(), S.gen.data(), &out, env, ei, st, S.etas.data(),
+                                       (uint32_t)S.etas.size(), S.eidx.data(), S.v.data(), &stop, &done);
+    env->block_no = nullptr;
+    env->header_hash = nullptr;
+    env->header_size = nullptr;
+    env->body_size = nullptr;
+    stats->ms_fold += ms_since(t_fold);
+    if (rc != PRAOS_OK) return true;
+    for (size_t k = 0; k < done && S.index0 + k < verdicts_cap; k++) verdicts[S.index0 + k] = S.v[k];
+    if (stop < done) {          // the chain stops at the first invalid header
+      stats->validated += stop;
+      stats->stop_index = S.index0 + stop;
+      stats->stop_verdict = S.v[stop];
+      stats->headers = S.index0 + stop + 1;
+      return true;
+    }
+    if (done < n) {             // every header valid so far, yet a nonce the fold disagrees with
+      praos_set_error_(ctx, "replay: epoch nonce of header " + std::to_string(S.index0 + done) + " diverged");
+      rc = PRAOS_E_STATE;
+      return true;
+    }
+    stats->validated += n;
+    stats->headers = S.index0 + n;
+    return false;
+  };
+  auto release = [&](Stage& S) {
+    if (S.b) praos_batch_free(ctx, S.b);
+    S.b = nullptr;
+  };
+  bool stopped = false;
+  int rc = PRAOS_OK;
+  int cur = 0;
+  bool have_cur = prepare(stage[cur], rc);
+  if (rc == PRAOS_OK && have_cur) rc = launch(stage[cur]);
+  while (rc == PRAOS_OK && have_cur) {
+    Stage& C = stage[cur];
+    Stage& N = stage[cur ^ 1];
+    // the next batch is read and decoded while C's crypto runs; its decode queues behind it
+    const bool have_next = !sp.dead && prepare(N, rc);
+    if (rc != PRAOS_OK) break;
+    rc = download(C);
+    if (rc != PRAOS_OK) break;
+    if (have_next) {
+      rc = launch(N);           // N's crypto overlaps C's fold
+      if (rc != PRAOS_OK) break;
+    }
+    stopped = fold(C, rc);
+    release(C);
+    if (stopped || rc != PRAOS_OK) break;
+    have_cur = have_next;
+    cur ^= 1;
   }
+  release(stage[0]);
+  release(stage[1]);
+  if (rc != PRAOS_OK) return rc;
+  const uint64_t index0 = stopped ? stats->headers : next_index;
   if (!stopped) stats->stop_index = index0;
   stats->chunks = (uint32_t)rd.chunk;
   return PRAOS_OK;

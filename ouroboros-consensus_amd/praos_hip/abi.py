@@ -108,7 +108,7 @@ class ReplayStats(ctypes.Structure):
     _fields_ = [("skipped", ctypes.c_uint64), ("headers", ctypes.c_uint64), ("validated", ctypes.c_uint64), ("stop_index", ctypes.c_uint64),
                 ("stop_verdict", ctypes.c_uint32), ("epochs", ctypes.c_uint32), ("batches", ctypes.c_uint32),
                 ("chunks", ctypes.c_uint32), ("ms_io", ctypes.c_double), ("ms_device", ctypes.c_double),
-                ("ms_fold", ctypes.c_double)]
+                ("ms_fold", ctypes.c_double), ("ms_nonce", ctypes.c_double)]
 
 
 class Counters(ctypes.Structure):
@@ -216,6 +216,15 @@ SIGNATURES = {
                                                  ctypes.POINTER(Decoded)]),
     "praos_batch_upload_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
     "praos_batch_download_decoded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Decoded)]),
+    "praos_batch_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "praos_batch_set_nonces": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Nonce), ctypes.c_uint32,
+                                              u8p]),
+    "praos_validate_headers_nonces": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), u8p, u8p,
+                                                     ctypes.POINTER(Out), ctypes.POINTER(Envelope),
+                                                     ctypes.POINTER(EpochInfo), ctypes.POINTER(ChainState),
+                                                     ctypes.POINTER(Nonce), ctypes.c_uint32, u8p, u8p,
+                                                     ctypes.POINTER(ctypes.c_size_t),
+                                                     ctypes.POINTER(ctypes.c_size_t)]),
     "praos_verify_block_integrity": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.c_uint64,
                                                     u8p, u8p]),
     "praos_block_batch_upload": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
@@ -494,19 +503,38 @@ class Context:
             self.check(-3)
         return b
 
+    def batch_decode(self, b):
+        self.check(self.L.praos_batch_decode(self.h, b))
+
+    @staticmethod
+    def nonce_array(etas):
+        arr = (Nonce * max(1, len(etas)))()
+        for k, e in enumerate(etas):
+            arr[k].neutral = int(e is None)
+            if e is not None:
+                ctypes.memmove(arr[k].hash, bytes(e), 32)
+        return arr
+
+    def set_nonces(self, b, etas, eta_idx):
+        """praos_batch_set_nonces: header i of batch b is verified under etas[eta_idx[i]]
+        (None = NeutralNonce)."""
+        idx = np.ascontiguousarray(eta_idx, dtype=np.uint8)
+        self.check(self.L.praos_batch_set_nonces(self.h, b, self.nonce_array(etas), len(etas), ptr(idx)))
+
     def download_decoded(self, b, n):
         D, d = self.alloc_decoded(n)
         self.check(self.L.praos_batch_download_decoded(self.h, b, ctypes.byref(d)))
         return D
 
     def update_chain_dep_state(self, H, crypto, prev_hash, state: dict, epoch_info, prev_is_genesis=None,
-                               envelope=None):
+                               envelope=None, etas=None, eta_idx=None):
         """state: dict(last_slot (None = Origin), counters {hash28: n}, evolving, candidate, epoch_nonce,
         lab, leb) with nonces None (Neutral) or 32 bytes; updated in place.  epoch_info: (base_slot,
         base_no, length, stability_window).  envelope (praos_validate_headers): dict(block_no u64[n],
         header_hash u8[n,32], header_size u32[n], body_size u32[n], tip (None = Origin, or (slot,
         block_no, hash32)), max_major_pv, lv_prot_major, max_header_size, max_body_size); its "tip" is
-        updated in place.  Returns (verdict u8[n], chain_stop, processed)."""
+        updated in place.  etas / eta_idx: the per-header nonces the crypto ran under
+        (praos_validate_headers_nonces).  Returns (verdict u8[n], chain_stop, processed)."""
         n = len(H["slot"])
         hs = self.headers_struct(H)
         os_ = self.out_struct(crypto)
@@ -537,7 +565,31 @@ class Context:
         pg = None if prev_is_genesis is None else np.ascontiguousarray(prev_is_genesis, dtype=np.uint8)
         verdict = np.zeros(n, np.uint8)
         stop, done = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        if envelope is None:
+        E = None
+        if envelope is not None:
+            E = Envelope()
+            arrs = {k: np.ascontiguousarray(envelope[k], dtype=dt) for k, dt in
+                    (("block_no", np.uint64), ("header_hash", np.uint8), ("header_size", np.uint32),
+                     ("body_size", np.uint32))}
+            E.block_no, E.header_hash = ptr(arrs["block_no"], u64p), ptr(arrs["header_hash"])
+            E.header_size, E.body_size = ptr(arrs["header_size"], u32p), ptr(arrs["body_size"], u32p)
+            tip = envelope["tip"]
+            E.tip_is_origin = int(tip is None)
+            if tip is not None:
+                E.tip_slot, E.tip_block_no = tip[0], tip[1]
+                ctypes.memmove(E.tip_hash, bytes(tip[2]), 32)
+            for k in ("max_major_pv", "lv_prot_major", "max_header_size", "max_body_size"):
+                setattr(E, k, envelope[k])
+        if etas is not None:
+            idx = np.ascontiguousarray(eta_idx, dtype=np.uint8)
+            self.check(self.L.praos_validate_headers_nonces(
+                self.h, ctypes.byref(hs), ptr(ph), ptr(pg) if pg is not None else None, ctypes.byref(os_),
+                ctypes.byref(E) if E is not None else None, ctypes.byref(ei), ctypes.byref(st),
+                self.nonce_array(etas), len(etas), ptr(idx), ptr(verdict), ctypes.byref(stop), ctypes.byref(done)))
+            if envelope is not None:
+                envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no),
+                                                                bytes(E.tip_hash))
+        elif envelope is None:
             self.check(self.L.praos_update_chain_dep_state(self.h, ctypes.byref(hs), ptr(ph),
                                                            ptr(pg) if pg is not None else None, ctypes.byref(os_),
                                                            ctypes.byref(ei), ctypes.byref(st), ptr(verdict),

@@ -108,7 +108,7 @@ def test_replay_all_valid(ctx, chain, batch_max):
     assert (stats["headers"], stats["validated"], stats["stop_index"], stats["stop_verdict"]) == (n, n, n, 0)
     assert int((v != 0).sum()) == 0
     assert stats["epochs"] == EPOCHS and stats["chunks"] == chain["nchunks"]
-    assert stats["batches"] >= (EPOCHS if batch_max > n else n // batch_max)
+    assert stats["batches"] == -(-n // batch_max)      # batches span epochs (per-header nonces)
     assert st == chain["state"]
     assert env["tip"] == (int(chain["slots"][-1]), n - 1, bytes(chain["header_hash"][-1]))
     ov, ost, otip, etas, ostop = _oracle_fold(ctx, chain, n)
@@ -198,3 +198,53 @@ def test_replay_resume_from_checkpoint(ctx, chain, tmp_path):
     assert st2 == chain["state"] and env2["tip"][2] == bytes(chain["header_hash"][-1])
     with pytest.raises(abi.PraosError, match="tip is not a block"):
         _replay(ctx, chain, state=dict(st), tip=(env["tip"][0], env["tip"][1], b"\x00" * 32))
+
+
+def test_multi_epoch_batch_nonces(ctx, chain):
+    """One device batch over all four epochs with per-header nonces (praos_batch_set_nonces)
+    gives the same outputs as per-epoch batches under praos_set_epoch; the fold over it
+    with those nonces (praos_validate_headers_nonces) ends in the generator's state; a
+    header verified under the wrong nonce ends the fold there (processed < n)."""
+    arena, off, ln = chain["arena"], chain["off"], chain["len"]
+    n = len(off)
+    epoch = (chain["slots"] // EPOCH_LEN).astype(np.uint8)
+    ctx.set_epoch(chain["nonces"][0], chain["pools"], chain["params"])
+    b = ctx.upload_bytes(arena, off, ln)
+    try:
+        ctx.batch_decode(b)
+        D = ctx.download_decoded(b, n)
+        ctx.set_nonces(b, chain["nonces"], epoch)
+        ctx.run(b)
+        o = ctx.download(b, n)
+    finally:
+        ctx.free(b)
+    assert int((o["bits"] != 0).sum()) == 0
+    for e in range(EPOCHS):
+        rows = np.nonzero(epoch == e)[0]
+        ctx.set_epoch(chain["nonces"][e], chain["pools"], chain["params"])
+        oe = ctx.verify_header_bytes(arena, off[rows], ln[rows])
+        for k in ("bits", "pool_idx", "beta", "leader", "nonce"):
+            assert np.array_equal(oe[k], o[k][rows]), (e, k)
+    st = _genesis_state(chain["cfg"]["eta0"])
+    v, stop, done = ctx.update_chain_dep_state(_soa(D, n), o, D["prev_hash"], st, chain["epoch_info"],
+                                               prev_is_genesis=D["prev_is_genesis"], etas=chain["nonces"],
+                                               eta_idx=epoch)
+    assert (stop, done) == (n, n) and st == chain["state"]
+    # epoch 2's headers claimed under epoch 1's nonce: the fold stops at the first of them
+    bad = epoch.copy()
+    first2 = int(np.nonzero(epoch == 2)[0][0])
+    bad[epoch == 2] = 1
+    st = _genesis_state(chain["cfg"]["eta0"])
+    v, stop, done = ctx.update_chain_dep_state(_soa(D, n), o, D["prev_hash"], st, chain["epoch_info"],
+                                               prev_is_genesis=D["prev_is_genesis"], etas=chain["nonces"],
+                                               eta_idx=bad)
+    assert done == first2 and stop == first2
+
+
+def _soa(D, n):
+    """praos_headers view of decoded fields (the fold reads slot, cold_vk, ocert_n)."""
+    z = lambda shape, dt: np.zeros(shape, dt)  # noqa: E731
+    return {"slot": D["slot"], "cold_vk": D["cold_vk"], "vrf_vk": D["vrf_vk"], "vrf_out": D["vrf_out"],
+            "vrf_proof": D["vrf_proof"], "hot_vk": D["hot_vk"], "ocert_n": D["ocert_n"], "ocert_c0": D["ocert_c0"],
+            "ocert_sig": D["ocert_sig"], "kes_sig": D["kes_sig"], "body_off": z(n, np.uint64),
+            "body_len": z(n, np.uint32), "body_bytes": z(8, np.uint8)}
