@@ -13,11 +13,78 @@ static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+
+// A small persistent pool of host threads for the staging copies (pageable caller
+// memory <-> pinned buffers): one job at a time, each worker takes its share.
+class CopyPool {
+ public:
+  explicit CopyPool(unsigned n) : nt_(n) {
+    for (unsigned t = 0; t < nt_; t++) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~CopyPool() {
+    { std::lock_guard<std::mutex> g(m_); stop_ = true; }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return nt_; }
+  void run(const std::function<void(unsigned)>& f) {
+    std::unique_lock<std::mutex> g(m_);
+    job_ = &f;
+    pending_ = nt_;
+    gen_++;
+    cv_.notify_all();
+    done_.wait(g, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  // dst[0, n) = src[0, n), split over the workers
+  void copy(void* dst, const void* src, size_t n) {
+    if (n < (1u << 20)) { std::memcpy(dst, src, n); return; }
+    run([&](unsigned t) {
+      const size_t a = n * t / nt_, b = n * (t + 1) / nt_;
+      std::memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a);
+    });
+  }
+
+ private:
+  void loop(unsigned t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned)>* f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(t);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  unsigned nt_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  unsigned pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2 x 16 MB per context
 
 struct praos_ctx {
   int device = 0;
@@ -45,7 +112,70 @@ struct praos_ctx {
   uint32_t* d_eta0 = nullptr;
   std::vector<praos_pool> pools;     // caller order
   std::map<std::string, int32_t> pool_by_hash;
+  // host <-> device staging for large transfers from pageable caller memory
+  uint8_t* pin[2] = {nullptr, nullptr};
+  hipEvent_t pin_ev[2] = {};
+  std::unique_ptr<CopyPool> pool;
+  // device buffers of the last freed batch, reused by the next one in allocation
+  // order (hipMalloc / hipFree of ~40 buffers cost ~20 ms per 432k batch)
+  std::vector<void*> spare;
+  std::vector<size_t> spare_sz;
 };
+
+static void free_spare(praos_ctx* c) {
+  for (void* p : c->spare)
+    if (p) (void)hipFree(p);
+  c->spare.clear();
+  c->spare_sz.clear();
+}
+
+// Large H2D / D2H copies through two pinned buffers: the host threads fill (drain) one
+// piece while the DMA engine moves the other, so pageable caller memory moves at PCIe
+// speed instead of through the runtime's own pageable path.  Small copies go direct.
+static bool stage_init(praos_ctx* c) {
+  if (c->pin[0]) return true;
+  for (int k = 0; k < 2; k++) {
+    if (hipHostMalloc((void**)&c->pin[k], STAGE_PIECE, hipHostMallocDefault) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&c->pin_ev[k], hipEventDisableTiming) != hipSuccess) return false;
+  }
+  const unsigned hw = std::thread::hardware_concurrency();
+  c->pool.reset(new CopyPool(std::max(1u, std::min(8u, hw ? hw : 1u))));
+  return true;
+}
+
+static hipError_t h2d(praos_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (bytes < (4u << 20) || !stage_init(c)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream);
+  for (size_t off = 0, k = 0; off < bytes; off += STAGE_PIECE, k++) {
+    const size_t len = std::min(STAGE_PIECE, bytes - off);
+    hipError_t e = hipEventSynchronize(c->pin_ev[k & 1]);    // the DMA that last read this buffer
+    if (e != hipSuccess) return e;
+    c->pool->copy(c->pin[k & 1], (const uint8_t*)src + off, len);
+    e = hipMemcpyAsync((uint8_t*)dst + off, c->pin[k & 1], len, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(c->pin_ev[k & 1], c->stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// blocking: the stream is drained first (the producer kernels), then piecewise
+static hipError_t d2h(praos_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (bytes < (4u << 20) || !stage_init(c)) return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  hipError_t e = hipStreamSynchronize(c->stream);
+  const size_t np = (bytes + STAGE_PIECE - 1) / STAGE_PIECE;
+  for (size_t k = 0; k <= np && e == hipSuccess; k++) {
+    if (k < np) {     // start piece k, then drain piece k - 1 while it moves
+      const size_t off = k * STAGE_PIECE, len = std::min(STAGE_PIECE, bytes - off);
+      e = hipMemcpyAsync(c->pin[k & 1], (const uint8_t*)src + off, len, hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess) e = hipEventRecord(c->pin_ev[k & 1], c->stream);
+    }
+    if (e == hipSuccess && k > 0) {
+      const size_t j = k - 1, off = j * STAGE_PIECE, len = std::min(STAGE_PIECE, bytes - off);
+      e = hipEventSynchronize(c->pin_ev[j & 1]);
+      if (e == hipSuccess) c->pool->copy((uint8_t*)dst + off, c->pin[j & 1], len);
+    }
+  }
+  return e;
+}
 
 struct praos_batch {
   size_t n = 0;
@@ -92,6 +222,8 @@ struct praos_batch {
   uint32_t *blk_len = nullptr, *seg_len = nullptr;
   uint8_t *nseg = nullptr, *split_status = nullptr, *seg_hash = nullptr, *blk_result = nullptr, *blk_hash = nullptr;
   std::vector<void*> owned;
+  std::vector<size_t> owned_sz;
+  praos_ctx* owner = nullptr;
 };
 
 static constexpr size_t KT_BYTES = 4 * 8 * 4 * 32;  // per cached key: 4 tables x 8 cached points
@@ -115,8 +247,18 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 template <typename T>
 static hipError_t dalloc(praos_batch* b, T** p, size_t bytes) {
   void* q = nullptr;
-  hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
-  if (e == hipSuccess) { b->owned.push_back(q); *p = (T*)q; }
+  size_t sz = bytes ? bytes : 16;
+  const size_t k = b->owned.size();
+  praos_ctx* c = b->owner;
+  hipError_t e = hipSuccess;
+  if (c && k < c->spare.size() && c->spare[k] && c->spare_sz[k] >= sz && c->spare_sz[k] <= 2 * sz + 4096) {
+    q = c->spare[k];                 // the previous batch's buffer at the same position
+    sz = c->spare_sz[k];
+    c->spare[k] = nullptr;
+  } else {
+    e = hipMalloc(&q, sz);
+  }
+  if (e == hipSuccess) { b->owned.push_back(q); b->owned_sz.push_back(sz); *p = (T*)q; }
   return e;
 }
 
@@ -168,7 +310,13 @@ void praos_close(praos_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_epoch(c);
+  free_spare(c);
   (void)hipFree(c->btab);
+  c->pool.reset();
+  for (int k = 0; k < 2; k++) {
+    if (c->pin[k]) (void)hipHostFree(c->pin[k]);
+    if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
+  }
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   for (auto& e : c->side_ev) (void)hipEventDestroy(e);
   for (auto& st : c->side) (void)hipStreamDestroy(st);
@@ -246,6 +394,16 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
 
 void praos_batch_free(praos_ctx* c, praos_batch* b) {
   if (!b) return;
+  if (c && c->device >= 0 && b->owner == c) {
+    // keep the buffers for the next batch (its kernels are ordered after this one's on
+    // the ctx stream, so no wait is needed); drop the older spares it did not take
+    (void)hipSetDevice(c->device);
+    free_spare(c);
+    c->spare.swap(b->owned);
+    c->spare_sz.swap(b->owned_sz);
+    delete b;
+    return;
+  }
   if (c) (void)hipSetDevice(c->device);
   for (void* p : b->owned) (void)hipFree(p);
   delete b;
@@ -302,6 +460,7 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   if (!c || !h) return nullptr;
   if (hipSetDevice(c->device) != hipSuccess) return nullptr;
   praos_batch* b = new praos_batch();
+  b->owner = c;
   const size_t n = h->n;
   b->n = n;
   // repack bodies 8-byte aligned (the SHA-512 feeder reads 64-bit words)
@@ -313,19 +472,41 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
     if (h->body_off[i] > h->body_bytes_len || h->body_len[i] > h->body_bytes_len - h->body_off[i]) bad_range = true;
     total += (h->body_len[i] + 7) & ~(size_t)7;
   }
-  std::vector<uint8_t> arena(total + 16, 0);
+  auto tr0 = std::chrono::steady_clock::now();
+  std::unique_ptr<uint8_t[]> arena(new uint8_t[total + 16]);
   std::vector<uint32_t> len(n);
-  for (size_t i = 0; i < n; i++) {
-    const bool ok = h->body_off[i] <= h->body_bytes_len && h->body_len[i] <= h->body_bytes_len - h->body_off[i];
-    len[i] = ok ? h->body_len[i] : 0xffffffffu;  // marks out-of-range (kernel flags PRAOS_BIT_INPUT)
-    if (ok) std::memcpy(arena.data() + off[i], h->body_bytes + h->body_off[i], h->body_len[i]);
+  auto repack = [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; i++) {
+      const bool ok = h->body_off[i] <= h->body_bytes_len && h->body_len[i] <= h->body_bytes_len - h->body_off[i];
+      len[i] = ok ? h->body_len[i] : 0xffffffffu;  // marks out-of-range (kernel flags PRAOS_BIT_INPUT)
+      const size_t pad = ((size_t)h->body_len[i] + 7) & ~(size_t)7;
+      uint8_t* d = arena.get() + off[i];
+      if (ok) std::memcpy(d, h->body_bytes + h->body_off[i], h->body_len[i]);
+      if (pad > (ok ? (size_t)h->body_len[i] : 0)) std::memset(d + (ok ? h->body_len[i] : 0), 0, pad - (ok ? h->body_len[i] : 0));
+    }
+  };
+  if (n >= 65536 && stage_init(c)) {
+    const unsigned nt = c->pool->size();
+    c->pool->run([&](unsigned t) { repack(n * t / nt, n * (t + 1) / nt); });
+  } else {
+    repack(0, n);
   }
+  std::memset(arena.get() + total, 0, 16);
+  if (std::getenv("PRAOS_TRACE_UPLOAD"))
+    fprintf(stderr, "upload: repack %.2f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count());
   (void)bad_range;
   b->body_bytes_len = total;
+  static const bool trace = std::getenv("PRAOS_TRACE_UPLOAD") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto t0 = now();
   bool ok = alloc_soa(b, n, total + 16);
   if (!ok) { c->err = "device allocation failed"; praos_batch_free(c, b); return nullptr; }
+  if (trace) fprintf(stderr, "upload: alloc %.2f ms\n", std::chrono::duration<double, std::milli>(now() - t0).count());
   auto up = [&](void* d, const void* s, size_t bytes) {
-    if (bytes) ok &= hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    auto t = now();
+    if (bytes) ok &= h2d(c, d, s, bytes) == hipSuccess;
+    if (trace) fprintf(stderr, "upload: %zu bytes %.2f ms\n", bytes, std::chrono::duration<double, std::milli>(now() - t).count());
   };
   up(b->slot, h->slot, 8 * n);
   up(b->ocert_n, h->ocert_n, 8 * n);
@@ -339,8 +520,10 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   up(b->hot_vk, h->hot_vk, 32 * n);
   up(b->ocert_sig, h->ocert_sig, 64 * n);
   up(b->kes_sig, h->kes_sig, 448 * n);
-  up(b->body, arena.data(), total + 16);
+  up(b->body, arena.get(), total + 16);
+  auto ts = now();
   ok &= hipStreamSynchronize(c->stream) == hipSuccess;
+  if (trace) fprintf(stderr, "upload: final sync %.2f ms\n", std::chrono::duration<double, std::milli>(now() - ts).count());
   if (!ok) { c->err = "upload failed"; praos_batch_free(c, b); return nullptr; }
   return b;
 }
@@ -350,6 +533,7 @@ praos_batch* praos_batch_upload_bytes(praos_ctx* c, const praos_header_bytes* in
   if (c->device < 0) { c->err = "host-only context: no HIP device"; return nullptr; }
   if (hipSetDevice(c->device) != hipSuccess) return nullptr;
   praos_batch* b = new praos_batch();
+  b->owner = c;
   const size_t n = in->n;
   b->n = n;
   b->from_bytes = true;
@@ -372,7 +556,7 @@ praos_batch* praos_batch_upload_bytes(praos_ctx* c, const praos_header_bytes* in
   const size_t pad = ((in->bytes_len + 7) & ~(size_t)7) + 16 - in->bytes_len;
   ok &= hipMemsetAsync(b->arena + in->bytes_len, 0, pad, c->stream) == hipSuccess;
   if (in->bytes_len)
-    ok &= hipMemcpyAsync(b->arena, in->bytes, in->bytes_len, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    ok &= h2d(c, b->arena, in->bytes, in->bytes_len) == hipSuccess;
   if (n) {
     ok &= hipMemcpyAsync(b->hoff, in->off, 8 * n, hipMemcpyHostToDevice, c->stream) == hipSuccess;
     ok &= hipMemcpyAsync(b->hlen, in->len, 4 * n, hipMemcpyHostToDevice, c->stream) == hipSuccess;
@@ -661,11 +845,11 @@ int praos_batch_download(praos_ctx* c, praos_batch* b, praos_out* out) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const size_t n = b->n;
   if (n == 0) return PRAOS_OK;
-  HIPCHK(c, hipMemcpy(out->bits, b->bits, 2 * n, hipMemcpyDeviceToHost));
-  if (out->pool_idx) HIPCHK(c, hipMemcpy(out->pool_idx, b->pool_idx, 4 * n, hipMemcpyDeviceToHost));
-  if (out->beta) HIPCHK(c, hipMemcpy(out->beta, b->beta, 64 * n, hipMemcpyDeviceToHost));
-  if (out->leader) HIPCHK(c, hipMemcpy(out->leader, b->leader, 32 * n, hipMemcpyDeviceToHost));
-  if (out->nonce) HIPCHK(c, hipMemcpy(out->nonce, b->nonce, 32 * n, hipMemcpyDeviceToHost));
+  HIPCHK(c, d2h(c, out->bits, b->bits, 2 * n));
+  if (out->pool_idx) HIPCHK(c, d2h(c, out->pool_idx, b->pool_idx, 4 * n));
+  if (out->beta) HIPCHK(c, d2h(c, out->beta, b->beta, 64 * n));
+  if (out->leader) HIPCHK(c, d2h(c, out->leader, b->leader, 32 * n));
+  if (out->nonce) HIPCHK(c, d2h(c, out->nonce, b->nonce, 32 * n));
   return PRAOS_OK;
 }
 
@@ -720,7 +904,7 @@ int praos_batch_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d)
   const size_t n = b->n;
   if (n == 0) return PRAOS_OK;
   auto dn = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-    return dst ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+    return dst ? d2h(c, dst, src, bytes) : hipSuccess;
   };
   HIPCHK(c, dn(d->status, b->dec_status, 2 * n));
   HIPCHK(c, dn(d->block_no, b->block_no, 8 * n));
