@@ -50,6 +50,23 @@ from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  #
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02c_traffic.json")   # tools/profile.sh r02c
+FEMUL_FILE = os.path.join(ROOT, "profiles", "r02", "femul_microbench.txt")  # tools/microbench/femul.hip
+
+
+def issue_weighted_peak():
+    """The integer ceiling the field multiply itself reaches (measured, femul microbench):
+    a multiply is 154 counted ops (tools/workmodel.py M) and takes C SIMD cycles per wave
+    when the SIMD is kept full, so mul-bound work peaks at 154 x 64 / C lane-ops per
+    SIMD-cycle -- below the 128 lane-ops/clk/CU issue peak because v_mad_u64_u32 issues
+    at ~5.2 cycles per wave instruction instead of 2."""
+    try:
+        for line in open(FEMUL_FILE):
+            if line.startswith("radix 2^32, asm MAC"):
+                cyc = float(line.split("SIMD cycles")[0].split()[-1])
+                return 154 * 64 / cyc * 4 * 256 * 2.4e9, cyc
+    except (OSError, ValueError, IndexError):
+        pass
+    return None, None
 
 CONFIGS = {
     "c1": dict(items=10_000, kernels=7, metric="Praos headers validated/sec (CPU config C1)",
@@ -447,6 +464,7 @@ def main():
     dom_kernel = f"k_{dominant}_ck" if (args.keycache and kst.get(f"{'cold' if dominant == 'ocert' else dominant}_hits")) \
         else f"k_{dominant}"
     traffic, traffic_src = load_traffic(dom_kernel, cfg["workload"])
+    iw_peak, iw_cyc = issue_weighted_peak()
     line = {
         "metric": cfg["metric"],
         "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
@@ -467,7 +485,12 @@ def main():
                      "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": round(w_pipe),
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},
                      "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent),
-                     "peak_basis": "128 int32 lane-ops/clk/CU x 256 CU x 2.4 GHz (VALU issue, MI355X_MICROARCH.md)"},
+                     "peak_basis": "128 int32 lane-ops/clk/CU x 256 CU x 2.4 GHz (VALU issue, MI355X_MICROARCH.md)",
+                     "issue_weighted_peak": round(iw_peak / 1e12, 2) if iw_peak else None,
+                     "frac_of_issue_weighted": round(dom_achieved / iw_peak, 4) if iw_peak else None,
+                     "issue_weighted_basis": (f"field multiply = 154 counted ops in {iw_cyc} SIMD cycles per wave "
+                                              f"(femul microbench, {os.path.relpath(FEMUL_FILE, ROOT)})")
+                                             if iw_peak else None},
         "keycache": dict(kst, min_uses=args.keycache),
         "self_check": {"clean": int(clean.sum()), "clean_ok": clean_ok, "corrupted": int((~clean).sum()),
                        "corrupted_rejected": corrupt_caught, "corrupted_in_checked_fields": int(rel.sum()),

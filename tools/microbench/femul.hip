@@ -4,11 +4,14 @@
 //   r32c   : radix 2^32, the same schedule with the carries left to the compiler (__builtin_addc)
 //   r26    : radix 2^25.5, 10 limbs, 100 v_mad_u64_u32 into 10 independent 64-bit column sums
 //            (no carry flags), one carry pass
+//   r32col : radix 2^32, one asm block per column (fe_col.hpp): the MACs' carries in
+//            separate SGPR pairs, counted after the column, no s_nop per MAC
 // Each lane runs a dependent chain of multiplies (like a scalar-multiplication
 // chain); results are compared across variants mod p.
 // Build: hipcc --offload-arch=gfx950 -O3 -o femul femul.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include "fe_col.hpp"
 #include <cstdio>
 #include <cstring>
 
@@ -71,6 +74,43 @@ DI void mul32(f32& r, const f32& a, const f32& b) {
   red512(r, t);
 }
 
+template <int M>
+DI void col_dispatch(uint64_t& acc, uint32_t& top, const uint32_t* x, const uint32_t* y) { FeCol<M>::mac(acc, top, x, y); }
+
+DI void mul32col(f32& r, const f32& a, const f32& b) {
+  uint32_t t[16];
+  uint64_t acc = (uint64_t)a.v[0] * b.v[0];
+  t[0] = (uint32_t)acc;
+  acc >>= 32;
+#pragma unroll
+  for (int k = 1; k < 15; k++) {
+    uint32_t top = 0, x[8], y[8];
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      x[m] = a.v[i];
+      y[m] = b.v[j];
+      m++;
+    }
+    switch (m) {
+      case 1: col_dispatch<1>(acc, top, x, y); break;
+      case 2: col_dispatch<2>(acc, top, x, y); break;
+      case 3: col_dispatch<3>(acc, top, x, y); break;
+      case 4: col_dispatch<4>(acc, top, x, y); break;
+      case 5: col_dispatch<5>(acc, top, x, y); break;
+      case 6: col_dispatch<6>(acc, top, x, y); break;
+      case 7: col_dispatch<7>(acc, top, x, y); break;
+      default: col_dispatch<8>(acc, top, x, y); break;
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+  }
+  t[15] = (uint32_t)acc;
+  red512(r, t);
+}
+
 // ---------------------------------------------------------------- radix 2^25.5
 // limbs: even i 26 bits, odd i 25 bits; value = sum f_i 2^ceil(25.5 i)
 struct f26 { uint32_t v[10]; };
@@ -115,12 +155,15 @@ DI void mul26(f26& r, const f26& f, const f26& g) {
 template <int V>
 __global__ void __launch_bounds__(256) kern(uint32_t* out, uint32_t seed) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if constexpr (V < 2) {
+  if constexpr (V < 2 || V == 3) {
     f32 x, y;
 #pragma unroll
     for (int i = 0; i < 8; i++) { x.v[i] = seed * (t + 3 * i + 1); y.v[i] = seed ^ (t * 7 + i); }
     x.v[7] &= 0x7fffffff; y.v[7] &= 0x7fffffff;
-    for (int it = 0; it < ITERS; it++) mul32<V == 0>(x, x, y);
+    for (int it = 0; it < ITERS; it++) {
+      if constexpr (V == 3) mul32col(x, x, y);
+      else mul32<V == 0>(x, x, y);
+    }
 #pragma unroll
     for (int i = 0; i < 8; i++) out[10 * t + i] = x.v[i];
   } else {
@@ -178,19 +221,21 @@ int main() {
   const int blocks = ncu * 16;              // 16 waves / CU = 4 per SIMD
   const size_t lanes = (size_t)blocks * 256;
   uint32_t* d; CHK(hipMalloc(&d, lanes * 40));
-  uint32_t* h[3];
-  const char* names[3] = {"radix 2^32, asm MAC (v_mad_u64_u32 + s_nop + v_addc)", "radix 2^32, compiler carries",
-                          "radix 2^25.5, 100 MACs into 10 column sums"};
-  double ms[3];
-  for (int v = 0; v < 3; v++) {
+  uint32_t* h[4];
+  const char* names[4] = {"radix 2^32, asm MAC (v_mad_u64_u32 + s_nop + v_addc)", "radix 2^32, compiler carries",
+                          "radix 2^25.5, 100 MACs into 10 column sums",
+                          "radix 2^32, column asm blocks (carries in SGPR pairs)"};
+  double ms[4];
+  for (int v = 0; v < 4; v++) {
     h[v] = new uint32_t[lanes * 8];
-    int rc = v == 0 ? run<0>(d, blocks, &ms[v]) : v == 1 ? run<1>(d, blocks, &ms[v]) : run<2>(d, blocks, &ms[v]);
+    int rc = v == 0 ? run<0>(d, blocks, &ms[v]) : v == 1 ? run<1>(d, blocks, &ms[v]) :
+             v == 2 ? run<2>(d, blocks, &ms[v]) : run<3>(d, blocks, &ms[v]);
     if (rc) return rc;
     uint32_t* raw = new uint32_t[lanes * 10];
     CHK(hipMemcpy(raw, d, lanes * 40, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < lanes; i++) {
       uint32_t* w = h[v] + 8 * i;
-      if (v < 2) { memcpy(w, raw + 10 * i, 32); }
+      if (v != 2) { memcpy(w, raw + 10 * i, 32); }
       else {   // sum limb_l * 2^pos_l into 9 words with carries
         static const int pos[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
         uint64_t acc[9] = {0};
@@ -213,7 +258,7 @@ int main() {
            muls / ms[v] / 1e6, ms[v] * 1e-3 * 2.4e9 * ncu * 4 / (muls / 64), ncu);
   }
   size_t bad = 0;
-  for (size_t i = 0; i < lanes * 8; i++) bad += (h[0][i] != h[1][i]) + (h[0][i] != h[2][i]);
+  for (size_t i = 0; i < lanes * 8; i++) bad += (h[0][i] != h[1][i]) + (h[0][i] != h[2][i]) + (h[0][i] != h[3][i]);
   printf("results equal mod p across variants: %s (%zu word mismatches)\n", bad ? "NO" : "yes", bad);
   return bad ? 2 : 0;
 }
