@@ -348,11 +348,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # PRAOS_BENCH_REHEARSAL=1: every rank on device 0 over gloo (a multi-rank rehearsal of
+    # this code path on a one-GPU box; the real multi-GPU run uses RCCL, one GPU per rank)
+    rehearsal = os.environ.get("PRAOS_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearsal else "nccl")
     import torch
 
     import praos_hip
@@ -386,7 +391,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt], device="cpu" if rehearsal else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # per-kernel durations for the roofline: serial launches (HIP events on the

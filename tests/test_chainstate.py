@@ -154,6 +154,62 @@ def test_chain_dep_state_fold_across_epochs(hctx, seed):
     assert ref["epoch_nonce"] == eta != eta_a
 
 
+@pytest.mark.parametrize("seed", [4, 5])
+def test_fold_with_per_header_nonces(hctx, seed):
+    """praos_validate_headers_nonces (update_chain_dep_state with etas/eta_idx, no envelope):
+    the same two-epoch batch as above folds in ONE call when every header carries the
+    nonce of its epoch, and matches the restatement epoch by epoch; a header labelled
+    with the wrong nonce ends the fold exactly there (processed), with the state of the
+    headers before it; praos_ticked_epoch_nonce gives the second epoch's nonce."""
+    from praos_hip import abi
+    r = random.Random(seed)
+    pools = _pools(r, 6)
+    base, length, window = 3000, 600, 180
+    n = 160
+    H, crypto, prev, hk = _batch(r, n, pools, base + 40, 7)
+    crypto["bits"][:] = 0
+    for i in range(n):
+        H["ocert_n"][i] = 0
+        if crypto["pool_idx"][i] < 0:
+            crypto["pool_idx"][i] = 0
+            hk[i] = pools[0][0]
+    genesis = np.zeros(n, np.uint8)
+    genesis[0] = 1
+    eta_a = _b2b(b"epoch-a")
+    st0 = {"last_slot": None, "counters": {}, "evolving": _b2b(b"ev"), "candidate": _b2b(b"cand"),
+           "epoch_nonce": eta_a, "lab": None, "leb": _b2b(b"leb")}
+    known = {p[0] for p in pools}
+    ei = (base, 0, length, window)
+    prev_l = [None if genesis[i] else bytes(prev[i]) for i in range(n)]
+    epoch = ((H["slot"] - base) // length).astype(np.uint8)
+    k1 = int(np.nonzero(epoch == 1)[0][0])
+    # the restatement, epoch by epoch, gives the second nonce and the final state
+    ref = {k: (dict(v) if isinstance(v, dict) else v) for k, v in st0.items()}
+    cs.fold(ref, hk[:k1], H["slot"][:k1], crypto["bits"][:k1], H["ocert_n"][:k1], crypto["nonce"][:k1],
+            prev_l[:k1], known, eta_a, base, 0, length, window)
+    eta_b = cs.combine(ref["candidate"], ref["leb"])
+    assert abi.ticked_epoch_nonce(ref, ei, int(H["slot"][k1])) == eta_b
+    cs.fold(ref, hk[k1:], H["slot"][k1:], crypto["bits"][k1:], H["ocert_n"][k1:], crypto["nonce"][k1:],
+            prev_l[k1:], known, eta_b, base, 0, length, window)
+    hctx.set_epoch(eta_a, pools, _params())
+    st = {k: (dict(v) if isinstance(v, dict) else v) for k, v in st0.items()}
+    v, stop, done = hctx.update_chain_dep_state(H, crypto, prev, st, ei, prev_is_genesis=genesis,
+                                                etas=[eta_a, eta_b], eta_idx=epoch)
+    assert (stop, done) == (n, n) and int((v != 0).sum()) == 0 and st == ref
+    # epoch 1 claimed under epoch 0's nonce: the fold ends at its first header
+    st = {k: (dict(v) if isinstance(v, dict) else v) for k, v in st0.items()}
+    wrong = epoch.copy()
+    wrong[k1:] = 0
+    v, stop, done = hctx.update_chain_dep_state(H, crypto, prev, st, ei, prev_is_genesis=genesis,
+                                                etas=[eta_a, eta_b], eta_idx=wrong)
+    assert done == k1 and stop == k1 and st["last_slot"] == int(H["slot"][k1 - 1])
+    with pytest.raises(abi.PraosError):          # an index past the table
+        bad = epoch.copy()
+        bad[3] = 7
+        hctx.update_chain_dep_state(H, crypto, prev, dict(st0), ei, prev_is_genesis=genesis,
+                                    etas=[eta_a, eta_b], eta_idx=bad)
+
+
 def test_host_only_refuses_gpu_calls(hctx):
     from praos_hip import abi
     r = random.Random(9)
