@@ -103,7 +103,7 @@ FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], co
   sc_recode16(hw, h);
   sc_recode256(sw, s);
   ge_p1p1 x;
-  straus<64, 64, 0, 32, false>(x, tab, hw, nullptr, nullptr, btab, sw);   // [s]B - [h]A
+  STRAUS<64, 64, 0, 32, false>(x, tab, hw, nullptr, nullptr, btab, sw);   // [s]B - [h]A
   ge_p2 Rp;
   ge_p1p1_to_p2(Rp, x);
   uint32_t enc[8];
@@ -129,7 +129,7 @@ FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], c
   sc_recode16(hw, h);
   sc_recode256(sw, s);
   ge_p1p1 x;
-  straus_chunked<4, false>(x, ktab, hw, btab, sw);   // [s]B - [h]A, 16-window chain
+  STRAUS_CHUNKED<4, false>(x, ktab, hw, btab, sw);   // [s]B - [h]A, 16-window chain
   ge_p2 Rp;
   ge_p1p1_to_p2(Rp, x);
   uint32_t enc[8];
@@ -378,7 +378,7 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
     sc_recode16(cw, c);
     sc_recode256(sw, s);
     ge_p1p1 x;
-    straus_chunked<2, true>(x, ktab, cw, btab, sw);
+    STRAUS_CHUNKED<2, true>(x, ktab, cw, btab, sw);
     ge_p1p1_to_p2(U, x);
   } else {  // U = [s]B - [c]Y
     ge_p3 nY = Y;
@@ -390,7 +390,7 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
     sc_recode16(cw, c);
     sc_recode256(sw, s);
     ge_p1p1 x;
-    straus<33, 33, 0, 16, true>(x, ty, cw, nullptr, nullptr, btab, sw);
+    STRAUS<33, 33, 0, 16, true>(x, ty, cw, nullptr, nullptr, btab, sw);
     ge_p1p1_to_p2(U, x);
   }
   {  // V = [s]H - [c]Gamma
@@ -405,7 +405,7 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
     sc_recode16(sw, s);
     sc_recode16(cw, c);
     ge_p1p1 x;
-    straus<64, 64, 33, 0, false>(x, th, sw, tg, cw, nullptr, nullptr);
+    STRAUS<64, 64, 33, 0, false>(x, th, sw, tg, cw, nullptr, nullptr);
     ge_p1p1_to_p2(V, x);
   }
   // 8 Gamma

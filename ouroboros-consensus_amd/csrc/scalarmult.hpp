@@ -169,6 +169,89 @@ FE_INLINE void straus(ge_p1p1& out, const ge_cached* tp, uint32_t pw[8], const g
   out = x;
 }
 
+// ---------------------------------------------------------------- rolled chains
+// The same schedules with every group operation emitted ONCE per chain: the 4
+// doublings of a window are a runtime loop, and so are the per-lane-table
+// terms and the fixed-base terms of a window (their digits and tables picked
+// by the uniform loop index).  A fully unrolled window of the V chain is ~60 KB
+// of code -- the size of the instruction cache two CUs share -- and the
+// OCert / KES / VRF kernels run concurrently, so waves stalled on instruction
+// fetch (SQ_WAIT_INST_ANY ~19 % of k_vrf_ck's wave cycles).  Rolled, a chain's
+// working set is one doubling + one addition + one mixed addition (~25 KB).
+// Operation counts and results are identical to straus / straus_chunked.
+#ifndef PRAOS_ROLLED
+#define PRAOS_ROLLED 1
+#endif
+
+// x <- 16 x (4 doublings; p1p1 in and out)
+FE_INLINE void dbl4_rolled(ge_p1p1& x) {
+#pragma clang loop unroll(disable)
+  for (int k = 0; k < 4; k++) {
+    ge_p2 q;
+    ge_p1p1_to_p2(q, x);
+    ge_p2_dbl(x, q);
+  }
+}
+FE_INLINE void add_cached_p1p1(ge_p1p1& x, const ge_cached& c) {
+  ge_p3 a3;
+  ge_p1p1_to_p3(a3, x);
+  ge_add(x, a3, c);
+}
+FE_INLINE void add_niels_p1p1(ge_p1p1& x, const ge_niels& n) {
+  ge_p3 a3;
+  ge_p1p1_to_p3(a3, x);
+  ge_madd(x, a3, n);
+}
+
+template <int NWIN, int NP, int NQ, int NB, bool TWO_B>
+FE_INLINE void straus_rolled(ge_p1p1& out, const ge_cached* tp, uint32_t pw[8], const ge_cached* tq,
+                             uint32_t qw[8], const ge_niels* __restrict__ btab, uint32_t fw[8]) {
+  static_assert(NWIN >= 1 && NWIN <= 64 && NP <= NWIN && NQ <= NP, "window counts (terms ordered NQ <= NP)");
+  static_assert(NB == 0 || (NB == 32 && !TWO_B) || (NB == 16 && TWO_B), "fixed-base layout");
+  static_assert(NB == 0 || 2 * (NB - 1) <= NWIN - 1, "fixed-base bytes beyond the chain");
+  static_assert(NB == 0 || NWIN - 1 <= 2 * NB, "chain starts above the top fixed-base byte");
+  if constexpr (NP > 0) shl_const<8, 4 * (64 - NWIN)>(pw);
+  if constexpr (NQ > 0) shl_const<8, 4 * (64 - NWIN)>(qw);
+  ge_p1p1 x;
+  ge_p1p1_identity(x);
+#pragma clang loop unroll(disable)
+  for (int j = NWIN - 1; j >= 0; j--) {
+    if (j != NWIN - 1) dbl4_rolled(x);
+    if constexpr (NP > 0) {
+      const int nt = (NQ > 0 && j < NQ) ? 2 : (j < NP ? 1 : 0);
+#pragma clang loop unroll(disable)
+      for (int t = 0; t < nt; t++) {
+        uint32_t top = pw[7];
+        if constexpr (NQ > 0) top = t == 0 ? pw[7] : qw[7];
+        ge_cached c;
+        select_cached(c, (NQ > 0 && t != 0) ? tq : tp, (int)(top >> 28) - 8);
+        add_cached_p1p1(x, c);
+      }
+      shl_small<8, 4>(pw);
+      if constexpr (NQ > 0) shl_small<8, 4>(qw);
+    }
+    if constexpr (NB > 0) {
+      if ((j & 1) == 0 && (j >> 1) < NB) {
+        constexpr int NT2 = TWO_B ? 2 : 1;
+#pragma clang loop unroll(disable)
+        for (int t = 0; t < NT2; t++) {
+          const uint32_t top = TWO_B ? (t == 0 ? fw[3] : fw[7]) : fw[7];
+          ge_niels nb;
+          select_niels(nb, btab + BTAB_N * t, (int)(top >> 24) - 128);
+          add_niels_p1p1(x, nb);
+        }
+        if constexpr (TWO_B) {
+          shl_small<4, 8>(fw);
+          shl_small<4, 8>(fw + 4);
+        } else {
+          shl_small<8, 8>(fw);
+        }
+      }
+    }
+  }
+  out = x;
+}
+
 // R = [s]B (fixed base only), s < 2^253 (reduce mod L first)
 FE_INLINE void ge_scalarmult_base(ge_p3& R, const uint32_t s[8], const ge_niels* __restrict__ btab) {
   uint32_t fw[8];
@@ -251,6 +334,57 @@ FE_INLINE void straus_chunked(ge_p1p1& out, const ge_cached* __restrict__ ktab, 
   }
   out = x;
 }
+
+// word 2k+1 of w for a uniform runtime k < N (a select chain; no dynamic register index)
+template <int N>
+FE_INLINE uint32_t odd_word(const uint32_t w[8], int k) {
+  uint32_t r = w[1];
+  if constexpr (N > 1) r = k == 1 ? w[3] : r;
+  if constexpr (N > 2) r = k == 2 ? w[5] : r;
+  if constexpr (N > 3) r = k == 3 ? w[7] : r;
+  return r;
+}
+
+// straus_chunked with each group operation emitted once (see straus_rolled)
+template <int NPC, bool P_TOP>
+FE_INLINE void straus_chunked_rolled(ge_p1p1& out, const ge_cached* __restrict__ ktab, uint32_t pw[8],
+                                     const ge_niels* __restrict__ btab, uint32_t fw[8]) {
+  static_assert(NPC >= 1 && NPC + (P_TOP ? 1 : 0) <= KT_CHUNKS, "chunk count");
+  const int dtop = P_TOP ? (int)(pw[2 * NPC] & 15u) - 8 : 0;
+  ge_p1p1 x;
+  ge_p1p1_identity(x);
+#pragma clang loop unroll(disable)
+  for (int m = 15; m >= 0; m--) {
+    if (m != 15) dbl4_rolled(x);
+    const int nt = NPC + ((P_TOP && m == 0) ? 1 : 0);
+#pragma clang loop unroll(disable)
+    for (int k = 0; k < nt; k++) {
+      const int d = k < NPC ? (int)(odd_word<NPC>(pw, k) >> 28) - 8 : dtop;
+      ge_cached c;
+      select_cached(c, ktab + 8 * k, d);
+      add_cached_p1p1(x, c);
+    }
+    shl64_chunks<2 * NPC, 4>(pw);
+    if ((m & 1) == 0) {
+#pragma clang loop unroll(disable)
+      for (int k = 0; k < 4; k++) {
+        ge_niels nb;
+        select_niels(nb, btab + BTAB_N * k, (int)(odd_word<4>(fw, k) >> 24) - 128);
+        add_niels_p1p1(x, nb);
+      }
+      shl64_chunks<8, 8>(fw);
+    }
+  }
+  out = x;
+}
+
+#if PRAOS_ROLLED
+#define STRAUS straus_rolled
+#define STRAUS_CHUNKED straus_chunked_rolled
+#else
+#define STRAUS straus
+#define STRAUS_CHUNKED straus_chunked
+#endif
 
 // ktab[8k + j] = (j+1) 2^(64k) P for k < nchunks (global memory)
 FE_INLINE void build_key_tables(ge_cached* __restrict__ ktab, const ge_p3& P, int nchunks) {
