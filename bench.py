@@ -339,6 +339,8 @@ def main():
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
     ap.add_argument("--keycache", type=int, default=2,
                     help="min uses of a public key for the per-batch key cache (0 = off)")
+    ap.add_argument("--dedup", type=int, default=1,
+                    help="verify each distinct OCert tuple once per batch (PRAOS_OPT_DEDUP; 0 = off)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     if args.scaling == "strong" and args.config not in ("c1", "c5"):
@@ -367,6 +369,7 @@ def main():
     ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
     ctx.set_option(abi.OPT_KERNELS, cfg["kernels"])
     ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
+    ctx.set_option(abi.OPT_DEDUP, args.dedup)
     t0 = time.perf_counter()
     H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank, world)
     n = len(H["slot"])
@@ -405,6 +408,24 @@ def main():
     kser /= 3
     ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
     kst = ctx.batch_stats(b)
+    dds = ctx.dedup_stats(b)
+    # the same steps with the OCert dedup off (every header's OCert signature verified
+    # on its own), reported beside the headline for transparency
+    nodedup = None
+    if args.dedup and cfg["kernels"] & 1:
+        ctx.set_option(abi.OPT_DEDUP, 0)
+        ctx.run(b)
+        ctx.sync()
+        torch.cuda.synchronize()
+        t0n = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.run(b)
+            ctx.sync()
+        torch.cuda.synchronize()
+        nodedup = n * args.steps / (time.perf_counter() - t0n)
+        ctx.set_option(abi.OPT_DEDUP, args.dedup)
+        ctx.run(b)
+        ctx.sync()
     out = ctx.download(b, n)
     ctx.free(b)
     # end to end through the blocking entry point: host SoA in, H2D, all kernels,
@@ -460,6 +481,8 @@ def main():
             "vrf": kst["vrf_hits"] * W_VRF_CK + kst["vrf_misses"] * W_VRF + kst["vrf_keys"] * W_KEY_VRF}
     if args.keycache == 0:
         work["ocert"], work["vrf"], work["kes"] = n * W_OCERT, n * W_VRF, n * W_KES
+        if dds["ocert_unique"]:
+            work["ocert"] = dds["ocert_unique"] * W_OCERT
     dominant = max(ran, key=lambda k: per_kernel[k])
     wk = work[dominant] / n
     dom_achieved = work[dominant] / (per_kernel[dominant] * 1e-3)
@@ -497,6 +520,10 @@ def main():
                                               f"(femul microbench, {os.path.relpath(FEMUL_FILE, ROOT)})")
                                              if iw_peak else None},
         "keycache": dict(kst, min_uses=args.keycache),
+        "ocert_dedup": {"on": bool(args.dedup), "distinct_ocerts_verified": dds["ocert_unique"], "headers": n,
+                        "value_without_dedup": round(nodedup, 1) if nodedup else None,
+                        "note": "each distinct (cold vk, hot vk, n, c0, sigma) tuple of a batch is verified once "
+                                "and its verdict copied to every header carrying the same bytes (PRAOS_OPT_DEDUP)"},
         "self_check": {"clean": int(clean.sum()), "clean_ok": clean_ok, "corrupted": int((~clean).sum()),
                        "corrupted_rejected": corrupt_caught, "corrupted_in_checked_fields": int(rel.sum()),
                        "corrupted_in_checked_fields_rejected": corrupt_caught_rel,

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 7
+#define PRAOS_ABI_VERSION 8
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -186,12 +186,22 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * windows long instead of 64 (k_keys.hip).  0 disables the cache.  Verdicts
  * are identical either way (keys are matched byte for byte). */
 #define PRAOS_OPT_KEYCACHE 3
+/* PRAOS_OPT_DEDUP (default 1): the OCert signature check (Praos.hs:580) depends only
+ * on the 144 bytes (cold vk, hot vk, n, c0, sigma); a pool forges every header of an
+ * epoch under one operational certificate, so each distinct tuple of a batch is
+ * verified once (tuples compared byte for byte on the device) and its verdict is
+ * copied to every header carrying the same bytes; the KES-period checks stay per
+ * header.  Verdicts are identical either way. */
+#define PRAOS_OPT_DEDUP 4
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items
  * uncached; out[3..5] = the same for VRF keys; out[6..8] for the KES leaf keys
  * (the Ed25519 key each Sum6KES signature ends on).  Returns 0. */
 int praos_batch_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[9]);
+/* OCert dedup of the last praos_batch_run: out[0] = distinct OCert tuples verified,
+ * out[1] = headers (out[0] = 0 when the dedup did not run).  Returns 0. */
+int praos_batch_dedup_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[2]);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
  * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run, 5 = header
  * decode (batches from praos_batch_upload_bytes; 0 otherwise).  With concurrent

@@ -83,7 +83,7 @@ foreign import ccall safe "praos_replay_immutable" c_replay_immutable
   -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 7
+abiVersion = 8
 
 -- ---------------------------------------------------------------- context
 

@@ -26,10 +26,13 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t k[8]) {
   return h;
 }
 
-__global__ void k_key_insert(size_t n, const uint8_t* __restrict__ keys, uint32_t mask, uint32_t* slot_rep,
+// Items: i in [0, n), or list[0 .. *count) (e.g. the distinct OCerts of k_ocert_dedup).
+__global__ void k_key_insert(size_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                             const uint8_t* __restrict__ keys, uint32_t mask, uint32_t* slot_rep,
                              uint32_t* slot_cnt, int32_t* __restrict__ item_slot) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (list ? (size_t)*count : n)) return;
+  const size_t i = list ? list[t] : t;
   uint32_t k[8];
   load_words(k, keys + 32 * i, 8);
   uint32_t h = key_hash(k) & mask;
@@ -81,12 +84,14 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t*
   }
 }
 
-__global__ void k_key_partition(size_t n, const int32_t* __restrict__ item_slot, const int32_t* __restrict__ slot_entry,
+__global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                const int32_t* __restrict__ item_slot, const int32_t* __restrict__ slot_entry,
                                 int32_t* __restrict__ item_entry, uint32_t* __restrict__ entry_pos,
                                 uint32_t* __restrict__ hit_list, uint32_t* __restrict__ miss_list,
                                 uint32_t* counters) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = i < n;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = t < (list ? (size_t)*count : n);   // every lane stays for the ballots
+  const size_t i = in ? (list ? list[t] : t) : 0;
   const int32_t e = in ? slot_entry[item_slot[i]] : -1;
   if (in) item_entry[i] = e;
   if (in && e >= 0) hit_list[atomicAdd(&entry_pos[e], 1u)] = (uint32_t)i;
@@ -131,10 +136,78 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
   build_key_tables(ktab + (size_t)e * KT_STRIDE, P, kind == 0 ? 4 : 3);
 }
 
+// ---- OCert signature dedup (PRAOS_OPT_DEDUP)
+// The OCert signature check depends only on (cold vk, hot vk, n, c0, sigma)
+// (Praos.hs:580): every header a pool forges under one operational certificate
+// carries the same 144 bytes, so a mainnet-shaped epoch has ~one distinct OCert
+// per pool.  k_ocert_dedup keys a hash set on the whole tuple, compared byte for
+// byte; the first item of each distinct tuple (its representative) is verified
+// and k_ocert_fanout copies that verdict to every item carrying identical bytes,
+// adding each header's own KES-period checks (which depend on its slot).
+struct OcertTuple { uint32_t w[36]; };   // cold 8 | hot 8 | n 2 | c0 2 | sigma 16
+__device__ __forceinline__ void ocert_tuple(OcertTuple& t, const uint8_t* cold, const uint8_t* hot, const uint64_t* on,
+                                            const uint64_t* oc, const uint8_t* sig, size_t i) {
+  load_words(t.w, cold + 32 * i, 8);
+  load_words(t.w + 8, hot + 32 * i, 8);
+  const uint64_t n = on[i], c0 = oc[i];
+  t.w[16] = (uint32_t)n; t.w[17] = (uint32_t)(n >> 32);
+  t.w[18] = (uint32_t)c0; t.w[19] = (uint32_t)(c0 >> 32);
+  load_words(t.w + 20, sig + 64 * i, 16);
+}
+
+// counters[0] = distinct tuples (representatives, listed in reps)
+__global__ void k_ocert_dedup(size_t n, const uint8_t* __restrict__ cold, const uint8_t* __restrict__ hot,
+                              const uint64_t* __restrict__ on, const uint64_t* __restrict__ oc,
+                              const uint8_t* __restrict__ sig, uint32_t mask, uint32_t* slot_rep,
+                              uint32_t* __restrict__ item_rep, uint32_t* __restrict__ reps, uint32_t* counters) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n;                              // every lane stays for the ballot
+  bool rep = false;
+  if (in) {
+    OcertTuple t;
+    ocert_tuple(t, cold, hot, on, oc, sig, i);
+    uint32_t h = t.w[0] * 0x9E3779B1u;
+    h ^= t.w[9] + 0x7F4A7C15u + (h << 6) + (h >> 2);
+    h ^= t.w[16] + (h << 6) + (h >> 2);
+    h ^= t.w[20] + (h << 6) + (h >> 2);
+    h ^= t.w[27] + (h << 6) + (h >> 2);
+    h &= mask;
+    uint32_t r = (uint32_t)i;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+      const uint32_t cur = atomicCAS(&slot_rep[h], 0u, (uint32_t)i + 1u);
+      if (cur == 0u) { rep = true; break; }           // first of its tuple
+      OcertTuple o;
+      ocert_tuple(o, cold, hot, on, oc, sig, cur - 1u);
+      bool same = true;
+#pragma unroll
+      for (int q = 0; q < 36; q++) same &= o.w[q] == t.w[q];
+      if (same) { r = cur - 1u; break; }
+      h = (h + 1u) & mask;
+    }
+    item_rep[i] = r;
+  }
+  wave_append(rep, (uint32_t)i, &counters[0], reps);
+}
+
+// bits[i] = verdict of i's representative (ok[rep] written by the verify kernels in
+// ok_out mode) + i's own KES-period checks (Praos.hs:567-568, 596-599)
+__global__ void k_ocert_fanout(size_t n, const uint32_t* __restrict__ item_rep, const uint8_t* __restrict__ ok,
+                               const uint64_t* __restrict__ slot, const uint64_t* __restrict__ oc,
+                               uint64_t slots_per_kes_period, uint64_t max_kes_evo, uint16_t* __restrict__ bits) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint16_t b = ok[item_rep[i]] ? 0 : PRAOS_BIT_OCERT_SIG;
+  const uint64_t c0 = oc[i];
+  const uint64_t kp = slot[i] / slots_per_kes_period;
+  if (!(c0 <= kp)) b |= PRAOS_BIT_KES_BEFORE_START;
+  if (!(kp < c0 + max_kes_evo)) b |= PRAOS_BIT_KES_AFTER_END;
+  bits[i] = b;
+}
+
 // ---- host launchers
-void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* keys, uint32_t mask,
-                       uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot) {
-  hipLaunchKernelGGL(k_key_insert, grid, block, 0, stream, n, keys, mask, slot_rep, slot_cnt, item_slot);
+void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                       const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot) {
+  hipLaunchKernelGGL(k_key_insert, grid, block, 0, stream, n, list, count, keys, mask, slot_rep, slot_cnt, item_slot);
 }
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
@@ -142,15 +215,28 @@ void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, 
   hipLaunchKernelGGL(k_key_assign, grid, block, 0, stream, cap, slot_rep, slot_cnt, min_count, max_entries, slot_entry,
                      entry_rep, entry_pos, counters);
 }
-void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const int32_t* item_slot,
-                          const int32_t* slot_entry, int32_t* item_entry, uint32_t* entry_pos, uint32_t* hit_list,
-                          uint32_t* miss_list, uint32_t* counters) {
-  hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, item_slot, slot_entry, item_entry, entry_pos,
-                     hit_list, miss_list, counters);
+void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list,
+                          const uint32_t* count, const int32_t* item_slot, const int32_t* slot_entry,
+                          int32_t* item_entry, uint32_t* entry_pos, uint32_t* hit_list, uint32_t* miss_list,
+                          uint32_t* counters) {
+  hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, list, count, item_slot, slot_entry, item_entry,
+                     entry_pos, hit_list, miss_list, counters);
 }
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
                            uint32_t* kinfo) {
   hipLaunchKernelGGL(k_key_precompute, grid, block, 0, stream, kind, counters, max_entries, entry_rep, keys, ktab,
                      kinfo);
+}
+void launch_ocert_dedup(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* cold, const uint8_t* hot,
+                        const uint64_t* on, const uint64_t* oc, const uint8_t* sig, uint32_t mask, uint32_t* slot_rep,
+                        uint32_t* item_rep, uint32_t* reps, uint32_t* counters) {
+  hipLaunchKernelGGL(k_ocert_dedup, grid, block, 0, stream, n, cold, hot, on, oc, sig, mask, slot_rep, item_rep, reps,
+                     counters);
+}
+void launch_ocert_fanout(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* item_rep,
+                         const uint8_t* ok, const uint64_t* slot, const uint64_t* oc, uint64_t slots_per_kes_period,
+                         uint64_t max_kes_evo, uint16_t* bits) {
+  hipLaunchKernelGGL(k_ocert_fanout, grid, block, 0, stream, n, item_rep, ok, slot, oc, slots_per_kes_period,
+                     max_kes_evo, bits);
 }

@@ -93,6 +93,7 @@ struct praos_ctx {
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
+  int dedup = 1;                                       // PRAOS_OPT_DEDUP
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -200,6 +201,12 @@ struct praos_batch {
   } kc[3];                       // [2] KES leaf keys
   uint8_t* kes_leaf = nullptr;   // n*32: the leaf key of each header's KES signature
   bool kc_used = false;
+  // OCert dedup (k_keys.hip k_ocert_dedup): hash set over the 144-byte OCert tuple,
+  // representative per item, list of representatives, their verify results
+  uint32_t dd_cap = 0;
+  uint32_t *dd_slot = nullptr, *dd_item_rep = nullptr, *dd_reps = nullptr, *dd_counters = nullptr;
+  uint8_t* dd_ok = nullptr;
+  bool dd_used = false;
   // batches from stored bytes (praos_batch_upload_bytes): the arena and the
   // decoded HeaderBody fields beyond the SoA above (k_decode.hip)
   bool from_bytes = false;
@@ -436,6 +443,13 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   ok &= dalloc(b, (uint8_t**)&b->tab_kes, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_vrf, LT_VRF_B * n) == hipSuccess;
   ok &= dalloc(b, &b->kes_leaf, 32 * n) == hipSuccess;
+  b->dd_cap = 256;
+  while (b->dd_cap < 2 * n) b->dd_cap <<= 1;
+  ok &= dalloc(b, &b->dd_slot, 4 * (size_t)b->dd_cap) == hipSuccess;
+  ok &= dalloc(b, &b->dd_item_rep, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->dd_reps, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->dd_counters, 16) == hipSuccess;
+  ok &= dalloc(b, &b->dd_ok, n) == hipSuccess;
   for (auto& k : b->kc) {
     k.cap = 256;
     while (k.cap < 2 * n) k.cap <<= 1;
@@ -609,20 +623,46 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   const bool kc = c->keycache > 0 && n >= 2;
   b->kc_used = kc;
   // key cache prepass on the kernel's own stream: hash set, entries, hit/miss lists, tables
-  auto keycache_prepass = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) -> int {
+  // (items: all n, or list[0 .. *count) when list != null)
+  auto keycache_prepass = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st,
+                              const uint32_t* list = nullptr, const uint32_t* count = nullptr) -> int {
     HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
     HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
     HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
-    launch_key_insert(g, blk, st, n, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
+    launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
     launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)c->keycache,
                       k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
-    launch_key_partition(g, blk, st, n, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit, k.miss,
-                         k.counters);
+    launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit,
+                         k.miss, k.counters);
     launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries,
                           k.entry_rep, keys, k.ktab, k.kinfo);
     return PRAOS_OK;
   };
-  if (c->kernels & 1) {
+  b->dd_used = false;
+  if ((c->kernels & 1) && c->dedup && n >= 2) {
+    // distinct OCert tuples only; their verdicts fan out to every header carrying them
+    b->dd_used = true;
+    HIPCHK(c, hipMemsetAsync(b->dd_slot, 0, 4 * (size_t)b->dd_cap, so));
+    HIPCHK(c, hipMemsetAsync(b->dd_counters, 0, 16, so));
+    launch_ocert_dedup(g, blk, so, n, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->dd_cap - 1,
+                       b->dd_slot, b->dd_item_rep, b->dd_reps, b->dd_counters);
+    if (kc) {
+      praos_batch::KeyCache& k = b->kc[0];
+      int r = keycache_prepass(k, b->cold_vk, 0, so, b->dd_reps, b->dd_counters);
+      if (r != PRAOS_OK) return r;
+      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
+                      b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
+                      P.max_kes_evo, bo, b->dd_ok);
+      launch_ocert(g, blk, so, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
+    } else {
+      launch_ocert(g, blk, so, n, b->dd_reps, b->dd_counters, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
+                   b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
+                   b->tab_ocert);
+    }
+    launch_ocert_fanout(g, blk, so, n, b->dd_item_rep, b->dd_ok, b->slot, b->ocert_c0, P.slots_per_kes_period,
+                        P.max_kes_evo, bo);
+  } else if (c->kernels & 1) {
     if (kc) {
       praos_batch::KeyCache& k = b->kc[0];
       int r = keycache_prepass(k, b->cold_vk, 0, so);
@@ -802,11 +842,23 @@ int praos_batch_stats(praos_ctx* c, praos_batch* b, uint32_t out[9]) {
   return PRAOS_OK;
 }
 
+int praos_batch_dedup_stats(praos_ctx* c, praos_batch* b, uint32_t out[2]) {
+  if (!c || !b || !out) return PRAOS_E_ARG;
+  out[0] = 0;
+  out[1] = (uint32_t)b->n;
+  if (!b->dd_used) return PRAOS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, b->dd_counters, 4, hipMemcpyDeviceToHost));
+  return PRAOS_OK;
+}
+
 int praos_set_option(praos_ctx* c, int opt, int value) {
   if (!c) return PRAOS_E_ARG;
   if (opt == PRAOS_OPT_CONCURRENT) { c->concurrent = value != 0; return PRAOS_OK; }
   if (opt == PRAOS_OPT_KERNELS) { c->kernels = value & 7; return PRAOS_OK; }
   if (opt == PRAOS_OPT_KEYCACHE) { c->keycache = value < 0 ? 0 : value; return PRAOS_OK; }
+  if (opt == PRAOS_OPT_DEDUP) { c->dedup = value != 0; return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 

@@ -166,6 +166,7 @@ SIGNATURES = {
     "praos_batch_kernel_ms": (ctypes.c_float, [ctypes.c_void_p, ctypes.c_int]),
     "praos_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "praos_batch_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u32p]),
+    "praos_batch_dedup_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u32p]),
     "praos_verify_ocert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u8p, u64p, u64p, u8p, u8p]),
     "praos_verify_kes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u8p, u32p, u8p, u64p, u32p, u8p,
                                         ctypes.c_size_t, u8p]),
@@ -268,7 +269,7 @@ def ptr(a, t=u8p):
     return a.ctypes.data_as(t)
 
 
-OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE = 1, 2, 3     # praos_set_option (include/praos_hip.h)
+OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP = 1, 2, 3, 4     # praos_set_option (include/praos_hip.h)
 
 
 class PraosError(RuntimeError):
@@ -407,6 +408,12 @@ class Context:
         return {"cold_keys": int(out[0]), "cold_hits": int(out[1]), "cold_misses": int(out[2]),
                 "vrf_keys": int(out[3]), "vrf_hits": int(out[4]), "vrf_misses": int(out[5]),
                 "kes_keys": int(out[6]), "kes_hits": int(out[7]), "kes_misses": int(out[8])}
+
+    def dedup_stats(self, b):
+        """OCert dedup of the last run: distinct OCert tuples verified, headers."""
+        out = np.zeros(2, np.uint32)
+        self.check(self.L.praos_batch_dedup_stats(self.h, b, ptr(out, u32p)))
+        return {"ocert_unique": int(out[0]), "headers": int(out[1])}
 
     def kernel_ms(self, which):
         return float(self.L.praos_batch_kernel_ms(self.h, which))

@@ -137,11 +137,16 @@ def test_c5_shaped_batch(ctx, oracle):
     ctx.sync()
     o = ctx.download(b, n)
     st = ctx.batch_stats(b)
+    dd = ctx.dedup_stats(b)
     ctx.free(b)
     clean = corrupted == 0
     assert int((o["bits"][clean] != 0).sum()) == 0
     assert int((o["bits"][~clean] == 0).sum()) == 0
-    assert st["cold_hits"] + st["cold_misses"] == n and st["cold_keys"] > 2000
+    # OCert dedup: ~one distinct OCert per pool (+ the corrupted ones); the cold-key
+    # cache sees only those; the VRF key cache sees every header
+    assert dd["headers"] == n and 2000 < dd["ocert_unique"] < 4000, dd
+    assert st["cold_hits"] + st["cold_misses"] == dd["ocert_unique"]
+    assert st["vrf_hits"] + st["vrf_misses"] == n and st["vrf_keys"] > 2000
     assert list(o["pool_idx"][clean]) == list(sched[1][:n][clean])
     c_raw = fixed.active_slot_log(cfg["f"])
     ep = oracle.make_epoch(cfg["eta0"], cfg["slots_per_kes_period"], cfg["max_kes_evo"], c_raw, pool_list)

@@ -62,19 +62,22 @@ def test_synth_chain_parity(ctx, oracle):
     assert any(corrupted) and any(int(o["bits"][i]) != 0 for i in range(len(ref)) if corrupted[i])
 
 
-def _run_batch(ctx, H, keycache):
+def _run_batch(ctx, H, keycache, dedup=0, want_dedup_stats=False):
     from praos_hip import abi
     ctx.set_option(abi.OPT_KEYCACHE, keycache)
+    ctx.set_option(abi.OPT_DEDUP, dedup)
     try:
         b = ctx.upload(H)
         ctx.run(b)
         ctx.sync()
         st = ctx.batch_stats(b)
+        dd = ctx.dedup_stats(b)
         o = ctx.download(b, len(H["slot"]))
         ctx.free(b)
     finally:
         ctx.set_option(abi.OPT_KEYCACHE, 2)
-    return o, st
+        ctx.set_option(abi.OPT_DEDUP, 1)
+    return (o, st, dd) if want_dedup_stats else (o, st)
 
 
 def test_keycache_equivalence(ctx, oracle):
@@ -213,3 +216,40 @@ def test_chain_dep_state_fold_gpu(ctx):
     wv, wstop, wdone = cs.fold(ref, hk, H["slot"], o["bits"], H["ocert_n"], o["nonce"], [bytes(x) for x in prev],
                                {q[0] for q in pool_list}, eta0, base, 0, 432000, 129600)
     assert (done, stop) == (wdone, wstop) and list(v) == wv and st == ref
+
+
+def test_ocert_dedup_equivalence(ctx, oracle):
+    """OCert dedup (PRAOS_OPT_DEDUP, k_keys.hip k_ocert_dedup / k_ocert_fanout): every
+    header's outputs are identical with and without it, with and without the key
+    cache -- including invalid tuples repeated over several headers, and headers
+    sharing a tuple whose KES-period checks differ (slot-dependent, per header)."""
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 1500, 23, 1500, seed=b"\x5a" * 32)
+    bad = [i for i in range(1500) if corrupted[i]]
+    assert bad
+    # an invalid OCert signature carried by five headers (copies of one tuple)
+    src = 100
+    H["ocert_sig"][src][3] ^= 0x40
+    for j in range(101, 105):
+        for f in ("cold_vk", "hot_vk", "ocert_sig"):
+            H[f][j] = H[f][src]
+        H["ocert_n"][j] = H["ocert_n"][src]
+        H["ocert_c0"][j] = H["ocert_c0"][src]
+    # a header sharing its pool's tuple, in a KES period past the OCert's end
+    H["slot"][201] = int(H["slot"][201]) + 129600 * 70
+    outs = {}
+    for kc in (2, 0):
+        for dd in (1, 0):
+            outs[(kc, dd)] = _run_batch(ctx, H, kc, dedup=dd, want_dedup_stats=True)
+    o_ref = outs[(0, 0)][0]
+    for key, (o, st, d) in outs.items():
+        for f in ("bits", "beta", "leader", "nonce", "pool_idx"):
+            assert np.array_equal(o[f], o_ref[f]), (key, f)
+        if key[1]:
+            assert d["headers"] == 1500 and 23 <= d["ocert_unique"] < 400, d
+        else:
+            assert d["ocert_unique"] == 0
+    assert all(int(o_ref["bits"][j]) & 0x0004 for j in range(100, 105))
+    assert int(o_ref["bits"][201]) & 0x0002
+    ref = _oracle_bits(oracle, H, pool_list, c_raw, eta0)
+    for i, r in enumerate(ref):
+        assert int(o_ref["bits"][i]) & BITS_FROM_ORACLE == r["bits"], (i, hex(o_ref["bits"][i]), hex(r["bits"]))
