@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 8
+#define PRAOS_ABI_VERSION 9
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -68,6 +68,14 @@ extern "C" {
 /* TPraos (praos_verify_tpraos_headers) reuses bits 0-4, 8, 9, 12 and replaces 10/11: */
 #define PRAOS_BIT_TP_VRF_NONCE       0x0400u /* VRFKeyBadNonce (eta cert: proof or output) */
 #define PRAOS_BIT_TP_VRF_LEADER      0x0800u /* VRFKeyBadLeaderValue (leader cert) */
+/* ... and, with an overlay schedule (praos_set_overlay, d > 0): */
+#define PRAOS_BIT_TP_OVERLAY         0x2000u /* informational: an ACTIVE overlay slot (genesis delegate's
+                                                slot); bits 8/9 then mean the two bits below and no
+                                                pool lookup or leader test applies */
+#define PRAOS_BIT_TP_GEN_COLD        0x0100u /* (with TP_OVERLAY) WrongGenesisColdKeyOVERLAY */
+#define PRAOS_BIT_TP_GEN_VRF         0x0200u /* (with TP_OVERLAY) WrongGenesisVRFKeyOVERLAY */
+#define PRAOS_BIT_TP_NOT_ACTIVE      0x4000u /* NotActiveSlotOVERLAY (an overlay slot nobody may fill;
+                                                no VRF check is made) */
 
 /* ---- verdict codes of praos_apply_batch (first failing check, Praos.hs order) ---- */
 enum praos_verdict {
@@ -325,6 +333,40 @@ typedef struct {
 } praos_tpraos_out;
 int praos_verify_tpraos_headers(praos_ctx* ctx, const praos_tpraos_headers* h, praos_tpraos_out* out);
 
+/* ---- TPraos decentralisation overlay (d > 0; Shelley..Alonzo before d reached 0) ----
+ * cardano-protocol-tpraos OVERLAY (lookupInOverlaySchedule, the same call
+ * TPraos.checkIsLeader makes at TPraos.hs:304-337): with s = slot - first slot of its
+ * epoch, the slot is in the overlay schedule iff ceiling(s d) < ceiling((s + 1) d);
+ * then position = ceiling(s d) is active iff position mod ascInv == 0 (ascInv =
+ * floor(1 / f)), and its genesis key is the (position div ascInv) mod |genDelegs|-th
+ * of the genesis key hashes in ascending byte order.  An active overlay slot must be
+ * forged by that key's delegate (WrongGenesisColdKeyOVERLAY) with the delegate's VRF
+ * key (WrongGenesisVRFKeyOVERLAY), both certificates verify (VRFKeyBadNonce /
+ * VRFKeyBadLeaderValue), and no leader-value test applies; a non-active overlay slot
+ * fails NotActiveSlotOVERLAY.  Other slots take the Praos checks (pool, VRF key,
+ * certificates, leader value).  The OCERT rule runs for every header; genesis
+ * delegates count as known issuers (currentIssueNo). */
+typedef struct {
+  uint8_t genesis_hash28[28];     /* KeyHash 'Genesis: a key of lvGenDelegs */
+  uint8_t delegate_hash28[28];    /* genDelegKeyHash: the delegate's cold-key hash */
+  uint8_t vrf_hash32[32];         /* genDelegVrfHash */
+} praos_gen_deleg;
+typedef struct {
+  uint64_t d_num, d_den;          /* lvD, a UnitInterval: d = d_num / d_den (d_den > 0, d_num <= d_den) */
+  uint64_t asc_num, asc_den;      /* activeSlotVal f = asc_num / asc_den (0 < f <= 1) */
+  uint64_t epoch_base_slot;       /* fixed-size epochs (first slot of the slot's epoch = epochInfoFirst) */
+  uint64_t epoch_length;
+  const praos_gen_deleg* gen_delegs;  /* any order (sorted by genesis hash inside) */
+  uint32_t n_gen_delegs;          /* > 0 when d > 0 */
+} praos_overlay;
+/* ov == NULL or d_num == 0: no overlay (the d = 0 behaviour).  Kept until replaced. */
+int praos_set_overlay(praos_ctx* ctx, const praos_overlay* ov);
+/* The schedule itself (host-side; host-only contexts too): cls[i] = -1 (not an overlay
+ * slot), -2 (NonActiveSlot) or k >= 0 (ActiveSlot of the k-th genesis key in ascending
+ * hash order). */
+int praos_overlay_classify(praos_ctx* ctx, size_t n, const uint64_t* slots, int32_t* cls);
+
+
 /* ---- single-primitive batches (configs C2-C4); outputs 1 = valid, 0 = invalid ---- */
 /* Ed25519 over the OCert signable hot_vk || BE64(n) || BE64(c0). */
 int praos_verify_ocert(praos_ctx* ctx, size_t n, const uint8_t* cold_vk, const uint8_t* hot_vk,
@@ -450,6 +492,43 @@ int praos_validate_headers_nonces(praos_ctx* ctx, const praos_headers* h, const 
                                   const praos_epoch_info* ei, praos_chain_state* st, const praos_nonce* etas,
                                   uint32_t k, const uint8_t* eta_idx, uint8_t* verdict, size_t* chain_stop,
                                   size_t* processed);
+
+/* ---- TPraos chain-dependent state: SL.tickChainDepState + SL.updateChainDepState
+ *      (TPraos.hs:361-387; cardano-protocol-tpraos TICKN, PRTCL = UPDN + OVERLAY + OCERT)
+ * The state has the Praos shape (praos_chain_state: counters = csProtocol's OCert map,
+ * evolving / candidate = eta_v / eta_c, epoch_nonce / last_epoch_block = TicknState eta_0 /
+ * eta_h, lab = csLabNonce).  Per header: tick on a new epoch: epoch_nonce := candidate ⭒
+ * last_epoch_block ⭒ extra_entropy, last_epoch_block := lab; the envelope (env != NULL;
+ * chainChecks are the Praos envelope checks); then the predicate failures of PRTCL,
+ * collected as the ledger's STS rules collect them (ValidateAll): OVERLAY's
+ * Either-chains (first failure within praosVrfChecks / pbftVrfChecks) plus every OCERT
+ * predicate, into failures[i] (PRAOS_TPF_*); verdict[i] = PRAOS_V_OK, PRAOS_V_ENV_*,
+ * PRAOS_V_INPUT or PRAOS_V_TPRAOS (failures[i] != 0).  On a valid header: eta_v :=
+ * eta_v ⭒ mkNonceFromOutputVRF(eta cert), eta_c := eta_v' if slot + window <
+ * firstSlotNextEpoch (ei->stability_window: the caller's UPDN window), lab :=
+ * prevHashToNonce prev, counters[hk] := n.  chain_stop / processed / state at the stop
+ * as praos_update_chain_dep_state. */
+#define PRAOS_V_TPRAOS 19
+#define PRAOS_TPF_KES_BEFORE_START  0x0001u /* KESBeforeStartOCERT */
+#define PRAOS_TPF_KES_AFTER_END     0x0002u /* KESAfterEndOCERT */
+#define PRAOS_TPF_OCERT_SIG         0x0004u /* InvalidSignatureOCERT */
+#define PRAOS_TPF_KES_SIG           0x0008u /* InvalidKesSignatureOCERT */
+#define PRAOS_TPF_COUNTER_MISSING   0x0010u /* NoCounterForKeyHashOCERT */
+#define PRAOS_TPF_COUNTER_TOO_SMALL 0x0020u /* CounterTooSmallOCERT */
+#define PRAOS_TPF_COUNTER_OVER_INC  0x0040u /* CounterOverIncrementedOCERT */
+#define PRAOS_TPF_VRF_KEY_UNKNOWN   0x0100u /* VRFKeyUnknown */
+#define PRAOS_TPF_VRF_KEY_WRONG     0x0200u /* VRFKeyWrongVRFKey */
+#define PRAOS_TPF_BAD_NONCE         0x0400u /* VRFKeyBadNonce */
+#define PRAOS_TPF_BAD_LEADER        0x0800u /* VRFKeyBadLeaderValue */
+#define PRAOS_TPF_LEADER_TOO_BIG    0x1000u /* VRFLeaderValueTooBig */
+#define PRAOS_TPF_NOT_ACTIVE        0x2000u /* NotActiveSlotOVERLAY */
+#define PRAOS_TPF_GEN_COLD          0x4000u /* WrongGenesisColdKeyOVERLAY */
+#define PRAOS_TPF_GEN_VRF           0x8000u /* WrongGenesisVRFKeyOVERLAY */
+int praos_tpraos_update_chain_dep_state(praos_ctx* ctx, const praos_tpraos_headers* h, const uint8_t* prev_hash,
+                                        const uint8_t* prev_is_genesis, const praos_tpraos_out* crypto,
+                                        praos_envelope* env, const praos_epoch_info* ei,
+                                        const praos_nonce* extra_entropy, praos_chain_state* st, uint8_t* verdict,
+                                        uint16_t* failures, size_t* chain_stop, size_t* processed);
 
 /* ---- chain replay from an ImmutableDB directory (db-analyser) ----
  * Replaces the per-block loop of DBAnalyser/Analysis.hs:815-847 (processAllImmutableDB

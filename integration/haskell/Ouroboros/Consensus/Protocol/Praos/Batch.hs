@@ -83,7 +83,7 @@ foreign import ccall safe "praos_replay_immutable" c_replay_immutable
   -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 8
+abiVersion = 9
 
 -- ---------------------------------------------------------------- context
 

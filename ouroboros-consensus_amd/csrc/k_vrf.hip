@@ -147,11 +147,16 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_ck(const uint32_t* __restric
 }
 
 
-// ------------------------------------------------------------------ TPraos VRF (d = 0)
+// ------------------------------------------------------------------ TPraos VRF
 // cardano-protocol-tpraos OVERLAY.praosVrfChecks: pool lookup, VRF key hash,
 // verifyCertified for the eta cert with mkSeed seedEta and for the leader cert
 // with mkSeed seedL (VRFKeyBadNonce / VRFKeyBadLeaderValue); the leader value is
 // the certified leader output itself (checked by k_leader with a 2^512 bound).
+// Overlay schedule (ovl_class != null, host-classified, praos_set_overlay): class -2
+// = NotActiveSlotOVERLAY (no VRF check); class k >= 0 = the k-th genesis key's slot:
+// pbftVrfChecks against its delegate (gen: delegate hash 7 words + pad | VRF hash 8)
+// -- cold-key hash and VRF-key hash compared, both certificates verified, no pool
+// and no leader test (pool_sorted = -1 makes k_leader skip the header).
 __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     size_t n, const ge_niels* __restrict__ gbtab, const uint8_t* __restrict__ cold_vk,
     const uint8_t* __restrict__ vrf_vk, const uint8_t* __restrict__ eta_out, const uint8_t* __restrict__ eta_proof,
@@ -160,7 +165,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
     const uint32_t* __restrict__ pool_vrf, const int32_t* __restrict__ pool_map, uint32_t npools, int check_output,
     uint16_t* __restrict__ bits, int32_t* __restrict__ pool_idx, int32_t* __restrict__ pool_sorted_idx,
     uint8_t* __restrict__ beta_eta, uint8_t* __restrict__ beta_l, uint8_t* __restrict__ nonce_out,
-    ge_cached* __restrict__ tabs) {
+    ge_cached* __restrict__ tabs, const int32_t* __restrict__ ovl_class, const uint32_t* __restrict__ gen) {
   if ((size_t)blockIdx.x * NT >= n) return;
   __shared__ ge_niels sbtab[2 * BTAB_N];
   const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
@@ -174,16 +179,34 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
   uint32_t cv[8], hk[8];
   load_words(cv, cold_vk + 32 * i, 8);
   blake2b_32(hk, cv, 28);
-  const int32_t sidx = pool_search(hk, pool_hash, npools);
-  if (sidx < 0) {
-    b |= PRAOS_BIT_VRF_KEY_UNKNOWN;
-  } else {
+  const int32_t cls = ovl_class ? ovl_class[i] : -1;
+  int32_t sidx = -1;
+  if (cls == -2) {
+    b |= PRAOS_BIT_TP_NOT_ACTIVE;                    // NotActiveSlotOVERLAY
+  } else if (cls >= 0) {                             // pbftVrfChecks vs the genesis delegate
+    b |= PRAOS_BIT_TP_OVERLAY;
+    const uint32_t* gd = gen + 16 * cls;
+    bool cold_ok = true, vrf_ok = true;
+#pragma unroll
+    for (int k = 0; k < 7; k++) cold_ok &= hk[k] == gd[k];
     uint32_t vh[8];
     blake2b_32(vh, pk, 32);
-    bool same = true;
 #pragma unroll
-    for (int k = 0; k < 8; k++) same &= vh[k] == pool_vrf[8 * sidx + k];
-    if (!same) b |= PRAOS_BIT_VRF_KEY_WRONG;
+    for (int k = 0; k < 8; k++) vrf_ok &= vh[k] == gd[8 + k];
+    if (!cold_ok) b |= PRAOS_BIT_TP_GEN_COLD;
+    if (!vrf_ok) b |= PRAOS_BIT_TP_GEN_VRF;
+  } else {
+    sidx = pool_search(hk, pool_hash, npools);
+    if (sidx < 0) {
+      b |= PRAOS_BIT_VRF_KEY_UNKNOWN;
+    } else {
+      uint32_t vh[8];
+      blake2b_32(vh, pk, 32);
+      bool same = true;
+#pragma unroll
+      for (int k = 0; k < 8; k++) same &= vh[k] == pool_vrf[8 * sidx + k];
+      if (!same) b |= PRAOS_BIT_VRF_KEY_WRONG;
+    }
   }
   const uint64_t s = slot[i];
   for (int cert = 0; cert < 2; cert++) {     // 0: eta (nonce) cert, 1: leader cert
@@ -202,7 +225,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_tp(
 #pragma unroll
     for (int k = 0; k < 16; k++) eq &= beta[k] == out[k];
     const uint16_t bad = cert ? PRAOS_BIT_TP_VRF_LEADER : PRAOS_BIT_TP_VRF_NONCE;
-    if (!ok || (check_output && !eq)) b |= bad;
+    if ((!ok || (check_output && !eq)) && cls != -2) b |= bad;
     store_words((cert ? beta_l : beta_eta) + 64 * i, beta, 16);
     if (cert == 0) {
       uint32_t nn[8];
@@ -244,8 +267,9 @@ void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge
                    const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
                    const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
                    int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta,
-                   uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs) {
+                   uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs, const int32_t* ovl_class,
+                   const uint32_t* gen) {
   hipLaunchKernelGGL(k_vrf_tp, grid, block, 0, stream, n, gbtab, cold_vk, vrf_vk, eta_out, eta_proof, l_out, l_proof,
                      slot, eta0, eta0_neutral, pool_hash, pool_vrf, pool_map, npools, check_output, bits, pool_idx,
-                     pool_sorted_idx, beta_eta, beta_l, nonce_out, tabs);
+                     pool_sorted_idx, beta_eta, beta_l, nonce_out, tabs, ovl_class, gen);
 }

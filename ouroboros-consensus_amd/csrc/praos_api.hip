@@ -20,6 +20,7 @@ static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBo
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -113,6 +114,13 @@ struct praos_ctx {
   uint32_t* d_eta0 = nullptr;
   std::vector<praos_pool> pools;     // caller order
   std::map<std::string, int32_t> pool_by_hash;
+  // TPraos overlay schedule (praos_set_overlay): d, ascInv, epochs, genesis delegates
+  // sorted by genesis key hash; device table: delegate hash (7 words + 0) | VRF hash (8)
+  bool ovl_on = false;
+  uint64_t ovl_d_num = 0, ovl_d_den = 1, ovl_asc_inv = 1, ovl_base = 0, ovl_len = 1;
+  std::vector<praos_gen_deleg> gen_delegs;
+  std::set<std::string> gen_delegate_hashes;
+  uint32_t* d_gen = nullptr;
   // host <-> device staging for large transfers from pageable caller memory
   uint8_t* pin[2] = {nullptr, nullptr};
   hipEvent_t pin_ev[2] = {};
@@ -318,6 +326,7 @@ void praos_close(praos_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   free_epoch(c);
   free_spare(c);
+  (void)hipFree(c->d_gen);
   (void)hipFree(c->btab);
   c->pool.reset();
   for (int k = 0; k < 2; k++) {
@@ -1183,6 +1192,45 @@ static uint8_t header_verdict(uint16_t b, bool have, uint64_t m, uint64_t n) {
   return PRAOS_V_OK;
 }
 
+// TPraos predicate failures of one header (PRAOS_TPF_*), as PRTCL collects them
+// (small-steps ValidateAll: every `?!` of OVERLAY and OCERT is recorded):
+//   OVERLAY (cardano-protocol-tpraos Rules/Overlay.hs): NotActiveSlotOVERLAY; or, in an
+//     active overlay slot, WrongGenesisColdKeyOVERLAY (?!) and pbftVrfChecks (an Either:
+//     its first failure -- WrongGenesisVRFKey, BadNonce, BadLeaderValue); or, outside the
+//     overlay, praosVrfChecks (an Either: VRFKeyUnknown, VRFKeyWrongVRFKey, BadNonce,
+//     BadLeaderValue, VRFLeaderValueTooBig -- first failure);
+//   OCERT (Rules/OCert.hs): KESBeforeStart, KESAfterEnd, InvalidSignature, InvalidKesSignature,
+//     then the counter (currentIssueNo: Nothing -> NoCounterForKeyHash; else CounterTooSmall,
+//     CounterOverIncremented).
+static uint16_t tpraos_failures(uint16_t b, bool have, uint64_t m, uint64_t n) {
+  uint16_t f = 0;
+  if (b & PRAOS_BIT_TP_NOT_ACTIVE) {
+    f |= PRAOS_TPF_NOT_ACTIVE;
+  } else if (b & PRAOS_BIT_TP_OVERLAY) {
+    if (b & PRAOS_BIT_TP_GEN_COLD) f |= PRAOS_TPF_GEN_COLD;
+    if (b & PRAOS_BIT_TP_GEN_VRF) f |= PRAOS_TPF_GEN_VRF;
+    else if (b & PRAOS_BIT_TP_VRF_NONCE) f |= PRAOS_TPF_BAD_NONCE;
+    else if (b & PRAOS_BIT_TP_VRF_LEADER) f |= PRAOS_TPF_BAD_LEADER;
+  } else {
+    if (b & PRAOS_BIT_VRF_KEY_UNKNOWN) f |= PRAOS_TPF_VRF_KEY_UNKNOWN;
+    else if (b & PRAOS_BIT_VRF_KEY_WRONG) f |= PRAOS_TPF_VRF_KEY_WRONG;
+    else if (b & PRAOS_BIT_TP_VRF_NONCE) f |= PRAOS_TPF_BAD_NONCE;
+    else if (b & PRAOS_BIT_TP_VRF_LEADER) f |= PRAOS_TPF_BAD_LEADER;
+    else if (b & PRAOS_BIT_LEADER) f |= PRAOS_TPF_LEADER_TOO_BIG;
+  }
+  if (b & PRAOS_BIT_KES_BEFORE_START) f |= PRAOS_TPF_KES_BEFORE_START;
+  if (b & PRAOS_BIT_KES_AFTER_END) f |= PRAOS_TPF_KES_AFTER_END;
+  if (b & PRAOS_BIT_OCERT_SIG) f |= PRAOS_TPF_OCERT_SIG;
+  if (b & (PRAOS_BIT_KES_MERKLE | PRAOS_BIT_KES_LEAF)) f |= PRAOS_TPF_KES_SIG;
+  if (!have) {
+    f |= PRAOS_TPF_COUNTER_MISSING;
+  } else {
+    if (!(m <= n)) f |= PRAOS_TPF_COUNTER_TOO_SMALL;
+    if (!(n <= m + 1)) f |= PRAOS_TPF_COUNTER_OVER_INC;
+  }
+  return f;
+}
+
 static std::string issuer_hash(const praos_ctx* c, const praos_headers* h, const praos_out* crypto, size_t i) {
   const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
   if (pidx >= 0 && (uint32_t)pidx < c->npools) return std::string((const char*)c->pools[pidx].hash28, 28);
@@ -1278,7 +1326,8 @@ static uint32_t counter_slot(const praos_ctx* c, CounterTab& T, const uint8_t* h
 static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
                      const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei,
                      praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed,
-                     const praos_nonce* etas = nullptr, uint32_t netas = 0, const uint8_t* eta_idx = nullptr) {
+                     const praos_nonce* etas = nullptr, uint32_t netas = 0, const uint8_t* eta_idx = nullptr,
+                     bool tpraos = false, const praos_nonce* extra_entropy = nullptr, uint16_t* failures = nullptr) {
   if (!c || !h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash ||
       ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter)))
     return PRAOS_E_ARG;
@@ -1338,6 +1387,7 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     praos_nonce tick_epoch = W.epoch_nonce, tick_leb = W.leb;
     if (e_new > e_old) {
       tick_epoch = nonce_combine(W.candidate, W.leb);
+      if (tpraos && extra_entropy) tick_epoch = nonce_combine(tick_epoch, *extra_entropy);   // TICKN
       tick_leb = W.lab;
     }
     // the crypto outputs of header i were computed for this nonce: a tick to another one
@@ -1356,11 +1406,24 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     }
     const uint64_t n = h->ocert_n[i];
     const bool has = T.has[k];
-    uint8_t v = header_verdict(crypto->bits[i], has || k < np, has ? T.ctr[k] : 0, n);
+    uint8_t v;
+    if (tpraos) {
+      // currentIssueNo: the counter map, else 0 for a pool or a genesis delegate
+      const bool known = has || k < np || c->gen_delegate_hashes.count(T.extra_keys[k - np]) > 0;
+      const uint16_t f = (crypto->bits[i] & PRAOS_BIT_INPUT) ? 0 : tpraos_failures(crypto->bits[i], known,
+                                                                                    has ? T.ctr[k] : 0, n);
+      if (failures) failures[i] = f;
+      v = (crypto->bits[i] & PRAOS_BIT_INPUT) ? PRAOS_V_INPUT : (f ? PRAOS_V_TPRAOS : PRAOS_V_OK);
+    } else {
+      v = header_verdict(crypto->bits[i], has || k < np, has ? T.ctr[k] : 0, n);
+    }
     // validateHeader (HeaderValidation.hs:419-428): the envelope before the protocol checks
     if (env && v != PRAOS_V_INPUT) {
       const uint8_t ve = envelope_verdict(env, W.tip, h, prev_hash, prev_is_genesis, i);
-      if (ve != PRAOS_V_OK) v = ve;
+      if (ve != PRAOS_V_OK) {
+        v = ve;
+        if (failures) failures[i] = 0;               // validateEnvelope failed: PRTCL does not run
+      }
     }
     verdict[i] = v;
     if (v != PRAOS_V_OK) {
@@ -1461,6 +1524,20 @@ int praos_validate_headers_nonces(praos_ctx* c, const praos_headers* h, const ui
   if (!eta_idx || !etas || k == 0) return PRAOS_E_ARG;
   return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, env, ei, st, verdict, chain_stop, processed, etas, k,
                    eta_idx);
+}
+
+int praos_tpraos_update_chain_dep_state(praos_ctx* c, const praos_tpraos_headers* th, const uint8_t* prev_hash,
+                                        const uint8_t* prev_is_genesis, const praos_tpraos_out* crypto,
+                                        praos_envelope* env, const praos_epoch_info* ei,
+                                        const praos_nonce* extra_entropy, praos_chain_state* st, uint8_t* verdict,
+                                        uint16_t* failures, size_t* chain_stop, size_t* processed) {
+  if (!th || !crypto) return PRAOS_E_ARG;
+  praos_out o{};
+  o.bits = crypto->bits;
+  o.pool_idx = crypto->pool_idx;
+  o.nonce = crypto->nonce;                           // mkNonceFromOutputVRF of the eta certificate
+  return fold_impl(c, &th->h, prev_hash, prev_is_genesis, &o, env, ei, st, verdict, chain_stop, processed, nullptr, 0,
+                   nullptr, true, extra_entropy, failures);
 }
 
 
@@ -1756,6 +1833,76 @@ int praos_leader_schedule(praos_ctx* c, const uint8_t seed[32], uint32_t npools,
   return PRAOS_OK;
 }
 
+// ---- TPraos overlay schedule (cardano-protocol-tpraos Rules/Overlay.hs, restated):
+//   isOverlaySlot firstSlotNo d slot = step s < step (s + 1), step x = ceiling (x * d),
+//     s = slot - firstSlotNo;
+//   classifyOverlaySlot: position = ceiling (s * d); active iff position mod ascInv == 0,
+//     ascInv = floor (1 / activeSlotVal f); genesis key = Set.elemAt ((position div ascInv)
+//     mod |gkeys|) gkeys (ascending byte order of the 28-byte key hashes).
+int praos_set_overlay(praos_ctx* c, const praos_overlay* ov) {
+  if (!c) return PRAOS_E_ARG;
+  if (!ov) {
+    c->ovl_on = false;
+    c->gen_delegs.clear();
+    c->gen_delegate_hashes.clear();
+    return PRAOS_OK;
+  }
+  // d = 0 keeps the genesis delegates for the OCERT counter rule only (currentIssueNo)
+  if (ov->d_den == 0 || ov->d_num > ov->d_den || ov->asc_num == 0 || ov->asc_den == 0 || ov->asc_num > ov->asc_den ||
+      ov->epoch_length == 0 || (ov->n_gen_delegs && !ov->gen_delegs) || (ov->d_num && ov->n_gen_delegs == 0))
+    return PRAOS_E_ARG;
+  std::vector<praos_gen_deleg> g(ov->gen_delegs, ov->gen_delegs + ov->n_gen_delegs);
+  std::sort(g.begin(), g.end(), [](const praos_gen_deleg& a, const praos_gen_deleg& b) {
+    return std::memcmp(a.genesis_hash28, b.genesis_hash28, 28) < 0;
+  });
+  for (size_t k = 1; k < g.size(); k++)
+    if (std::memcmp(g[k - 1].genesis_hash28, g[k].genesis_hash28, 28) == 0) return PRAOS_E_ARG;   // a Map
+  if (c->device >= 0 && ov->d_num) {
+    std::vector<uint32_t> t(16 * g.size(), 0);
+    for (size_t k = 0; k < g.size(); k++) {
+      std::memcpy(&t[16 * k], g[k].delegate_hash28, 28);
+      std::memcpy(&t[16 * k + 8], g[k].vrf_hash32, 32);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->d_gen);
+    c->d_gen = nullptr;
+    c->ovl_on = false;
+    HIPCHK(c, hipMalloc(&c->d_gen, 4 * t.size()));
+    HIPCHK(c, hipMemcpy(c->d_gen, t.data(), 4 * t.size(), hipMemcpyHostToDevice));
+  }
+  c->ovl_d_num = ov->d_num;
+  c->ovl_d_den = ov->d_den;
+  c->ovl_asc_inv = ov->asc_den / ov->asc_num;          // floor (1 / f), >= 1
+  c->ovl_base = ov->epoch_base_slot;
+  c->ovl_len = ov->epoch_length;
+  c->gen_delegs.swap(g);
+  c->gen_delegate_hashes.clear();
+  for (const auto& e : c->gen_delegs) c->gen_delegate_hashes.insert(std::string((const char*)e.delegate_hash28, 28));
+  c->ovl_on = ov->d_num != 0;
+  return PRAOS_OK;
+}
+
+static int32_t overlay_class(const praos_ctx* c, uint64_t slot) {
+  if (!c->ovl_on || slot < c->ovl_base) return -1;
+  const uint64_t first = c->ovl_base + (slot - c->ovl_base) / c->ovl_len * c->ovl_len;
+  const unsigned __int128 x = slot - first;
+  auto step = [&](unsigned __int128 v) {             // ceiling (v * d), v * d_num < 2^128
+    const unsigned __int128 num = v * c->ovl_d_num;
+    return (num + c->ovl_d_den - 1) / c->ovl_d_den;
+  };
+  const unsigned __int128 position = step(x);
+  if (!(position < step(x + 1))) return -1;
+  if (position % c->ovl_asc_inv != 0) return -2;
+  return (int32_t)((position / c->ovl_asc_inv) % c->gen_delegs.size());
+}
+
+int praos_overlay_classify(praos_ctx* c, size_t n, const uint64_t* slots, int32_t* cls) {
+  if (!c || (n && (!slots || !cls))) return PRAOS_E_ARG;
+  for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, slots[i]);
+  return PRAOS_OK;
+}
+
 // TPraos batch: OCert + KES kernels are shared with Praos; VRF checks use the
 // two-certificate kernel and the leader test the 2^512 bound.
 int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, praos_tpraos_out* out) {
@@ -1766,9 +1913,10 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
   praos_batch* b = praos_batch_upload(c, &th->h);
   if (!b) return PRAOS_E_OOM;
   uint8_t *dlout = nullptr, *dlproof = nullptr, *dbeta_l = nullptr;
+  int32_t* dcls = nullptr;
   int rc = PRAOS_OK;
   if (dalloc(b, &dlout, 64 * n) != hipSuccess || dalloc(b, &dlproof, 80 * n) != hipSuccess ||
-      dalloc(b, &dbeta_l, 64 * n) != hipSuccess) {
+      dalloc(b, &dbeta_l, 64 * n) != hipSuccess || (c->ovl_on && dalloc(b, &dcls, 4 * n) != hipSuccess)) {
     praos_batch_free(c, b);
     return PRAOS_E_OOM;
   }
@@ -1780,6 +1928,11 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
   auto body = [&]() -> int {
     HIPCHK(c, hipMemcpy(dlout, th->leader_out, 64 * n, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
+    if (c->ovl_on) {
+      std::vector<int32_t> cls(n);
+      for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, th->h.slot[i]);
+      HIPCHK(c, hipMemcpy(dcls, cls.data(), 4 * n, hipMemcpyHostToDevice));
+    }
     launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
                  P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
     launch_kes(g, blk, c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
@@ -1787,7 +1940,8 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
                (uint8_t*)nullptr, b->tab_kes);
     launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
                   b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
-                  (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce, b->tab_vrf);
+                  (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce, b->tab_vrf,
+                  dcls, c->d_gen);
     launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
                   (int)P.f_is_one, 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
                   (const uint16_t*)nullptr);

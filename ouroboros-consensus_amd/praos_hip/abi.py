@@ -80,6 +80,17 @@ class TPOut(ctypes.Structure):
     _fields_ = [("bits", u16p), ("pool_idx", i32p), ("beta_eta", u8p), ("beta_leader", u8p), ("nonce", u8p)]
 
 
+class GenDeleg(ctypes.Structure):
+    _fields_ = [("genesis_hash28", ctypes.c_uint8 * 28), ("delegate_hash28", ctypes.c_uint8 * 28),
+                ("vrf_hash32", ctypes.c_uint8 * 32)]
+
+
+class Overlay(ctypes.Structure):
+    _fields_ = [("d_num", ctypes.c_uint64), ("d_den", ctypes.c_uint64), ("asc_num", ctypes.c_uint64),
+                ("asc_den", ctypes.c_uint64), ("epoch_base_slot", ctypes.c_uint64), ("epoch_length", ctypes.c_uint64),
+                ("gen_delegs", ctypes.POINTER(GenDeleg)), ("n_gen_delegs", ctypes.c_uint32)]
+
+
 class Nonce(ctypes.Structure):
     _fields_ = [("hash", ctypes.c_uint8 * 32), ("neutral", ctypes.c_int32)]
 
@@ -209,6 +220,14 @@ SIGNATURES = {
                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, i32p]),
     "praos_verify_tpraos_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders),
                                                    ctypes.POINTER(TPOut)]),
+    "praos_set_overlay": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Overlay)]),
+    "praos_overlay_classify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, u64p, i32p]),
+    "praos_tpraos_update_chain_dep_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders), u8p, u8p,
+                                                           ctypes.POINTER(TPOut), ctypes.POINTER(Envelope),
+                                                           ctypes.POINTER(EpochInfo), ctypes.POINTER(Nonce),
+                                                           ctypes.POINTER(ChainState), u8p, u16p,
+                                                           ctypes.POINTER(ctypes.c_size_t),
+                                                           ctypes.POINTER(ctypes.c_size_t)]),
     "praos_synthesize_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params),
                                                u8p, ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p,
                                                u8p, u8p, u64p, u32p, u8p, u8p, u8p, u8p]),
@@ -384,6 +403,62 @@ class Context:
         to.nonce = ptr(o["nonce"])
         self.check(self.L.praos_verify_tpraos_headers(self.h, ctypes.byref(th), ctypes.byref(to)))
         return o
+
+    def set_overlay(self, d, f, epoch_base_slot, epoch_length, gen_delegs):
+        """TPraos overlay schedule (praos_set_overlay): d, f Fractions; gen_delegs list of
+        (genesis_hash28, delegate_hash28, vrf_hash32).  d = None clears everything."""
+        if d is None:
+            self.check(self.L.praos_set_overlay(self.h, None))
+            return
+        arr = (GenDeleg * max(1, len(gen_delegs)))()
+        for k, (g, dl, v) in enumerate(gen_delegs):
+            ctypes.memmove(arr[k].genesis_hash28, bytes(g), 28)
+            ctypes.memmove(arr[k].delegate_hash28, bytes(dl), 28)
+            ctypes.memmove(arr[k].vrf_hash32, bytes(v), 32)
+        ov = Overlay(d.numerator, d.denominator, f.numerator, f.denominator, epoch_base_slot, epoch_length,
+                     ctypes.cast(arr, ctypes.POINTER(GenDeleg)), len(gen_delegs))
+        self._overlay_keep = arr
+        self.check(self.L.praos_set_overlay(self.h, ctypes.byref(ov)))
+
+    def overlay_classify(self, slots):
+        s = np.ascontiguousarray(slots, dtype=np.uint64)
+        out = np.zeros(len(s), np.int32)
+        self.check(self.L.praos_overlay_classify(self.h, len(s), ptr(s, u64p), ptr(out, i32p)))
+        return out
+
+    def tpraos_update_chain_dep_state(self, H, crypto, prev_hash, state: dict, epoch_info, prev_is_genesis=None,
+                                      extra_entropy=None):
+        """praos_tpraos_update_chain_dep_state over TPraos outputs (verify_tpraos_headers);
+        state as for update_chain_dep_state (updated in place).  Returns (verdict u8[n],
+        failures u16[n], chain_stop, processed)."""
+        n = len(H["slot"])
+        th = TPHeaders()
+        th.h = self.headers_struct(H)
+        th.leader_out = ptr(H["leader_out"])
+        th.leader_proof = ptr(H["leader_proof"])
+        to = TPOut()
+        to.bits = ptr(crypto["bits"], u16p)
+        to.pool_idx = ptr(crypto["pool_idx"], i32p)
+        to.nonce = ptr(crypto["nonce"])
+        st, hk, cv = _state_struct(state, len(state.get("counters", {})) + n)
+        ei = EpochInfo(*epoch_info)
+        ph = np.ascontiguousarray(prev_hash, dtype=np.uint8)
+        pg = None if prev_is_genesis is None else np.ascontiguousarray(prev_is_genesis, dtype=np.uint8)
+        xe = None
+        if extra_entropy is not None:
+            xe = Nonce()
+            ctypes.memmove(xe.hash, bytes(extra_entropy), 32)
+        verdict = np.zeros(n, np.uint8)
+        fails = np.zeros(n, np.uint16)
+        stop, done = ctypes.c_size_t(0), ctypes.c_size_t(0)
+        self.check(self.L.praos_tpraos_update_chain_dep_state(
+            self.h, ctypes.byref(th), ptr(ph), ptr(pg) if pg is not None else None, ctypes.byref(to), None,
+            ctypes.byref(ei), ctypes.byref(xe) if xe is not None else None, ctypes.byref(st), ptr(verdict),
+            ptr(fails, u16p), ctypes.byref(stop), ctypes.byref(done)))
+        new = _state_from_struct(st, hk, cv)
+        state.clear()
+        state.update(new)
+        return verdict, fails, int(stop.value), int(done.value)
 
     def upload(self, H):
         hs = self.headers_struct(H)

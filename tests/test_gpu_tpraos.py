@@ -103,3 +103,77 @@ def test_leader512_vs_oracle(ctx, oracle):
         idx = int(o["pool_idx"][i])
         want, _ = oracle.check_leader512(bytes(H["leader_out"][i]), pool_list[idx][2], c_raw)
         assert bool(int(o["bits"][i]) & 0x1000) == (not want)
+
+
+def test_tpraos_overlay_chain_parity(ctx, oracle):
+    """d = 1/2 overlay schedule (praos_set_overlay): active overlay slots forged by the
+    scheduled genesis delegate (or, seeded, by a wrong pool), non-active overlay slots,
+    and Praos slots, all through praos_verify_tpraos_headers and the TPraos fold, against
+    oracle/tpraos.py (overlay classification, pbftVrfChecks / praosVrfChecks, OCERT) on top
+    of the oracle's per-header crypto."""
+    import random
+    import tpraos as tp
+    from praos_hip import fixed
+    r = random.Random(77)
+    p, c_raw = _params(Fraction(1, 2))
+    eta0 = b2b(b"tpraos-overlay-epoch")
+    d, f = Fraction(1, 2), Fraction(1, 20)
+    base, length = 0, 432000
+    npools, n = 8, 256
+    genesis = [b2b(b"genesis-key" + bytes([k]), 28) for k in range(3)]
+    order = sorted(range(3), key=lambda k: genesis[k])                 # Set.elemAt order
+    slots = sorted(r.sample(range(40, 4000), n))
+    cls = [tp.classify(s, d, f, base, length, 3) for s in slots]
+    # forger per header: the delegate of the scheduled genesis key (pools 5..7), sometimes a
+    # wrong pool; any pool for non-active and Praos slots
+    forger = []
+    for c in cls:
+        if c >= 0:
+            forger.append(5 + order[c] if r.random() < 0.85 else r.randrange(5))
+        else:
+            forger.append(r.randrange(npools))
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, b"\x39" * 32, tpraos=True, corrupt_per_10000=800,
+                                         schedule=(np.array(slots, np.uint64), np.array(forger, np.uint32)))
+    sig = [fixed.from_rational(Fraction(1, 8))] * npools
+    pool_list = [(h, v, s) for (h, v), s in zip(pools, sig)]
+    gen = [(genesis[k], pools[5 + k][0], pools[5 + k][1]) for k in range(3)]
+    gen_sorted = sorted(gen)
+    ctx.set_epoch(eta0, pool_list, p)
+    ctx.set_overlay(d, f, base, length, gen)
+    try:
+        assert list(ctx.overlay_classify(np.array(slots, np.uint64))) == cls
+        o = ctx.verify_tpraos_headers(H)
+        ep = oracle.make_epoch(eta0, 129600, 62, c_raw, pool_list)
+        mask = TP_BITS | 0x2000 | 0x4000
+        for i in range(n):
+            off, ln = int(H["body_off"][i]), int(H["body_len"][i])
+            h = {"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
+                 "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
+                 "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
+                 "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
+                 "body": bytes(H["body_bytes"][off:off + ln]), "leader_out": bytes(H["leader_out"][i]),
+                 "leader_proof": bytes(H["leader_proof"][i])}
+            rr = oracle.tpraos_header(ep, h)
+            want = tp.overlay_bits(rr["bits"], cls[i], h["cold_vk"], h["vrf_vk"], gen_sorted)
+            assert int(o["bits"][i]) & mask == want, (i, cls[i], hex(o["bits"][i]), hex(want), corrupted[i])
+            assert bytes(o["nonce"][i]) == rr["nonce"]
+        kinds = {"active": sum(c >= 0 for c in cls), "non_active": cls.count(-2), "praos": cls.count(-1)}
+        assert all(v > 5 for v in kinds.values()), kinds
+        clean_active = [i for i in range(n) if cls[i] >= 0 and not corrupted[i] and forger[i] >= 5]
+        assert clean_active and all(int(o["bits"][i]) & ~0x2000 == 0 for i in clean_active)
+        # the TPraos fold over these outputs
+        prev = np.frombuffer(bytes(r.getrandbits(8) for _ in range(32 * n)), np.uint8).reshape(n, 32).copy()
+        state = {"last_slot": None, "counters": {}, "evolving": None, "candidate": None, "epoch_nonce": eta0,
+                 "lab": None, "leb": None}
+        ref_state = {k: (dict(v) if isinstance(v, dict) else v) for k, v in state.items()}
+        ei = (base, 0, length, 1000)
+        v, fails, stop, done = ctx.tpraos_update_chain_dep_state(H, o, prev, state, ei)
+        hk = [b2b(bytes(H["cold_vk"][i]), 28) for i in range(n)]
+        known = {pl[0] for pl in pool_list} | {g[1] for g in gen}
+        rv, rf, rstop, rdone = tp.fold(ref_state, hk, H["slot"], o["bits"], H["ocert_n"], o["nonce"],
+                                       [bytes(x) for x in prev], known, eta0, base, 0, length, 1000)
+        assert (done, stop) == (rdone, rstop) and done == n
+        assert list(v) == rv and list(fails) == rf and state == ref_state
+        assert any(x & tp.TPF_NOT_ACTIVE for x in rf) and any(x & tp.TPF_GEN_COLD for x in rf)
+    finally:
+        ctx.set_overlay(None, None, 0, 1, [])
