@@ -24,6 +24,10 @@ struct fe { uint32_t v[8]; };
 #define FE_MAC(acc, top, a, b)                                                     \
   asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc" \
       : "+v"(acc), "+v"(top) : "v"(a), "v"(b) : "vcc")
+// first MAC of a column: top := carry-out (no zero-initialised top register to copy in)
+#define FE_MAC0(acc, top, a, b)                                                    \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_cndmask_b32_e64 %1, 0, 1, vcc" \
+      : "+v"(acc), "=v"(top) : "v"(a), "v"(b) : "vcc")
 
 FE_INLINE uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
   return __builtin_addc(a, b, cin, cout);
@@ -67,12 +71,14 @@ FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   acc >>= 32;
 #pragma unroll
   for (int k = 1; k < 15; k++) {
-    uint32_t top = 0;
+    uint32_t top;
+    const int i0 = k < 8 ? 0 : k - 7;                // first i of column k (j = k - i <= 7)
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j < 0 || j > 7) continue;
-      FE_MAC(acc, top, a.v[i], b.v[j]);
+      if (i == i0) FE_MAC0(acc, top, a.v[i], b.v[j]);
+      else FE_MAC(acc, top, a.v[i], b.v[j]);
     }
     t[k] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)top << 32);
@@ -88,12 +94,14 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
   t[0] = 0;
 #pragma unroll
   for (int k = 1; k < 15; k++) {
-    uint32_t top = 0;
+    uint32_t top = 0;                                // stays 0 in column 14 (no i < j there)
+    const int i0 = k < 8 ? 0 : k - 7;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j <= i || j > 7) continue;
-      FE_MAC(acc, top, a.v[i], a.v[j]);
+      if (i == i0) FE_MAC0(acc, top, a.v[i], a.v[j]);
+      else FE_MAC(acc, top, a.v[i], a.v[j]);
     }
     t[k] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)top << 32);
@@ -112,6 +120,121 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
     t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(d >> 32), c, &c);
   }
   fe_reduce512(r, t);
+}
+
+// ---- two independent products interleaved MAC by MAC (ILP for the group formulas,
+// whose multiplications come in independent groups of 2-4).  Each product keeps its
+// carry in its own SGPR pair; the other product's mad + an s_nop 0 give the two wait
+// states between a carry write and its read.  tools/microbench/femul2.hip: at 3 waves
+// per SIMD (the verify kernels' occupancy) 835 -> 788 SIMD cycles per multiply.
+#ifndef PRAOS_ILP2
+#define PRAOS_ILP2 1
+#endif
+#define FE_MAC2(acc1, top1, a1, b1, acc2, top2, a2, b2)                                    \
+  do {                                                                                   \
+    uint64_t c1_, c2_;                                                                   \
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %1, %5, %8, %9, %1\n\ts_nop 0\n\t" \
+        "v_addc_co_u32 %2, %4, 0, %2, %4\n\tv_addc_co_u32 %3, %5, 0, %3, %5"              \
+        : "+v"(acc1), "+v"(acc2), "+v"(top1), "+v"(top2), "=&s"(c1_), "=&s"(c2_)         \
+        : "v"(a1), "v"(b1), "v"(a2), "v"(b2));                                           \
+  } while (0)
+#define FE_MAC2_0(acc1, top1, a1, b1, acc2, top2, a2, b2)                                  \
+  do {                                                                                   \
+    uint64_t c1_, c2_;                                                                   \
+    asm("v_mad_u64_u32 %0, %4, %6, %7, %0\n\tv_mad_u64_u32 %1, %5, %8, %9, %1\n\ts_nop 0\n\t" \
+        "v_cndmask_b32_e64 %2, 0, 1, %4\n\tv_cndmask_b32_e64 %3, 0, 1, %5"                \
+        : "+v"(acc1), "+v"(acc2), "=v"(top1), "=v"(top2), "=&s"(c1_), "=&s"(c2_)         \
+        : "v"(a1), "v"(b1), "v"(a2), "v"(b2));                                           \
+  } while (0)
+
+// r1 = a1 b1, r2 = a2 b2 (outputs may alias any input: written after both products)
+FE_INLINE void fe_mul2(fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2, const fe& b2) {
+#if PRAOS_ILP2
+  uint32_t t1[16], t2[16];
+  uint64_t acc1 = (uint64_t)a1.v[0] * b1.v[0], acc2 = (uint64_t)a2.v[0] * b2.v[0];
+  t1[0] = (uint32_t)acc1;
+  t2[0] = (uint32_t)acc2;
+  acc1 >>= 32;
+  acc2 >>= 32;
+#pragma unroll
+  for (int k = 1; k < 15; k++) {
+    uint32_t top1, top2;
+    const int i0 = k < 8 ? 0 : k - 7;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      if (i == i0) FE_MAC2_0(acc1, top1, a1.v[i], b1.v[j], acc2, top2, a2.v[i], b2.v[j]);
+      else FE_MAC2(acc1, top1, a1.v[i], b1.v[j], acc2, top2, a2.v[i], b2.v[j]);
+    }
+    t1[k] = (uint32_t)acc1;
+    t2[k] = (uint32_t)acc2;
+    acc1 = (acc1 >> 32) | ((uint64_t)top1 << 32);
+    acc2 = (acc2 >> 32) | ((uint64_t)top2 << 32);
+  }
+  t1[15] = (uint32_t)acc1;
+  t2[15] = (uint32_t)acc2;
+  fe_reduce512(r1, t1);
+  fe_reduce512(r2, t2);
+#else
+  fe x, y;
+  fe_mul(x, a1, b1);
+  fe_mul(y, a2, b2);
+  r1 = x;
+  r2 = y;
+#endif
+}
+
+// r1 = a1^2, r2 = a2^2 (outputs may alias inputs)
+FE_INLINE void fe_sq2(fe& r1, const fe& a1, fe& r2, const fe& a2) {
+#if PRAOS_ILP2
+  uint32_t t1[16], t2[16];
+  uint64_t acc1 = 0, acc2 = 0;
+  t1[0] = 0;
+  t2[0] = 0;
+#pragma unroll
+  for (int k = 1; k < 15; k++) {
+    uint32_t top1 = 0, top2 = 0;
+    const int i0 = k < 8 ? 0 : k - 7;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j <= i || j > 7) continue;
+      if (i == i0) FE_MAC2_0(acc1, top1, a1.v[i], a1.v[j], acc2, top2, a2.v[i], a2.v[j]);
+      else FE_MAC2(acc1, top1, a1.v[i], a1.v[j], acc2, top2, a2.v[i], a2.v[j]);
+    }
+    t1[k] = (uint32_t)acc1;
+    t2[k] = (uint32_t)acc2;
+    acc1 = (acc1 >> 32) | ((uint64_t)top1 << 32);
+    acc2 = (acc2 >> 32) | ((uint64_t)top2 << 32);
+  }
+  t1[15] = (uint32_t)acc1;
+  t2[15] = (uint32_t)acc2;
+#pragma unroll
+  for (int i = 15; i > 0; i--) {
+    t1[i] = (t1[i] << 1) | (t1[i - 1] >> 31);
+    t2[i] = (t2[i] << 1) | (t2[i - 1] >> 31);
+  }
+  t1[0] = 0;
+  t2[0] = 0;
+  uint32_t c1 = 0, c2 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t d1 = (uint64_t)a1.v[i] * a1.v[i], d2 = (uint64_t)a2.v[i] * a2.v[i];
+    t1[2 * i] = addc(t1[2 * i], (uint32_t)d1, c1, &c1);
+    t1[2 * i + 1] = addc(t1[2 * i + 1], (uint32_t)(d1 >> 32), c1, &c1);
+    t2[2 * i] = addc(t2[2 * i], (uint32_t)d2, c2, &c2);
+    t2[2 * i + 1] = addc(t2[2 * i + 1], (uint32_t)(d2 >> 32), c2, &c2);
+  }
+  fe_reduce512(r1, t1);
+  fe_reduce512(r2, t2);
+#else
+  fe x, y;
+  fe_sq(x, a1);
+  fe_sq(y, a2);
+  r1 = x;
+  r2 = y;
+#endif
 }
 
 FE_INLINE void fe_add(fe& r, const fe& a, const fe& b) {

@@ -21,16 +21,14 @@ FE_INLINE void ge_p2_identity(ge_p2& p) { fe_set(p.X, 0); fe_set(p.Y, 1); fe_set
 FE_INLINE void ge_cached_identity(ge_cached& c) { fe_set(c.YpX, 1); fe_set(c.YmX, 1); fe_set(c.Z, 1); fe_set(c.T2d, 0); }
 FE_INLINE void ge_niels_identity(ge_niels& c) { fe_set(c.ypx, 1); fe_set(c.ymx, 1); fe_set(c.xy2d, 0); }
 
+// (r and p are distinct objects at every call site; the paired products read p only)
 FE_INLINE void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
 }
 FE_INLINE void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
-  fe_mul(r.T, p.X, p.Y);
+  fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
+  fe_mul2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
 }
 FE_INLINE void ge_p3_to_p2(ge_p2& r, const ge_p3& p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
 
@@ -46,12 +44,10 @@ FE_INLINE void ge_p3_to_cached(ge_cached& c, const ge_p3& p) {
 // r = 2p  (dbl-2008-hwcd with a = -1)
 FE_INLINE void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe t0;
-  fe_sq(r.X, p.X);
-  fe_sq(r.Z, p.Y);
-  fe_sq(r.T, p.Z);
-  fe_add(r.T, r.T, r.T);
   fe_add(r.Y, p.X, p.Y);
-  fe_sq(t0, r.Y);
+  fe_sq2(r.X, p.X, r.Z, p.Y);
+  fe_sq2(r.T, p.Z, t0, r.Y);
+  fe_add(r.T, r.T, r.T);
   fe_add(r.Y, r.Z, r.X);
   fe_sub(r.Z, r.Z, r.X);
   fe_sub(r.X, t0, r.Y);
@@ -63,10 +59,8 @@ FE_INLINE void ge_add(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe t0;
   fe_add(r.X, p.Y, p.X);
   fe_sub(r.Y, p.Y, p.X);
-  fe_mul(r.Z, r.X, q.YpX);
-  fe_mul(r.Y, r.Y, q.YmX);
-  fe_mul(r.T, q.T2d, p.T);
-  fe_mul(r.X, p.Z, q.Z);
+  fe_mul2(r.Z, r.X, q.YpX, r.Y, r.Y, q.YmX);
+  fe_mul2(r.T, q.T2d, p.T, r.X, p.Z, q.Z);
   fe_add(t0, r.X, r.X);
   fe_sub(r.X, r.Z, r.Y);
   fe_add(r.Y, r.Z, r.Y);
@@ -79,8 +73,7 @@ FE_INLINE void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe t0;
   fe_add(r.X, p.Y, p.X);
   fe_sub(r.Y, p.Y, p.X);
-  fe_mul(r.Z, r.X, q.ypx);
-  fe_mul(r.Y, r.Y, q.ymx);
+  fe_mul2(r.Z, r.X, q.ypx, r.Y, r.Y, q.ymx);
   fe_mul(r.T, q.xy2d, p.T);
   fe_add(t0, p.Z, p.Z);
   fe_sub(r.X, r.Z, r.Y);

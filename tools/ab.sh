@@ -8,6 +8,6 @@ for lib in ${LIBS:-libpraos_hip.so}; do
       --concurrent $conc > gpurun_out/ab/${lib}_c$conc.json 2> gpurun_out/ab/${lib}_c$conc.err
     rc=$?
     if [ $rc -ge 124 ]; then echo "$lib c$conc rc=$rc"; exit $rc; fi
-    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/${lib}_c$conc.json')); print('$lib', 'conc=$conc', round(d['value']), d['ms_per_step'], d['roofline']['kernel_ms_serial'], d['self_check']['clean_crypto_ok'])"
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/${lib}_c$conc.json')); print('$lib', 'conc=$conc', round(d['value']), d['ms_per_step'], d['roofline']['kernel_ms_serial'], d['self_check'].get('clean_ok'))"
   done
 done
