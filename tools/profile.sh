@@ -24,4 +24,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   if [ $rc -ne 0 ]; then echo "pmc pass $n rc=$rc, stopping"; tail -5 $OUT/pmc$n.err; exit 1; fi
   echo "pmc pass $n ok"
 done
-python3 tools/prof_summary.py $OUT $TAG > $OUT/summary.txt && echo summary written
+python3 tools/prof_summary.py $OUT $TAG > $OUT/summary.txt && cp profiles/${TAG}_* $OUT/ && echo summary written
