@@ -71,23 +71,39 @@ FE_INLINE void build_cached_table(ge_cached* __restrict__ tab, const ge_p3& P) {
   }
 }
 
+// Table selects are branch-free: the gather of entry max(|d|, 1) is issued
+// unconditionally and the identity / negation applied after it arrives.  (An
+// `if (d == 0)` around the load compiles to an exec-masked branch whose join waits
+// for the load at once; straight-line code lets the caller's independent work --
+// the p1p1 -> p3 conversion of the accumulator -- run under the load's latency.)
+FE_INLINE void cached_fix(ge_cached& c, bool zero, bool neg) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c.YpX.v[i] = zero ? (i == 0 ? 1u : 0u) : c.YpX.v[i];
+    c.YmX.v[i] = zero ? (i == 0 ? 1u : 0u) : c.YmX.v[i];
+    c.Z.v[i] = zero ? (i == 0 ? 1u : 0u) : c.Z.v[i];
+    c.T2d.v[i] = zero ? 0u : c.T2d.v[i];
+  }
+  ge_cached_cneg(c, neg);
+}
+FE_INLINE void niels_fix(ge_niels& c, bool zero, bool neg) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c.ypx.v[i] = zero ? (i == 0 ? 1u : 0u) : c.ypx.v[i];
+    c.ymx.v[i] = zero ? (i == 0 ? 1u : 0u) : c.ymx.v[i];
+    c.xy2d.v[i] = zero ? 0u : c.xy2d.v[i];
+  }
+  ge_niels_cneg(c, neg);
+}
 FE_INLINE void select_cached(ge_cached& c, const ge_cached tab[8], int d) {
   const int a = d < 0 ? -d : d;
-  if (a == 0) {
-    ge_cached_identity(c);
-  } else {
-    c = tab[a - 1];
-  }
-  ge_cached_cneg(c, d < 0);
+  c = tab[a == 0 ? 0 : a - 1];
+  cached_fix(c, a == 0, d < 0);
 }
 FE_INLINE void select_niels(ge_niels& c, const ge_niels* __restrict__ tab, int d) {
   const int a = d < 0 ? -d : d;
-  if (a == 0) {
-    ge_niels_identity(c);
-  } else {
-    c = tab[a - 1];
-  }
-  ge_niels_cneg(c, d < 0);
+  c = tab[a == 0 ? 0 : a - 1];
+  niels_fix(c, a == 0, d < 0);
 }
 
 // x (p1p1) <- 4 doublings of acc (p2); the last one is left unconverted
@@ -192,15 +208,23 @@ FE_INLINE void dbl4_rolled(ge_p1p1& x) {
     ge_p2_dbl(x, q);
   }
 }
-FE_INLINE void add_cached_p1p1(ge_p1p1& x, const ge_cached& c) {
+// x += signed-digit multiple from a table: the entry's gather is issued first and
+// the accumulator's p1p1 -> p3 conversion (independent of it) runs under its latency
+FE_INLINE void add_cached_sel(ge_p1p1& x, const ge_cached* __restrict__ tab, int d) {
+  const int a = d < 0 ? -d : d;
+  ge_cached c = tab[a == 0 ? 0 : a - 1];
   ge_p3 a3;
   ge_p1p1_to_p3(a3, x);
+  cached_fix(c, a == 0, d < 0);
   ge_add(x, a3, c);
 }
-FE_INLINE void add_niels_p1p1(ge_p1p1& x, const ge_niels& n) {
+FE_INLINE void add_niels_sel(ge_p1p1& x, const ge_niels* __restrict__ tab, int d) {
+  const int a = d < 0 ? -d : d;
+  ge_niels c = tab[a == 0 ? 0 : a - 1];
   ge_p3 a3;
   ge_p1p1_to_p3(a3, x);
-  ge_madd(x, a3, n);
+  niels_fix(c, a == 0, d < 0);
+  ge_madd(x, a3, c);
 }
 
 template <int NWIN, int NP, int NQ, int NB, bool TWO_B>
@@ -223,9 +247,7 @@ FE_INLINE void straus_rolled(ge_p1p1& out, const ge_cached* tp, uint32_t pw[8], 
       for (int t = 0; t < nt; t++) {
         uint32_t top = pw[7];
         if constexpr (NQ > 0) top = t == 0 ? pw[7] : qw[7];
-        ge_cached c;
-        select_cached(c, (NQ > 0 && t != 0) ? tq : tp, (int)(top >> 28) - 8);
-        add_cached_p1p1(x, c);
+        add_cached_sel(x, (NQ > 0 && t != 0) ? tq : tp, (int)(top >> 28) - 8);
       }
       shl_small<8, 4>(pw);
       if constexpr (NQ > 0) shl_small<8, 4>(qw);
@@ -236,9 +258,7 @@ FE_INLINE void straus_rolled(ge_p1p1& out, const ge_cached* tp, uint32_t pw[8], 
 #pragma clang loop unroll(disable)
         for (int t = 0; t < NT2; t++) {
           const uint32_t top = TWO_B ? (t == 0 ? fw[3] : fw[7]) : fw[7];
-          ge_niels nb;
-          select_niels(nb, btab + BTAB_N * t, (int)(top >> 24) - 128);
-          add_niels_p1p1(x, nb);
+          add_niels_sel(x, btab + BTAB_N * t, (int)(top >> 24) - 128);
         }
         if constexpr (TWO_B) {
           shl_small<4, 8>(fw);
@@ -360,17 +380,13 @@ FE_INLINE void straus_chunked_rolled(ge_p1p1& out, const ge_cached* __restrict__
 #pragma clang loop unroll(disable)
     for (int k = 0; k < nt; k++) {
       const int d = k < NPC ? (int)(odd_word<NPC>(pw, k) >> 28) - 8 : dtop;
-      ge_cached c;
-      select_cached(c, ktab + 8 * k, d);
-      add_cached_p1p1(x, c);
+      add_cached_sel(x, ktab + 8 * k, d);
     }
     shl64_chunks<2 * NPC, 4>(pw);
     if ((m & 1) == 0) {
 #pragma clang loop unroll(disable)
       for (int k = 0; k < 4; k++) {
-        ge_niels nb;
-        select_niels(nb, btab + BTAB_N * k, (int)(odd_word<4>(fw, k) >> 24) - 128);
-        add_niels_p1p1(x, nb);
+        add_niels_sel(x, btab + BTAB_N * k, (int)(odd_word<4>(fw, k) >> 24) - 128);
       }
       shl64_chunks<8, 8>(fw);
     }
