@@ -369,6 +369,10 @@ def main():
     ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
     ctx.set_option(abi.OPT_KERNELS, cfg["kernels"])
     ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
+    # the dedup belongs to the header pipeline (c1/c5: a chain repeats each pool's OCert);
+    # the single-primitive configs measure every signature on its own
+    if cfg["kernels"] != 7:
+        args.dedup = 0
     ctx.set_option(abi.OPT_DEDUP, args.dedup)
     t0 = time.perf_counter()
     H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank, world)
