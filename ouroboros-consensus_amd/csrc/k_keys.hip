@@ -4,8 +4,8 @@
 // OCerts with one cold key and proves leadership with one VRF key: a 432k-
 // header epoch of 3000 pools has ~144 headers per key).  The cache decodes
 // each recurring key once and expands it into the multi-power tables of
-// scalarmult.hpp (KT_CHUNKS x {1..8} 2^(64k) (-P)), so the per-header chains
-// of those headers are 16 windows long instead of 64.  Keys are compared
+// scalarmult.hpp (KT_CHUNKS x {1..8} 2^(16k) (-P)), so the per-header chains
+// of those headers are 4 windows long instead of 64 (straus_comb).  Keys are compared
 // byte for byte (open addressing on the 32 key bytes), so a cached header
 // sees exactly the point, validity flags and encoding its own bytes give.
 //
@@ -102,9 +102,9 @@ __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, con
 }
 
 // kind 0 (cold key, Ed25519): flag = ge_is_canonical && !ge_has_small_order &&
-//        decodes; tables of -A (ge25519_frombytes_negate_vartime), 4 chunks.
+//        decodes; tables of -A (ge25519_frombytes_negate_vartime), 16 chunks.
 // kind 1 (VRF key): flag = !ge_has_small_order && decodes (vrf_validate_key);
-//        kinfo[1..8] = canonical encoding of Y; tables of -Y, 3 chunks.
+//        kinfo[1..8] = canonical encoding of Y; tables of -Y, 9 chunks.
 __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t* __restrict__ counters,
                                                         uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
                                                         const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
     fe_neg(P.T, Y.T);
   }
   info[0] = ok ? 1u : 0u;
-  build_key_tables(ktab + (size_t)e * KT_STRIDE, P, kind == 0 ? 4 : 3);
+  build_key_tables(ktab + (size_t)e * KT_STRIDE, P, kind == 0 ? KT_CHUNKS : 9);   // c < 2^128: 8 chunks + top
 }
 
 // ---- OCert signature dedup (PRAOS_OPT_DEDUP)

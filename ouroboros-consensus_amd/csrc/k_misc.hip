@@ -2,18 +2,18 @@
 #include "kcommon.hpp"
 
 // ------------------------------------------------------------------ init
-// btab[BTAB_N t + k] = (k+1) 2^(64 t) B (t < 4, k < BTAB_N) as affine niels
+// btab[BTAB_N t + k] = (k+1) 256^t B (t < BCOMB_T, k < BTAB_N) as affine niels
 // (y+x, y-x, 2dxy); one lane per entry (runs once per context).
 __global__ void k_init_btab(ge_niels* btab) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 4 * BTAB_N) return;
+  if (e >= BCOMB_T * BTAB_N) return;
   const int k = e % BTAB_N, tb = e / BTAB_N;
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   ge_p3 B, acc;
   ge_frombytes(B, benc, false);
   if (tb > 0) {
-    for (int i = 0; i < 64 * tb; i++) {
+    for (int i = 0; i < 8 * tb; i++) {
       ge_p3_dbl_to_p3(acc, B);
       B = acc;
     }

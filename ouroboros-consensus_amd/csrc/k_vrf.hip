@@ -137,8 +137,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_ck(const uint32_t* __restric
                                                        const ge_niels* __restrict__ gbtab, VrfIn a) {
   const size_t items = *count;
   if ((size_t)blockIdx.x * NT >= items) return;
-  __shared__ ge_niels sbtab[4 * BTAB_N];
-  const ge_niels* btab = stage_btab<15>(gbtab, sbtab);
+  const ge_niels* btab = gbtab;                                 // the comb, read in place (L2)
   const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
   if (t >= items) return;
   const size_t i = list[t];

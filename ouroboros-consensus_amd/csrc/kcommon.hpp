@@ -45,10 +45,11 @@ __device__ __forceinline__ void store_words(uint8_t* p, const uint32_t* w, int n
   for (int i = 0; i < nwords / 4; i++) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
-// Fixed-base tables in global memory (k_init_btab): 4 tables of BTAB_N niels,
-// table t = {1..128} 2^(64 t) B.  Kernels stage the ones they use into LDS,
-// compacted in increasing t: MASK 0b0001 = {B} (Ed25519 verify), 0b0101 =
-// {B, 2^128 B} (VRF U, signing), 0b1111 = all four (cached-key chains).
+// Fixed-base comb in global memory (k_init_btab): BCOMB_T tables of BTAB_N niels,
+// table j = {1..128} 256^j B.  The cached-key chains read it in place (L2-resident);
+// the per-lane-base chains stage the ones they use into LDS, compacted in increasing
+// t: MASK bit t = comb table 8t = {1..128} 2^(64 t) B, i.e. 0b0001 = {B} (Ed25519
+// verify), 0b0101 = {B, 2^128 B} (VRF U, signing).
 template <int MASK>
 __device__ __forceinline__ const ge_niels* stage_btab(const ge_niels* __restrict__ g, ge_niels* s) {
   constexpr int W4 = BTAB_WORDS / 4;                  // uint4 per table
@@ -56,7 +57,7 @@ __device__ __forceinline__ const ge_niels* stage_btab(const ge_niels* __restrict
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     if (MASK & (1 << t)) {
-      const uint4* src = (const uint4*)g + t * W4;
+      const uint4* src = (const uint4*)g + 8 * t * W4;
       uint4* dst = (uint4*)s + slot * W4;
       for (int i = threadIdx.x; i < W4; i += blockDim.x) dst[i] = src[i];
       slot++;

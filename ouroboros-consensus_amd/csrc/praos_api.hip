@@ -8,6 +8,7 @@
 static constexpr size_t NT = 256;                  // threads per block of the crypto kernels
 static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
 static constexpr size_t BTAB_N = 128;              // entries per fixed-base table (scalarmult.hpp)
+static constexpr size_t BCOMB_TABLES = 32;         // fixed-base comb: 256^j B, j < 32 (scalarmult.hpp BCOMB_T)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
 static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
@@ -241,7 +242,7 @@ struct praos_batch {
   praos_ctx* owner = nullptr;
 };
 
-static constexpr size_t KT_BYTES = 4 * 8 * 4 * 32;  // per cached key: 4 tables x 8 cached points
+static constexpr size_t KT_BYTES = 16 * 8 * 4 * 32; // per cached key: 16 tables x 8 cached points
 static constexpr uint32_t KC_MAX_ENTRIES = 1u << 16;
 
 #define HIPCHK(ctx, x)                                                                    \
@@ -303,8 +304,8 @@ praos_ctx* praos_open(int device) {
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
   for (auto& st : c->side) (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-  if (hipMalloc(&c->btab, 4 * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
-  launch_init_btab(dim3(2), dim3(2 * BTAB_N), c->stream, c->btab);
+  if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
+  launch_init_btab(dim3(BCOMB_TABLES * BTAB_N / 256), dim3(256), c->stream, c->btab);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
     fprintf(stderr, "praos_open: init kernel failed\n");
     delete c;

@@ -129,7 +129,7 @@ FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], c
   sc_recode16(hw, h);
   sc_recode256(sw, s);
   ge_p1p1 x;
-  STRAUS_CHUNKED<4, false>(x, ktab, hw, btab, sw);   // [s]B - [h]A, 16-window chain
+  straus_comb<16, false>(x, ktab, hw, btab, sw);     // [s]B - [h]A: 4-window chain + comb (btab = global comb)
   ge_p2 Rp;
   ge_p1p1_to_p2(Rp, x);
   uint32_t enc[8];
@@ -338,8 +338,8 @@ FE_INLINE void vrf_hash_points(uint32_t c[4], const uint32_t h[8], const uint32_
 //   V = [s]H - [c]Gamma : 64-window chain, both bases per lane (radix 16)
 // One batched inversion encodes H, U, V and 8 Gamma.
 // CACHED: the VRF key comes from k_keys.hip (kinfo[0] bit 0 = key valid,
-// kinfo[1..8] = canonical encoding of Y, ktab = tables of -Y at 2^0, 2^64,
-// 2^128) and U runs on a 16-window chain over the four fixed-base tables.
+// kinfo[1..8] = canonical encoding of Y, ktab = tables of -Y at 2^(16k), k < 9)
+// and U runs on a 4-window chain plus the fixed-base comb (btab = the global comb).
 // vt: the lane's 16-entry table region (see ed25519_verify_core): {1..8}H, {1..8}(-Gamma)
 // and, uncached, {1..8}(-Y) in its first half before H's table replaces it.
 template <bool CACHED>
@@ -378,7 +378,7 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
     sc_recode16(cw, c);
     sc_recode256(sw, s);
     ge_p1p1 x;
-    STRAUS_CHUNKED<2, true>(x, ktab, cw, btab, sw);
+    straus_comb<8, true>(x, ktab, cw, btab, sw);   // btab = the global comb
     ge_p1p1_to_p2(U, x);
   } else {  // U = [s]B - [c]Y
     ge_p3 nY = Y;

@@ -293,116 +293,57 @@ FE_INLINE void ge_scalarmult_var(ge_p3& R, const uint32_t s[8], const ge_p3& P) 
 }
 
 // ---------------------------------------------------------------- cached keys
-// A public key that recurs in a batch (pool cold keys, VRF keys) is decoded
-// once and expanded into KT_CHUNKS tables {1..8} (2^(64k) P) in global memory
-// (k_keys.hip).  A scalar below 2^256 is then 4 chunks of 64 bits sharing one
-// 16-window (64-bit) chain instead of a 64-window one: 4x fewer doublings.
-// The fixed base uses the matching tables 2^(64k) B (radix 256) in LDS.
-#define KT_CHUNKS 4
+// A public key that recurs in a batch (pool cold keys, VRF keys, KES leaf keys)
+// is decoded once and expanded into KT_CHUNKS tables {1..8} (2^(16k) P) in global
+// memory (k_keys.hip).  A scalar below 2^256 is then 16 chunks of 16 bits sharing
+// one 4-window chain (12 doublings) instead of a 64-window one (252 doublings).
+// The fixed-base term needs no doublings at all: byte j of its radix-256 recoding
+// is added after the chain from the comb table j = {1..128} 256^j B (BCOMB_T
+// tables in global memory, 384 KB: resident in every XCD's L2).
+#define KT_CHUNKS 16
 #define KT_STRIDE (KT_CHUNKS * 8)      // ge_cached entries per cached key
+#define BCOMB_T 32                     // comb tables: 256^j B, j < 32
 
-template <int NW, int SH>
-FE_INLINE void shl64_chunks(uint32_t w[NW]) {      // each 64-bit chunk (w[2k], w[2k+1]) <<= SH
-#pragma unroll
-  for (int k = 0; k < NW / 2; k++) {
-    w[2 * k + 1] = __builtin_amdgcn_alignbit(w[2 * k + 1], w[2 * k], 32 - SH);
-    w[2 * k] <<= SH;
-  }
-}
-
-// out = [p] P + [b] B (as p1p1) with P cached (ktab: KT_CHUNKS tables of P):
-//   p: radix-16 recoding pw; chunks k < NPC use table k at nibble 16k + m;
-//      P_TOP: digit 32 (in {0, 1} for p < 2^128) comes from table NPC at m = 0;
-//   b: radix-256 recoding fw (b < 2^253); byte 8k + m/2 on btab + 128 k at even m.
-template <int NPC, bool P_TOP>
-FE_INLINE void straus_chunked(ge_p1p1& out, const ge_cached* __restrict__ ktab, uint32_t pw[8],
-                              const ge_niels* __restrict__ btab, uint32_t fw[8]) {
-  static_assert(NPC >= 1 && NPC + (P_TOP ? 1 : 0) <= KT_CHUNKS, "chunk count");
-  const int dtop = P_TOP ? (int)(pw[2 * NPC] & 15u) - 8 : 0;
-  ge_p2 acc;
-  ge_p1p1 x;
-  ge_p3 a3;
-#pragma clang loop unroll(disable)
-  for (int m = 15; m >= 0; m--) {
-    if (m == 15) ge_p1p1_identity(x);
-    else dbl4_p1p1(x, acc);
-#pragma unroll
-    for (int k = 0; k < NPC; k++) {
-      ge_cached c;
-      select_cached(c, ktab + 8 * k, (int)(pw[2 * k + 1] >> 28) - 8);
-      ge_p1p1_to_p3(a3, x);
-      ge_add(x, a3, c);
-    }
-    shl64_chunks<2 * NPC, 4>(pw);
-    if (P_TOP && m == 0) {
-      ge_cached c;
-      select_cached(c, ktab + 8 * NPC, dtop);
-      ge_p1p1_to_p3(a3, x);
-      ge_add(x, a3, c);
-    }
-    if ((m & 1) == 0) {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        ge_niels nb;
-        select_niels(nb, btab + BTAB_N * k, (int)(fw[2 * k + 1] >> 24) - 128);
-        ge_p1p1_to_p3(a3, x);
-        ge_madd(x, a3, nb);
-      }
-      shl64_chunks<8, 8>(fw);
-    }
-    if (m > 0) ge_p1p1_to_p2(acc, x);
-  }
-  out = x;
-}
-
-// word 2k+1 of w for a uniform runtime k < N (a select chain; no dynamic register index)
+// w[k] for a uniform runtime k < N (a select chain; no dynamic register index)
 template <int N>
-FE_INLINE uint32_t odd_word(const uint32_t w[8], int k) {
-  uint32_t r = w[1];
-  if constexpr (N > 1) r = k == 1 ? w[3] : r;
-  if constexpr (N > 2) r = k == 2 ? w[5] : r;
-  if constexpr (N > 3) r = k == 3 ? w[7] : r;
+FE_INLINE uint32_t word_sel(const uint32_t w[8], int k) {
+  uint32_t r = w[0];
+#pragma unroll
+  for (int i = 1; i < N; i++) r = k == i ? w[i] : r;
   return r;
 }
 
-// straus_chunked with each group operation emitted once (see straus_rolled)
+// out = [p] P + [b] B (as p1p1) with P cached (ktab: KT_CHUNKS tables of P):
+//   p: radix-16 recoding pw; chunk k < NPC (nibbles 4k .. 4k+3) adds its nibble
+//      4k + m at window m from table k; P_TOP: nibble 4 NPC (in {0, 1} for
+//      p < 2^(16 NPC)) comes from table NPC at m = 0;
+//   b: radix-256 recoding fw (b < 2^253); byte j from comb table j after the chain.
+// Each group operation is emitted once (runtime loops, see straus_rolled).
 template <int NPC, bool P_TOP>
-FE_INLINE void straus_chunked_rolled(ge_p1p1& out, const ge_cached* __restrict__ ktab, uint32_t pw[8],
-                                     const ge_niels* __restrict__ btab, uint32_t fw[8]) {
+FE_INLINE void straus_comb(ge_p1p1& out, const ge_cached* __restrict__ ktab, const uint32_t pw[8],
+                           const ge_niels* __restrict__ comb, const uint32_t fw[8]) {
   static_assert(NPC >= 1 && NPC + (P_TOP ? 1 : 0) <= KT_CHUNKS, "chunk count");
-  const int dtop = P_TOP ? (int)(pw[2 * NPC] & 15u) - 8 : 0;
   ge_p1p1 x;
   ge_p1p1_identity(x);
 #pragma clang loop unroll(disable)
-  for (int m = 15; m >= 0; m--) {
-    if (m != 15) dbl4_rolled(x);
+  for (int m = 3; m >= 0; m--) {
+    if (m != 3) dbl4_rolled(x);
     const int nt = NPC + ((P_TOP && m == 0) ? 1 : 0);
 #pragma clang loop unroll(disable)
     for (int k = 0; k < nt; k++) {
-      const int d = k < NPC ? (int)(odd_word<NPC>(pw, k) >> 28) - 8 : dtop;
-      add_cached_sel(x, ktab + 8 * k, d);
+      const uint32_t w = word_sel<(NPC + 2) / 2>(pw, k >> 1);       // nibble 4k + m
+      add_cached_sel(x, ktab + 8 * k, (int)((w >> (16 * (k & 1) + 4 * m)) & 15u) - 8);
     }
-    shl64_chunks<2 * NPC, 4>(pw);
-    if ((m & 1) == 0) {
+  }
 #pragma clang loop unroll(disable)
-      for (int k = 0; k < 4; k++) {
-        add_niels_sel(x, btab + BTAB_N * k, (int)(odd_word<4>(fw, k) >> 24) - 128);
-      }
-      shl64_chunks<8, 8>(fw);
-    }
+  for (int j = 0; j < BCOMB_T; j++) {
+    const uint32_t w = word_sel<8>(fw, j >> 2);                     // byte j
+    add_niels_sel(x, comb + BTAB_N * j, (int)((w >> (8 * (j & 3))) & 255u) - 128);
   }
   out = x;
 }
 
-#if PRAOS_ROLLED
-#define STRAUS straus_rolled
-#define STRAUS_CHUNKED straus_chunked_rolled
-#else
-#define STRAUS straus
-#define STRAUS_CHUNKED straus_chunked
-#endif
-
-// ktab[8k + j] = (j+1) 2^(64k) P for k < nchunks (global memory)
+// ktab[8k + j] = (j+1) 2^(16k) P for k < nchunks (global memory)
 FE_INLINE void build_key_tables(ge_cached* __restrict__ ktab, const ge_p3& P, int nchunks) {
   ge_p3 Q = P;
 #pragma clang loop unroll(disable)
@@ -416,9 +357,15 @@ FE_INLINE void build_key_tables(ge_cached* __restrict__ ktab, const ge_p3& P, in
       ge_p1p1 t;
       ge_p3_to_p2(q, Q);
 #pragma clang loop unroll(disable)
-      for (int d = 0; d < 63; d++) { ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t); }
+      for (int d = 0; d < 15; d++) { ge_p2_dbl(t, q); ge_p1p1_to_p2(q, t); }
       ge_p2_dbl(t, q);
       ge_p1p1_to_p3(Q, t);
     }
   }
 }
+
+#if PRAOS_ROLLED
+#define STRAUS straus_rolled
+#else
+#define STRAUS straus
+#endif
