@@ -98,6 +98,7 @@ struct praos_ctx {
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
+  hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
   float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
   bool last_from_bytes = false;
   std::string err;
@@ -303,7 +304,22 @@ praos_ctx* praos_open(int device) {
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
-  for (auto& st : c->side) (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  for (auto& e : c->miss_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
+  // work) gets the device's greatest priority, so its waves dispatch first and the
+  // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
+  // 14.3 ms per 432k-header step, tools/gpu_prio_ab.sh).  PRAOS_SIDE_PRIO = three
+  // digits overriding that (1 = greatest, 0 = default priority), an A/B knob.
+  {
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const char* pe = std::getenv("PRAOS_SIDE_PRIO");
+    if (!pe || std::strlen(pe) != 3) pe = "001";
+    for (int k = 0; k < 3; k++) {
+      const bool hi = pe && std::strlen(pe) == 3 && pe[k] == '1';
+      (void)hipStreamCreateWithPriority(&c->side[k], hipStreamNonBlocking, hi ? greatest : least);
+    }
+  }
   if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
   launch_init_btab(dim3(BCOMB_TABLES * BTAB_N / 256), dim3(256), c->stream, c->btab);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
@@ -336,6 +352,7 @@ void praos_close(praos_ctx* c) {
   }
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   for (auto& e : c->side_ev) (void)hipEventDestroy(e);
+  for (auto& e : c->miss_ev) (void)hipEventDestroy(e);
   for (auto& st : c->side) (void)hipStreamDestroy(st);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -634,8 +651,18 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   b->kc_used = kc;
   // key cache prepass on the kernel's own stream: hash set, entries, hit/miss lists, tables
   // (items: all n, or list[0 .. *count) when list != null)
-  auto keycache_prepass = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st,
-                              const uint32_t* list = nullptr, const uint32_t* count = nullptr) -> int {
+  // Miss lists go to the main stream as soon as their partition is known, so the
+  // uncached verifies run during the latency-bound key precompute instead of
+  // trailing the cached chains (ev_miss[t]: the partition of cache t is done).
+  hipStream_t sm = c->stream;
+  auto to_main = [&](int t, hipStream_t st) -> int {
+    if (st == sm) return PRAOS_OK;
+    HIPCHK(c, hipEventRecord(c->miss_ev[t], st));
+    HIPCHK(c, hipStreamWaitEvent(sm, c->miss_ev[t], 0));
+    return PRAOS_OK;
+  };
+  auto keycache_lists = [&](praos_batch::KeyCache& k, const uint8_t* keys, hipStream_t st,
+                            const uint32_t* list = nullptr, const uint32_t* count = nullptr) -> int {
     HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
     HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
     HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
@@ -644,9 +671,11 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                       k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
     launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit,
                          k.miss, k.counters);
+    return PRAOS_OK;
+  };
+  auto keycache_precompute = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
     launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries,
                           k.entry_rep, keys, k.ktab, k.kinfo);
-    return PRAOS_OK;
   };
   b->dd_used = false;
   if ((c->kernels & 1) && c->dedup && n >= 2) {
@@ -658,30 +687,39 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                        b->dd_slot, b->dd_item_rep, b->dd_reps, b->dd_counters);
     if (kc) {
       praos_batch::KeyCache& k = b->kc[0];
-      int r = keycache_prepass(k, b->cold_vk, 0, so, b->dd_reps, b->dd_counters);
+      int r = keycache_lists(k, b->cold_vk, so, b->dd_reps, b->dd_counters);
+      if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
+      launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
+      keycache_precompute(k, b->cold_vk, 0, so);
       launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, b->dd_ok);
-      launch_ocert(g, blk, so, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
     } else {
       launch_ocert(g, blk, so, n, b->dd_reps, b->dd_counters, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                    b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
                    b->tab_ocert);
+    }
+    // the fanout reads dd_ok of the misses (main stream) and of the hits (this stream)
+    if (kc && so != sm) {
+      HIPCHK(c, hipEventRecord(c->miss_ev[3], sm));
+      HIPCHK(c, hipStreamWaitEvent(so, c->miss_ev[3], 0));
     }
     launch_ocert_fanout(g, blk, so, n, b->dd_item_rep, b->dd_ok, b->slot, b->ocert_c0, P.slots_per_kes_period,
                         P.max_kes_evo, bo);
   } else if (c->kernels & 1) {
     if (kc) {
       praos_batch::KeyCache& k = b->kc[0];
-      int r = keycache_prepass(k, b->cold_vk, 0, so);
+      int r = keycache_lists(k, b->cold_vk, so);
+      if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
+      launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
+      keycache_precompute(k, b->cold_vk, 0, so);
       launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, (uint8_t*)nullptr);
-      launch_ocert(g, blk, so, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
     } else {
       launch_ocert(g, blk, so, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk,
                    b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo,
@@ -697,14 +735,16 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       // header a pool signs in one KES period
       praos_batch::KeyCache& k = b->kc[2];
       launch_kes_leafkeys(g, blk, sk, n, b->kes_sig, b->slot, b->ocert_c0, P.slots_per_kes_period, b->kes_leaf);
-      int r = keycache_prepass(k, b->kes_leaf, 0, sk);
+      int r = keycache_lists(k, b->kes_leaf, sk);
+      if (r == PRAOS_OK) r = to_main(1, sk);
       if (r != PRAOS_OK) return r;
+      launch_kes(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
+                 b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
+                 bk, (uint8_t*)nullptr, b->tab_kes);
+      keycache_precompute(k, b->kes_leaf, 0, sk);
       launch_kes_ck(g, blk, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                     P.slots_per_kes_period, bk);
-      launch_kes(g, blk, sk, n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
-                 b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
-                 bk, (uint8_t*)nullptr, b->tab_kes);
     } else {
       launch_kes(g, blk, sk, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
                  b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
@@ -717,16 +757,18 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (do_vrf) {
     if (kc) {
       praos_batch::KeyCache& k = b->kc[1];
-      int r = keycache_prepass(k, b->vrf_vk, 1, sv);
+      int r = keycache_lists(k, b->vrf_vk, sv);
+      if (r == PRAOS_OK) r = to_main(2, sv);
       if (r != PRAOS_OK) return r;
+      launch_vrf(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
+                 b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
+                 (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
+                 b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
+      keycache_precompute(k, b->vrf_vk, 1, sv);
       launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk, b->vrf_vk,
                     b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
                     c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
                     b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
-      launch_vrf(g, blk, sv, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
-                 b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
-                 (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
-                 b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
     } else {
       launch_vrf(g, blk, sv, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk, b->vrf_vk,
                  b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
@@ -1038,7 +1080,9 @@ struct Scratch {
   template <typename T>
   T* zeros(size_t bytes) {
     T* d = up<T>(nullptr, bytes);
-    if (d && hipMemset(d, 0, bytes ? bytes : 16) != hipSuccess) ok = false;
+    // on the ctx stream: a null-stream hipMemset is not ordered with the (non-blocking)
+    // stream the kernel runs on and could land after the kernel's writes
+    if (d && hipMemsetAsync(d, 0, bytes ? bytes : 16, c->stream) != hipSuccess) ok = false;
     return d;
   }
 };

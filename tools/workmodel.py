@@ -64,17 +64,17 @@ def vrf_verify():
     return w
 
 
-def straus_chunked(npc, p_top):
-    """16-window chain over cached multi-power key tables (scalarmult.hpp)."""
-    w = 15 * (4 * DBL + 3 * TO_P2) + 15 * TO_P2
-    w += (16 * npc + (1 if p_top else 0)) * (TO_P3 + ADD + CNEG)
-    w += 32 * (TO_P3 + MADD + CNEG)                  # 4 fixed-base tables at 8 even windows
+def straus_comb(npc, p_top):
+    """4-window chain over cached key tables (16-bit chunks) + 32 comb madds (scalarmult.hpp)."""
+    w = 3 * (4 * DBL + 3 * TO_P2) + 3 * TO_P2
+    w += (4 * npc + (1 if p_top else 0)) * (TO_P3 + ADD + CNEG)
+    w += 32 * (TO_P3 + MADD + CNEG)                  # fixed-base bytes from the comb, after the chain
     return w
 
 
 def key_precompute(nchunks):
-    """k_key_precompute: decode, nchunks tables, 64 doublings between chunks."""
-    return DECODE + nchunks * TABLE8 + (nchunks - 1) * 64 * (DBL + TO_P2)
+    """k_key_precompute: decode, nchunks tables, 16 doublings between chunks."""
+    return DECODE + nchunks * TABLE8 + (nchunks - 1) * 16 * (DBL + TO_P2)
 
 
 W_OCERT = ed25519_verify(2)
@@ -82,15 +82,15 @@ W_KES = ed25519_verify(4) + 6 * B2B
 W_VRF = vrf_verify() + 6 * B2B + 1000                # mkInputVRF, issuer/key hashes, L/N, search
 W_LEADER = 3000
 # key-cache path (k_keys.hip): per header on a cached key, and per cached key
-W_OCERT_CK = W_OCERT - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_chunked(4, False)
-W_VRF_CK = W_VRF - DECODE - TABLE8 - straus(33, 33, 0, 32) + straus_chunked(2, True)
-W_KES_CK = W_KES - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_chunked(4, False)
-W_KEY_COLD = key_precompute(4)
-W_KEY_KES = key_precompute(4)                        # leaf keys: same tables as cold keys
-W_KEY_VRF = key_precompute(3) + CANON
+W_OCERT_CK = W_OCERT - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_comb(16, False)
+W_VRF_CK = W_VRF - DECODE - TABLE8 - straus(33, 33, 0, 32) + straus_comb(8, True)
+W_KES_CK = W_KES - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_comb(16, False)
+W_KEY_COLD = key_precompute(16)
+W_KEY_KES = key_precompute(16)                       # leaf keys: same tables as cold keys
+W_KEY_VRF = key_precompute(9) + CANON
 
 if __name__ == "__main__":
     for k, v in (("ocert", W_OCERT), ("kes", W_KES), ("vrf", W_VRF), ("leader", W_LEADER),
-                 ("ocert_ck", W_OCERT_CK), ("vrf_ck", W_VRF_CK), ("key_cold", W_KEY_COLD), ("key_vrf", W_KEY_VRF)):
+                 ("ocert_ck", W_OCERT_CK), ("vrf_ck", W_VRF_CK), ("kes_ck", W_KES_CK), ("key_cold", W_KEY_COLD), ("key_vrf", W_KEY_VRF)):
         print(f"W_{k:7s} {v:>10,d} int32 ops / item")
     print(f"W_header  {W_OCERT + W_KES + W_VRF + W_LEADER:>10,d}")
