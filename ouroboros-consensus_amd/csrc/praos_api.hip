@@ -678,6 +678,11 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                           k.entry_rep, keys, k.ktab, k.kinfo);
   };
   b->dd_used = false;
+  // The OCert misses (a few dozen items, but one full uncached verify of latency) and,
+  // with the dedup, the fanout that needs them go to the END of the main stream's queue
+  // when the streams are concurrent, so the KES / VRF misses behind them start early.
+  std::function<void()> ocert_miss;
+  const bool defer_ocert = so != sm;
   if ((c->kernels & 1) && c->dedup && n >= 2) {
     // distinct OCert tuples only; their verdicts fan out to every header carrying them
     b->dd_used = true;
@@ -690,8 +695,10 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       int r = keycache_lists(k, b->cold_vk, so, b->dd_reps, b->dd_counters);
       if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
-      launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
+      ocert_miss = [&, k]() {
+        launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+                     b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
+      };
       keycache_precompute(k, b->cold_vk, 0, so);
       launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
@@ -702,20 +709,27 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                    b->tab_ocert);
     }
     // the fanout reads dd_ok of the misses (main stream) and of the hits (this stream)
-    if (kc && so != sm) {
-      HIPCHK(c, hipEventRecord(c->miss_ev[3], sm));
-      HIPCHK(c, hipStreamWaitEvent(so, c->miss_ev[3], 0));
-    }
-    launch_ocert_fanout(g, blk, so, n, b->dd_item_rep, b->dd_ok, b->slot, b->ocert_c0, P.slots_per_kes_period,
-                        P.max_kes_evo, bo);
+    auto fan = ocert_miss;
+    ocert_miss = [&, fan, kc]() {
+      if (fan) fan();
+      if (kc && so != sm) {
+        (void)hipEventRecord(c->miss_ev[3], sm);
+        (void)hipStreamWaitEvent(so, c->miss_ev[3], 0);
+      }
+      launch_ocert_fanout(g, blk, so, n, b->dd_item_rep, b->dd_ok, b->slot, b->ocert_c0, P.slots_per_kes_period,
+                          P.max_kes_evo, bo);
+    };
   } else if (c->kernels & 1) {
     if (kc) {
       praos_batch::KeyCache& k = b->kc[0];
       int r = keycache_lists(k, b->cold_vk, so);
       if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
-      launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                   b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
+      ocert_miss = [&, k]() {
+        launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+                     b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr,
+                     b->tab_ocert);
+      };
       keycache_precompute(k, b->cold_vk, 0, so);
       launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
@@ -728,7 +742,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   } else {
     HIPCHK(c, hipMemsetAsync(bo, 0, 2 * n, so));
   }
-  HIPCHK(c, hipEventRecord(c->side_ev[0], so));
+  if (ocert_miss && !defer_ocert) ocert_miss();
+  if (!defer_ocert) HIPCHK(c, hipEventRecord(c->side_ev[0], so));
   if (c->kernels & 2) {
     if (kc) {
       // leaf-key cache: the Ed25519 key a Sum6KES signature ends on repeats for every
@@ -781,6 +796,10 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(b->pool_sorted, 0xff, 4 * n, sv));   // no pool -> leader kernel skips
   }
   HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
+  if (defer_ocert) {
+    if (ocert_miss) ocert_miss();
+    HIPCHK(c, hipEventRecord(c->side_ev[0], so));
+  }
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
   launch_leader(g, blk, c->stream, n, b->leader, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
