@@ -436,9 +436,11 @@ def main():
     # D2H of bits/beta/leader/nonce (never the headline value)
     e2e = None
     if not args.no_e2e and rank == 0:
-        ctx.verify_headers(H)                          # warm (allocator, pinned staging)
-        te = time.perf_counter()
+        # output arrays owned by the caller and reused across calls (a replay loop's steady
+        # state: their pages are already mapped); the first call warms allocator and staging
         oe = ctx.verify_headers(H)
+        te = time.perf_counter()
+        ctx.verify_headers(H, out=oe)
         te = time.perf_counter() - te
         # the same path split into its stages (C ABI calls: upload = repack + staged H2D)
         t0 = time.perf_counter()
@@ -447,7 +449,7 @@ def main():
         ctx.run(b2)
         ctx.sync()
         t2 = time.perf_counter()
-        ctx.download(b2, n)
+        ctx.download(b2, n, out=oe)
         t3 = time.perf_counter()
         ctx.free(b2)
         in_bytes = sum(v.nbytes for v in H.values())
@@ -457,7 +459,8 @@ def main():
                              "download": round((t3 - t2) * 1e3, 2)},
                "input_bytes": in_bytes, "h2d_GBps": round(in_bytes / (t1 - t0) / 1e9, 1),
                "path": "praos_verify_headers: host SoA (pageable) -> repack + H2D through pinned staging "
-                       "buffers -> kernels -> D2H; serial stages (no copy/compute overlap)"}
+                       "buffers -> kernels -> D2H into caller-owned output arrays reused across calls; "
+                       "serial stages (no copy/compute overlap)"}
 
     # self-check on the whole shard: clean items must pass every check that ran
     clean = corrupted == 0

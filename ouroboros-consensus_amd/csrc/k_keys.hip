@@ -105,6 +105,10 @@ __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, con
 //        decodes; tables of -A (ge25519_frombytes_negate_vartime), 16 chunks.
 // kind 1 (VRF key): flag = !ge_has_small_order && decodes (vrf_validate_key);
 //        kinfo[1..8] = canonical encoding of Y; tables of -Y, 9 chunks.
+// chunk tables per key: Ed25519 scalars are < 2^256 (16 chunks); the VRF challenge c
+// is < 2^128 (8 chunks + the top digit's table)
+__device__ __forceinline__ int key_chunks(int kind) { return kind == 0 ? KT_CHUNKS : 9; }
+
 __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t* __restrict__ counters,
                                                         uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
                                                         const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
@@ -133,7 +137,16 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
     fe_neg(P.T, Y.T);
   }
   info[0] = ok ? 1u : 0u;
-  build_key_tables(ktab + (size_t)e * KT_STRIDE, P, kind == 0 ? KT_CHUNKS : 9);   // c < 2^128: 8 chunks + top
+  key_chunk_bases(ktab + (size_t)e * KT_STRIDE, P, key_chunks(kind));
+}
+
+// pass 2: lane (entry, chunk) expands the chunk base into its 8-entry table
+__global__ void __launch_bounds__(256) k_key_tables(int kind, const uint32_t* __restrict__ counters,
+                                                    uint32_t max_entries, ge_cached* __restrict__ ktab) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t e = t / KT_CHUNKS, k = t % KT_CHUNKS;
+  if (e >= min(counters[0], max_entries) || k >= (uint32_t)key_chunks(kind)) return;
+  key_chunk_table(ktab + (size_t)e * KT_STRIDE + 8 * k);
 }
 
 // ---- OCert signature dedup (PRAOS_OPT_DEDUP)
@@ -227,6 +240,9 @@ void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, 
                            uint32_t* kinfo) {
   hipLaunchKernelGGL(k_key_precompute, grid, block, 0, stream, kind, counters, max_entries, entry_rep, keys, ktab,
                      kinfo);
+  const size_t lanes = (size_t)max_entries * KT_CHUNKS;
+  hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, kind, counters,
+                     max_entries, ktab);
 }
 void launch_ocert_dedup(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* cold, const uint8_t* hot,
                         const uint64_t* on, const uint64_t* oc, const uint8_t* sig, uint32_t mask, uint32_t* slot_rep,

@@ -343,15 +343,15 @@ FE_INLINE void straus_comb(ge_p1p1& out, const ge_cached* __restrict__ ktab, con
   out = x;
 }
 
-// ktab[8k + j] = (j+1) 2^(16k) P for k < nchunks (global memory)
-FE_INLINE void build_key_tables(ge_cached* __restrict__ ktab, const ge_p3& P, int nchunks) {
+// Key tables in two passes (k_keys.hip), so no lane runs the whole precompute: pass 1
+// (one lane per key) writes the chunk bases Q_k = 2^(16k) P as p3 into entry 0 of
+// each chunk table (a p3 and a cached point are both 4 field elements); pass 2 (one
+// lane per key and chunk) expands Q_k into ktab[8k + j] = (j+1) Q_k.
+FE_INLINE void key_chunk_bases(ge_cached* __restrict__ ktab, const ge_p3& P, int nchunks) {
   ge_p3 Q = P;
 #pragma clang loop unroll(disable)
   for (int k = 0; k < nchunks; k++) {
-    ge_cached tab[8];
-    build_cached_table(tab, Q);
-#pragma unroll
-    for (int j = 0; j < 8; j++) ktab[8 * k + j] = tab[j];
+    *(ge_p3*)(ktab + 8 * k) = Q;
     if (k + 1 < nchunks) {
       ge_p2 q;
       ge_p1p1 t;
@@ -361,6 +361,24 @@ FE_INLINE void build_key_tables(ge_cached* __restrict__ ktab, const ge_p3& P, in
       ge_p2_dbl(t, q);
       ge_p1p1_to_p3(Q, t);
     }
+  }
+}
+FE_INLINE void key_chunk_table(ge_cached* __restrict__ tab8) {   // entries stored as they are made
+  const ge_p3 Q = *(const ge_p3*)tab8;
+  ge_cached c1, ck;
+  ge_p3_to_cached(c1, Q);
+  tab8[0] = c1;
+  ge_p3 acc;
+  ge_p3_dbl_to_p3(acc, Q);
+  ge_p3_to_cached(ck, acc);
+  tab8[1] = ck;
+#pragma clang loop unroll(disable)
+  for (int k = 2; k < 8; k++) {
+    ge_p1p1 t;
+    ge_add(t, acc, c1);
+    ge_p1p1_to_p3(acc, t);
+    ge_p3_to_cached(ck, acc);
+    tab8[k] = ck;
   }
 }
 

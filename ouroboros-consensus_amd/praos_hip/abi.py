@@ -377,9 +377,10 @@ class Context:
         s.nonce = ptr(o["nonce"])
         return s
 
-    def verify_headers(self, H):
+    def verify_headers(self, H, out=None):
+        """out: caller-owned output arrays (alloc_out) reused across calls, as a replay loop does."""
         n = len(H["slot"])
-        o = self.alloc_out(n)
+        o = self.alloc_out(n) if out is None else out
         hs = self.headers_struct(H)
         os_ = self.out_struct(o)
         self.check(self.L.praos_verify_headers(self.h, ctypes.byref(hs), ctypes.byref(os_)))
@@ -493,8 +494,8 @@ class Context:
     def kernel_ms(self, which):
         return float(self.L.praos_batch_kernel_ms(self.h, which))
 
-    def download(self, b, n):
-        o = self.alloc_out(n)
+    def download(self, b, n, out=None):
+        o = self.alloc_out(n) if out is None else out
         os_ = self.out_struct(o)
         self.check(self.L.praos_batch_download(self.h, b, ctypes.byref(os_)))
         return o

@@ -7,7 +7,7 @@ from fractions import Fraction
 import numpy as np
 import pytest
 
-from helpers import arr, b2b, corrupt, rng
+from helpers import arr, b2b, corrupt, rbytes, rng
 
 pytestmark = pytest.mark.gpu
 
@@ -109,6 +109,36 @@ def test_keycache_equivalence(ctx, oracle):
         assert int(o1["bits"][i]) & BITS_FROM_ORACLE == r["bits"], (i, hex(o1["bits"][i]), hex(r["bits"]))
         assert bytes(o1["beta"][i]) == r["beta"]
     assert all(int(o1["bits"][10 + j]) & 0x0004 for j in range(9))    # OCert rejected for the bad cold keys
+
+
+def test_stream_schedule_equivalence(ctx, oracle):
+    """The concurrent schedule of praos_batch_run (OCert / KES / VRF side streams, the
+    VRF stream at high priority, miss lists on the main stream, the OCert misses and
+    the dedup fanout at the end of its queue) gives the serial schedule's outputs bit
+    for bit, on a batch with cache hits AND misses in all three caches."""
+    from praos_hip import abi
+    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 1500, 23, 1500, seed=b"\x5a" * 32)
+    r = rng(77)
+    for j in range(0, 60, 3):                       # single-use cold / VRF keys: cache misses
+        H["cold_vk"][100 + j] = np.frombuffer(rbytes(r, 32), np.uint8)
+        H["vrf_vk"][400 + j] = np.frombuffer(rbytes(r, 32), np.uint8)
+        H["slot"][700 + j] += 129600 * (1 + j % 3)  # another KES period: a single-use leaf key
+    outs = []
+    try:
+        for conc in (0, 1, 1):
+            ctx.set_option(abi.OPT_CONCURRENT, conc)
+            o, st, dd = _run_batch(ctx, H, 2, dedup=1, want_dedup_stats=True)
+            outs.append(o)
+    finally:
+        ctx.set_option(abi.OPT_CONCURRENT, 1)
+    assert st["cold_misses"] > 0 and st["vrf_misses"] > 0 and st["kes_misses"] > 0, st
+    assert st["cold_hits"] > 0 and st["vrf_hits"] > 0 and st["kes_hits"] > 0, st
+    for o in outs[1:]:
+        for key in ("bits", "beta", "leader", "nonce", "pool_idx"):
+            assert np.array_equal(o[key], outs[0][key]), key
+    ref = _oracle_bits(oracle, H, pool_list, c_raw, eta0)
+    for i, rr in enumerate(ref):
+        assert int(outs[1]["bits"][i]) & BITS_FROM_ORACLE == rr["bits"], (i, hex(outs[1]["bits"][i]), hex(rr["bits"]))
 
 
 def test_header_edge_inputs(ctx, oracle):
