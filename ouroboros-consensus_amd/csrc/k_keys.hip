@@ -112,7 +112,11 @@ __device__ __forceinline__ int key_chunks(int kind) { return kind == 0 ? KT_CHUN
 __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t* __restrict__ counters,
                                                         uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
                                                         const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
-                                                        uint32_t* __restrict__ kinfo) {
+                                                        uint32_t* __restrict__ kinfo, int wave_prio) {
+  // latency-bound (a short list of long chains) and on the critical path of the cached
+  // chains: raised wave priority wins the SIMD's issue arbitration against the
+  // throughput kernels resident beside it
+  if (wave_prio) __builtin_amdgcn_s_setprio(3);
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ne = min(counters[0], max_entries);
   if (e >= ne) return;
@@ -142,7 +146,9 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
 
 // pass 2: lane (entry, chunk) expands the chunk base into its 8-entry table
 __global__ void __launch_bounds__(256) k_key_tables(int kind, const uint32_t* __restrict__ counters,
-                                                    uint32_t max_entries, ge_cached* __restrict__ ktab) {
+                                                    uint32_t max_entries, ge_cached* __restrict__ ktab,
+                                                    int wave_prio) {
+  if (wave_prio) __builtin_amdgcn_s_setprio(3);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t e = t / KT_CHUNKS, k = t % KT_CHUNKS;
   if (e >= min(counters[0], max_entries) || k >= (uint32_t)key_chunks(kind)) return;
@@ -237,12 +243,12 @@ void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 }
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
-                           uint32_t* kinfo) {
+                           uint32_t* kinfo, int wave_prio) {
   hipLaunchKernelGGL(k_key_precompute, grid, block, 0, stream, kind, counters, max_entries, entry_rep, keys, ktab,
-                     kinfo);
+                     kinfo, wave_prio);
   const size_t lanes = (size_t)max_entries * KT_CHUNKS;
   hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, kind, counters,
-                     max_entries, ktab);
+                     max_entries, ktab, wave_prio);
 }
 void launch_ocert_dedup(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* cold, const uint8_t* hot,
                         const uint64_t* on, const uint64_t* oc, const uint8_t* sig, uint32_t mask, uint32_t* slot_rep,

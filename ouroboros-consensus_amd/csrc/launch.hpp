@@ -47,7 +47,7 @@ void launch_ocert_fanout(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint64_t max_kes_evo, uint16_t* bits);
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
-                           uint32_t* kinfo);
+                           uint32_t* kinfo, int wave_prio);
 void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                 const ge_niels* gbtab, const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off,
                 const uint32_t* body_len, const uint8_t* body, size_t body_bytes_len, const uint64_t* slot,

@@ -96,6 +96,7 @@ struct praos_ctx {
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
+  int key_wave_prio = 0;                               // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO=1; A/B: no gain)
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
@@ -298,6 +299,7 @@ praos_ctx* praos_open(int device) {
   }
   praos_ctx* c = new praos_ctx();
   c->device = device;
+  if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return nullptr;
@@ -675,7 +677,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   };
   auto keycache_precompute = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
     launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries,
-                          k.entry_rep, keys, k.ktab, k.kinfo);
+                          k.entry_rep, keys, k.ktab, k.kinfo, c->key_wave_prio);
   };
   b->dd_used = false;
   // The OCert misses (a few dozen items, but one full uncached verify of latency) and,
