@@ -130,6 +130,30 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
 #ifndef PRAOS_ILP2
 #define PRAOS_ILP2 1
 #endif
+// The first product's carry goes through VCC (its carry add encodes as VOP2, issued in
+// fewer cycles than the VOP3 form an SGPR-pair carry needs), the second's through an
+// SGPR pair; PRAOS_MAC2_VCC=0 keeps both in SGPR pairs (the A/B reference).
+#ifndef PRAOS_MAC2_VCC
+#define PRAOS_MAC2_VCC 1
+#endif
+#if PRAOS_MAC2_VCC
+#define FE_MAC2(acc1, top1, a1, b1, acc2, top2, a2, b2)                                    \
+  do {                                                                                   \
+    uint64_t c2_;                                                                        \
+    asm("v_mad_u64_u32 %0, vcc, %5, %6, %0\n\tv_mad_u64_u32 %1, %4, %7, %8, %1\n\ts_nop 0\n\t" \
+        "v_addc_co_u32 %2, vcc, 0, %2, vcc\n\tv_addc_co_u32 %3, %4, 0, %3, %4"             \
+        : "+v"(acc1), "+v"(acc2), "+v"(top1), "+v"(top2), "=&s"(c2_)                     \
+        : "v"(a1), "v"(b1), "v"(a2), "v"(b2) : "vcc");                                   \
+  } while (0)
+#define FE_MAC2_0(acc1, top1, a1, b1, acc2, top2, a2, b2)                                  \
+  do {                                                                                   \
+    uint64_t c2_;                                                                        \
+    asm("v_mad_u64_u32 %0, vcc, %5, %6, %0\n\tv_mad_u64_u32 %1, %4, %7, %8, %1\n\ts_nop 0\n\t" \
+        "v_addc_co_u32 %2, vcc, 0, %9, vcc\n\tv_cndmask_b32_e64 %3, 0, 1, %4"              \
+        : "+v"(acc1), "+v"(acc2), "=v"(top1), "=v"(top2), "=&s"(c2_)                     \
+        : "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(0u) : "vcc");                          \
+  } while (0)
+#else
 #define FE_MAC2(acc1, top1, a1, b1, acc2, top2, a2, b2)                                    \
   do {                                                                                   \
     uint64_t c1_, c2_;                                                                   \
@@ -146,6 +170,8 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
         : "+v"(acc1), "+v"(acc2), "=v"(top1), "=v"(top2), "=&s"(c1_), "=&s"(c2_)         \
         : "v"(a1), "v"(b1), "v"(a2), "v"(b2));                                           \
   } while (0)
+
+#endif
 
 // r1 = a1 b1, r2 = a2 b2 (outputs may alias any input: written after both products)
 FE_INLINE void fe_mul2(fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2, const fe& b2) {
