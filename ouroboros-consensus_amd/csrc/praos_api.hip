@@ -132,6 +132,12 @@ struct praos_ctx {
   // order (hipMalloc / hipFree of ~40 buffers cost ~20 ms per 432k batch)
   std::vector<void*> spare;
   std::vector<size_t> spare_sz;
+  // host-side repack arena of praos_batch_upload, kept across calls (a fresh 170 MB
+  // allocation per 432k batch cost its page faults and its unmapping on every call)
+  std::unique_ptr<uint8_t[]> h_arena;
+  size_t h_arena_cap = 0;
+  std::vector<uint64_t> h_off;
+  std::vector<uint32_t> h_len;
 };
 
 static void free_spare(praos_ctx* c) {
@@ -151,7 +157,7 @@ static bool stage_init(praos_ctx* c) {
     if (hipEventCreateWithFlags(&c->pin_ev[k], hipEventDisableTiming) != hipSuccess) return false;
   }
   const unsigned hw = std::thread::hardware_concurrency();
-  c->pool.reset(new CopyPool(std::max(1u, std::min(8u, hw ? hw : 1u))));
+  c->pool.reset(new CopyPool(std::max(1u, std::min(16u, hw ? hw : 1u))));   // the box's CPU share per GPU
   return true;
 }
 
@@ -507,7 +513,8 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   const size_t n = h->n;
   b->n = n;
   // repack bodies 8-byte aligned (the SHA-512 feeder reads 64-bit words)
-  std::vector<uint64_t> off(n);
+  std::vector<uint64_t>& off = c->h_off;
+  off.resize(n);
   size_t total = 0;
   bool bad_range = false;
   for (size_t i = 0; i < n; i++) {
@@ -516,14 +523,19 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
     total += (h->body_len[i] + 7) & ~(size_t)7;
   }
   auto tr0 = std::chrono::steady_clock::now();
-  std::unique_ptr<uint8_t[]> arena(new uint8_t[total + 16]);
-  std::vector<uint32_t> len(n);
+  if (c->h_arena_cap < total + 16) {
+    c->h_arena.reset(new uint8_t[total + 16]);
+    c->h_arena_cap = total + 16;
+  }
+  uint8_t* const arena = c->h_arena.get();
+  std::vector<uint32_t>& len = c->h_len;
+  len.resize(n);
   auto repack = [&](size_t i0, size_t i1) {
     for (size_t i = i0; i < i1; i++) {
       const bool ok = h->body_off[i] <= h->body_bytes_len && h->body_len[i] <= h->body_bytes_len - h->body_off[i];
       len[i] = ok ? h->body_len[i] : 0xffffffffu;  // marks out-of-range (kernel flags PRAOS_BIT_INPUT)
       const size_t pad = ((size_t)h->body_len[i] + 7) & ~(size_t)7;
-      uint8_t* d = arena.get() + off[i];
+      uint8_t* d = arena + off[i];
       if (ok) std::memcpy(d, h->body_bytes + h->body_off[i], h->body_len[i]);
       if (pad > (ok ? (size_t)h->body_len[i] : 0)) std::memset(d + (ok ? h->body_len[i] : 0), 0, pad - (ok ? h->body_len[i] : 0));
     }
@@ -534,7 +546,7 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   } else {
     repack(0, n);
   }
-  std::memset(arena.get() + total, 0, 16);
+  std::memset(arena + total, 0, 16);
   if (std::getenv("PRAOS_TRACE_UPLOAD"))
     fprintf(stderr, "upload: repack %.2f ms\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count());
@@ -563,10 +575,12 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   up(b->hot_vk, h->hot_vk, 32 * n);
   up(b->ocert_sig, h->ocert_sig, 64 * n);
   up(b->kes_sig, h->kes_sig, 448 * n);
-  up(b->body, arena.get(), total + 16);
+  up(b->body, arena, total + 16);
   auto ts = now();
   ok &= hipStreamSynchronize(c->stream) == hipSuccess;
-  if (trace) fprintf(stderr, "upload: final sync %.2f ms\n", std::chrono::duration<double, std::milli>(now() - ts).count());
+  if (trace) fprintf(stderr, "upload: final sync %.2f ms, from the repack %.2f ms\n",
+                     std::chrono::duration<double, std::milli>(now() - ts).count(),
+                     std::chrono::duration<double, std::milli>(now() - tr0).count());
   if (!ok) { c->err = "upload failed"; praos_batch_free(c, b); return nullptr; }
   return b;
 }
