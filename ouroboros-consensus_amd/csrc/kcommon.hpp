@@ -12,7 +12,7 @@
 // Epoch tables: pool hash28 (7 words, sorted), vrf hash (8 words), x_raw (4 words).
 #include "praos_core.hpp"
 #include "leader.hpp"
-#include "praos_kernels.h"
+#include "praos_hip.h"
 #include "launch.hpp"
 
 #define NT 256                      // threads per block (4 waves)

@@ -1,7 +1,7 @@
 // praos_api.hip -- host side of libpraos_hip: context, device buffers, launches
 // and the sequential part of Praos.updateChainDepState (C++).
 // Single translation unit with the kernels (no relocatable device code).
-#include "praos_kernels.h"
+#include "praos_hip.h"
 #include "launch.hpp"
 #include "host_util.hpp"
 

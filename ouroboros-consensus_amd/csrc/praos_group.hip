@@ -9,7 +9,7 @@
 //
 // A device may appear several times (several contexts on one GPU: the multi-threaded
 // use the C ABI allows, one context per host thread).
-#include "praos_kernels.h"
+#include "praos_hip.h"
 
 #include <algorithm>
 #include <string>

@@ -21,7 +21,7 @@
 // headerSize u16 BE, checksum u32 BE, headerHash 32 bytes, blockOrEBB (slot) u64 BE.
 // The primary index maps relative slots to entries and is not needed for a full
 // sequential replay.  Chunks are read from 00000 upwards until one is missing.
-#include "praos_kernels.h"
+#include "praos_hip.h"
 #include "host_util.hpp"
 
 #include <algorithm>
