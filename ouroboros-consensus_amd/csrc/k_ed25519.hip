@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_ocert_ck(const uint32_t* __restri
                                                         const ge_niels* __restrict__ gbtab, OcertIn a) {
   const size_t items = *count;
   if ((size_t)blockIdx.x * NT >= items) return;
-  const ge_niels* btab = gbtab;                                 // the comb, read in place (L2)
+  const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
   const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
   if (t >= items) return;
   const size_t i = list[t];
@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck(const uint32_t* __restrict
                                                       const ge_niels* __restrict__ gbtab, KesIn a) {
   const size_t items = *count;
   if ((size_t)blockIdx.x * NT >= items) return;
-  const ge_niels* btab = gbtab;                                 // the comb, read in place (L2)
+  const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
   const size_t q = (size_t)blockIdx.x * NT + threadIdx.x;
   if (q >= items) return;
   const size_t i = list[q];

@@ -41,6 +41,38 @@ __global__ void k_init_btab(ge_niels* btab) {
   btab[e] = n;
 }
 
+// bcomb16[C16_N j + k] = (k+1) 65536^j B (j < C16_T, k < C16_N) as affine niels: one
+// lane per entry, a fixed-base multiplication by (k+1) 2^(16 j) mod L over the LDS
+// tables of the radix-256 comb, then the affine conversion (runs once per context).
+__global__ void __launch_bounds__(NT) k_init_bcomb16(const ge_niels* gbtab, ge_niels* bcomb16) {
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
+  const uint32_t e = blockIdx.x * NT + threadIdx.x;
+  if (e >= C16_T * C16_N) return;
+  const uint32_t j = e / C16_N, k = e % C16_N + 1;
+  uint32_t w[8], r[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) w[q] = 0;
+  const int bit = 16 * (int)j;                     // (k+1) << 16 j, k + 1 <= 2^15
+  w[bit >> 5] = k << (bit & 31);
+  sc_reduce256(r, w);
+  ge_p3 P;
+  ge_scalarmult_base(P, r, btab);
+  fe zi, x, y, xy, d2;
+  fe_invert(zi, P.Z);
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  fe_canon(x, x);
+  fe_canon(y, y);
+  ge_niels n;
+  fe_add(n.ypx, y, x);
+  fe_sub(n.ymx, y, x);
+  fe_mul(xy, x, y);
+  fe_const(d2, FE_D2);
+  fe_mul(n.xy2d, xy, d2);
+  bcomb16[e] = n;
+}
+
 // ------------------------------------------------------------------ leader
 // Header mode: leader bytes from leader_in (big-endian natural), x from the
 // pool table (sorted index), bit LEADER.  Plain mode (x_item != null): x per
@@ -181,6 +213,9 @@ __global__ void k_debug_h2c(size_t n, const uint8_t* pk, const uint8_t* alpha, u
 
 
 // ---- host launchers (kernels are only launchable from their own module)
+void launch_init_bcomb16(hipStream_t stream, const ge_niels* btab, ge_niels* bcomb16) {
+  hipLaunchKernelGGL(k_init_bcomb16, dim3((C16_T * C16_N + NT - 1) / NT), dim3(NT), 0, stream, btab, bcomb16);
+}
 void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab) {
   hipLaunchKernelGGL(k_init_btab, grid, block, 0, stream, btab);
 }

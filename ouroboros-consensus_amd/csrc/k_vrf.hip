@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_ck(const uint32_t* __restric
                                                        const ge_niels* __restrict__ gbtab, VrfIn a) {
   const size_t items = *count;
   if ((size_t)blockIdx.x * NT >= items) return;
-  const ge_niels* btab = gbtab;                                 // the comb, read in place (L2)
+  const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
   const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
   if (t >= items) return;
   const size_t i = list[t];

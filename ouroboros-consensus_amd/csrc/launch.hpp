@@ -62,6 +62,7 @@ void launch_kes_leafkeys(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
                          uint8_t* keys);
 void launch_init_btab(dim3 grid, dim3 block, hipStream_t stream, ge_niels* btab);
+void launch_init_bcomb16(hipStream_t stream, const ge_niels* btab, ge_niels* bcomb16);
 void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* leader_in, const int32_t* pool_sorted_idx, const uint32_t* pool_x, const uint32_t* x_item, int f_is_one, int leader_words, const uint16_t* b_ocert, const uint16_t* b_kes, const uint16_t* b_vrf, uint16_t* bits, uint8_t* is_leader, int32_t* iters, const uint16_t* dec_status);
 void launch_debug_fe(dim3 grid, dim3 block, hipStream_t stream, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);
 void launch_debug_sha512(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* prefix, const uint64_t* off, const uint32_t* len, const uint8_t* msg, uint8_t* out);

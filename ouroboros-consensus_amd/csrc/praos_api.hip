@@ -9,6 +9,7 @@ static constexpr size_t NT = 256;                  // threads per block of the c
 static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
 static constexpr size_t BTAB_N = 128;              // entries per fixed-base table (scalarmult.hpp)
 static constexpr size_t BCOMB_TABLES = 32;         // fixed-base comb: 256^j B, j < 32 (scalarmult.hpp BCOMB_T)
+static constexpr size_t C16_TABLES = 16, C16_ENTRIES = 32768;   // radix-2^16 comb (scalarmult.hpp C16_T, C16_N)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
 static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
@@ -104,6 +105,7 @@ struct praos_ctx {
   bool last_from_bytes = false;
   std::string err;
   ge_niels* btab = nullptr;
+  ge_niels* bcomb16 = nullptr;                         // radix-2^16 comb of the cached-key chains (48 MB)
   // epoch
   bool have_epoch = false;
   praos_params params{};
@@ -330,6 +332,8 @@ praos_ctx* praos_open(int device) {
   }
   if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
   launch_init_btab(dim3(BCOMB_TABLES * BTAB_N / 256), dim3(256), c->stream, c->btab);
+  if (hipMalloc(&c->bcomb16, C16_TABLES * C16_ENTRIES * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
+  launch_init_bcomb16(c->stream, c->btab, c->bcomb16);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
     fprintf(stderr, "praos_open: init kernel failed\n");
     delete c;
@@ -353,6 +357,7 @@ void praos_close(praos_ctx* c) {
   free_spare(c);
   (void)hipFree(c->d_gen);
   (void)hipFree(c->btab);
+  (void)hipFree(c->bcomb16);
   c->pool.reset();
   for (int k = 0; k < 2; k++) {
     if (c->pin[k]) (void)hipHostFree(c->pin[k]);
@@ -716,7 +721,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                      b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
+      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, b->dd_ok);
     } else {
@@ -747,7 +752,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                      b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk,
+      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, (uint8_t*)nullptr);
     } else {
@@ -773,7 +778,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                  b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
                  bk, (uint8_t*)nullptr, b->tab_kes);
       keycache_precompute(k, b->kes_leaf, 0, sk);
-      launch_kes_ck(g, blk, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->hot_vk, b->kes_sig,
+      launch_kes_ck(g, blk, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                     P.slots_per_kes_period, bk);
     } else {
@@ -796,7 +801,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                  (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
                  b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
       keycache_precompute(k, b->vrf_vk, 1, sv);
-      launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->btab, b->cold_vk, b->vrf_vk,
+      launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk, b->vrf_vk,
                     b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
                     c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
                     b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);

@@ -127,7 +127,7 @@ FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], c
   for (int i = 0; i < 8; i++) s[i] = ok ? S[i] : 0u;
   uint32_t hw[8], sw[8];
   sc_recode16(hw, h);
-  sc_recode256(sw, s);
+  sc_recode65536(sw, s);
   ge_p1p1 x;
   straus_comb<16, false>(x, ktab, hw, btab, sw);     // [s]B - [h]A: 4-window chain + comb (btab = global comb)
   ge_p2 Rp;
@@ -376,7 +376,7 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
   if constexpr (CACHED) {  // U = [s]B - [c]Y, cached -Y
     uint32_t cw[8], sw[8];
     sc_recode16(cw, c);
-    sc_recode256(sw, s);
+    sc_recode65536(sw, s);
     ge_p1p1 x;
     straus_comb<8, true>(x, ktab, cw, btab, sw);   // btab = the global comb
     ge_p1p1_to_p2(U, x);

@@ -298,11 +298,20 @@ FE_INLINE void ge_scalarmult_var(ge_p3& R, const uint32_t s[8], const ge_p3& P) 
 // memory (k_keys.hip).  A scalar below 2^256 is then 16 chunks of 16 bits sharing
 // one 4-window chain (12 doublings) instead of a 64-window one (252 doublings).
 // The fixed-base term needs no doublings at all: byte j of its radix-256 recoding
-// is added after the chain from the comb table j = {1..128} 256^j B (BCOMB_T
-// tables in global memory, 384 KB: resident in every XCD's L2).
+// is added after the chain: 16-bit digit j from the comb table j = {1..32768} 65536^j B
+// (C16_T tables in global memory, 48 MB: resident in the MALL), 16 mixed additions.
 #define KT_CHUNKS 16
 #define KT_STRIDE (KT_CHUNKS * 8)      // ge_cached entries per cached key
 #define BCOMB_T 32                     // comb tables: 256^j B, j < 32
+#define C16_T 16                       // radix-2^16 comb (cached-key chains): 65536^j B, j < 16,
+#define C16_N 32768                    //   entries {1..32768}: 48 MB of affine niels (MALL-resident)
+
+// w = s + 0x8000 8000 ... 8000 (radix-65536 signed recoding); requires s < 2^253
+FE_INLINE void sc_recode65536(uint32_t w[8], const uint32_t s[8]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w[i] = addc(s[i], 0x80008000u, c, &c);
+}
 
 // w[k] for a uniform runtime k < N (a select chain; no dynamic register index)
 template <int N>
@@ -317,7 +326,8 @@ FE_INLINE uint32_t word_sel(const uint32_t w[8], int k) {
 //   p: radix-16 recoding pw; chunk k < NPC (nibbles 4k .. 4k+3) adds its nibble
 //      4k + m at window m from table k; P_TOP: nibble 4 NPC (in {0, 1} for
 //      p < 2^(16 NPC)) comes from table NPC at m = 0;
-//   b: radix-256 recoding fw (b < 2^253); byte j from comb table j after the chain.
+//   b: radix-65536 recoding fw (sc_recode65536, b < 2^253); 16-bit digit j from the
+//      comb table j = {1..32768} 65536^j B (C16_T tables) after the chain.
 // Each group operation is emitted once (runtime loops, see straus_rolled).
 template <int NPC, bool P_TOP>
 FE_INLINE void straus_comb(ge_p1p1& out, const ge_cached* __restrict__ ktab, const uint32_t pw[8],
@@ -336,9 +346,9 @@ FE_INLINE void straus_comb(ge_p1p1& out, const ge_cached* __restrict__ ktab, con
     }
   }
 #pragma clang loop unroll(disable)
-  for (int j = 0; j < BCOMB_T; j++) {
-    const uint32_t w = word_sel<8>(fw, j >> 2);                     // byte j
-    add_niels_sel(x, comb + BTAB_N * j, (int)((w >> (8 * (j & 3))) & 255u) - 128);
+  for (int j = 0; j < C16_T; j++) {
+    const uint32_t w = word_sel<8>(fw, j >> 1);                     // 16-bit digit j
+    add_niels_sel(x, comb + (size_t)C16_N * j, (int)((w >> (16 * (j & 1))) & 0xffffu) - 32768);
   }
   out = x;
 }

@@ -65,10 +65,10 @@ def vrf_verify():
 
 
 def straus_comb(npc, p_top):
-    """4-window chain over cached key tables (16-bit chunks) + 32 comb madds (scalarmult.hpp)."""
+    """4-window chain over cached key tables (16-bit chunks) + 16 radix-2^16 comb madds (scalarmult.hpp)."""
     w = 3 * (4 * DBL + 3 * TO_P2) + 3 * TO_P2
     w += (4 * npc + (1 if p_top else 0)) * (TO_P3 + ADD + CNEG)
-    w += 32 * (TO_P3 + MADD + CNEG)                  # fixed-base bytes from the comb, after the chain
+    w += 16 * (TO_P3 + MADD + CNEG)                  # 16-bit fixed-base digits from the comb, after the chain
     return w
 
 
