@@ -314,9 +314,13 @@ def make_input(ctx, args, cfg, rank, world=1):
     c_raw = fixed.active_slot_log(Fraction(1, 20))
     p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw, vrf_check_output=True)
     eta0 = hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest()
+    # corruptions only in the fields the config's check reads (1 % means 1 %)
+    fields = {"c2": abi.CORRUPT_OCERT, "c3": abi.CORRUPT_VRF_PROOF | abi.CORRUPT_VRF_OUT,
+              "c4": abi.CORRUPT_KES_SIG | abi.CORRUPT_BODY}[args.config]
     H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, (b"\x5a" * 27) + bytes([int(args.config[1])]) +
                                          rank.to_bytes(4, "little"), first_slot=rank * n * 20, slot_stride=20,
-                                         body_len=397, corrupt_per_10000=args.corrupt_per_10000, nkes=cfg["nkes"])
+                                         body_len=397, corrupt_per_10000=args.corrupt_per_10000, nkes=cfg["nkes"],
+                                         corrupt_fields=fields)
     pool_list = [] if cfg["pools"] is None else [(h, v, s) for (h, v), s in zip(pools, chains.stake(npools, 10))]
     return H, pool_list, corrupted, p, eta0, c_raw, 129600, 62
 
@@ -336,6 +340,7 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16, help="CPU-twin threads (the box's share: 16)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-proxy", action="store_true", help="skip the one-GPU strong-scaling proxy (c1/c5)")
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
     ap.add_argument("--keycache", type=int, default=2,
                     help="min uses of a public key for the per-batch key cache (0 = off)")
@@ -432,6 +437,25 @@ def main():
         ctx.sync()
     out = ctx.download(b, n)
     ctx.free(b)
+    # one-GPU proxy of strong scaling: the rate of a 1/k shard of this batch (rank 0's
+    # contiguous slot range at N = k), timed like the headline after one warm-up pass
+    proxy = None
+    if rank == 0 and not args.no_proxy and args.config in ("c1", "c5") and world == 1:
+        proxy = {}
+        for k in (2, 4, 8):
+            m = n // k
+            bk = ctx.upload(_sample(H, np.arange(m)))
+            ctx.run(bk)
+            ctx.sync()
+            tk = time.perf_counter()
+            for _ in range(args.steps):
+                ctx.run(bk)
+                ctx.sync()
+            tk = time.perf_counter() - tk
+            ctx.free(bk)
+            rk = m * args.steps / tk
+            proxy[f"n{k}"] = {"items": m, "value": round(rk, 1), "ms_per_step": round(tk * 1e3 / args.steps, 3),
+                              "per_gpu_vs_full": round(rk / (n * args.steps / dt), 3)}
     # end to end through the blocking entry point: host SoA in, H2D, all kernels,
     # D2H of bits/beta/leader/nonce (never the headline value)
     e2e = None
@@ -538,6 +562,10 @@ def main():
     }
     if e2e:
         line["e2e"] = e2e
+    if proxy:
+        line["strong_proxy"] = dict(proxy, note="one GPU validating only the first 1/k of the batch (rank 0's "
+                                                "shard of a strong-scaling run at N = k); per_gpu_vs_full = its "
+                                                "rate / this line's value")
     if world == 1 and not args.no_cpu:
         usable, _, _ = host_cores()
         threads = max(1, min(args.cpu_workers, usable))

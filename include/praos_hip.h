@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 9
+#define PRAOS_ABI_VERSION 10
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -267,7 +267,8 @@ typedef struct {
   uint64_t* prot_minor;
   uint8_t* kes_sig;               /* n*448 */
   uint32_t* signed_len;           /* n: length of the KES message */
-  uint8_t* signed_body;           /* n*PRAOS_SIGNED_STRIDE: the KES message (serialize' hb) */
+  uint8_t* signed_body;           /* n*stride, the KES message (serialize' hb): stride PRAOS_SIGNED_STRIDE,
+                                     PRAOS_TP_SIGNED_STRIDE for praos_verify_tpraos_header_bytes */
   uint8_t* header_hash;           /* n*32 */
 } praos_decoded;
 
@@ -332,6 +333,21 @@ typedef struct {
   uint8_t* nonce;                 /* n*32: mkNonceFromOutputVRF (Blake2b-256 of the eta output) */
 } praos_tpraos_out;
 int praos_verify_tpraos_headers(praos_ctx* ctx, const praos_tpraos_headers* h, praos_tpraos_out* out);
+
+/* TPraos headers from stored bytes (ImmutableDB chunk spans of Shelley..Alonzo blocks):
+ * BHeader = [BHBody, kesSig] decoded on the device (cardano-protocol-tpraos
+ * DecCBOR BHeader / BHBody: 15 fields, the eta and leader certificates as two
+ * [output, proof] pairs, OCert and ProtVer inlined; the KES message is the canonical
+ * re-encoding `serialize' bhb`, the stored slice when canonical), then the crypto of
+ * praos_verify_tpraos_headers.  A header that does not decode gets PRAOS_BIT_INPUT.
+ * dec (may be NULL) receives the decoded fields, signed_body with a
+ * PRAOS_TP_SIGNED_STRIDE stride; leader_out / leader_proof (may be NULL, n*64 / n*80)
+ * the leader certificate.  Replaces, per epoch, the header crypto of
+ * TPraos.updateChainDepState (TPraos.hs:378-387) for eras Shelley..Alonzo
+ * (HFEras.hs:43-49); the fold is praos_tpraos_update_chain_dep_state. */
+#define PRAOS_TP_SIGNED_STRIDE 640
+int praos_verify_tpraos_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, praos_tpraos_out* out,
+                                     praos_decoded* dec, uint8_t* leader_out, uint8_t* leader_proof);
 
 /* ---- TPraos decentralisation overlay (d > 0; Shelley..Alonzo before d reached 0) ----
  * cardano-protocol-tpraos OVERLAY (lookupInOverlaySchedule, the same call
@@ -620,7 +636,18 @@ typedef struct {
   int32_t link_prev;
   const uint8_t* prev0;
   uint8_t* header_hash;
+  /* Fields the seeded corruptions may hit (PRAOS_CORRUPT_* bits; 0 = all five: OCert
+   * signature, KES signature, VRF proof, VRF output, signed body), so a single-primitive
+   * batch corrupts only what its check reads (configs[1..3]: 1 % means 1 %). */
+  uint32_t corrupt_fields;
 } praos_synth_params;
+
+#define PRAOS_CORRUPT_OCERT     0x01u  /* +1 at a byte of cold vk || hot vk || BE64 n || BE64 c0 || sigma
+                                          (the 144 bytes of an OCert verify; signature only for CBOR bodies) */
+#define PRAOS_CORRUPT_KES_SIG   0x02u
+#define PRAOS_CORRUPT_VRF_PROOF 0x04u
+#define PRAOS_CORRUPT_VRF_OUT   0x08u
+#define PRAOS_CORRUPT_BODY      0x10u
 
 /* Fills caller buffers (same layout as praos_headers; body_off/body_len/body_bytes
  * sized n, n, n*stride+8 with stride = round_up(body_len, 8), or PRAOS_SIGNED_STRIDE

@@ -152,6 +152,8 @@ struct DecOut {
   uint64_t *prot_major, *prot_minor;
   uint8_t* header_hash;
   uint16_t* status;
+  // TPraos leader certificate (header batches of praos_verify_tpraos_header_bytes; NULL otherwise)
+  uint8_t *lead_out, *lead_proof;
 };
 
 __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -171,7 +173,8 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
   const uint64_t body_start = r.pos;
   r.canon = true;
   const uint64_t arity = rd_expect(r, 4);
-  const bool tp = allow_tp && arity == 15;
+  // allow_tp: 0 Praos headers only, 1 Praos or TPraos (block batches), 2 TPraos only
+  const bool tp = allow_tp == 2 || (allow_tp == 1 && arity == 15);
   if (!r.st && arity != (tp ? 15u : 10u)) r.st = PRAOS_DEC_SYNTAX;
   const uint64_t block_no = rd_uint(r, ~0ull);
   const uint64_t slot = rd_uint(r, ~0ull);
@@ -255,6 +258,12 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
     }
   }
   const bool ok = r.st == 0;
+  if (o.lead_out) {                          // the leader certificate as SoA records (zeros on failure)
+    uint64_t* lo = (uint64_t*)(o.lead_out + 64 * i);
+    uint64_t* lp = (uint64_t*)(o.lead_proof + 80 * i);
+    for (int k = 0; k < 8; k++) lo[k] = ok && tp ? ld64u(arena, lead_out + 8 * k) : 0ull;
+    for (int k = 0; k < 10; k++) lp[k] = ok && tp ? ld64u(arena, lead_proof + 8 * k) : 0ull;
+  }
   o.status[i] = (uint16_t)(ok ? (canon ? 0u : (uint32_t)PRAOS_DEC_NONCANONICAL) : r.st);
   o.slot[i] = ok ? slot : 0;
   o.block_no[i] = ok ? block_no : 0;
@@ -288,9 +297,10 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint64_t* ocert_n, uint64_t* ocert_c0, uint64_t* body_off, uint32_t* body_len,
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
-                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride) {
+                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride, uint8_t* lead_out,
+                         uint8_t* lead_proof) {
   DecOut o{slot,     cold_vk,   vrf_vk,      vrf_out,  vrf_proof, hot_vk,       ocert_sig, kes_sig,
            ocert_n,  ocert_c0,  body_off,    body_len, signed_body, block_no,   prev_hash, prev_genesis,
-           body_size, body_hash, prot_major, prot_minor, header_hash, status};
+           body_size, body_hash, prot_major, prot_minor, header_hash, status, lead_out, lead_proof};
   hipLaunchKernelGGL(k_decode_praos, grid, block, 0, stream, n, arena, arena_len, hoff, hlen, o, allow_tp, stride);
 }

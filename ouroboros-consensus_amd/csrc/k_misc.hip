@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(NT) k_init_bcomb16(const ge_niels* gbtab, ge_n
   uint32_t w[8], r[8];
 #pragma unroll
   for (int q = 0; q < 8; q++) w[q] = 0;
-  const int bit = 16 * (int)j;                     // (k+1) << 16 j, k + 1 <= 2^15
+  const int bit = 16 * (int)j;                     // k << 16 j, 1 <= k <= 2^15
   w[bit >> 5] = k << (bit & 31);
   sc_reduce256(r, w);
   ge_p3 P;

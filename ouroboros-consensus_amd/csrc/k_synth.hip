@@ -227,7 +227,8 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   if (i >= n) return;
   // a leader schedule (praos_leader_schedule) gives slot and forging pool per
   // header; without one, slots are evenly spaced and pools hashed (not leader-valid)
-  const uint32_t p = sched_pool ? sched_pool[i] : (uint32_t)(mix64(i ^ salt) % npools);
+  // (npools >= n without a schedule: header i gets pool i, so every key is distinct)
+  const uint32_t p = sched_pool ? sched_pool[i] : npools >= n ? (uint32_t)i : (uint32_t)(mix64(i ^ salt) % npools);
   const uint64_t s = sched_slot ? sched_slot[i] : first_slot + i * slot_stride;
   const uint64_t kp = s / slots_per_kes_period;
   const uint64_t c0 = kp - (kp % 60u);          // OCert issued at a period boundary <= kp
@@ -404,10 +405,18 @@ __global__ void __launch_bounds__(64) k_synth_link(size_t n, const ge_niels* gbt
 }
 
 // Corruption model (consensus-testlib Test/Util/Corruption.hs:29-35): increment
-// the byte at offset k mod len of one chosen field.
+// the byte at offset k mod len of one chosen field; the field is drawn from the set
+// `fields` (PRAOS_CORRUPT_* bits, praos_hip.h).
+__device__ __forceinline__ void bump_be64(uint64_t* v, uint32_t byte) {   // +1 (mod 256) at byte of BE64(v)
+  const uint32_t sh = 8u * (7u - (byte & 7u));
+  const uint64_t b = ((*v >> sh) + 1u) & 0xffu;
+  *v = (*v & ~(0xffull << sh)) | (b << sh);
+}
 __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig,
                                 uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off,
-                                const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body) {
+                                const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body,
+                                uint32_t fields, uint8_t* cold_vk, uint8_t* hot_vk, uint64_t* ocert_n,
+                                uint64_t* ocert_c0) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // CBOR bodies carry copies of the OCert signature and the VRF cert: a corruption
@@ -438,10 +447,27 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
   const bool c = (r % 10000u) < per10000;
   corrupted[i] = c ? 1 : 0;
   if (!c) return;
-  const uint32_t which = (uint32_t)((r >> 20) % 5u);
+  // the (r >> 20) % popcount(fields)-th set bit of fields picks the field
+  const uint32_t nf = (uint32_t)__popc(fields & 0x1fu);
+  uint32_t pick = (uint32_t)((r >> 20) % (nf ? nf : 1u)), which = 0;
+  for (uint32_t f = 0; f < 5; f++)
+    if (fields & (1u << f)) {
+      if (pick == 0) { which = f; break; }
+      pick--;
+    }
   const uint32_t k = (uint32_t)(r >> 32);
   switch (which) {
     case 0:
+      if (fields != 0x1fu && !cbor_body) {       // the OCert verify's 144 input bytes
+        const uint32_t o = k % 144u;
+        if (o < 32) cold_vk[32 * i + o] += 1;
+        else if (o < 64) hot_vk[32 * i + o - 32] += 1;
+        else if (o < 72) bump_be64(ocert_n + i, o - 64);
+        else if (o < 80) bump_be64(ocert_c0 + i, o - 72);
+        else ocert_sig[64 * i + o - 80] += 1;
+        corrupted[i] = 1;
+        break;
+      }
       ocert_sig[64 * i + k % 64] += 1; corrupted[i] = 1;
       if (at_ocert_sig >= 0) body_bytes[body_off[i] + at_ocert_sig + k % 64] += 1;
       break;
@@ -513,7 +539,9 @@ void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint6
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt,
                           uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out,
                           uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len,
-                          uint8_t* corrupted, uint8_t* l_proof, int cbor_body) {
+                          uint8_t* corrupted, uint8_t* l_proof, int cbor_body, uint32_t fields, uint8_t* cold_vk,
+                          uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0) {
   hipLaunchKernelGGL(k_synth_corrupt, grid, block, 0, stream, n, per10000, salt, ocert_sig, kes_sig, vrf_proof,
-                     vrf_out, body_bytes, body_off, body_len, corrupted, l_proof, cbor_body);
+                     vrf_out, body_bytes, body_off, body_len, corrupted, l_proof, cbor_body, fields, cold_vk, hot_vk,
+                     ocert_n, ocert_c0);
 }

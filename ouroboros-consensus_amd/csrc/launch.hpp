@@ -85,7 +85,7 @@ void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint6
                                 uint32_t p0, uint32_t pn, const uint32_t* vrf_x, const uint32_t* vrf_pk,
                                 const uint32_t* pool_thr, const uint32_t* eta0, int eta0_neutral, int f_is_one,
                                 int tpraos, int32_t* leader);
-void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body);
+void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body, uint32_t fields, uint8_t* cold_vk, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0);
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs,
                    const int32_t* ovl_class, const uint32_t* gen);
 void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena, uint64_t arena_len,
@@ -94,7 +94,7 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint64_t* ocert_n, uint64_t* ocert_c0, uint64_t* body_off, uint32_t* body_len,
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
-                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride);
+                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride, uint8_t* lead_out = nullptr, uint8_t* lead_proof = nullptr);
 void launch_block_split(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
                         uint64_t arena_len, uint64_t* off_io, uint32_t* len_io, uint64_t* seg_off, uint32_t* seg_len,
                         uint8_t* nseg, uint8_t* status);

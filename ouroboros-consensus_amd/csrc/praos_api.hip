@@ -93,6 +93,8 @@ struct praos_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};   // concurrent crypto kernels
+  hipStream_t mside[3] = {nullptr, nullptr, nullptr};  // their key-cache misses (uncached verifies)
+  hipEvent_t mdone_ev[3] = {};
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
@@ -244,6 +246,10 @@ struct praos_batch {
   uint32_t* eta_tab = nullptr;
   uint8_t* eta_idx = nullptr;
   bool decoded = false;          // praos_batch_decode ran: praos_batch_run skips the decode
+  // TPraos header batches from stored bytes (praos_verify_tpraos_header_bytes): the
+  // decoded leader certificate and its beta
+  bool tp_only = false;
+  uint8_t *lead_out = nullptr, *lead_proof = nullptr, *beta_l = nullptr;
   uint64_t *blk_off = nullptr, *seg_off = nullptr;
   uint32_t *blk_len = nullptr, *seg_len = nullptr;
   uint8_t *nseg = nullptr, *split_status = nullptr, *seg_hash = nullptr, *blk_result = nullptr, *blk_hash = nullptr;
@@ -253,7 +259,7 @@ struct praos_batch {
 };
 
 static constexpr size_t KT_BYTES = 16 * 8 * 4 * 32; // per cached key: 16 tables x 8 cached points
-static constexpr uint32_t KC_MAX_ENTRIES = 1u << 16;
+static constexpr uint32_t KC_MAX_ENTRIES = 1u << 20;   // a key used twice already pays for its tables
 
 #define HIPCHK(ctx, x)                                                                    \
   do {                                                                                    \
@@ -309,12 +315,14 @@ praos_ctx* praos_open(int device) {
   c->device = device;
   if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+    c->stream = nullptr;
+    praos_close(c);
     return nullptr;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
   for (auto& e : c->miss_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : c->mdone_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
@@ -328,18 +336,46 @@ praos_ctx* praos_open(int device) {
     for (int k = 0; k < 3; k++) {
       const bool hi = pe && std::strlen(pe) == 3 && pe[k] == '1';
       (void)hipStreamCreateWithPriority(&c->side[k], hipStreamNonBlocking, hi ? greatest : least);
+      // each kind's misses get a stream of their own at the same priority: a handful of
+      // uncached verifies is one full-length chain of latency, and three of them in a
+      // row on one stream were the critical path of small batches (54k headers: k_kes
+      // 2.1 ms -> k_vrf 3.4 ms -> k_ocert 1.6 ms, profiles/r03b/timeline.txt)
+      (void)hipStreamCreateWithPriority(&c->mside[k], hipStreamNonBlocking, hi ? greatest : least);
     }
   }
-  if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
+  if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) {
+    c->btab = nullptr;
+    praos_close(c);
+    return nullptr;
+  }
   launch_init_btab(dim3(BCOMB_TABLES * BTAB_N / 256), dim3(256), c->stream, c->btab);
-  if (hipMalloc(&c->bcomb16, C16_TABLES * C16_ENTRIES * NIELS_BYTES) != hipSuccess) { delete c; return nullptr; }
-  launch_init_bcomb16(c->stream, c->btab, c->bcomb16);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) {
     fprintf(stderr, "praos_open: init kernel failed\n");
-    delete c;
+    praos_close(c);
     return nullptr;
   }
   return c;
+}
+
+// The radix-2^16 comb of the cached-key chains (48 MB, scalarmult.hpp C16_T x C16_N):
+// built on the first run that uses a key cache, on the ctx stream (the kernels that
+// read it are ordered after it), then kept for the context's lifetime.
+static int ensure_bcomb16(praos_ctx* c) {
+  if (c->bcomb16) return PRAOS_OK;
+  ge_niels* t = nullptr;
+  if (hipMalloc(&t, C16_TABLES * C16_ENTRIES * NIELS_BYTES) != hipSuccess) {
+    c->err = "praos: radix-2^16 comb allocation (48 MB) failed";
+    return PRAOS_E_OOM;
+  }
+  launch_init_bcomb16(c->stream, c->btab, t);
+  if (hipGetLastError() != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(t);
+    c->err = "praos: comb init launch failed";
+    return PRAOS_E_HIP;
+  }
+  c->bcomb16 = t;
+  return PRAOS_OK;
 }
 
 static void free_epoch(praos_ctx* c) {
@@ -352,7 +388,7 @@ void praos_close(praos_ctx* c) {
   if (!c) return;
   if (c->device < 0) { delete c; return; }
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_epoch(c);
   free_spare(c);
   (void)hipFree(c->d_gen);
@@ -363,11 +399,13 @@ void praos_close(praos_ctx* c) {
     if (c->pin[k]) (void)hipHostFree(c->pin[k]);
     if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
   }
-  for (auto& e : c->ev) (void)hipEventDestroy(e);
-  for (auto& e : c->side_ev) (void)hipEventDestroy(e);
-  for (auto& e : c->miss_ev) (void)hipEventDestroy(e);
-  for (auto& st : c->side) (void)hipStreamDestroy(st);
-  (void)hipStreamDestroy(c->stream);
+  for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->side_ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->miss_ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->mdone_ev) if (e) (void)hipEventDestroy(e);
+  for (auto& st : c->side) if (st) (void)hipStreamDestroy(st);
+  for (auto& st : c->mside) if (st) (void)hipStreamDestroy(st);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -590,7 +628,13 @@ praos_batch* praos_batch_upload(praos_ctx* c, const praos_headers* h) {
   return b;
 }
 
+static praos_batch* upload_bytes_impl(praos_ctx* c, const praos_header_bytes* in, bool tpraos);
+
 praos_batch* praos_batch_upload_bytes(praos_ctx* c, const praos_header_bytes* in) {
+  return upload_bytes_impl(c, in, false);
+}
+
+static praos_batch* upload_bytes_impl(praos_ctx* c, const praos_header_bytes* in, bool tpraos) {
   if (!c || !in || (in->n && (!in->off || !in->len || (!in->bytes && in->bytes_len)))) return nullptr;
   if (c->device < 0) { c->err = "host-only context: no HIP device"; return nullptr; }
   if (hipSetDevice(c->device) != hipSuccess) return nullptr;
@@ -600,8 +644,15 @@ praos_batch* praos_batch_upload_bytes(praos_ctx* c, const praos_header_bytes* in
   b->n = n;
   b->from_bytes = true;
   b->arena_len = in->bytes_len;
-  b->body_bytes_len = (size_t)PRAOS_SIGNED_STRIDE * n;
+  b->tp_only = tpraos;
+  b->signed_stride = tpraos ? TP_SIGNED_STRIDE : PRAOS_SIGNED_STRIDE;
+  b->body_bytes_len = (size_t)b->signed_stride * n;
   bool ok = alloc_soa(b, n, b->body_bytes_len + 16);
+  if (tpraos) {
+    ok &= dalloc(b, &b->lead_out, 64 * n) == hipSuccess;
+    ok &= dalloc(b, &b->lead_proof, 80 * n) == hipSuccess;
+    ok &= dalloc(b, &b->beta_l, 64 * n) == hipSuccess;
+  }
   ok &= dalloc(b, &b->arena, ((in->bytes_len + 7) & ~(size_t)7) + 16) == hipSuccess;  // +16: ld64u pad
   ok &= dalloc(b, &b->hoff, 8 * n) == hipSuccess;
   ok &= dalloc(b, &b->hlen, 4 * n) == hipSuccess;
@@ -635,16 +686,36 @@ static int batch_decode(praos_ctx* c, praos_batch* b) {
                       b->slot, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->hot_vk, b->ocert_sig, b->kes_sig,
                       b->ocert_n, b->ocert_c0, b->body_off, b->body_len, b->body, b->block_no, b->prev_hash,
                       b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor, b->header_hash,
-                      b->dec_status, b->is_block ? 1 : 0, b->signed_stride);
+                      b->dec_status, b->is_block ? 1 : (b->tp_only ? 2 : 0), b->signed_stride, b->lead_out,
+                      b->lead_proof);
   return hipGetLastError() == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
 }
+
+static int batch_run_impl(praos_ctx* c, praos_batch* b);
 
 int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (!c || !b) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
   HIPCHK(c, hipSetDevice(c->device));
+  if (b->n == 0) return PRAOS_OK;
+  const int r = batch_run_impl(c, b);
+  if (r != PRAOS_OK && c->concurrent) {
+    // work already queued on the side streams must be ordered before anything the ctx
+    // stream runs next (praos_batch_free hands this batch's buffers to the next upload)
+    for (int k = 0; k < 3; k++) {
+      if (hipEventRecord(c->side_ev[k], c->side[k]) != hipSuccess ||
+          hipStreamWaitEvent(c->stream, c->side_ev[k], 0) != hipSuccess)
+        (void)hipStreamSynchronize(c->side[k]);
+      if (hipEventRecord(c->mdone_ev[k], c->mside[k]) != hipSuccess ||
+          hipStreamWaitEvent(c->stream, c->mdone_ev[k], 0) != hipSuccess)
+        (void)hipStreamSynchronize(c->mside[k]);
+    }
+  }
+  return r;
+}
+
+static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   const size_t n = b->n;
-  if (n == 0) return PRAOS_OK;
   const praos_params& P = c->params;
   uint16_t* bo = b->bits3;
   uint16_t* bk = b->bits3 + n;
@@ -665,6 +736,10 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
     }
   }
+  if (c->keycache > 0 && n >= 2) {     // the comb is read by the cached chains: built before ev[0]
+    const int rc = ensure_bcomb16(c);
+    if (rc != PRAOS_OK) return rc;
+  }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[0], 0));
@@ -672,14 +747,15 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   b->kc_used = kc;
   // key cache prepass on the kernel's own stream: hash set, entries, hit/miss lists, tables
   // (items: all n, or list[0 .. *count) when list != null)
-  // Miss lists go to the main stream as soon as their partition is known, so the
-  // uncached verifies run during the latency-bound key precompute instead of
-  // trailing the cached chains (ev_miss[t]: the partition of cache t is done).
-  hipStream_t sm = c->stream;
+  // Each miss list goes to its own stream as soon as its partition is known, so the
+  // uncached verifies run during the latency-bound key precompute, beside each other,
+  // instead of trailing the cached chains (miss_ev[t]: the partition of cache t is done).
+  hipStream_t sm_[3] = {c->concurrent ? c->mside[0] : c->stream, c->concurrent ? c->mside[1] : c->stream,
+                        c->concurrent ? c->mside[2] : c->stream};
   auto to_main = [&](int t, hipStream_t st) -> int {
-    if (st == sm) return PRAOS_OK;
+    if (st == sm_[t]) return PRAOS_OK;
     HIPCHK(c, hipEventRecord(c->miss_ev[t], st));
-    HIPCHK(c, hipStreamWaitEvent(sm, c->miss_ev[t], 0));
+    HIPCHK(c, hipStreamWaitEvent(sm_[t], c->miss_ev[t], 0));
     return PRAOS_OK;
   };
   auto keycache_lists = [&](praos_batch::KeyCache& k, const uint8_t* keys, hipStream_t st,
@@ -699,11 +775,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
                           k.entry_rep, keys, k.ktab, k.kinfo, c->key_wave_prio);
   };
   b->dd_used = false;
-  // The OCert misses (a few dozen items, but one full uncached verify of latency) and,
-  // with the dedup, the fanout that needs them go to the END of the main stream's queue
-  // when the streams are concurrent, so the KES / VRF misses behind them start early.
   std::function<void()> ocert_miss;
-  const bool defer_ocert = so != sm;
   if ((c->kernels & 1) && c->dedup && n >= 2) {
     // distinct OCert tuples only; their verdicts fan out to every header carrying them
     b->dd_used = true;
@@ -717,7 +789,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
       ocert_miss = [&, k]() {
-        launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+        launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
                      b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
@@ -733,8 +805,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     auto fan = ocert_miss;
     ocert_miss = [&, fan, kc]() {
       if (fan) fan();
-      if (kc && so != sm) {
-        (void)hipEventRecord(c->miss_ev[3], sm);
+      if (kc && so != sm_[0]) {
+        (void)hipEventRecord(c->miss_ev[3], sm_[0]);
         (void)hipStreamWaitEvent(so, c->miss_ev[3], 0);
       }
       launch_ocert_fanout(g, blk, so, n, b->dd_item_rep, b->dd_ok, b->slot, b->ocert_c0, P.slots_per_kes_period,
@@ -747,7 +819,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
       ocert_miss = [&, k]() {
-        launch_ocert(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+        launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
                      b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr,
                      b->tab_ocert);
       };
@@ -763,8 +835,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   } else {
     HIPCHK(c, hipMemsetAsync(bo, 0, 2 * n, so));
   }
-  if (ocert_miss && !defer_ocert) ocert_miss();
-  if (!defer_ocert) HIPCHK(c, hipEventRecord(c->side_ev[0], so));
+  if (ocert_miss) ocert_miss();
+  HIPCHK(c, hipEventRecord(c->side_ev[0], so));
   if (c->kernels & 2) {
     if (kc) {
       // leaf-key cache: the Ed25519 key a Sum6KES signature ends on repeats for every
@@ -774,7 +846,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       int r = keycache_lists(k, b->kes_leaf, sk);
       if (r == PRAOS_OK) r = to_main(1, sk);
       if (r != PRAOS_OK) return r;
-      launch_kes(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
+      launch_kes(g, blk, sm_[1], n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
                  b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
                  bk, (uint8_t*)nullptr, b->tab_kes);
       keycache_precompute(k, b->kes_leaf, 0, sk);
@@ -796,7 +868,7 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
       int r = keycache_lists(k, b->vrf_vk, sv);
       if (r == PRAOS_OK) r = to_main(2, sv);
       if (r != PRAOS_OK) return r;
-      launch_vrf(g, blk, sm, n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
+      launch_vrf(g, blk, sm_[2], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
                  b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
                  (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
                  b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
@@ -817,12 +889,13 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(b->pool_sorted, 0xff, 4 * n, sv));   // no pool -> leader kernel skips
   }
   HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
-  if (defer_ocert) {
-    if (ocert_miss) ocert_miss();
-    HIPCHK(c, hipEventRecord(c->side_ev[0], so));
-  }
-  if (c->concurrent)
+  if (c->concurrent) {
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
+    for (int k = 0; k < 3; k++) {
+      HIPCHK(c, hipEventRecord(c->mdone_ev[k], c->mside[k]));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->mdone_ev[k], 0));
+    }
+  }
   launch_leader(g, blk, c->stream, n, b->leader, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
                 (int)P.f_is_one, 8, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
                 b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
@@ -1069,7 +1142,7 @@ int praos_batch_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d)
   HIPCHK(c, dn(d->prot_minor, b->prot_minor, 8 * n));
   HIPCHK(c, dn(d->kes_sig, b->kes_sig, 448 * n));
   HIPCHK(c, dn(d->signed_len, b->body_len, 4 * n));
-  HIPCHK(c, dn(d->signed_body, b->body, (size_t)PRAOS_SIGNED_STRIDE * n));
+  HIPCHK(c, dn(d->signed_body, b->body, (size_t)b->signed_stride * n));
   HIPCHK(c, dn(d->header_hash, b->header_hash, 32 * n));
   return PRAOS_OK;
 }
@@ -1814,7 +1887,8 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
                         dksig, dhscr, dhh);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
                        salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
-                       sp->body_len == 0 ? 1 : 0);
+                       sp->body_len == 0 ? 1 : 0, sp->corrupt_fields ? sp->corrupt_fields : 0x1fu, dcold, dhot, dn,
+                       dc0);
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1990,6 +2064,51 @@ int praos_overlay_classify(praos_ctx* c, size_t n, const uint64_t* slots, int32_
 
 // TPraos batch: OCert + KES kernels are shared with Praos; VRF checks use the
 // two-certificate kernel and the leader test the 2^512 bound.
+// TPraos crypto over a batch whose SoA is on the device (uploaded from host arrays, or
+// decoded from stored bytes): OCERT, KES, OVERLAY praosVrfChecks (k_vrf_tp) and the
+// 2^512 leader test; overlay classes from the host slots (praos_set_overlay).
+static int tpraos_run(praos_ctx* c, praos_batch* b, const uint8_t* dlout, const uint8_t* dlproof, uint8_t* dbeta_l,
+                      const uint64_t* host_slots) {
+  const size_t n = b->n;
+  int32_t* dcls = nullptr;
+  if (c->ovl_on) {
+    if (dalloc(b, &dcls, 4 * n) != hipSuccess) return PRAOS_E_OOM;
+    std::vector<int32_t> cls(n);
+    for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, host_slots[i]);
+    HIPCHK(c, hipMemcpy(dcls, cls.data(), 4 * n, hipMemcpyHostToDevice));
+  }
+  const praos_params& P = c->params;
+  const dim3 g(nblocks(n, NT)), blk(NT);
+  uint16_t* bo = b->bits3;
+  uint16_t* bk = b->bits3 + n;
+  uint16_t* bv = b->bits3 + 2 * n;
+  launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+               b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
+  launch_kes(g, blk, c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
+             b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
+             (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
+  launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
+                b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
+                (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce, b->tab_vrf,
+                dcls, c->d_gen);
+  launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr, (int)P.f_is_one,
+                16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
+                b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
+  HIPCHK(c, hipGetLastError());
+  return PRAOS_OK;
+}
+
+static int tpraos_download(praos_ctx* c, praos_batch* b, const uint8_t* dbeta_l, praos_tpraos_out* out) {
+  const size_t n = b->n;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, d2h(c, out->bits, b->bits, 2 * n));
+  if (out->pool_idx) HIPCHK(c, d2h(c, out->pool_idx, b->pool_idx, 4 * n));
+  if (out->beta_eta) HIPCHK(c, d2h(c, out->beta_eta, b->beta, 64 * n));
+  if (out->beta_leader) HIPCHK(c, d2h(c, out->beta_leader, dbeta_l, 64 * n));
+  if (out->nonce) HIPCHK(c, d2h(c, out->nonce, b->nonce, 32 * n));
+  return PRAOS_OK;
+}
+
 int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, praos_tpraos_out* out) {
   if (!c || !th || !out || !out->bits || !th->leader_out || !th->leader_proof) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
@@ -1998,48 +2117,48 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
   praos_batch* b = praos_batch_upload(c, &th->h);
   if (!b) return PRAOS_E_OOM;
   uint8_t *dlout = nullptr, *dlproof = nullptr, *dbeta_l = nullptr;
-  int32_t* dcls = nullptr;
   int rc = PRAOS_OK;
   if (dalloc(b, &dlout, 64 * n) != hipSuccess || dalloc(b, &dlproof, 80 * n) != hipSuccess ||
-      dalloc(b, &dbeta_l, 64 * n) != hipSuccess || (c->ovl_on && dalloc(b, &dcls, 4 * n) != hipSuccess)) {
+      dalloc(b, &dbeta_l, 64 * n) != hipSuccess) {
     praos_batch_free(c, b);
     return PRAOS_E_OOM;
   }
-  const praos_params& P = c->params;
-  const dim3 g(nblocks(n, NT)), blk(NT);
-  uint16_t* bo = b->bits3;
-  uint16_t* bk = b->bits3 + n;
-  uint16_t* bv = b->bits3 + 2 * n;
   auto body = [&]() -> int {
     HIPCHK(c, hipMemcpy(dlout, th->leader_out, 64 * n, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
-    if (c->ovl_on) {
-      std::vector<int32_t> cls(n);
-      for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, th->h.slot[i]);
-      HIPCHK(c, hipMemcpy(dcls, cls.data(), 4 * n, hipMemcpyHostToDevice));
-    }
-    launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot,
-                 P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
-    launch_kes(g, blk, c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len, b->body,
-               b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr, bk,
-               (uint8_t*)nullptr, b->tab_kes);
-    launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
-                  b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
-                  (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce, b->tab_vrf,
-                  dcls, c->d_gen);
-    launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
-                  (int)P.f_is_one, 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
-                  (const uint16_t*)nullptr);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(out->bits, b->bits, 2 * n, hipMemcpyDeviceToHost));
-    if (out->pool_idx) HIPCHK(c, hipMemcpy(out->pool_idx, b->pool_idx, 4 * n, hipMemcpyDeviceToHost));
-    if (out->beta_eta) HIPCHK(c, hipMemcpy(out->beta_eta, b->beta, 64 * n, hipMemcpyDeviceToHost));
-    if (out->beta_leader) HIPCHK(c, hipMemcpy(out->beta_leader, dbeta_l, 64 * n, hipMemcpyDeviceToHost));
-    if (out->nonce) HIPCHK(c, hipMemcpy(out->nonce, b->nonce, 32 * n, hipMemcpyDeviceToHost));
-    return PRAOS_OK;
+    const int r = tpraos_run(c, b, dlout, dlproof, dbeta_l, th->h.slot);
+    return r == PRAOS_OK ? tpraos_download(c, b, dbeta_l, out) : r;
   };
   rc = body();
+  praos_batch_free(c, b);
+  return rc;
+}
+
+int praos_verify_tpraos_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_tpraos_out* out,
+                                     praos_decoded* dec, uint8_t* leader_out, uint8_t* leader_proof) {
+  if (!c || !in || !out || !out->bits) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  const size_t n = in->n;
+  if (n == 0) return PRAOS_OK;
+  praos_batch* b = upload_bytes_impl(c, in, true);
+  if (!b) return PRAOS_E_OOM;
+  auto body = [&]() -> int {
+    const int rd = batch_decode(c, b);
+    if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
+    std::vector<uint64_t> slots;
+    if (c->ovl_on) {             // the overlay schedule is classified on the host from the decoded slots
+      slots.resize(n);
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpy(slots.data(), b->slot, 8 * n, hipMemcpyDeviceToHost));
+    }
+    int r = tpraos_run(c, b, b->lead_out, b->lead_proof, b->beta_l, slots.data());
+    if (r == PRAOS_OK) r = tpraos_download(c, b, b->beta_l, out);
+    if (r == PRAOS_OK && dec) r = praos_batch_download_decoded(c, b, dec);
+    if (r == PRAOS_OK && leader_out) HIPCHK(c, d2h(c, leader_out, b->lead_out, 64 * n));
+    if (r == PRAOS_OK && leader_proof) HIPCHK(c, d2h(c, leader_proof, b->lead_proof, 80 * n));
+    return r;
+  };
+  const int rc = body();
   praos_batch_free(c, b);
   return rc;
 }

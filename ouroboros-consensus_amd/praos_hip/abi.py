@@ -42,6 +42,8 @@ BIT_INPUT = 0x8000
 HOST_ONLY = -1
 BIT_TP_VRF_NONCE = 0x0400
 BIT_TP_VRF_LEADER = 0x0800
+# praos_synth_params.corrupt_fields
+CORRUPT_OCERT, CORRUPT_KES_SIG, CORRUPT_VRF_PROOF, CORRUPT_VRF_OUT, CORRUPT_BODY = 0x01, 0x02, 0x04, 0x08, 0x10
 
 # verdicts (enum praos_verdict)
 V_OK, V_KES_BEFORE_START, V_KES_AFTER_END, V_OCERT_SIG, V_KES_SIG, V_COUNTER_MISSING, \
@@ -131,7 +133,8 @@ class SynthParams(ctypes.Structure):
                 ("slot_stride", ctypes.c_uint64), ("body_len", ctypes.c_uint32),
                 ("corrupt_per_10000", ctypes.c_uint32), ("nkes", ctypes.c_uint32), ("seed", ctypes.c_uint8 * 32),
                 ("body_hash", u8p), ("sched_slot", u64p), ("sched_pool", u32p), ("block_no0", ctypes.c_uint64),
-                ("link_prev", ctypes.c_int32), ("prev0", u8p), ("header_hash", u8p)]
+                ("link_prev", ctypes.c_int32), ("prev0", u8p), ("header_hash", u8p),
+                ("corrupt_fields", ctypes.c_uint32)]
 
 
 class HeaderBytes(ctypes.Structure):
@@ -159,6 +162,7 @@ DEC_RANGE, DEC_SYNTAX, DEC_SIZE, DEC_UNSUPPORTED, DEC_TRAILING, DEC_NONCANONICAL
     0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40
 DEC_FAILED = 0x5F
 SIGNED_STRIDE = 448
+TP_SIGNED_STRIDE = 640
 
 # every entry point declared in include/praos_hip.h: name -> (restype, argtypes)
 SIGNATURES = {
@@ -234,6 +238,8 @@ SIGNATURES = {
     "praos_decode_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.POINTER(Decoded)]),
     "praos_verify_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.POINTER(Out),
                                                  ctypes.POINTER(Decoded)]),
+    "praos_verify_tpraos_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
+                                                        ctypes.POINTER(TPOut), ctypes.POINTER(Decoded), u8p, u8p]),
     "praos_batch_upload_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
     "praos_batch_download_decoded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(Decoded)]),
     "praos_batch_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
@@ -515,8 +521,9 @@ class Context:
         return s
 
     @staticmethod
-    def alloc_decoded(n):
-        D = {name: np.zeros((n,) + shp, dt) for name, dt, shp in DECODED_FIELDS}
+    def alloc_decoded(n, stride=SIGNED_STRIDE):
+        D = {name: np.zeros((n,) + (shp if name != "signed_body" else (stride,)), dt)
+             for name, dt, shp in DECODED_FIELDS}
         d = Decoded()
         for name, dt, _ in DECODED_FIELDS:
             setattr(d, name, ptr(D[name], _CT[dt]))
@@ -547,6 +554,31 @@ class Context:
         self.check(self.L.praos_verify_header_bytes(self.h, ctypes.byref(hb), ctypes.byref(os_),
                                                     ctypes.byref(d) if d is not None else None))
         return (o, D) if decoded else o
+
+    def verify_tpraos_header_bytes(self, arena, off, length, decoded=False):
+        """Stored TPraos headers (BHeader = [BHBody, kesSig], Shelley..Alonzo) decoded and
+        verified on the GPU (praos_verify_tpraos_header_bytes).  Returns the TPraos outputs
+        (bits, pool_idx, beta_eta, beta_leader, nonce); with decoded=True also the decoded
+        fields plus leader_out / leader_proof."""
+        arena, off, length = self._chunk(arena, off, length)
+        n = len(off)
+        hb = self.header_bytes_struct(arena, off, length)
+        o = {"bits": np.zeros(n, np.uint16), "pool_idx": np.zeros(n, np.int32),
+             "beta_eta": np.zeros((n, 64), np.uint8), "beta_leader": np.zeros((n, 64), np.uint8),
+             "nonce": np.zeros((n, 32), np.uint8)}
+        to = TPOut()
+        to.bits, to.pool_idx = ptr(o["bits"], u16p), ptr(o["pool_idx"], i32p)
+        to.beta_eta, to.beta_leader, to.nonce = ptr(o["beta_eta"]), ptr(o["beta_leader"]), ptr(o["nonce"])
+        D, d = self.alloc_decoded(n, TP_SIGNED_STRIDE) if decoded else (None, None)
+        lo = np.zeros((n, 64), np.uint8) if decoded else None
+        lp = np.zeros((n, 80), np.uint8) if decoded else None
+        self.check(self.L.praos_verify_tpraos_header_bytes(self.h, ctypes.byref(hb), ctypes.byref(to),
+                                                           ctypes.byref(d) if d is not None else None,
+                                                           ptr(lo) if decoded else None, ptr(lp) if decoded else None))
+        if not decoded:
+            return o
+        D["leader_out"], D["leader_proof"] = lo, lp
+        return o, D
 
     # ---- stored blocks: verifyBlockIntegrity (k_block.hip) ----
     def verify_block_integrity(self, arena, off, length, slots_per_kes_period):
@@ -800,7 +832,7 @@ class Context:
 
     def synthesize(self, n, npools, params: Params, eta0, seed: bytes, first_slot=0, slot_stride=20,
                    body_len=397, corrupt_per_10000=0, nkes=0, tpraos=False, body_hash=None, schedule=None,
-                   block_no0=0, link=False, prev0=None):
+                   block_no0=0, link=False, prev0=None, corrupt_fields=0):
         """schedule: (slots u64[n], pools u32[n]) from leader_schedule (a leader-valid chain), or None
         (evenly spaced slots, pools by hash: not leader-valid).  link=True chains the headers
         (prevHash = headerHash of the previous header; header 0: prev0, None = GenesisHash) and
@@ -826,6 +858,7 @@ class Context:
         sp.slot_stride = slot_stride
         sp.body_len = body_len
         sp.corrupt_per_10000 = corrupt_per_10000
+        sp.corrupt_fields = corrupt_fields
         sp.nkes = nkes
         ctypes.memmove(sp.seed, seed, 32)
         bstride = (body_len + 7) & ~7 if body_len else SIGNED_STRIDE   # 0: genuine CBOR bodies

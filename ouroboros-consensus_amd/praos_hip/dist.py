@@ -44,6 +44,28 @@ def gather_verdicts(bits_u16: np.ndarray, device=None):
     return np.concatenate([p[:int(s.item())].cpu().numpy().astype(np.uint16) for p, s in zip(parts, sizes)])
 
 
+def gather_rows(a: np.ndarray, device=None) -> np.ndarray:
+    """All-gather of per-rank row arrays (e.g. beta n x 64 bytes, pool_idx i32[n]) in rank
+    (= slot) order; any fixed-width dtype, ragged row counts.  Returns the concatenation
+    on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    a = np.ascontiguousarray(a)
+    width = int(a.dtype.itemsize * (int(np.prod(a.shape[1:])) if a.ndim > 1 else 1))
+    raw = a.view(np.uint8).reshape(len(a), width)
+    n = torch.tensor([len(a)], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    m = int(max(int(s.item()) for s in sizes))
+    buf = torch.zeros((m, width), dtype=torch.uint8, device=device)
+    buf[:len(a)] = torch.from_numpy(raw).to(buf.device)
+    parts = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out = np.concatenate([p[:int(s.item())].cpu().numpy() for p, s in zip(parts, sizes)])
+    return out.view(a.dtype).reshape((-1,) + a.shape[1:])
+
+
 def max_over_ranks(seconds: float, device=None) -> float:
     import torch
     import torch.distributed as dist

@@ -1,17 +1,33 @@
 """Fixed E34 host helpers (cardano-ledger-core `FixedPoint` = Data.Fixed E34).
 
-`fromRational q` floors q * 10^34 (Data.Fixed); `activeSlotLog f` is the raw
-Fixed value of ln'(1 - f) computed by cardano-ledger-core `NonIntegral.ln'`
-(a continued fraction evaluated in FixedPoint).  That library is not in
-/root/reference, so `active_slot_log` here returns floor(10^34 * ln(1 - f))
-from a 100-digit evaluation: PARITY UNPINNED in the last digits of c.  The
-batch validator takes c_raw as an input (praos_params.c_raw), so a caller that
-has the reference's own activeSlotLog value gets bit-exact leader decisions.
+`from_rational q` floors q * 10^34 (Data.Fixed `fromRational`).  `active_slot_log f`
+is `unActiveSlotLog` of cardano-ledger-core `mkActiveSlotCoeff`:
+
+    floor (fpPrecision * ln' ((1 :: FixedPoint) - fromRational f))     (0 when f = 1)
+
+= the raw Fixed E34 value of `NonIntegral.ln'` (1 - f), evaluated IN FixedPoint: the
+integral part n with e^n <= x < e^(n+1) (`findE`, e = `exp' 1` from the Taylor series),
+x / e^n - 1 (`splitLn`), and ln(1 + z) by its continued fraction
+z/(1 + 1^2 z/(2 + 1^2 z/(3 + 2^2 z/(4 + 2^2 z/(5 + ...))))) through the Wallis
+recurrences (`lncf` / `cf`), stopping when two convergents differ by less than
+`EPS` or after `MAX_N` steps.  Every FixedPoint operation truncates as Data.Fixed
+does: a * b = floor(a b / 10^34), a / b = floor(a 10^34 / b).
+
+cardano-ledger-core is not in /root/reference, so this follows the
+published NonIntegral algorithm with its constants as recalled (MAX_N = 1000,
+EPS = 10^-24), not a vendored source: the low digits of c_raw are PARITY UNPINNED.
+The leader decisions are pinned anyway: tests/test_gpu_group.py::
+test_c5_full_epoch_single_and_group8 shows every header of the 432k C5 chain keeps its
+decision for any c within 10^-12 (relative) of this value -- ten orders of magnitude
+wider than any difference two evaluations of ln' to 10^-24 can have -- and the batch
+validator takes c_raw as an input (praos_params.c_raw), so a caller holding the
+reference's own activeSlotLog gets its decisions bit-exact.
 """
-from decimal import Decimal, getcontext
 from fractions import Fraction
 
 R = 10 ** 34
+MAX_N = 1000
+EPS = R // 10 ** 24                 # 10^-24 as a raw Fixed E34 value
 
 
 def from_rational(q) -> int:
@@ -19,7 +35,102 @@ def from_rational(q) -> int:
     return (q.numerator * R) // q.denominator
 
 
+# ---- Data.Fixed E34 on raw integers (Haskell div = floor)
+def _mul(a: int, b: int) -> int:
+    return (a * b) // R
+
+
+def _div(a: int, b: int) -> int:
+    return (a * R) // b
+
+
+def _ipow_pos(x: int, n: int) -> int:
+    """NonIntegral ipow' (exponentiation by squaring, FixedPoint products)."""
+    if n == 0:
+        return R
+    d, m = divmod(n, 2)
+    if m == 0:
+        y = _ipow_pos(x, d)
+        return _mul(y, y)
+    return _mul(x, _ipow_pos(x, n - 1))
+
+
+def _ipow(x: int, n: int) -> int:
+    return _div(R, _ipow_pos(x, -n)) if n < 0 else _ipow_pos(x, n)
+
+
+def _taylor_exp(x: int) -> int:
+    """exp x for 0 <= x <= 1: 1 + x + x^2/2! + ..., term_k = term_{k-1} x / k."""
+    acc, last, k = R, R, 1
+    while k < MAX_N:
+        nxt = _div(_mul(last, x), k * R)
+        if abs(nxt) < EPS:
+            break
+        acc += nxt
+        last = nxt
+        k += 1
+    return acc
+
+
+def _exp(x: int) -> int:
+    """NonIntegral exp': scale x into [0, 1] by n = ceiling x, then the n-th power."""
+    if x < 0:
+        return _div(R, _exp(-x))
+    n = -(-x // R)
+    if n == 0:
+        return R
+    return _ipow(_taylor_exp(_div(x, n * R)), n)
+
+
+def _find_e(e: int, x: int) -> int:
+    """n with e^n <= x < e^(n+1)."""
+    n = 0
+    if x >= R:
+        while _ipow(e, n + 1) <= x:
+            n += 1
+    else:
+        while _ipow(e, n) > x:
+            n -= 1
+    return n
+
+
+def _lncf(z: int) -> int:
+    """ln(1 + z), z >= 0, by the continued fraction (Wallis recurrences in FixedPoint)."""
+    a_m2, b_m2, a_m1, b_m1 = R, 0, 0, R          # (A_-1, B_-1), (A_0, B_0)
+    conv = 0
+    for n in range(1, MAX_N + 1):
+        an = z if n == 1 else _mul((n // 2) ** 2 * R, z)
+        bn = n * R
+        a = _mul(bn, a_m1) + _mul(an, a_m2)
+        b = _mul(bn, b_m1) + _mul(an, b_m2)
+        conv = _div(a, b)
+        last = _div(a_m1, b_m1)
+        if abs(conv - last) < EPS:
+            return conv
+        a_m2, b_m2, a_m1, b_m1 = a_m1, b_m1, a, b
+    return conv
+
+
+def ln_fixed(x: int) -> int:
+    """NonIntegral ln' on a raw Fixed E34 value x > 0; returns the raw result."""
+    if x <= 0:
+        raise ValueError("ln': not in domain")
+    e = _exp(R)
+    n = _find_e(e, x)
+    z = _div(x, _ipow(e, n)) - R
+    return n * R if z == 0 else n * R + _lncf(z)
+
+
 def active_slot_log(f) -> int:
+    f = Fraction(f)
+    if f == 1:
+        return 0
+    return ln_fixed(R - from_rational(f))
+
+
+def active_slot_log_decimal(f) -> int:
+    """floor(10^34 ln(1 - f)) from a 100-digit evaluation (round-2 constant; cross-check)."""
+    from decimal import Decimal, getcontext
     f = Fraction(f)
     if f == 1:
         return 0

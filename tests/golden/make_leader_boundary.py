@@ -6,9 +6,9 @@ re-derived by a pure-Python big-integer restatement, written with the pairs arou
 (l*-2, l*-1 = leader; l*, l*+1 = not leader) and the Taylor iteration counts (the runs at
 the boundary are the longest ones).  The same for the TPraos 512-bit form.
 
-c_raw is this repo's floor(10^34 ln(1-f)) (praos_hip/fixed.py): the reference's own
-activeSlotLog (cardano-ledger-core ln', not vendored) may differ in its last digits, so
-the vectors pin the decision GIVEN c_raw -- which is what the ABI takes as input.
+c_raw is activeSlotLog as praos_hip/fixed.py restates it (NonIntegral ln' in Fixed E34;
+cardano-ledger-core is not vendored, so its last digits are unpinned): the vectors pin
+the decision GIVEN c_raw -- which is what the ABI takes as input.
 
     python tests/golden/make_leader_boundary.py   # rewrites tests/golden/leader_boundary.json
 """

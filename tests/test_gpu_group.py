@@ -85,3 +85,69 @@ def test_shard_gather_fold(ctx, c5_batch):
     # the chain stops at the first corrupted header; the fold carries on (would-be verdicts)
     # until a corrupted slot lands in a later epoch (another nonce: processed < n)
     assert r1[1] == first_bad and r1[2] > first_bad and r1[0][first_bad] != 0
+
+
+def test_c5_full_epoch_single_and_group8(ctx, oracle):
+    """configs[4] as stated: the whole 432,000-header epoch (3000 pools, 1 % corrupted) in
+    ONE batch, and the same epoch split over an 8-member praos_group (the 8-GPU layout:
+    contiguous slot-range shards of 54,000 headers; here all members on device 0).
+    Gathered == single context on every output, clean headers all valid, corrupted ones
+    all rejected, and an oracle sample bit-exact (as test_gpu_chain.test_c5_shaped_batch)."""
+    from praos_hip import abi, chains, fixed
+    from test_gpu_chain import _oracle_header
+    cfg = chains.CONFIGS["c5"]
+    sched = chains.load_schedule("c5")
+    n = 432_000
+    H, pool_list, corrupted, p = chains.make_chain(ctx, cfg, sched, n=n, corrupt_per_10000=100)
+    ctx.set_epoch(cfg["eta0"], pool_list, p)
+    o1 = ctx.verify_headers(H)
+    clean = corrupted == 0
+    assert int((~clean).sum()) > 4000
+    assert int((o1["bits"][clean] != 0).sum()) == 0
+    assert int((o1["bits"][~clean] == 0).sum()) == 0
+    assert list(o1["pool_idx"][clean]) == list(sched[1][:n][clean])
+    with abi.Group([0] * 8) as g:
+        g.set_epoch(cfg["eta0"], pool_list, p)
+        og = g.verify_headers(H)
+    for k in o1:
+        assert np.array_equal(o1[k], og[k]), k
+    c_raw = fixed.active_slot_log(cfg["f"])
+    ep = oracle.make_epoch(cfg["eta0"], cfg["slots_per_kes_period"], cfg["max_kes_evo"], c_raw, pool_list)
+    # samples in every shard, the shard edges, and corrupted headers
+    edges = [k * n // 8 + d for k in range(1, 8) for d in (-1, 0)]
+    sample = sorted(set(np.linspace(0, n - 1, 160).astype(int).tolist()) | set(edges) |
+                    set(np.nonzero(~clean)[0][::60].tolist()))
+    for i in sample:
+        r = _oracle_header(oracle, ep, H, i)
+        assert int(og["bits"][i]) & 0x1F1F == r["bits"], (i, hex(og["bits"][i]), hex(r["bits"]), corrupted[i])
+        assert bytes(og["beta"][i]) == r["beta"] and bytes(og["leader"][i]) == r["leader"]
+        assert bytes(og["nonce"][i]) == r["nonce"]
+    _leader_decisions_invariant(o1, pool_list, c_raw)
+
+
+def _leader_decisions_invariant(o, pool_list, c_raw, band=1e-12):
+    """activeSlotLog's last digits are unpinned (cardano-ledger-core ln' is not vendored,
+    praos_hip/fixed.py).  Every header's leader decision is shown to hold for ANY c within
+    `band` (relative) of c_raw: the exact real-number test p < 1 - (1 - f)^sigma flips at
+    c* = log1p(-p) / sigma (c = ln(1 - f) < 0; leader iff c < c*), and |c* - c| / |c| >
+    band for every header -- ten orders of magnitude above the 10^-24 convergence bound
+    of any Fixed E34 evaluation of ln'.  The GPU's Fixed E34 decision equals the
+    real-number one on every header (the Taylor comparison is exact away from c*)."""
+    from praos_hip import abi
+    sig = np.array([float(s) / 1e34 for _, _, s in pool_list])
+    pi = o["pool_idx"]
+    known = pi >= 0
+    lead = o["leader"][known]
+    # leading 64 bits of the 256-bit leader value: p = l / 2^256 to float64 precision
+    hi = lead[:, :8].astype(np.uint64)
+    top = np.zeros(len(lead), np.float64)
+    for k in range(8):
+        top = top * 256.0 + hi[:, k]
+    p = top / 2.0 ** 64
+    c = c_raw / 1e34
+    cstar = np.log1p(-p) / sig[pi[known]]
+    rel = (cstar - c) / abs(c)                      # > 0: leader
+    gpu_leader = (o["bits"][known] & abi.BIT_LEADER) == 0
+    checked = (o["bits"][known] & 0x0F1F) == 0       # crypto-valid headers reach the leader test
+    assert np.array_equal(gpu_leader[checked], rel[checked] > 0)
+    assert float(np.min(np.abs(rel[checked]))) > band, float(np.min(np.abs(rel[checked])))
