@@ -348,6 +348,11 @@ int praos_verify_tpraos_headers(praos_ctx* ctx, const praos_tpraos_headers* h, p
 #define PRAOS_TP_SIGNED_STRIDE 640
 int praos_verify_tpraos_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, praos_tpraos_out* out,
                                      praos_decoded* dec, uint8_t* leader_out, uint8_t* leader_proof);
+/* Device-resident form (the TPraos replay): praos_batch_run on such a batch decodes and
+ * runs the TPraos kernels (under per-header nonces after praos_batch_set_nonces);
+ * praos_batch_download_decoded / praos_batch_download_tpraos copy the results. */
+praos_batch* praos_batch_upload_tpraos_bytes(praos_ctx* ctx, const praos_header_bytes* in);
+int praos_batch_download_tpraos(praos_ctx* ctx, praos_batch* b, praos_tpraos_out* out);
 
 /* ---- TPraos decentralisation overlay (d > 0; Shelley..Alonzo before d reached 0) ----
  * cardano-protocol-tpraos OVERLAY (lookupInOverlaySchedule, the same call
@@ -545,6 +550,16 @@ int praos_tpraos_update_chain_dep_state(praos_ctx* ctx, const praos_tpraos_heade
                                         praos_envelope* env, const praos_epoch_info* ei,
                                         const praos_nonce* extra_entropy, praos_chain_state* st, uint8_t* verdict,
                                         uint16_t* failures, size_t* chain_stop, size_t* processed);
+/* The same fold over outputs verified under per-header nonces (praos_batch_set_nonces): it
+ * goes on while the nonce the state ticks to at header i equals etas[eta_idx[i]]
+ * (praos_validate_headers_nonces for TPraos). */
+int praos_tpraos_validate_headers_nonces(praos_ctx* ctx, const praos_tpraos_headers* h, const uint8_t* prev_hash,
+                                         const uint8_t* prev_is_genesis, const praos_tpraos_out* crypto,
+                                         praos_envelope* env, const praos_epoch_info* ei,
+                                         const praos_nonce* extra_entropy, praos_chain_state* st,
+                                         const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx,
+                                         uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
+                                         size_t* processed);
 
 /* ---- chain replay from an ImmutableDB directory (db-analyser) ----
  * Replaces the per-block loop of DBAnalyser/Analysis.hs:815-847 (processAllImmutableDB
@@ -582,6 +597,16 @@ int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* po
                            const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                            praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
                            praos_replay_stats* stats);
+/* The same replay over a TPraos (Shelley..Alonzo) ImmutableDB: stored BHeaders, the TPraos
+ * nonce rules (mkNonceFromOutputVRF of the eta certificate; TICKN with extra_entropy, NULL
+ * = NeutralNonce) and the TPraos fold; failures (may be NULL, verdicts_cap entries) gets
+ * each header's PRAOS_TPF_* set.  Replaces db-analyser's header revalidation over the
+ * TPraos eras (TPraos.hs:361-387 per block). */
+int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
+                                  const praos_params* params, const praos_epoch_info* ei,
+                                  const praos_nonce* extra_entropy, praos_envelope* env, praos_chain_state* st,
+                                  size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
+                                  praos_replay_stats* stats);
 
 /* ---- several GPUs from one process ----
  * A group = one context per entry of devices[] (a device may repeat: several
@@ -615,7 +640,8 @@ typedef struct {
   uint64_t slot_stride;           /* slot of header i = first_slot + i * slot_stride */
   uint32_t body_len;              /* > 0: pseudo-random signed bodies of this length;
                                      0: the genuine canonical HeaderBody CBOR of each header
-                                     (Praos only; PRAOS_SIGNED_STRIDE bytes per header) */
+                                     (PRAOS_SIGNED_STRIDE bytes per header; praos_synthesize_tpraos:
+                                     the 15-field BHBody, PRAOS_TP_SIGNED_STRIDE bytes) */
   uint32_t corrupt_per_10000;     /* seeded corruptions (Corruption.hs model: +1 at a byte) */
   uint32_t nkes;                  /* distinct Sum6KES keys (0 = one per pool); header of pool p uses key p mod nkes */
   uint8_t seed[32];
@@ -628,7 +654,7 @@ typedef struct {
   const uint64_t* sched_slot;
   const uint32_t* sched_pool;
   uint64_t block_no0;
-  /* Chain linking (CBOR bodies, Praos): link_prev = 1 makes hbPrev of header i the
+  /* Chain linking (CBOR bodies, Praos or TPraos): link_prev = 1 makes hbPrev of header i the
    * headerHash of header i-1 -- header 0 gets prev0, or GenesisHash when prev0 is NULL --
    * re-signing each KES signature in order (sequential on the device: ~0.1 ms per
    * header).  header_hash (optional, n*32) receives the header hashes (before any

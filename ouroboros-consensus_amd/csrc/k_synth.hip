@@ -277,8 +277,10 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   // body: blen > 0: deterministic pseudo-random bytes (a signed-message stand-in);
   // blen == 0: the genuine canonical HeaderBody CBOR (Praos/Header.hs:160-185) of
   // this header, 448-byte stride, so the header bytes can be decoded and the KES
-  // message is exactly `serialize' hb`.
-  const uint64_t bstride = blen ? (((uint64_t)blen + 7) & ~7ull) : 448ull;
+  // message is exactly `serialize' hb`; with tpraos the 15-field BHBody of
+  // cardano-protocol-tpraos (encodeBHBody: both certificates, OCert and ProtVer
+  // inlined), 640-byte stride.
+  const uint64_t bstride = blen ? (((uint64_t)blen + 7) & ~7ull) : (tpraos ? 640ull : 448ull);
   const uint64_t boff = (uint64_t)i * bstride;
   uint32_t bl = blen;
   uint64_t st = mix64(i * 0x9e3779b97f4a7c15ULL ^ salt ^ 0xb0d1);
@@ -290,7 +292,7 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     for (uint32_t k = blen; k < ((blen + 7) & ~7u); k++) body_bytes[boff + k] = 0;
   } else {
     SynthWr w{body_bytes + boff, 0};
-    sw_head(w, 4, 10);
+    sw_head(w, 4, tpraos ? 15 : 10);
     sw_head(w, 0, sched_slot ? block_no0 + i : first_slot / slot_stride + i);   // blockNo
     sw_head(w, 0, s);                                           // slotNo
     sw_head(w, 2, 32);                                          // prevHash (pseudo-random)
@@ -300,6 +302,11 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
     sw_head(w, 4, 2);
     sw_bytes(w, vrf_out + 64 * i, 64);
     sw_bytes(w, vrf_proof + 80 * i, 80);
+    if (tpraos) {                                               // bheaderL
+      sw_head(w, 4, 2);
+      sw_bytes(w, l_out + 64 * i, 64);
+      sw_bytes(w, l_proof + 80 * i, 80);
+    }
     st = mix64(st + 17);
     sw_head(w, 0, st & 0xffffu);                                // bodySize
     sw_head(w, 2, 32);                                          // bodyHash (caller's, else pseudo-random)
@@ -308,13 +315,13 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
       for (int b = 0; b < 8; b++)
         sw_byte(w, body_hash_in ? (uint32_t)body_hash_in[32 * i + 8 * k + b] : (uint32_t)(st >> (8 * b)));
     }
-    sw_head(w, 4, 4);
+    if (!tpraos) sw_head(w, 4, 4);
     sw_bytes(w, hot_vk + 32 * i, 32);
     sw_head(w, 0, nn);
     sw_head(w, 0, c0);
     sw_bytes(w, ocert_sig + 64 * i, 64);
-    sw_head(w, 4, 2);
-    sw_head(w, 0, 8);                                           // protocol version 8.0 (Babbage)
+    if (!tpraos) sw_head(w, 4, 2);
+    sw_head(w, 0, tpraos ? 6 : 8);                              // protocol version 8.0 (Babbage) / 6.0 (Alonzo)
     sw_head(w, 0, 0);
     bl = w.n;
     for (uint32_t k = bl; k < ((bl + 7) & ~7u); k++) body_bytes[boff + k] = 0;
@@ -350,7 +357,8 @@ __global__ void __launch_bounds__(64) k_synth_link(size_t n, const ge_niels* gbt
                                                    const uint32_t* __restrict__ tree, const uint32_t* __restrict__ leaf_of,
                                                    uint8_t* __restrict__ body_bytes, const uint64_t* __restrict__ body_off,
                                                    uint32_t* __restrict__ body_len, uint8_t* __restrict__ kes_sig,
-                                                   uint8_t* __restrict__ hdr_scratch, uint8_t* __restrict__ header_hash) {
+                                                   uint8_t* __restrict__ hdr_scratch, uint8_t* __restrict__ header_hash,
+                                                   uint32_t stride) {
   __shared__ ge_niels sbtab[2 * BTAB_N];
   const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
   if (threadIdx.x != 0) return;
@@ -372,7 +380,7 @@ __global__ void __launch_bounds__(64) k_synth_link(size_t n, const ge_niels* gbt
         for (uint32_t k = q + 1; k + 33 < bl; k++) b[k] = b[k + 33];
         b[q] = 0xf6;
         bl -= 33;
-        for (uint32_t k = bl; k < ((bl + 7) & ~7u) + 8 && k < 448; k++) b[k] = 0;
+        for (uint32_t k = bl; k < ((bl + 7) & ~7u) + 8 && k < stride; k++) b[k] = 0;
         body_len[i] = bl;
       }
     } else {
@@ -422,8 +430,8 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
   // CBOR bodies carry copies of the OCert signature and the VRF cert: a corruption
   // of those fields is applied to the copy as well, so the stored header bytes
   // (praos_hip/chunk.py) hold exactly the corrupted header.
-  int32_t at_vrf_out = -1, at_vrf_proof = -1, at_ocert_sig = -1;
-  if (cbor_body) {
+  int32_t at_vrf_out = -1, at_vrf_proof = -1, at_ocert_sig = -1, at_l_proof = -1;
+  if (cbor_body) {                         // 1: Praos HeaderBody, 2: TPraos BHBody
     const uint8_t* b = body_bytes + body_off[i];
     auto ulen = [](uint32_t ib) -> int32_t {
       const uint32_t ai = ib & 31u;
@@ -437,8 +445,12 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
     q += 66;
     at_vrf_proof = q + 2;
     q += 82;
+    if (cbor_body == 2) {                  // [ leader out, leader proof ]
+      at_l_proof = q + 1 + 66 + 2;
+      q += 1 + 66 + 82;
+    }
     q += ulen(b[q]);                       // bodySize
-    q += 34 + 1 + 34;                      // bodyHash, [ of the OCert, hotVk
+    q += cbor_body == 2 ? 34 + 34 : 34 + 1 + 34;   // bodyHash, ([ of the OCert,) hotVk
     q += ulen(b[q]);                       // n
     q += ulen(b[q]);                       // c0
     at_ocert_sig = q + 2;
@@ -473,7 +485,11 @@ __global__ void k_synth_corrupt(size_t n, uint32_t per10000, uint64_t salt, uint
       break;
     case 1: kes_sig[448 * i + k % 448] += 1; corrupted[i] = 2; break;
     case 2:
-      if (l_proof && (k & 0x10000)) { l_proof[80 * i + k % 80] += 1; corrupted[i] = 6; break; }
+      if (l_proof && (k & 0x10000)) {
+        l_proof[80 * i + k % 80] += 1; corrupted[i] = 6;
+        if (at_l_proof >= 0) body_bytes[body_off[i] + at_l_proof + k % 80] += 1;
+        break;
+      }
       vrf_proof[80 * i + k % 80] += 1; corrupted[i] = 3;
       if (at_vrf_proof >= 0) body_bytes[body_off[i] + at_vrf_proof + k % 80] += 1;
       break;
@@ -521,9 +537,9 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 void launch_synth_link(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
                        const uint32_t* leaf_seed, const uint32_t* tree, const uint32_t* leaf_of, uint8_t* body_bytes,
                        const uint64_t* body_off, uint32_t* body_len, uint8_t* kes_sig, uint8_t* hdr_scratch,
-                       uint8_t* header_hash) {
+                       uint8_t* header_hash, uint32_t stride) {
   hipLaunchKernelGGL(k_synth_link, grid, block, 0, stream, n, gbtab, prev0, leaf_seed, tree, leaf_of, body_bytes,
-                     body_off, body_len, kes_sig, hdr_scratch, header_hash);
+                     body_off, body_len, kes_sig, hdr_scratch, header_hash, stride);
 }
 void launch_synth_vrf_scalar(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const uint32_t* vrf_seed,
                              uint32_t* vrf_x) {

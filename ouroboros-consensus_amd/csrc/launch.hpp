@@ -78,7 +78,7 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 void launch_synth_link(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
                        const uint32_t* leaf_seed, const uint32_t* tree, const uint32_t* leaf_of, uint8_t* body_bytes,
                        const uint64_t* body_off, uint32_t* body_len, uint8_t* kes_sig, uint8_t* hdr_scratch,
-                       uint8_t* header_hash);
+                       uint8_t* header_hash, uint32_t stride);
 void launch_synth_vrf_scalar(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const uint32_t* vrf_seed,
                              uint32_t* vrf_x);
 void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint64_t first_slot, uint64_t nslots,
@@ -86,8 +86,20 @@ void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint6
                                 const uint32_t* pool_thr, const uint32_t* eta0, int eta0_neutral, int f_is_one,
                                 int tpraos, int32_t* leader);
 void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, uint32_t per10000, uint64_t salt, uint8_t* ocert_sig, uint8_t* kes_sig, uint8_t* vrf_proof, uint8_t* vrf_out, uint8_t* body_bytes, const uint64_t* body_off, const uint32_t* body_len, uint8_t* corrupted, uint8_t* l_proof, int cbor_body, uint32_t fields, uint8_t* cold_vk, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0);
+// two-stage VRF of the header pipeline (k_vrf.hip): stage V over all n headers into the
+// record `mid` (VRF_MID_PLANES x 16 x n bytes); stage F over list[0 .. *count) (or all n when
+// list is null), cached (ktab != null: k_vrf_fin) or per-lane U (k_vrf_fin_nc)
+void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
+                  const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid);
+void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
+                    const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
+                    const uint8_t* vrf_proof, const uint32_t* pool_hash, const uint32_t* pool_vrf,
+                    const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx,
+                    int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out,
+                    ge_cached* tabs, const void* mid);
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs,
-                   const int32_t* ovl_class, const uint32_t* gen);
+                   const int32_t* ovl_class, const uint32_t* gen, const uint8_t* eta_idx = nullptr);
 void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena, uint64_t arena_len,
                          const uint64_t* hoff, const uint32_t* hlen, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk,
                          uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint8_t* ocert_sig, uint8_t* kes_sig,

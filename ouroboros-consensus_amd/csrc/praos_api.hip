@@ -12,6 +12,7 @@ static constexpr size_t BCOMB_TABLES = 32;         // fixed-base comb: 256^j B, 
 static constexpr size_t C16_TABLES = 16, C16_ENTRIES = 32768;   // radix-2^16 comb (scalarmult.hpp C16_T, C16_N)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
 static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
+static constexpr size_t VRF_MID_BYTES = 21 * 16;    // per-header record of the two-stage VRF (praos_core.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
 #include <algorithm>
@@ -95,6 +96,8 @@ struct praos_ctx {
   hipStream_t side[3] = {nullptr, nullptr, nullptr};   // concurrent crypto kernels
   hipStream_t mside[3] = {nullptr, nullptr, nullptr};  // their key-cache misses (uncached verifies)
   hipEvent_t mdone_ev[3] = {};
+  hipStream_t vstream = nullptr;                       // VRF stage V (no key-cache dependence)
+  hipEvent_t v_ev = nullptr;
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
@@ -212,6 +215,7 @@ struct praos_batch {
   uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
   // per-lane point tables of the three crypto kernels (kcommon.hpp lane_tab)
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
+  uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
     uint32_t cap = 0, max_entries = 0;
@@ -323,6 +327,7 @@ praos_ctx* praos_open(int device) {
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
   for (auto& e : c->miss_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->mdone_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->v_ev, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
@@ -342,6 +347,8 @@ praos_ctx* praos_open(int device) {
       // 2.1 ms -> k_vrf 3.4 ms -> k_ocert 1.6 ms, profiles/r03b/timeline.txt)
       (void)hipStreamCreateWithPriority(&c->mside[k], hipStreamNonBlocking, hi ? greatest : least);
     }
+    // the VRF's stage V is the longest chain of a batch and starts at once: greatest priority
+    (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, greatest);
   }
   if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) {
     c->btab = nullptr;
@@ -405,6 +412,8 @@ void praos_close(praos_ctx* c) {
   for (auto& e : c->mdone_ev) if (e) (void)hipEventDestroy(e);
   for (auto& st : c->side) if (st) (void)hipStreamDestroy(st);
   for (auto& st : c->mside) if (st) (void)hipStreamDestroy(st);
+  if (c->vstream) (void)hipStreamDestroy(c->vstream);
+  if (c->v_ev) (void)hipEventDestroy(c->v_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -520,6 +529,7 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   ok &= dalloc(b, (uint8_t**)&b->tab_ocert, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_kes, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_vrf, LT_VRF_B * n) == hipSuccess;
+  ok &= dalloc(b, &b->vrf_mid, VRF_MID_BYTES * n) == hipSuccess;
   ok &= dalloc(b, &b->kes_leaf, 32 * n) == hipSuccess;
   b->dd_cap = 256;
   while (b->dd_cap < 2 * n) b->dd_cap <<= 1;
@@ -692,6 +702,9 @@ static int batch_decode(praos_ctx* c, praos_batch* b) {
 }
 
 static int batch_run_impl(praos_ctx* c, praos_batch* b);
+static int tpraos_run(praos_ctx* c, praos_batch* b, const uint8_t* dlout, const uint8_t* dlproof, uint8_t* dbeta_l,
+                      const uint64_t* host_slots);
+static int tpraos_download(praos_ctx* c, praos_batch* b, const uint8_t* dbeta_l, praos_tpraos_out* out);
 
 int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (!c || !b) return PRAOS_E_ARG;
@@ -710,6 +723,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
           hipStreamWaitEvent(c->stream, c->mdone_ev[k], 0) != hipSuccess)
         (void)hipStreamSynchronize(c->mside[k]);
     }
+    if (hipEventRecord(c->v_ev, c->vstream) != hipSuccess || hipStreamWaitEvent(c->stream, c->v_ev, 0) != hipSuccess)
+      (void)hipStreamSynchronize(c->vstream);
   }
   return r;
 }
@@ -739,6 +754,20 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   if (c->keycache > 0 && n >= 2) {     // the comb is read by the cached chains: built before ev[0]
     const int rc = ensure_bcomb16(c);
     if (rc != PRAOS_OK) return rc;
+  }
+  if (b->tp_only) {          // TPraos headers from stored bytes: the TPraos kernels, in order
+    std::vector<uint64_t> slots;
+    if (c->ovl_on) {         // the overlay schedule is classified on the host from the decoded slots
+      slots.resize(n);
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpy(slots.data(), b->slot, 8 * n, hipMemcpyDeviceToHost));
+    }
+    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    for (int k = 0; k < 3; k++) HIPCHK(c, hipEventRecord(c->side_ev[k], c->stream));
+    const int r = tpraos_run(c, b, b->lead_out, b->lead_proof, b->beta_l, slots.data());
+    if (r != PRAOS_OK) return r;
+    HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+    return PRAOS_OK;
   }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
@@ -863,25 +892,38 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
   const bool do_vrf = (c->kernels & 4) != 0;
   if (do_vrf) {
+    // two stages (k_vrf.hip): V over every header on its own stream, from ev[0] on (it
+    // needs no key); F after it -- the hits on sv once their key tables exist, the misses
+    // on their miss stream (per-lane U)
+    const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
+    hipStream_t sV = c->concurrent ? c->vstream : c->stream;
+    if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
+    launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf, b->vrf_mid);
+    HIPCHK(c, hipEventRecord(c->v_ev, sV));
+    auto after_v = [&](hipStream_t st) -> int {
+      if (st != sV) HIPCHK(c, hipStreamWaitEvent(st, c->v_ev, 0));
+      return PRAOS_OK;
+    };
+    auto fin = [&](hipStream_t st, const uint32_t* list, const uint32_t* count, const praos_batch::KeyCache* k) {
+      launch_vrf_fin(st, n, list, count, k ? k->item_entry : nullptr, k ? k->ktab : nullptr, k ? k->kinfo : nullptr,
+                     c->bcomb16, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, c->d_pool_hash,
+                     c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx,
+                     b->pool_sorted, b->beta, b->leader, b->nonce, b->tab_vrf, b->vrf_mid);
+    };
     if (kc) {
       praos_batch::KeyCache& k = b->kc[1];
       int r = keycache_lists(k, b->vrf_vk, sv);
       if (r == PRAOS_OK) r = to_main(2, sv);
+      if (r == PRAOS_OK) r = after_v(sm_[2]);
       if (r != PRAOS_OK) return r;
-      launch_vrf(g, blk, sm_[2], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof,
-                 b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
-                 (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx, b->pool_sorted, b->beta,
-                 b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
+      fin(sm_[2], k.miss, k.counters + 2, nullptr);
       keycache_precompute(k, b->vrf_vk, 1, sv);
-      launch_vrf_ck(g, blk, sv, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk, b->vrf_vk,
-                    b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
-                    c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
-                    b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
+      if ((r = after_v(sv)) != PRAOS_OK) return r;
+      fin(sv, k.hit, k.counters + 1, &k);
     } else {
-      launch_vrf(g, blk, sv, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk, b->vrf_vk,
-                 b->vrf_out, b->vrf_proof, b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, b->eta_idx, c->d_pool_hash, c->d_pool_vrf,
-                 c->d_pool_map, c->npools, (int)P.vrf_check_output, (const uint8_t*)nullptr, bv, b->pool_idx,
-                 b->pool_sorted, b->beta, b->leader, b->nonce, (uint8_t*)nullptr, b->tab_vrf);
+      const int r = after_v(sv);
+      if (r != PRAOS_OK) return r;
+      fin(sv, nullptr, nullptr, nullptr);
     }
   }
   else {
@@ -1819,9 +1861,10 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
   if (!c || !sp || !params || sp->npools == 0 || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = sp->n, np = sp->npools;
-  // body_len 0: genuine CBOR HeaderBody (Praos only), PRAOS_SIGNED_STRIDE bytes per header
-  if (sp->body_len == 0 && tpraos) return PRAOS_E_ARG;
-  const size_t bstride = sp->body_len ? (((size_t)sp->body_len + 7) & ~(size_t)7) : (size_t)PRAOS_SIGNED_STRIDE;
+  // body_len 0: genuine CBOR bodies, PRAOS_SIGNED_STRIDE (Praos HeaderBody) or
+  // TP_SIGNED_STRIDE (TPraos BHBody) bytes per header
+  const size_t bstride = sp->body_len ? (((size_t)sp->body_len + 7) & ~(size_t)7)
+                                      : (size_t)(tpraos ? TP_SIGNED_STRIDE : PRAOS_SIGNED_STRIDE);
   Scratch s(c);
   uint32_t master[8], e0[8] = {0};
   std::memcpy(master, sp->seed, 32);
@@ -1863,10 +1906,10 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
   const uint64_t* dss = sp->sched_slot ? s.up(sp->sched_slot, 8 * n) : nullptr;
   const uint32_t* dsp = sp->sched_pool ? s.up(sp->sched_pool, 4 * n) : nullptr;
   const bool link = sp->link_prev != 0;
-  if (link && (sp->body_len != 0 || tpraos)) { c->err = "link_prev needs CBOR Praos bodies (body_len 0)"; return PRAOS_E_ARG; }
+  if (link && sp->body_len != 0) { c->err = "link_prev needs CBOR bodies (body_len 0)"; return PRAOS_E_ARG; }
   auto dleaf = s.zeros<uint32_t>(4 * n);
   auto dprev0 = link && sp->prev0 ? s.up(sp->prev0, 32) : nullptr;
-  auto dhscr = s.zeros<uint8_t>(link ? 1024 + 16 : 16);
+  auto dhscr = s.zeros<uint8_t>(link ? 1100 : 16);     // [body <= 598 B, kesSig 448 B] + heads
   auto dhh = s.zeros<uint8_t>(link ? 32 * n : 16);
   if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
   uint64_t salt = 0;
@@ -1881,13 +1924,13 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
                        (uint32_t)nk, sp->first_slot, sp->slot_stride, params->slots_per_kes_period, sp->body_len, salt, de0,
                        eta0 ? 0 : 1, cold_seed, cold_pk, vrf_seed, vrf_pk, leaf_seed, tree, scratch, dslot, dcold,
                        dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof,
-                       sp->body_len == 0 && !tpraos ? dbh : nullptr, dss, dsp, sp->block_no0, dleaf);
+                       sp->body_len == 0 ? dbh : nullptr, dss, dsp, sp->block_no0, dleaf);
     if (link)
       launch_synth_link(dim3(1), dim3(64), c->stream, n, c->btab, dprev0, leaf_seed, tree, dleaf, dbody, doff, dlen,
-                        dksig, dhscr, dhh);
+                        dksig, dhscr, dhh, (uint32_t)bstride);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
                        salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
-                       sp->body_len == 0 ? 1 : 0, sp->corrupt_fields ? sp->corrupt_fields : 0x1fu, dcold, dhot, dn,
+                       sp->body_len == 0 ? (tpraos ? 2 : 1) : 0, sp->corrupt_fields ? sp->corrupt_fields : 0x1fu, dcold, dhot, dn,
                        dc0);
   }
   HIPCHK(c, hipGetLastError());
@@ -2088,9 +2131,9 @@ static int tpraos_run(praos_ctx* c, praos_batch* b, const uint8_t* dlout, const 
              b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
              (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
   launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
-                b->slot, c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf, c->d_pool_map, c->npools,
-                (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l, b->nonce, b->tab_vrf,
-                dcls, c->d_gen);
+                b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l,
+                b->nonce, b->tab_vrf, dcls, c->d_gen, b->eta_idx);
   launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr, (int)P.f_is_one,
                 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
                 b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
@@ -2132,6 +2175,33 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
   rc = body();
   praos_batch_free(c, b);
   return rc;
+}
+
+praos_batch* praos_batch_upload_tpraos_bytes(praos_ctx* c, const praos_header_bytes* in) {
+  return upload_bytes_impl(c, in, true);
+}
+
+int praos_batch_download_tpraos(praos_ctx* c, praos_batch* b, praos_tpraos_out* out) {
+  if (!c || !b || !out || !out->bits || !b->tp_only) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (b->n == 0) return PRAOS_OK;
+  return tpraos_download(c, b, b->beta_l, out);
+}
+
+int praos_tpraos_validate_headers_nonces(praos_ctx* c, const praos_tpraos_headers* th, const uint8_t* prev_hash,
+                                         const uint8_t* prev_is_genesis, const praos_tpraos_out* crypto,
+                                         praos_envelope* env, const praos_epoch_info* ei,
+                                         const praos_nonce* extra_entropy, praos_chain_state* st,
+                                         const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx,
+                                         uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
+                                         size_t* processed) {
+  if (!th || !crypto || !etas || !eta_idx || k == 0) return PRAOS_E_ARG;
+  praos_out o{};
+  o.bits = crypto->bits;
+  o.pool_idx = crypto->pool_idx;
+  o.nonce = crypto->nonce;
+  return fold_impl(c, &th->h, prev_hash, prev_is_genesis, &o, env, ei, st, verdict, chain_stop, processed, etas, k,
+                   eta_idx, true, extra_entropy, failures);
 }
 
 int praos_verify_tpraos_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_tpraos_out* out,

@@ -440,6 +440,176 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
   return ok && gamma_ok && eq;
 }
 
+// ------------------------------------------------------------------ VRF verify in two stages
+// The same verification as vrf_verify_core, split at the only point where the public key's
+// precomputed tables are needed (k_vrf.hip): stage V (k_vrf_v) -- H = hash_to_curve,
+// Gamma decode, 8 Gamma, V = [s]H - [c]Gamma -- depends on the header alone and runs while
+// the key cache is being built; stage F (k_vrf_fin / k_vrf_fin_nc) -- U = [s]B - [c]Y from
+// the key's tables (or a per-lane chain), one batched inversion, the challenge hash, beta.
+// Stage V leaves a per-header record in SoA planes of uint4 (plane p of item i at
+// mid[p * stride + i], so a wave's access is one contiguous KB):
+//   planes 0-5 V (X, Y, Z), 6-11 H, 12-17 8 Gamma, 18-19 enc(Gamma), 20 flags (x: Gamma decoded)
+#define VRF_MID_PLANES 21
+#define VRF_MID_V 0
+#define VRF_MID_H 6
+#define VRF_MID_G8 12
+#define VRF_MID_GS 18
+#define VRF_MID_FLAGS 20
+
+FE_INLINE void mid_put(uint4* __restrict__ mid, size_t stride, size_t i, int plane, const uint32_t w[8]) {
+  mid[(size_t)plane * stride + i] = make_uint4(w[0], w[1], w[2], w[3]);
+  mid[(size_t)(plane + 1) * stride + i] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+FE_INLINE void mid_get(uint32_t w[8], const uint4* __restrict__ mid, size_t stride, size_t i, int plane) {
+  const uint4 a = mid[(size_t)plane * stride + i], b = mid[(size_t)(plane + 1) * stride + i];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+FE_INLINE void mid_put_xyz(uint4* __restrict__ mid, size_t stride, size_t i, int plane, const fe& X, const fe& Y,
+                           const fe& Z) {
+  mid_put(mid, stride, i, plane, X.v);
+  mid_put(mid, stride, i, plane + 2, Y.v);
+  mid_put(mid, stride, i, plane + 4, Z.v);
+}
+FE_INLINE void mid_get_xyz(fe& X, fe& Y, fe& Z, const uint4* __restrict__ mid, size_t stride, size_t i, int plane) {
+  mid_get(X.v, mid, stride, i, plane);
+  mid_get(Y.v, mid, stride, i, plane + 2);
+  mid_get(Z.v, mid, stride, i, plane + 4);
+}
+
+// The canonical encoding ge_enc_affine(ge_frombytes(pk)) that hash_to_curve reads, without
+// the decode: y mod p with pk's sign bit.  Equal for every key that passes
+// vrf_validate_key (x != 0 off the small-order points, so the sign bit is x's); for any
+// other key the proof is rejected from the key flags whatever H is.
+FE_INLINE void vrf_key_canonical(uint32_t ys[8], const uint32_t pk[8]) {
+  fe y;
+  fe_frombytes32(y, pk);
+  fe_tobytes32(ys, y);
+  ys[7] |= pk[7] & 0x80000000u;
+}
+
+// Stage V: writes H, 8 Gamma, enc(Gamma), the Gamma flag (before the chain, so none of
+// them is live across it) and V.  vt: the lane's 16-entry table region ({1..8}H, {1..8}(-Gamma)).
+FE_INLINE void vrf_v_core(uint4* __restrict__ mid, size_t stride, size_t i, const uint32_t pk[8],
+                          const uint32_t gamma[8], const uint32_t c4[4], const uint32_t s8[8],
+                          const uint32_t alpha[8], ge_cached* __restrict__ vt) {
+  {
+    uint32_t ys[8];
+    vrf_key_canonical(ys, pk);
+    ge_p3 H;
+    vrf_hash_to_curve(H, ys, alpha);
+    mid_put_xyz(mid, stride, i, VRF_MID_H, H.X, H.Y, H.Z);
+    build_cached_table(vt, H);
+  }
+  {
+    ge_p3 G;
+    const bool gamma_ok = ge_frombytes(G, gamma, false);
+    uint32_t gs[8];
+    ge_enc_affine(gs, G);
+    mid_put(mid, stride, i, VRF_MID_GS, gs);
+    mid[(size_t)VRF_MID_FLAGS * stride + i] = make_uint4(gamma_ok ? 1u : 0u, 0u, 0u, 0u);
+    ge_p3 G2, G4;
+    ge_p3_dbl_to_p3(G2, G);
+    ge_p3_dbl_to_p3(G4, G2);
+    ge_p1p1 t;
+    ge_p2 q;
+    ge_p3_to_p2(q, G4);
+    ge_p2_dbl(t, q);
+    ge_p2 G8;
+    ge_p1p1_to_p2(G8, t);
+    mid_put_xyz(mid, stride, i, VRF_MID_G8, G8.X, G8.Y, G8.Z);
+    fe_neg(G.X, G.X);
+    fe_neg(G.T, G.T);
+    build_cached_table(vt + 8, G);
+  }
+  uint32_t sx[16], s[8], c[8], sw[8], cw[8];
+#pragma unroll
+  for (int k = 0; k < 16; k++) sx[k] = k < 8 ? s8[k] : 0u;
+  sc_reduce512(s, sx);
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[k] = k < 4 ? c4[k] : 0u;
+  sc_recode16(sw, s);
+  sc_recode16(cw, c);
+  ge_p1p1 x;
+  STRAUS<64, 64, 33, 0, false>(x, vt, sw, vt + 8, cw, nullptr, nullptr);   // V = [s]H - [c]Gamma
+  ge_p2 V;
+  ge_p1p1_to_p2(V, x);
+  mid_put_xyz(mid, stride, i, VRF_MID_V, V.X, V.Y, V.Z);
+}
+
+// Stage F: U, the batched inversion of U.Z V.Z (8 Gamma).Z H.Z, the challenge, beta.
+// CACHED: kinfo / ktab of k_keys.hip and btab = the global radix-2^16 comb; otherwise Y is
+// decoded per lane ({1..8}(-Y) in vt) and btab = the LDS tables {B, 2^128 B}.
+template <bool CACHED>
+FE_INLINE bool vrf_fin_core(uint32_t beta[16], bool& gamma_ok, const uint4* __restrict__ mid, size_t stride,
+                            size_t i, const uint32_t pk[8], const uint32_t c4[4], const uint32_t s8[8],
+                            const ge_niels* __restrict__ btab, ge_cached* __restrict__ vt,
+                            const ge_cached* __restrict__ ktab, const uint32_t* __restrict__ kinfo) {
+  bool ok;
+  uint32_t sx[16], s[8], c[8], cw[8], sw[8];
+#pragma unroll
+  for (int k = 0; k < 16; k++) sx[k] = k < 8 ? s8[k] : 0u;
+  sc_reduce512(s, sx);
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[k] = k < 4 ? c4[k] : 0u;
+  sc_recode16(cw, c);
+  ge_p2 U;
+  if constexpr (CACHED) {
+    ok = (kinfo[0] & 1u) != 0;
+    sc_recode65536(sw, s);
+    ge_p1p1 x;
+    straus_comb<8, true>(x, ktab, cw, btab, sw);
+    ge_p1p1_to_p2(U, x);
+  } else {
+    ge_p3 Y;
+    ok = !ge_has_small_order(pk);
+    ok = ge_frombytes(Y, pk, false) && ok;
+    fe_neg(Y.X, Y.X);
+    fe_neg(Y.T, Y.T);
+    build_cached_table(vt, Y);
+    sc_recode256(sw, s);
+    ge_p1p1 x;
+    STRAUS<33, 33, 0, 16, true>(x, vt, cw, nullptr, nullptr, btab, sw);
+    ge_p1p1_to_p2(U, x);
+  }
+  gamma_ok = (mid[(size_t)VRF_MID_FLAGS * stride + i].x & 1u) != 0;
+  fe z12, z123, z1234, inv, zi;
+  uint32_t hs[8], us[8], vs[8], gs[8], g8s[8];
+  {
+    ge_p2 V, G8;
+    fe HZ;
+    mid_get_xyz(V.X, V.Y, V.Z, mid, stride, i, VRF_MID_V);
+    mid_get_xyz(G8.X, G8.Y, G8.Z, mid, stride, i, VRF_MID_G8);
+    mid_get(HZ.v, mid, stride, i, VRF_MID_H + 4);
+    fe_mul(z12, U.Z, V.Z);
+    fe_mul(z123, z12, G8.Z);
+    fe_mul(z1234, z123, HZ);
+    fe_invert(inv, z1234);
+    fe_mul(zi, inv, z123);            // 1/H.Z
+    fe_mul(inv, inv, HZ);             // 1/(U.Z V.Z G8.Z)
+    {
+      fe HX, HY;
+      mid_get(HX.v, mid, stride, i, VRF_MID_H);
+      mid_get(HY.v, mid, stride, i, VRF_MID_H + 2);
+      ge_tobytes_zi(hs, HX, HY, zi);
+    }
+    fe_mul(zi, inv, z12);             // 1/G8.Z
+    ge_tobytes_zi(g8s, G8.X, G8.Y, zi);
+    fe_mul(inv, inv, G8.Z);           // 1/(U.Z V.Z)
+    fe_mul(zi, inv, V.Z);             // 1/U.Z
+    ge_tobytes_zi(us, U.X, U.Y, zi);
+    fe_mul(zi, inv, U.Z);             // 1/V.Z
+    ge_tobytes_zi(vs, V.X, V.Y, zi);
+  }
+  mid_get(gs, mid, stride, i, VRF_MID_GS);
+  uint32_t cp[4];
+  vrf_hash_points(cp, hs, gs, us, vs);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) eq &= cp[k] == c4[k];
+  vrf_beta(beta, g8s);
+  return ok && gamma_ok && eq;
+}
+
 // ------------------------------------------------------------------ signing (generator only)
 // az = SHA-512(seed), clamped
 FE_INLINE void ed25519_expand(uint32_t az[16], const uint32_t seed[8]) {

@@ -102,10 +102,16 @@ struct ChunkReader {
 
 }  // namespace
 
-extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
-                                      const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
-                                      praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
-                                      size_t verdicts_cap, praos_replay_stats* stats) {
+// TPraos mode (eras Shelley..Alonzo, HFEras.hs:43-49; TPraos.hs:361-387): stored BHeaders
+// (praos_batch_upload_tpraos_bytes), the TPraos nonce rules -- the header's nonce is
+// mkNonceFromOutputVRF of its eta certificate (Blake2b-256 of the output, no range
+// extension) and TICKN adds the extra entropy (eta0 := eta_c ⭒ eta_h ⭒ extraEntropy) --
+// and the TPraos fold (PRTCL predicate-failure sets into failures[]).
+static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
+                       const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                       praos_chain_state* st, size_t batch_max, uint8_t* verdicts, uint16_t* failures,
+                       size_t verdicts_cap, praos_replay_stats* stats, bool tpraos,
+                       const praos_nonce* extra_entropy) {
   if (!ctx || !dir || !params || (npools && !pools) || !ei || !env || !st || !stats || batch_max == 0 ||
       ei->epoch_length == 0 || (verdicts_cap && !verdicts))
     return PRAOS_E_ARG;
@@ -144,6 +150,7 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
       praos_set_error_(ctx, "replay: first slot before the epoch base");
       return PRAOS_E_ARG;
     }
+    // (the installed nonce only seeds praos_set_epoch: every batch carries its own nonces)
     if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); return PRAOS_E_ARG; }
     const int r = praos_set_epoch(ctx, eta0.neutral ? nullptr : eta0.hash, pools, npools, params);
     if (r != PRAOS_OK) return r;
@@ -158,7 +165,7 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
     std::vector<uint64_t> off, slot, block_no, ocn;
     std::vector<uint32_t> len, bsize;
     std::vector<uint8_t> prev, gen, cold, hh, nonce, v, vout, eidx;
-    std::vector<uint16_t> dstat, bits;
+    std::vector<uint16_t> dstat, bits, fails;
     std::vector<int32_t> pidx;
     std::vector<praos_nonce> etas;
   };
@@ -207,11 +214,11 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
     next_index += n;
     auto t_dev = std::chrono::steady_clock::now();
     praos_header_bytes hb{n, S.arena.data(), S.arena.size(), S.off.data(), S.len.data()};
-    S.b = praos_batch_upload_bytes(ctx, &hb);
+    S.b = tpraos ? praos_batch_upload_tpraos_bytes(ctx, &hb) : praos_batch_upload_bytes(ctx, &hb);
     if (!S.b) { rc = PRAOS_E_OOM; return false; }
     S.dstat.resize(n); S.block_no.resize(n); S.slot.resize(n); S.ocn.resize(n); S.bsize.resize(n);
     S.prev.resize(32 * n); S.gen.resize(n); S.cold.resize(32 * n); S.hh.resize(32 * n); S.vout.resize(64 * n);
-    S.bits.resize(n); S.pidx.resize(n); S.nonce.resize(32 * n); S.v.resize(n); S.eidx.resize(n);
+    S.bits.resize(n); S.pidx.resize(n); S.nonce.resize(32 * n); S.v.resize(n); S.eidx.resize(n); S.fails.resize(n);
     praos_decoded dec{};
     dec.status = S.dstat.data(); dec.block_no = S.block_no.data(); dec.slot = S.slot.data();
     dec.prev_hash = S.prev.data(); dec.prev_is_genesis = S.gen.data(); dec.cold_vk = S.cold.data();
@@ -230,11 +237,15 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
       for (unsigned t = 0; t < nthreads; t++)
         th.emplace_back([&, t] {
           for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) {
-            uint8_t m[65], h1[32];
-            m[0] = 'N';
-            std::memcpy(m + 1, S.vout.data() + 64 * i, 64);
-            praos_host::blake2b(h1, 32, m, 65);
-            praos_host::blake2b(eta_of[i].hash, 32, h1, 32);
+            if (tpraos) {        // mkNonceFromOutputVRF (the eta certificate's output)
+              praos_host::blake2b(eta_of[i].hash, 32, S.vout.data() + 64 * i, 64);
+            } else {
+              uint8_t m[65], h1[32];
+              m[0] = 'N';
+              std::memcpy(m + 1, S.vout.data() + 64 * i, 64);
+              praos_host::blake2b(h1, 32, m, 65);
+              praos_host::blake2b(eta_of[i].hash, 32, h1, 32);
+            }
             eta_of[i].neutral = 0;
           }
         });
@@ -245,6 +256,7 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
       const uint64_t e_new = epoch_of(S.slot[i]);
       if (!sp.dead && e_new > (sp.origin ? 0 : epoch_of(sp.last))) {
         sp.epoch_nonce = praos_host::nonce_combine(sp.candidate, sp.leb);
+        if (tpraos && extra_entropy) sp.epoch_nonce = praos_host::nonce_combine(sp.epoch_nonce, *extra_entropy);
         sp.leb = sp.lab;
       }
       if (S.etas.empty() || !praos_host::nonce_eq(S.etas.back(), sp.epoch_nonce)) S.etas.push_back(sp.epoch_nonce);
@@ -295,15 +307,27 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
     env->header_size = S.len.data();
     env->body_size = S.bsize.data();
     size_t stop = 0, done = 0;
-    rc = praos_validate_headers_nonces(ctx, &h, S.prev.data(), S.gen.data(), &out, env, ei, st, S.etas.data(),
-                                       (uint32_t)S.etas.size(), S.eidx.data(), S.v.data(), &stop, &done);
+    if (tpraos) {
+      praos_tpraos_headers th{};
+      th.h = h;
+      praos_tpraos_out to{S.bits.data(), S.pidx.data(), nullptr, nullptr, S.nonce.data()};
+      rc = praos_tpraos_validate_headers_nonces(ctx, &th, S.prev.data(), S.gen.data(), &to, env, ei, extra_entropy,
+                                                st, S.etas.data(), (uint32_t)S.etas.size(), S.eidx.data(),
+                                                S.v.data(), S.fails.data(), &stop, &done);
+    } else {
+      rc = praos_validate_headers_nonces(ctx, &h, S.prev.data(), S.gen.data(), &out, env, ei, st, S.etas.data(),
+                                         (uint32_t)S.etas.size(), S.eidx.data(), S.v.data(), &stop, &done);
+    }
     env->block_no = nullptr;
     env->header_hash = nullptr;
     env->header_size = nullptr;
     env->body_size = nullptr;
     stats->ms_fold += ms_since(t_fold);
     if (rc != PRAOS_OK) return true;
-    for (size_t k = 0; k < done && S.index0 + k < verdicts_cap; k++) verdicts[S.index0 + k] = S.v[k];
+    for (size_t k = 0; k < done && S.index0 + k < verdicts_cap; k++) {
+      verdicts[S.index0 + k] = S.v[k];
+      if (failures) failures[S.index0 + k] = tpraos ? S.fails[k] : 0;
+    }
     if (stop < done) {          // the chain stops at the first invalid header
       stats->validated += stop;
       stats->stop_index = S.index0 + stop;
@@ -354,4 +378,21 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
   if (!stopped) stats->stop_index = index0;
   stats->chunks = (uint32_t)rd.chunk;
   return PRAOS_OK;
+}
+
+extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
+                                      const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                                      praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
+                                      size_t verdicts_cap, praos_replay_stats* stats) {
+  return replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap, stats,
+                     false, nullptr);
+}
+
+extern "C" int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, const praos_pool* pools,
+                                             uint32_t npools, const praos_params* params, const praos_epoch_info* ei,
+                                             const praos_nonce* extra_entropy, praos_envelope* env,
+                                             praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
+                                             uint16_t* failures, size_t verdicts_cap, praos_replay_stats* stats) {
+  return replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap, stats,
+                     true, extra_entropy);
 }

@@ -50,6 +50,12 @@ V_OK, V_KES_BEFORE_START, V_KES_AFTER_END, V_OCERT_SIG, V_KES_SIG, V_COUNTER_MIS
     V_COUNTER_TOO_SMALL, V_COUNTER_OVER_INC, V_VRF_KEY_UNKNOWN, V_VRF_KEY_WRONG, V_VRF_BAD_PROOF, \
     V_LEADER_TOO_BIG, V_INPUT, V_ENV_BLOCK_NO, V_ENV_SLOT_NO, V_ENV_PREV_HASH, V_ENV_OBSOLETE_NODE, \
     V_ENV_HEADER_SIZE, V_ENV_BLOCK_SIZE = range(19)
+V_TPRAOS = 19
+# TPraos PRTCL predicate failures (PRAOS_TPF_*)
+TPF_KES_BEFORE_START, TPF_KES_AFTER_END, TPF_OCERT_SIG, TPF_KES_SIG, TPF_COUNTER_MISSING, \
+    TPF_COUNTER_TOO_SMALL, TPF_COUNTER_OVER_INC = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20, 0x40
+TPF_VRF_KEY_UNKNOWN, TPF_VRF_KEY_WRONG, TPF_BAD_NONCE, TPF_BAD_LEADER, TPF_LEADER_TOO_BIG, TPF_NOT_ACTIVE, \
+    TPF_GEN_COLD, TPF_GEN_VRF = 0x100, 0x200, 0x400, 0x800, 0x1000, 0x2000, 0x4000, 0x8000
 
 
 class Params(ctypes.Structure):
@@ -204,6 +210,21 @@ SIGNATURES = {
                                               ctypes.POINTER(Params), ctypes.POINTER(EpochInfo),
                                               ctypes.POINTER(Envelope), ctypes.POINTER(ChainState), ctypes.c_size_t,
                                               u8p, ctypes.c_size_t, ctypes.POINTER(ReplayStats)]),
+    "praos_replay_immutable_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(Pool),
+                                                     ctypes.c_uint32, ctypes.POINTER(Params),
+                                                     ctypes.POINTER(EpochInfo), ctypes.POINTER(Nonce),
+                                                     ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
+                                                     ctypes.c_size_t, u8p, u16p, ctypes.c_size_t,
+                                                     ctypes.POINTER(ReplayStats)]),
+    "praos_batch_upload_tpraos_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
+    "praos_batch_download_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(TPOut)]),
+    "praos_tpraos_validate_headers_nonces": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders), u8p, u8p,
+                                                            ctypes.POINTER(TPOut), ctypes.POINTER(Envelope),
+                                                            ctypes.POINTER(EpochInfo), ctypes.POINTER(Nonce),
+                                                            ctypes.POINTER(ChainState), ctypes.POINTER(Nonce),
+                                                            ctypes.c_uint32, u8p, u8p, u16p,
+                                                            ctypes.POINTER(ctypes.c_size_t),
+                                                            ctypes.POINTER(ctypes.c_size_t)]),
     "praos_ticked_epoch_nonce": (ctypes.c_int, [ctypes.POINTER(ChainState), ctypes.POINTER(EpochInfo), ctypes.c_uint64,
                                                 ctypes.POINTER(Nonce)]),
     "praos_group_open": (ctypes.c_void_p, [i32p, ctypes.c_int]),
@@ -736,10 +757,11 @@ class Context:
         return verdict, stop.value, done.value
 
     def replay_immutable(self, path, pools, params: Params, epoch_info, state: dict, envelope: dict,
-                         batch_max=1 << 16, verdicts_cap=0, counter_cap=1 << 16):
+                         batch_max=1 << 16, verdicts_cap=0, counter_cap=1 << 16, tpraos=False, extra_entropy=None):
         """praos_replay_immutable over an ImmutableDB directory.  state (chain state dict, as
         update_chain_dep_state) and envelope (limits + "tip") are updated in place.
-        Returns (stats dict, verdict u8[verdicts_cap])."""
+        Returns (stats dict, verdict u8[verdicts_cap]); tpraos=True (praos_replay_immutable_tpraos,
+        extra_entropy None = NeutralNonce) returns (stats, verdict, failures u16[verdicts_cap])."""
         arr = self.pool_array(pools)
         st, hk, cv = _state_struct(state, counter_cap)
         E = Envelope()
@@ -752,14 +774,27 @@ class Context:
             setattr(E, k, envelope[k])
         ei = EpochInfo(*epoch_info)
         verdict = np.zeros(max(verdicts_cap, 1), np.uint8)
+        fails = np.zeros(max(verdicts_cap, 1), np.uint16)
         S = ReplayStats()
-        self.check(self.L.praos_replay_immutable(self.h, os.fsencode(str(path)), arr, len(pools),
-                                                 ctypes.byref(params), ctypes.byref(ei), ctypes.byref(E),
-                                                 ctypes.byref(st), batch_max, ptr(verdict), verdicts_cap,
-                                                 ctypes.byref(S)))
+        if tpraos:
+            xe = None
+            if extra_entropy is not None:
+                xe = Nonce()
+                ctypes.memmove(xe.hash, bytes(extra_entropy), 32)
+            self.check(self.L.praos_replay_immutable_tpraos(
+                self.h, os.fsencode(str(path)), arr, len(pools), ctypes.byref(params), ctypes.byref(ei),
+                ctypes.byref(xe) if xe is not None else None, ctypes.byref(E), ctypes.byref(st), batch_max,
+                ptr(verdict), ptr(fails, u16p), verdicts_cap, ctypes.byref(S)))
+        else:
+            self.check(self.L.praos_replay_immutable(self.h, os.fsencode(str(path)), arr, len(pools),
+                                                     ctypes.byref(params), ctypes.byref(ei), ctypes.byref(E),
+                                                     ctypes.byref(st), batch_max, ptr(verdict), verdicts_cap,
+                                                     ctypes.byref(S)))
         envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no), bytes(E.tip_hash))
         state.update(_state_from_struct(st, hk, cv))
         stats = {name: getattr(S, name) for name, _ in ReplayStats._fields_}
+        if tpraos:
+            return stats, verdict[:verdicts_cap], fails[:verdicts_cap]
         return stats, verdict[:verdicts_cap]
 
     def apply_batch(self, H, crypto, counters=None):
@@ -861,7 +896,7 @@ class Context:
         sp.corrupt_fields = corrupt_fields
         sp.nkes = nkes
         ctypes.memmove(sp.seed, seed, 32)
-        bstride = (body_len + 7) & ~7 if body_len else SIGNED_STRIDE   # 0: genuine CBOR bodies
+        bstride = (body_len + 7) & ~7 if body_len else (TP_SIGNED_STRIDE if tpraos else SIGNED_STRIDE)
         H = {"slot": np.zeros(n, np.uint64), "cold_vk": np.zeros((n, 32), np.uint8),
              "vrf_vk": np.zeros((n, 32), np.uint8), "vrf_out": np.zeros((n, 64), np.uint8),
              "vrf_proof": np.zeros((n, 80), np.uint8), "hot_vk": np.zeros((n, 32), np.uint8),

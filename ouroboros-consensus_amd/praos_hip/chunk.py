@@ -23,8 +23,10 @@ HEADER_OFFSET = len(BLOCK_PREFIX)
 OVERHEAD = len(BLOCK_PREFIX) + len(HEADER_PREFIX) + len(SIG_HEAD) + 448 + len(BLOCK_SUFFIX)
 
 
-def pack_chunk(H):
-    """H: synthesize() output with CBOR bodies.  Returns (arena u8[], off u64[n], len u32[n])."""
+def pack_chunk(H, era_tag=6):
+    """H: synthesize() output with CBOR bodies.  Returns (arena u8[], off u64[n], len u32[n]).
+    era_tag: the HardForkBlock era of the stored blocks (6 Babbage; 5 Alonzo for TPraos
+    headers from praos_synthesize_tpraos -- the same 4 segments)."""
     n = len(H["slot"])
     bl = H["body_len"].astype(np.int64)
     blk = bl + OVERHEAD
@@ -42,7 +44,7 @@ def pack_chunk(H):
             m = len(R)
             bodies = body[boff[R][:, None] + np.arange(L)[None, :]]
             rec = np.concatenate([
-                np.broadcast_to(np.frombuffer(BLOCK_PREFIX + HEADER_PREFIX, np.uint8), (m, 4)), bodies,
+                np.broadcast_to(np.frombuffer(bytes([0x82, era_tag, 0x85]) + HEADER_PREFIX, np.uint8), (m, 4)), bodies,
                 np.broadcast_to(np.frombuffer(SIG_HEAD, np.uint8), (m, 3)), H["kes_sig"][R],
                 np.broadcast_to(np.frombuffer(BLOCK_SUFFIX, np.uint8), (m, 4))], axis=1)
             arena[start[R][:, None] + np.arange(L + OVERHEAD)[None, :]] = rec

@@ -82,11 +82,13 @@ def _combine(a, b):
     return hashlib.blake2b(a + b, digest_size=32).digest()
 
 
-def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window):
+def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpraos=False, extra_entropy=None):
     """A linked chain over `epochs` epochs of `epoch_length` slots from slot 0 (Origin,
     GenesisHash, epoch 0 nonce = cfg["eta0"]).  Returns dict(arena, off, len, slots,
     header_hash, pools, params, nonces (per epoch), state (after the last
-    block, as Context.update_chain_dep_state keeps it))."""
+    block, as Context.update_chain_dep_state keeps it)).  tpraos=True: a Shelley..Alonzo
+    chain (TPraos leader schedule and BHeaders, stored as Alonzo blocks, era tag 5; the
+    TPraos nonce rules with TICKN's extra_entropy)."""
     sig = chains.stake(cfg["npools"], cfg["stake_offset"])
     p = chains.params(cfg)
     st = {"last_slot": None, "counters": {}, "evolving": cfg["eta0"], "candidate": cfg["eta0"],
@@ -98,18 +100,20 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window):
     for e in range(epochs):
         if e > 0:
             eta = _combine(st["candidate"], st["leb"])      # the tick into epoch e
+            if tpraos:
+                eta = _combine(eta, extra_entropy)          # TICKN
         nonces.append(eta)
-        lead = ctx.leader_schedule(cfg["seed"], sig, p, eta, e * epoch_length, epoch_length)
+        lead = ctx.leader_schedule(cfg["seed"], sig, p, eta, e * epoch_length, epoch_length, tpraos=tpraos)
         idx = np.nonzero(lead >= 0)[0]
         sl = (e * epoch_length + idx).astype(np.uint64)
         pl = lead[idx].astype(np.uint32)
         n = len(sl)
         H, keys, _ = ctx.synthesize(n, cfg["npools"], p, eta, cfg["seed"], body_len=0, schedule=(sl, pl),
-                                    block_no0=block_no, link=True, prev0=prev)
+                                    block_no0=block_no, link=True, prev0=prev, tpraos=tpraos)
         pool_list = [(h, v, s) for (h, v), s in zip(keys, sig)]
         # fold the clean chain to learn the next nonce (the generator's own ledger)
         ctx.set_epoch(eta, pool_list, p)
-        o = ctx.verify_headers(H)
+        o = ctx.verify_tpraos_headers(H) if tpraos else ctx.verify_headers(H)
         prev_hash = np.zeros((n, 32), np.uint8)
         gen = np.zeros(n, np.uint8)
         if prev is None:
@@ -117,7 +121,11 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window):
         else:
             prev_hash[0] = np.frombuffer(prev, np.uint8)
         prev_hash[1:] = H["header_hash"][:-1]
-        _, stop, _ = ctx.update_chain_dep_state(H, o, prev_hash, st, ei, prev_is_genesis=gen)
+        if tpraos:
+            _, _, stop, _ = ctx.tpraos_update_chain_dep_state(H, o, prev_hash, st, ei, prev_is_genesis=gen,
+                                                              extra_entropy=extra_entropy)
+        else:
+            _, stop, _ = ctx.update_chain_dep_state(H, o, prev_hash, st, ei, prev_is_genesis=gen)
         if stop != n:
             raise RuntimeError(f"epoch {e}: generated header {stop} does not validate")
         parts.append(H)
@@ -128,7 +136,7 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window):
     # one stored-bytes arena over all epochs
     arenas, offs, lens, base = [], [], [], 0
     for H in parts:
-        a, o_, l_ = pack_chunk(H)
+        a, o_, l_ = pack_chunk(H, era_tag=5 if tpraos else 6)
         arenas.append(a)
         offs.append(o_ + np.uint64(base))
         lens.append(l_)

@@ -248,3 +248,96 @@ def _soa(D, n):
             "vrf_proof": D["vrf_proof"], "hot_vk": D["hot_vk"], "ocert_n": D["ocert_n"], "ocert_c0": D["ocert_c0"],
             "ocert_sig": D["ocert_sig"], "kes_sig": D["kes_sig"], "body_off": z(n, np.uint64),
             "body_len": z(n, np.uint32), "body_bytes": z(8, np.uint8)}
+
+
+# ---------------------------------------------------------------- TPraos (Shelley..Alonzo)
+TP_EXTRA = b2b(b"tpraos-extra-entropy")
+
+
+@pytest.fixture(scope="module")
+def tchain(ctx, tmp_path_factory):
+    """A linked TPraos chain over 3 epochs (TPraos leader schedule, BHeaders in Alonzo
+    blocks, TICKN with an extra entropy nonce), written as an ImmutableDB."""
+    from praos_hip import immutable
+    cfg = dict(npools=12, stake_offset=1, f=Fraction(1, 2), slots_per_kes_period=129600, max_kes_evo=62,
+               eta0=b2b(b"tpraos-replay-genesis"), seed=b"\x2b" * 32)
+    data = immutable.make_multi_epoch_chain(ctx, cfg, 3, EPOCH_LEN, WINDOW, tpraos=True, extra_entropy=TP_EXTRA)
+    path = str(tmp_path_factory.mktemp("immdb_tp") / "immutable")
+    nchunks = immutable.write_immutable(path, data["arena"], data["off"], data["len"], data["slots"],
+                                        data["header_hash"], CHUNK_SLOTS)
+    data.update(cfg=cfg, path=path, nchunks=nchunks)
+    return data
+
+
+def _tp_replay(ctx, data, path=None, batch_max=1 << 16):
+    st = _genesis_state(data["cfg"]["eta0"])
+    env = dict(ENV, tip=None, lv_prot_major=6)
+    n = len(data["off"])
+    stats, v, f = ctx.replay_immutable(path or data["path"], data["pools"], data["params"], data["epoch_info"], st,
+                                       env, batch_max=batch_max, verdicts_cap=n, tpraos=True,
+                                       extra_entropy=TP_EXTRA)
+    return stats, v, f, st, env
+
+
+def _tp_oracle_fold(ctx, data, upto):
+    """oracle/tpraos.py's fold (TICKN with the extra entropy, PRTCL failure sets) epoch by
+    epoch over headers [0, upto), the TPraos crypto of each epoch from the GPU (stored bytes,
+    praos_verify_tpraos_header_bytes) under that epoch's nonce."""
+    import chainstate as cs
+    import tpraos as tp
+    st = _genesis_state(data["cfg"]["eta0"])
+    known = {h for h, _, _ in data["pools"]}
+    epoch = (data["slots"][:upto] // EPOCH_LEN).astype(int)
+    verdicts, fails, etas = [], [], []
+    for e in range(3):
+        rows = np.nonzero(epoch == e)[0]
+        if len(rows) == 0:
+            break
+        eta = st["epoch_nonce"] if e == 0 else cs.combine(cs.combine(st["candidate"], st["leb"]), TP_EXTRA)
+        etas.append(eta)
+        ctx.set_epoch(eta, data["pools"], data["params"])
+        o, D = ctx.verify_tpraos_header_bytes(data["arena"], data["off"][rows], data["len"][rows], decoded=True)
+        hk = [b2b(bytes(c), 28) for c in D["cold_vk"]]
+        prev = [None if D["prev_is_genesis"][i] else bytes(D["prev_hash"][i]) for i in range(len(rows))]
+        v, f, stop, done = tp.fold(st, hk, D["slot"], o["bits"], D["ocert_n"], o["nonce"], prev, known, eta, 0, 0,
+                                   EPOCH_LEN, WINDOW, extra_entropy=TP_EXTRA)
+        verdicts += v
+        fails += f
+        assert done == len(rows)
+        if stop < len(rows):
+            return verdicts, fails, st, etas, int(rows[stop])
+    return verdicts, fails, st, etas, upto
+
+
+@pytest.mark.parametrize("batch_max", [1 << 16, 61])
+def test_tpraos_replay_all_valid(ctx, tchain, batch_max):
+    """praos_replay_immutable_tpraos over the whole TPraos database: every header valid, the
+    final state = the generator's and the oracle's fold, the epoch nonces include TICKN's
+    extra entropy."""
+    n = len(tchain["off"])
+    stats, v, f, st, env = _tp_replay(ctx, tchain, batch_max=batch_max)
+    assert (stats["headers"], stats["validated"], stats["stop_index"], stats["stop_verdict"]) == (n, n, n, 0)
+    assert int((v != 0).sum()) == 0 and int((f != 0).sum()) == 0
+    assert stats["epochs"] == 3 and stats["batches"] == -(-n // batch_max)
+    assert st == tchain["state"]
+    assert env["tip"] == (int(tchain["slots"][-1]), n - 1, bytes(tchain["header_hash"][-1]))
+    ov, of, ost, etas, ostop = _tp_oracle_fold(ctx, tchain, n)
+    assert ostop == n and etas == tchain["nonces"] and len(set(etas)) == 3
+    assert st == ost
+
+
+def test_tpraos_replay_stops_at_corruption(ctx, tchain, tmp_path):
+    """A KES signature damaged on disk in epoch 1: the replay stops there with the PRTCL
+    failure set {InvalidKesSignatureOCERT} (PRAOS_V_TPRAOS), state = the oracle's."""
+    from praos_hip import abi
+    k = int(np.nonzero(tchain["slots"] >= EPOCH_LEN)[0][7])
+    db = _copy_db(tchain, tmp_path, "tp_kes")
+    fname, pos = _locate(tchain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + int(tchain["len"][k]) - 100] ^= 0x40
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    stats, v, f, st, env = _tp_replay(ctx, tchain, path=db)
+    assert (stats["stop_index"], stats["stop_verdict"], stats["validated"]) == (k, abi.V_TPRAOS, k)
+    assert int((v[:k] != 0).sum()) == 0 and f[k] == abi.TPF_KES_SIG
+    _, _, ost, _, ostop = _tp_oracle_fold(ctx, tchain, k)
+    assert ostop == k and st == ost

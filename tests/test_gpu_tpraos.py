@@ -177,3 +177,79 @@ def test_tpraos_overlay_chain_parity(ctx, oracle):
         assert any(x & tp.TPF_NOT_ACTIVE for x in rf) and any(x & tp.TPF_GEN_COLD for x in rf)
     finally:
         ctx.set_overlay(None, None, 0, 1, [])
+
+
+def test_tpraos_header_bytes_vs_soa_and_oracle(ctx, oracle):
+    """Stored TPraos headers (BHeader = [BHBody, kesSig] in Alonzo blocks, CBOR bodies from the
+    GPU generator) decoded and verified on the device (praos_verify_tpraos_header_bytes):
+    every output equal to the host-SoA path on the same headers, the decoded fields equal the
+    generator's, and a sample bit-exact against the oracle."""
+    from praos_hip import abi, fixed
+    from praos_hip.chunk import pack_chunk
+    p, c_raw = _params(Fraction(1, 2))
+    eta0 = b2b(b"tpraos-bytes-epoch")
+    n = 2048
+    H, pools, corrupted = ctx.synthesize(n, 6, p, eta0, b"\x34" * 32, first_slot=9000, slot_stride=5,
+                                         body_len=0, corrupt_per_10000=400, tpraos=True)
+    assert (H["body_len"] > 540).all() and (H["body_len"] <= 598).all()
+    sig = [fixed.from_rational(Fraction(1, 6))] * 6
+    pool_list = [(h, v, s) for (h, v), s in zip(pools, sig)]
+    ctx.set_epoch(eta0, pool_list, p)
+    o1 = ctx.verify_tpraos_headers(H)
+    arena, off, ln = pack_chunk(H, era_tag=5)
+    o2, D = ctx.verify_tpraos_header_bytes(arena, off, ln, decoded=True)
+    # a body corruption (kind 5: +1 at any byte of the stored BHBody) may land in any decoded
+    # field, so the SoA path (which keeps the generator's fields) only matches elsewhere
+    same = corrupted != 5
+    assert same.sum() > n - 60
+    for k in o1:
+        assert np.array_equal(o1[k][same], o2[k][same]), (k, np.nonzero((o1[k] != o2[k]).reshape(n, -1).any(1))[0][:8])
+    assert (o2["bits"][~same] != 0).all()
+    assert (D["status"][same] == 0).all()
+    for k in ("slot", "cold_vk", "vrf_vk", "vrf_out", "vrf_proof", "hot_vk", "ocert_n", "ocert_c0", "ocert_sig",
+              "kes_sig", "leader_out", "leader_proof"):
+        assert np.array_equal(D[k][same], H[k][same]), k
+    for i in np.nonzero(same)[0]:
+        off_i, ln_i = int(H["body_off"][i]), int(H["body_len"][i])
+        assert int(D["signed_len"][i]) == ln_i
+        assert bytes(D["signed_body"][i][:ln_i]) == bytes(H["body_bytes"][off_i:off_i + ln_i])
+    clean = corrupted == 0
+    assert int((o2["bits"][clean] & ~np.uint16(0x1000)).astype(bool).sum()) == 0
+    assert int((o2["bits"][~clean] == 0).sum()) == 0
+    ep = oracle.make_epoch(eta0, 129600, 62, c_raw, pool_list)
+    for i in list(range(0, n, 97)) + list(np.nonzero(~clean & same)[0][:40]):
+        i = int(i)
+        o_, l_ = int(H["body_off"][i]), int(H["body_len"][i])
+        h = {"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
+             "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
+             "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
+             "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
+             "body": bytes(H["body_bytes"][o_:o_ + l_]), "leader_out": bytes(H["leader_out"][i]),
+             "leader_proof": bytes(H["leader_proof"][i])}
+        r = oracle.tpraos_header(ep, h)
+        assert int(o2["bits"][i]) & TP_BITS == r["bits"], (i, hex(o2["bits"][i]), hex(r["bits"]), corrupted[i])
+        assert bytes(o2["beta_eta"][i]) == r["beta_eta"] and bytes(o2["nonce"][i]) == r["nonce"]
+
+
+def test_tpraos_header_bytes_golden_and_malformed(ctx):
+    """The reference's golden TPraos headers as stored bytes: decoded fields equal the golden
+    ones, OCERT passes, proof_to_hash equals the stored outputs; a Praos (10-field) header and
+    a truncated one are PRAOS_BIT_INPUT."""
+    from praos_hip import abi
+    p, c_raw = _params()
+    ctx.set_epoch(None, [], p)
+    H = bytes.fromhex
+    praos_kat = [k for k in json.load(open(os.path.join(HERE, "golden", "reference_kats.json")))["kats"]
+                 if k["kind"] != "tpraos"][0]
+    hdrs = [H(k["header_cbor"]) for k in KATS] + [H(praos_kat["header_cbor"]), H(KATS[0]["header_cbor"])[:-9]]
+    off = np.cumsum([0] + [len(h) for h in hdrs[:-1]]).astype(np.uint64)
+    ln = np.array([len(h) for h in hdrs], np.uint32)
+    o, D = ctx.verify_tpraos_header_bytes(np.frombuffer(b"".join(hdrs), np.uint8).copy(), off, ln, decoded=True)
+    for i, k in enumerate(KATS):
+        assert D["status"][i] == 0 and int(D["slot"][i]) == k["slot"] and int(D["block_no"][i]) == k["block_no"]
+        assert bytes(D["cold_vk"][i]) == H(k["cold_vk"]) and bytes(D["leader_out"][i]) == H(k["leader_out"])
+        assert bytes(D["leader_proof"][i]) == H(k["leader_proof"]) and bytes(D["body_hash"][i]) == H(k["body_hash"])
+        assert int(o["bits"][i]) & 0x001F == 0, k["era"]
+        assert bytes(o["beta_eta"][i]) == H(k["eta_out"]) and bytes(o["beta_leader"][i]) == H(k["leader_out"])
+    for i in (len(KATS), len(KATS) + 1):
+        assert D["status"][i] & abi.DEC_FAILED and o["bits"][i] & abi.BIT_INPUT
