@@ -201,6 +201,11 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * copied to every header carrying the same bytes; the KES-period checks stay per
  * header.  Verdicts are identical either way. */
 #define PRAOS_OPT_DEDUP 4
+/* PRAOS_OPT_PIPELINE (default 0 = auto): praos_verify_header_bytes runs a batch in this
+ * many chunks (1 = one batch, up to 8), the stored bytes of chunk k+1 moving host ->
+ * device on a copy stream while the kernels of chunk k run and chunk k-1's results move
+ * back; auto = up to 4 chunks of at least 65,536 headers. */
+#define PRAOS_OPT_PIPELINE 5
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items
@@ -499,6 +504,10 @@ typedef struct {
  * validating headers of that slot's epoch.  Pure: st is not changed. */
 int praos_ticked_epoch_nonce(const praos_chain_state* st, const praos_epoch_info* ei, uint64_t slot,
                              praos_nonce* out);
+/* The TPraos tick (cardano-protocol-tpraos TICKN, TPraos.hs:361-376): candidate ⭒
+ * lastEpochBlock ⭒ extra_entropy (NULL = NeutralNonce) on a new epoch. */
+int praos_tpraos_ticked_epoch_nonce(const praos_chain_state* st, const praos_epoch_info* ei, uint64_t slot,
+                                    const praos_nonce* extra_entropy, praos_nonce* out);
 
 int praos_validate_headers(praos_ctx* ctx, const praos_headers* h, const uint8_t* prev_hash,
                            const uint8_t* prev_is_genesis, const praos_out* crypto, praos_envelope* env,

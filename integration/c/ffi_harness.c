@@ -12,6 +12,11 @@
  *   epoch <base_slot> <base_no> <length> <stability_window>
  *   env <max_major_pv> <lv_prot_major> <max_header_size> <max_body_size>
  *   pool <hash28 56 hex> <vrf_hash32 64 hex> <sigma_fp 32 hex, LE>
+ *   tpraos <extra entropy 64 hex | neutral>   (optional) a TPraos (Shelley..Alonzo) database:
+ *                                      the binding's TPraos sequence (praos_tpraos_ticked_epoch_nonce
+ *                                      -> praos_set_epoch -> praos_verify_tpraos_header_bytes ->
+ *                                      praos_tpraos_update_chain_dep_state) and
+ *                                      praos_replay_immutable_tpraos; no "threads" phase
  *
  * Output: one JSON object per phase.
  *   "binding":  praosReplayEpochs as the Haskell module runs it (stream the chunk files,
@@ -72,6 +77,8 @@ static praos_epoch_info g_ei;
 static praos_envelope g_env0;
 static praos_pool* g_pools;
 static uint32_t g_npools;
+static int g_tpraos;
+static praos_nonce g_extra;              /* TICKN's extra entropy (TPraos) */
 
 static void read_epoch_file(const char* path) {
   FILE* f = fopen(path, "r");
@@ -92,6 +99,10 @@ static void read_epoch_file(const char* path) {
       g_ei.epoch_base_slot = x; g_ei.epoch_base_no = y; g_ei.epoch_length = z; g_ei.stability_window = w;
     } else if (sscanf(line, "env %llu %llu %llu %llu", &x, &y, &z, &w) == 4) {
       g_env0.max_major_pv = x; g_env0.lv_prot_major = y; g_env0.max_header_size = z; g_env0.max_body_size = w;
+    } else if (sscanf(line, "tpraos %127s", a) == 1) {
+      g_tpraos = 1;
+      if (strcmp(a, "neutral") == 0) g_extra.neutral = 1;
+      else hex_in(a, g_extra.hash, 32);
     } else if (sscanf(line, "pool %127s %127s %127s", a, b, c) == 3) {
       if (g_npools == cap) {
         cap = cap ? 2 * cap : 64;
@@ -204,7 +215,8 @@ static void phase_binding(const chain_t* ch) {
     while (j < ch->n && (ch->slot[j] - g_ei.epoch_base_slot) / g_ei.epoch_length == e) j++;
     const size_t n = j - i;
     praos_nonce eta;
-    CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
+    if (g_tpraos) CK(ctx, praos_tpraos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &g_extra, &eta));
+    else CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
     CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
     epochs++;
     uint64_t* off = malloc(8 * n);
@@ -221,14 +233,26 @@ static void phase_binding(const chain_t* ch) {
     uint32_t* bsz = calloc(n, 4);
     dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;
     dec.cold_vk = cold; dec.header_hash = hh; dec.body_size = bsz;
-    CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
     praos_headers h;
     memset(&h, 0, sizeof h);
     h.n = n; h.slot = slot; h.cold_vk = cold; h.ocert_n = ocn;
     env.block_no = bno; env.header_hash = hh; env.header_size = ch->hlen + i; env.body_size = bsz;
     uint8_t* verdict = calloc(n, 1);
     size_t stop = 0, done = 0;
-    CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
+    if (g_tpraos) {
+      uint16_t* fails = calloc(n, 2);
+      praos_tpraos_out tout = {bits, pidx, NULL, NULL, nonce};
+      CK(ctx, praos_verify_tpraos_header_bytes(ctx, &hb, &tout, &dec, NULL, NULL));
+      praos_tpraos_headers th;
+      memset(&th, 0, sizeof th);
+      th.h = h;
+      CK(ctx, praos_tpraos_update_chain_dep_state(ctx, &th, prev, gen, &tout, &env, &g_ei, &g_extra, &S.st, verdict,
+                                                  fails, &stop, &done));
+      free(fails);
+    } else {
+      CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
+      CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
+    }
     if (done != n) DIE("an epoch batch did not fold through (%zu of %zu)", done, n);
     const int stopped = stop < n;
     if (stopped) { stop_index = i + stop; stop_verdict = verdict[stop]; validated += stop; }
@@ -250,7 +274,12 @@ static void phase_replay(const char* dir) {
   genesis_state(&S);
   praos_envelope env = g_env0;
   praos_replay_stats rs;
-  CK(ctx, praos_replay_immutable(ctx, dir, g_pools, g_npools, &g_params, &g_ei, &env, &S.st, 1 << 16, NULL, 0, &rs));
+  if (g_tpraos)
+    CK(ctx, praos_replay_immutable_tpraos(ctx, dir, g_pools, g_npools, &g_params, &g_ei, &g_extra, &env, &S.st,
+                                          1 << 16, NULL, NULL, 0, &rs));
+  else
+    CK(ctx, praos_replay_immutable(ctx, dir, g_pools, g_npools, &g_params, &g_ei, &env, &S.st, 1 << 16, NULL, 0,
+                                   &rs));
   print_state("replay", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs);
   praos_close(ctx);
 }
@@ -334,6 +363,6 @@ int main(int argc, char** argv) {
   read_chain(argv[1], &ch);
   phase_binding(&ch);
   phase_replay(argv[1]);
-  phase_threads(&ch, atoi(argv[3]));
+  if (!g_tpraos) phase_threads(&ch, atoi(argv[3]));
   return 0;
 }

@@ -24,15 +24,21 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
   , withPraosBatchCtx
   , PraosBatchError (..)
     -- * Per epoch
+  , PraosParamsC (..)
   , praosSetEpoch
   , praosTickedEpochNonce
     -- * Headers from stored bytes
   , BatchResult (..)
   , praosValidateHeaderBytes
+    -- * TPraos (Shelley..Alonzo) headers from stored bytes
+  , TPraosBatchResult (..)
+  , praosTickedEpochNonceTPraos
+  , praosValidateTPraosHeaderBytes
     -- * Whole ImmutableDB replay (db-analyser)
   , ReplayStats (..)
   , praosReplayImmutable
-    -- * Error reconstruction
+  , praosReplayImmutableTPraos
+    -- * Error reconstruction (typed constructors: module Batch.Errors)
   , verdictToError
   ) where
 
@@ -60,6 +66,8 @@ data PraosCtx
 -- struct praos_envelope (120 bytes): block_no@0 header_hash@8 header_size@16 body_size@24 tip_is_origin@32 tip_slot@40 tip_block_no@48 tip_hash@56 max_major_pv@88 lv_prot_major@96 max_header_size@104 max_body_size@112
 -- struct praos_replay_stats (80 bytes): skipped@0 headers@8 validated@16 stop_index@24 stop_verdict@32 epochs@36 batches@40 chunks@44 ms_io@48 ms_device@56 ms_fold@64 ms_nonce@72
 -- struct praos_decoded (168 bytes): status@0 block_no@8 slot@16 prev_hash@24 prev_is_genesis@32 cold_vk@40 body_size@72 ocert_n@96 header_hash@160
+-- struct praos_tpraos_headers (136 bytes): h@0 leader_out@120 leader_proof@128
+-- struct praos_tpraos_out (40 bytes): bits@0 pool_idx@8 beta_eta@16 beta_leader@24 nonce@32
 
 foreign import ccall safe "praos_open"        c_open        :: CInt -> IO (Ptr PraosCtx)
 foreign import ccall safe "praos_close"       c_close       :: Ptr PraosCtx -> IO ()
@@ -81,9 +89,20 @@ foreign import ccall safe "praos_state_decode" c_state_decode
 foreign import ccall safe "praos_replay_immutable" c_replay_immutable
   :: Ptr PraosCtx -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
   -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
+-- TPraos (include/praos_hip.h: praos_tpraos_*)
+foreign import ccall safe "praos_tpraos_ticked_epoch_nonce" c_tpraos_ticked_epoch_nonce
+  :: Ptr () -> Ptr () -> Word64 -> Ptr () -> Ptr () -> IO CInt
+foreign import ccall safe "praos_verify_tpraos_header_bytes" c_verify_tpraos_header_bytes
+  :: Ptr PraosCtx -> Ptr () -> Ptr () -> Ptr () -> Ptr Word8 -> Ptr Word8 -> IO CInt
+foreign import ccall safe "praos_tpraos_update_chain_dep_state" c_tpraos_update_chain_dep_state
+  :: Ptr PraosCtx -> Ptr () -> Ptr Word8 -> Ptr Word8 -> Ptr () -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> Ptr Word8 -> Ptr Word16 -> Ptr CSize -> Ptr CSize -> IO CInt
+foreign import ccall safe "praos_replay_immutable_tpraos" c_replay_immutable_tpraos
+  :: Ptr PraosCtx -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> CSize -> Ptr Word8 -> Ptr Word16 -> CSize -> Ptr () -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 9
+abiVersion = 10
 
 -- ---------------------------------------------------------------- context
 
@@ -122,12 +141,22 @@ pokeBS :: Ptr a -> Int -> BS.ByteString -> IO ()
 pokeBS p off bs = BSU.unsafeUseAsCStringLen bs $ \(src, n) -> copyBytes (p `plusPtr` off) (castPtr src) n
 
 -- | PraosParams as the ABI wants them (praos_params): slotsPerKESPeriod, maxKESEvo,
--- f == 1, and activeSlotLog f (unActiveSlotLog, Fixed E34 raw, <= 0).
+-- f == 1, activeSlotLog f (unActiveSlotLog, Fixed E34 raw, <= 0), and whether
+-- 'VRF.verifyCertified' compares the certified output with the proof's hash.
+--
+-- ppVrfCheckOutput: cardano-crypto-class >= 2.1 (the CHaP index-state this snapshot
+-- pins, cabal.project:15-20) defines @verifyCertified ctx vk a c = verifyVRF ctx vk a
+-- (certifiedProof c) == Just (certifiedOutput c)@ -- True, the default a caller should pass.
+-- Older cardano-crypto-class releases (1.x: @verifyVRF ... (output, proof) -> Bool@ whose
+-- PraosVRF instance ignored the output) correspond to False.  Either way the batch reports
+-- both facts: PRAOS_BIT_VRF_PROOF (proof) and PRAOS_BIT_VRF_OUTPUT (output mismatch, set
+-- only when checked).
 data PraosParamsC = PraosParamsC
   { ppSlotsPerKESPeriod :: !Word64
   , ppMaxKESEvo         :: !Word64
   , ppFIsOne            :: !Bool
   , ppActiveSlotLogRaw  :: !Integer
+  , ppVrfCheckOutput    :: !Bool
   }
 
 withParams :: PraosParamsC -> (Ptr () -> IO a) -> IO a
@@ -136,7 +165,7 @@ withParams pp k = allocaBytes 40 $ \p -> do
   pokeByteOff p 0 (ppSlotsPerKESPeriod pp)
   pokeByteOff p 8 (ppMaxKESEvo pp)
   pokeByteOff p 16 (if ppFIsOne pp then 1 else 0 :: Word32)
-  pokeByteOff p 20 (1 :: Word32)                       -- verifyCertified checks the output
+  pokeByteOff p 20 (if ppVrfCheckOutput pp then 1 else 0 :: Word32)
   pokeLE (p `plusPtr` 24) 16 (ppActiveSlotLogRaw pp)
   k (castPtr p)
 
@@ -283,6 +312,95 @@ praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
         pure (Just (s, b, h))
       pure (BatchResult vs bs (fromIntegral stop) st' tip')
 
+-- ---------------------------------------------------------------- TPraos headers from stored bytes
+
+-- | tickChainDepState's epoch nonce for TPraos (TICKN: candidate ⭒ lastEpochBlock ⭒ the
+-- extra entropy of the protocol parameters; Nothing = NeutralNonce).
+praosTickedEpochNonceTPraos :: BS.ByteString -> (Word64, Word64, Word64, Word64) -> Word64 -> Maybe BS.ByteString
+                            -> IO (Maybe BS.ByteString)
+praosTickedEpochNonceTPraos stateCbor ei slot extra =
+  withChainState stateCbor (1 + 65536) $ \st -> withEpochInfo ei $ \eip -> allocaBytes 36 $ \xe ->
+  allocaBytes 36 $ \out -> do
+    pokeNonce xe 0 extra
+    rc <- c_tpraos_ticked_epoch_nonce st eip slot (castPtr xe) (castPtr out)
+    when (rc /= 0) $ throwIO (PraosBatchError (fromIntegral rc) "praos_tpraos_ticked_epoch_nonce")
+    peekNonce out 0
+
+-- | One epoch's stored TPraos headers validated (TPraos.updateChainDepState over the
+-- batch, TPraos.hs:378-387, with the envelope): verdicts (PRAOS_V_OK / _ENV_* / _INPUT /
+-- PRAOS_V_TPRAOS), the PRTCL predicate-failure set of each header (PRAOS_TPF_*), the chain
+-- stop and the state / tip after it.
+data TPraosBatchResult = TPraosBatchResult
+  { tbrVerdicts  :: ![Word8]
+  , tbrFailures  :: ![Word16]
+  , tbrBits      :: ![Word16]
+  , tbrChainStop :: !Int
+  , tbrState     :: !BS.ByteString
+  , tbrTip       :: !(Maybe (Word64, Word64, BS.ByteString))
+  }
+
+-- | praos_verify_tpraos_header_bytes (BHeader decode + OCERT, KES, both VRF certificates
+-- and the 2^512 leader test on the GPU) then praos_tpraos_update_chain_dep_state.  The
+-- epoch must have been installed with 'praosSetEpoch' under
+-- 'praosTickedEpochNonceTPraos''s nonce.
+praosValidateTPraosHeaderBytes :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
+                               -> Maybe BS.ByteString -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString
+                               -> [BS.ByteString] -> IO TPraosBatchResult
+praosValidateTPraosHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor hdrs = do
+  let n = length hdrs
+      arena = BS.concat hdrs
+      lens = map BS.length hdrs
+      offs = take n (scanl (+) 0 lens)
+  BSU.unsafeUseAsCString arena $ \ap ->
+    withArray (map fromIntegral offs :: [Word64]) $ \offp ->
+    withArray (map fromIntegral lens :: [Word32]) $ \lenp ->
+    allocaBytes 40 $ \hb ->
+    allocaArray n $ \(bits :: Ptr Word16) -> allocaArray n $ \(pidx :: Ptr Int32) ->
+    allocaBytes (32 * n) $ \nonce ->
+    allocaArray n $ \(slot :: Ptr Word64) -> allocaArray n $ \(bno :: Ptr Word64) ->
+    allocaArray n $ \(ocn :: Ptr Word64) -> allocaArray n $ \(bsz :: Ptr Word32) ->
+    allocaBytes (32 * n) $ \prev -> allocaBytes n $ \gen -> allocaBytes (32 * n) $ \cold ->
+    allocaBytes (32 * n) $ \hh -> allocaBytes 168 $ \dec -> allocaBytes 40 $ \out ->
+    allocaBytes 136 $ \th -> allocaBytes 120 $ \env -> allocaBytes 36 $ \xe ->
+    allocaArray n $ \(verdict :: Ptr Word8) -> allocaArray n $ \(fails :: Ptr Word16) ->
+    alloca $ \stopp -> alloca $ \donep ->
+    withChainState stateCbor (n + 65536) $ \st -> withEpochInfo ei $ \eip -> do
+      pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
+      pokeByteOff hb 16 (fromIntegral (BS.length arena) :: CSize)
+      pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
+      -- praos_tpraos_out: bits, pool_idx, (beta_eta, beta_leader not needed), nonce
+      fillBytes out 0 40 >> pokeByteOff out 0 bits >> pokeByteOff out 8 pidx >> pokeByteOff out 32 nonce
+      fillBytes dec 0 168
+      pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
+      pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
+      check ctx (c_verify_tpraos_header_bytes p (castPtr hb) (castPtr out) (castPtr dec) nullPtr nullPtr)
+      -- praos_tpraos_headers: h = praos_headers (n, slot, cold_vk, ocert_n read by the fold)
+      fillBytes th 0 136
+      pokeByteOff th 0 (fromIntegral n :: CSize) >> pokeByteOff th 8 slot >> pokeByteOff th 16 cold
+      pokeByteOff th 56 ocn
+      fillBytes env 0 120
+      pokeByteOff env 0 bno >> pokeByteOff env 8 hh >> pokeByteOff env 16 lenp >> pokeByteOff env 24 bsz
+      case tip of
+        Nothing -> pokeByteOff env 32 (1 :: Int32)
+        Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+      pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
+      pokeByteOff env 112 maxBS
+      pokeNonce xe 0 extra
+      check ctx (c_tpraos_update_chain_dep_state p (castPtr th) prev gen (castPtr out) (castPtr env) eip
+                                                 (castPtr xe) st verdict fails stopp donep)
+      stop <- peek stopp
+      vs <- peekArray n verdict
+      fs <- peekArray n fails
+      bs <- peekArray n bits
+      st' <- encodeChainState st
+      origin :: Int32 <- peekByteOff env 32
+      tip' <- if origin /= 0 then pure Nothing else do
+        s <- peekByteOff env 40
+        b <- peekByteOff env 48
+        h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+        pure (Just (s, b, h))
+      pure (TPraosBatchResult vs fs bs (fromIntegral stop) st' tip')
+
 -- ---------------------------------------------------------------- ImmutableDB replay
 
 data ReplayStats = ReplayStats
@@ -323,10 +441,49 @@ praosReplayImmutable ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxH
       pure (Just (s, b, h))
     pure (stats, st', tip')
 
+-- | praos_replay_immutable_tpraos: the same replay over a TPraos (Shelley..Alonzo)
+-- ImmutableDB (TICKN's extra entropy, Nothing = NeutralNonce).  Also returns the PRTCL
+-- failure set of every header up to the stop (PRAOS_TPF_*).
+praosReplayImmutableTPraos :: PraosBatchCtx -> FilePath -> [(BS.ByteString, BS.ByteString, Integer)] -> PraosParamsC
+                           -> (Word64, Word64, Word64, Word64) -> EnvLimits -> Maybe BS.ByteString
+                           -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> Int -> Int
+                           -> IO (ReplayStats, [Word8], [Word16], BS.ByteString, Maybe (Word64, Word64, BS.ByteString))
+praosReplayImmutableTPraos ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor
+                           batchMax cap =
+  withCString dir $ \cdir -> withPools pools $ \pp' np -> withParams pp $ \par ->
+  withEpochInfo ei $ \eip -> withChainState stateCbor 65536 $ \st ->
+  allocaBytes 120 $ \env -> allocaBytes 80 $ \rs -> allocaBytes 36 $ \xe ->
+  allocaArray (max 1 cap) $ \(verdicts :: Ptr Word8) -> allocaArray (max 1 cap) $ \(fails :: Ptr Word16) -> do
+    fillBytes env 0 120
+    case tip of
+      Nothing -> pokeByteOff env 32 (1 :: Int32)
+      Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+    pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
+    pokeByteOff env 112 maxBS
+    pokeNonce xe 0 extra
+    check ctx (c_replay_immutable_tpraos p cdir pp' np par eip (castPtr xe) (castPtr env) st (fromIntegral batchMax)
+                                         verdicts fails (fromIntegral cap) (castPtr rs))
+    stats <- ReplayStats <$> peekByteOff rs 0 <*> peekByteOff rs 8 <*> peekByteOff rs 16 <*> peekByteOff rs 24
+                         <*> peekByteOff rs 32 <*> peekByteOff rs 36 <*> peekByteOff rs 40 <*> peekByteOff rs 44
+                         <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64 <*> peekByteOff rs 72
+    let upto = min cap (fromIntegral (rsHeaders stats))
+    vs <- peekArray upto verdicts
+    fs <- peekArray upto fails
+    st' <- encodeChainState st
+    origin :: Int32 <- peekByteOff env 32
+    tip' <- if origin /= 0 then pure Nothing else do
+      s <- peekByteOff env 40
+      b <- peekByteOff env 48
+      h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+      pure (Just (s, b, h))
+    pure (stats, vs, fs, st', tip')
+
 -- ---------------------------------------------------------------- errors
 
--- | The reference error a verdict stands for, as a constructor name plus the payload
--- the caller fills from the header it holds (Praos.hs:319-356 / HeaderValidation.hs).
+-- | The reference error a verdict stands for, by name (logs, traces).  The typed
+-- constructors with their exact payloads (PraosValidationErr, PraosEnvelopeError,
+-- HeaderEnvelopeError, the TPraos PRTCL failures) are built by
+-- "Ouroboros.Consensus.Protocol.Praos.Batch.Errors".
 -- The bits split KES failures into "Reject" (Merkle path, 0x08) and the Ed25519 leaf
 -- ("Verification failed", 0x10), as verifySignedKES reports them.
 verdictToError :: Word8 -> Word16 -> Maybe String
@@ -350,4 +507,5 @@ verdictToError v bits = case v of
   16 -> Just "ObsoleteNode"
   17 -> Just "HeaderSizeTooLarge"
   18 -> Just "BlockSizeTooLarge"
+  19 -> Just "ChainTransitionError (TPraos PRTCL failures)"
   _  -> Just ("unknown verdict " ++ show v)

@@ -257,6 +257,12 @@ __global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __
       for (uint32_t k = slen; k < ((slen + 7) & ~7u); k++) sb[k] = 0;
     }
   }
+  {
+    // the rest of the row is zero too (a batch reused across calls holds no stale bytes)
+    const uint32_t used = slen == 0xffffffffu ? 0u : ((slen + 7) & ~7u);
+    uint64_t* d = (uint64_t*)sb;
+    for (uint32_t k = used; k < stride; k += 8) d[k / 8] = 0ull;
+  }
   const bool ok = r.st == 0;
   if (o.lead_out) {                          // the leader certificate as SoA records (zeros on failure)
     uint64_t* lo = (uint64_t*)(o.lead_out + 64 * i);

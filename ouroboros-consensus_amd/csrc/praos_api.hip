@@ -89,6 +89,9 @@ class CopyPool {
 };
 
 static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2 x 16 MB per context
+static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
+static constexpr size_t PIPE_MIN_CHUNK = 65536;     // headers per chunk at least (auto mode)
+struct praos_batch;
 
 struct praos_ctx {
   int device = 0;
@@ -98,6 +101,13 @@ struct praos_ctx {
   hipEvent_t mdone_ev[3] = {};
   hipStream_t vstream = nullptr;                       // VRF stage V (no key-cache dependence)
   hipEvent_t v_ev = nullptr;
+  // chunked stored-bytes pipeline (praos_verify_header_bytes): a copy stream, per-chunk
+  // events and persistent chunk batches (reused while they are large enough)
+  int pipeline = 0;                                    // PRAOS_OPT_PIPELINE (0 = auto)
+  hipStream_t cstream = nullptr;
+  hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
+  praos_batch* pipe[PIPE_MAX] = {};
+  size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
@@ -166,6 +176,44 @@ static bool stage_init(praos_ctx* c) {
   const unsigned hw = std::thread::hardware_concurrency();
   c->pool.reset(new CopyPool(std::max(1u, std::min(16u, hw ? hw : 1u))));   // the box's CPU share per GPU
   return true;
+}
+
+static hipError_t h2d_on(praos_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (bytes < (4u << 20) || !stage_init(c)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+  for (size_t off = 0, k = 0; off < bytes; off += STAGE_PIECE, k++) {
+    const size_t len = std::min(STAGE_PIECE, bytes - off);
+    hipError_t e = hipEventSynchronize(c->pin_ev[k & 1]);    // the DMA that last used this buffer
+    if (e != hipSuccess) return e;
+    c->pool->copy(c->pin[k & 1], (const uint8_t*)src + off, len);
+    e = hipMemcpyAsync((uint8_t*)dst + off, c->pin[k & 1], len, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(c->pin_ev[k & 1], st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+// D2H on stream st, whose producers the caller has ordered before (an event wait); returns
+// when the bytes are in dst
+static hipError_t d2h_on(praos_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (bytes < (4u << 20) || !stage_init(c)) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    return e == hipSuccess ? hipStreamSynchronize(st) : e;
+  }
+  const size_t np = (bytes + STAGE_PIECE - 1) / STAGE_PIECE;
+  hipError_t e = hipSuccess;
+  for (size_t k = 0; k <= np && e == hipSuccess; k++) {
+    if (k < np) {
+      const size_t off = k * STAGE_PIECE, len = std::min(STAGE_PIECE, bytes - off);
+      e = hipEventSynchronize(c->pin_ev[k & 1]);
+      if (e == hipSuccess) e = hipMemcpyAsync(c->pin[k & 1], (const uint8_t*)src + off, len, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipEventRecord(c->pin_ev[k & 1], st);
+    }
+    if (e == hipSuccess && k > 0) {
+      const size_t j = k - 1, off = j * STAGE_PIECE, len = std::min(STAGE_PIECE, bytes - off);
+      e = hipEventSynchronize(c->pin_ev[j & 1]);
+      if (e == hipSuccess) c->pool->copy((uint8_t*)dst + off, c->pin[j & 1], len);
+    }
+  }
+  return e;
 }
 
 static hipError_t h2d(praos_ctx* c, void* dst, const void* src, size_t bytes) {
@@ -328,6 +376,8 @@ praos_ctx* praos_open(int device) {
   for (auto& e : c->miss_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->mdone_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->v_ev, hipEventDisableTiming);
+  for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
@@ -349,6 +399,7 @@ praos_ctx* praos_open(int device) {
     }
     // the VRF's stage V is the longest chain of a batch and starts at once: greatest priority
     (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, greatest);
+    (void)hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
   }
   if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) {
     c->btab = nullptr;
@@ -414,6 +465,16 @@ void praos_close(praos_ctx* c) {
   for (auto& st : c->mside) if (st) (void)hipStreamDestroy(st);
   if (c->vstream) (void)hipStreamDestroy(c->vstream);
   if (c->v_ev) (void)hipEventDestroy(c->v_ev);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+  for (int k = 0; k < PIPE_MAX; k++) {
+    if (c->pipe[k]) {
+      for (void* p : c->pipe[k]->owned) (void)hipFree(p);
+      delete c->pipe[k];
+    }
+    if (c->up_ev[k]) (void)hipEventDestroy(c->up_ev[k]);
+    if (c->done_ev[k]) (void)hipEventDestroy(c->done_ev[k]);
+  }
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -642,6 +703,44 @@ static praos_batch* upload_bytes_impl(praos_ctx* c, const praos_header_bytes* in
 
 praos_batch* praos_batch_upload_bytes(praos_ctx* c, const praos_header_bytes* in) {
   return upload_bytes_impl(c, in, false);
+}
+
+// device buffers of a from-bytes batch of n headers over an arena of bytes_len bytes
+// (owner == nullptr: fresh allocations, not taken from / given back to the spare list)
+static praos_batch* bytes_batch_alloc(praos_ctx* c, size_t n, size_t bytes_len, bool tpraos, praos_ctx* owner) {
+  praos_batch* b = new praos_batch();
+  b->owner = owner;
+  b->n = n;
+  b->from_bytes = true;
+  b->arena_len = bytes_len;
+  b->tp_only = tpraos;
+  b->signed_stride = tpraos ? TP_SIGNED_STRIDE : PRAOS_SIGNED_STRIDE;
+  b->body_bytes_len = (size_t)b->signed_stride * n;
+  bool ok = alloc_soa(b, n, b->body_bytes_len + 16);
+  if (tpraos) {
+    ok &= dalloc(b, &b->lead_out, 64 * n) == hipSuccess;
+    ok &= dalloc(b, &b->lead_proof, 80 * n) == hipSuccess;
+    ok &= dalloc(b, &b->beta_l, 64 * n) == hipSuccess;
+  }
+  ok &= dalloc(b, &b->arena, ((bytes_len + 7) & ~(size_t)7) + 16) == hipSuccess;  // +16: ld64u pad
+  ok &= dalloc(b, &b->hoff, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->hlen, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->block_no, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prot_major, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prot_minor, 8 * n) == hipSuccess;
+  ok &= dalloc(b, &b->body_size, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prev_hash, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->prev_genesis, n) == hipSuccess;
+  ok &= dalloc(b, &b->body_hash, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->header_hash, 32 * n) == hipSuccess;
+  ok &= dalloc(b, &b->dec_status, 2 * n) == hipSuccess;
+  if (!ok) {
+    c->err = "device allocation failed";
+    for (void* p : b->owned) (void)hipFree(p);
+    delete b;
+    return nullptr;
+  }
+  return b;
 }
 
 static praos_batch* upload_bytes_impl(praos_ctx* c, const praos_header_bytes* in, bool tpraos) {
@@ -1066,6 +1165,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_KERNELS) { c->kernels = value & 7; return PRAOS_OK; }
   if (opt == PRAOS_OPT_KEYCACHE) { c->keycache = value < 0 ? 0 : value; return PRAOS_OK; }
   if (opt == PRAOS_OPT_DEDUP) { c->dedup = value != 0; return PRAOS_OK; }
+  if (opt == PRAOS_OPT_PIPELINE) { c->pipeline = value < 0 ? 0 : std::min(value, PIPE_MAX); return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 
@@ -1201,10 +1301,128 @@ int praos_decode_headers(praos_ctx* c, const praos_header_bytes* in, praos_decod
   return r;
 }
 
+// Stored-bytes verification in K chunks (contiguous runs of headers): the arena slice of
+// chunk k+1 moves H2D on the copy stream (pinned staging, host threads) while the kernels
+// of chunk k run; chunk k's results come back D2H on the copy stream while later chunks
+// compute.  No stream synchronisation between the stages; one at the end.  The chunk
+// batches persist in the context (device buffers allocated once for a given size).
+static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec,
+                                  int K) {
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = in->n;
+  struct Piece {
+    size_t lo, hi;
+    uint64_t base, end;
+    std::vector<uint64_t> off;
+  };
+  std::vector<Piece> P(K);
+  for (int k = 0; k < K; k++) {
+    Piece& p = P[k];
+    p.lo = n * k / K;
+    p.hi = n * (k + 1) / K;
+    p.base = UINT64_MAX;
+    p.end = 0;
+    for (size_t i = p.lo; i < p.hi; i++) {
+      if (in->off[i] > in->bytes_len || in->len[i] > in->bytes_len - in->off[i]) continue;
+      p.base = std::min<uint64_t>(p.base, in->off[i]);
+      p.end = std::max<uint64_t>(p.end, in->off[i] + in->len[i]);
+    }
+    if (p.base == UINT64_MAX) p.base = p.end = 0;
+    p.off.resize(p.hi - p.lo);
+    for (size_t i = p.lo; i < p.hi; i++) {   // rebased; a span outside the caller's arena stays outside
+      const bool in_range = in->off[i] <= in->bytes_len && in->len[i] <= in->bytes_len - in->off[i];
+      p.off[i - p.lo] = in_range ? in->off[i] - p.base : UINT64_MAX / 2;
+    }
+  }
+  // launch: upload chunk k, then its decode + crypto behind the upload
+  for (int k = 0; k < K; k++) {
+    Piece& p = P[k];
+    const size_t m = p.hi - p.lo, bytes = p.end - p.base;
+    if (!c->pipe[k] || c->pipe_n[k] < m || c->pipe_bytes[k] < bytes) {
+      if (c->pipe[k]) {
+        HIPCHK(c, hipDeviceSynchronize());
+        for (void* q : c->pipe[k]->owned) (void)hipFree(q);
+        delete c->pipe[k];
+        c->pipe[k] = nullptr;
+      }
+      const size_t mc = m + m / 8 + 64, bc = bytes + bytes / 8 + 4096;   // headroom for the next call
+      c->pipe[k] = bytes_batch_alloc(c, mc, bc, false, nullptr);
+      if (!c->pipe[k]) return PRAOS_E_OOM;
+      c->pipe_n[k] = mc;
+      c->pipe_bytes[k] = bc;
+    }
+    praos_batch* b = c->pipe[k];
+    b->n = m;
+    b->arena_len = bytes;
+    b->body_bytes_len = (size_t)b->signed_stride * m;
+    b->decoded = false;
+    const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
+    HIPCHK(c, hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream));
+    if (bytes) HIPCHK(c, h2d_on(c, b->arena, in->bytes + p.base, bytes, c->cstream));
+    HIPCHK(c, hipMemcpyAsync(b->hoff, p.off.data(), 8 * m, hipMemcpyHostToDevice, c->cstream));
+    HIPCHK(c, hipMemcpyAsync(b->hlen, in->len + p.lo, 4 * m, hipMemcpyHostToDevice, c->cstream));
+    HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->up_ev[k], 0));
+    const int r = praos_batch_run(c, b);
+    if (r != PRAOS_OK) return r;
+    HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
+  }
+  // results, chunk by chunk, as each finishes
+  for (int k = 0; k < K; k++) {
+    const Piece& p = P[k];
+    praos_batch* b = c->pipe[k];
+    const size_t m = p.hi - p.lo, lo = p.lo;
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->done_ev[k], 0));
+    auto dn = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+      return dst && bytes ? d2h_on(c, dst, src, bytes, c->cstream) : hipSuccess;
+    };
+    HIPCHK(c, dn(out->bits + lo, b->bits, 2 * m));
+    HIPCHK(c, dn(out->pool_idx ? out->pool_idx + lo : nullptr, b->pool_idx, 4 * m));
+    HIPCHK(c, dn(out->beta ? out->beta + 64 * lo : nullptr, b->beta, 64 * m));
+    HIPCHK(c, dn(out->leader ? out->leader + 32 * lo : nullptr, b->leader, 32 * m));
+    HIPCHK(c, dn(out->nonce ? out->nonce + 32 * lo : nullptr, b->nonce, 32 * m));
+    if (dec) {
+      HIPCHK(c, dn(dec->status ? dec->status + lo : nullptr, b->dec_status, 2 * m));
+      HIPCHK(c, dn(dec->block_no ? dec->block_no + lo : nullptr, b->block_no, 8 * m));
+      HIPCHK(c, dn(dec->slot ? dec->slot + lo : nullptr, b->slot, 8 * m));
+      HIPCHK(c, dn(dec->prev_hash ? dec->prev_hash + 32 * lo : nullptr, b->prev_hash, 32 * m));
+      HIPCHK(c, dn(dec->prev_is_genesis ? dec->prev_is_genesis + lo : nullptr, b->prev_genesis, m));
+      HIPCHK(c, dn(dec->cold_vk ? dec->cold_vk + 32 * lo : nullptr, b->cold_vk, 32 * m));
+      HIPCHK(c, dn(dec->vrf_vk ? dec->vrf_vk + 32 * lo : nullptr, b->vrf_vk, 32 * m));
+      HIPCHK(c, dn(dec->vrf_out ? dec->vrf_out + 64 * lo : nullptr, b->vrf_out, 64 * m));
+      HIPCHK(c, dn(dec->vrf_proof ? dec->vrf_proof + 80 * lo : nullptr, b->vrf_proof, 80 * m));
+      HIPCHK(c, dn(dec->body_size ? dec->body_size + lo : nullptr, b->body_size, 4 * m));
+      HIPCHK(c, dn(dec->body_hash ? dec->body_hash + 32 * lo : nullptr, b->body_hash, 32 * m));
+      HIPCHK(c, dn(dec->hot_vk ? dec->hot_vk + 32 * lo : nullptr, b->hot_vk, 32 * m));
+      HIPCHK(c, dn(dec->ocert_n ? dec->ocert_n + lo : nullptr, b->ocert_n, 8 * m));
+      HIPCHK(c, dn(dec->ocert_c0 ? dec->ocert_c0 + lo : nullptr, b->ocert_c0, 8 * m));
+      HIPCHK(c, dn(dec->ocert_sig ? dec->ocert_sig + 64 * lo : nullptr, b->ocert_sig, 64 * m));
+      HIPCHK(c, dn(dec->prot_major ? dec->prot_major + lo : nullptr, b->prot_major, 8 * m));
+      HIPCHK(c, dn(dec->prot_minor ? dec->prot_minor + lo : nullptr, b->prot_minor, 8 * m));
+      HIPCHK(c, dn(dec->kes_sig ? dec->kes_sig + 448 * lo : nullptr, b->kes_sig, 448 * m));
+      HIPCHK(c, dn(dec->signed_len ? dec->signed_len + lo : nullptr, b->body_len, 4 * m));
+      HIPCHK(c, dn(dec->signed_body ? dec->signed_body + (size_t)PRAOS_SIGNED_STRIDE * lo : nullptr, b->body,
+                   (size_t)PRAOS_SIGNED_STRIDE * m));
+      HIPCHK(c, dn(dec->header_hash ? dec->header_hash + 32 * lo : nullptr, b->header_hash, 32 * m));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->cstream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PRAOS_OK;
+}
+
 int praos_verify_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec) {
   if (!c || !in || !out || !out->bits) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
   if (in->n == 0) return PRAOS_OK;
+  if (in->n && (!in->off || !in->len || (!in->bytes && in->bytes_len))) return PRAOS_E_ARG;
+  {
+    // chunked pipeline (PRAOS_OPT_PIPELINE: chunks; 0 = auto: up to 4 chunks of >= 64k headers)
+    int K = c->pipeline;
+    if (K == 0) K = (int)std::min<size_t>(4, in->n / PIPE_MIN_CHUNK);
+    K = std::min<int>(K, (int)std::min<size_t>(PIPE_MAX, in->n));
+    if (K >= 2 && c->device >= 0) return verify_bytes_pipelined(c, in, out, dec, K);
+  }
   praos_batch* b = praos_batch_upload_bytes(c, in);
   if (!b) return PRAOS_E_OOM;
   int r = praos_batch_run(c, b);
@@ -1705,6 +1923,22 @@ int praos_ticked_epoch_nonce(const praos_chain_state* st, const praos_epoch_info
   };
   const uint64_t e_old = st->last_slot_origin ? 0 : epoch_of(st->last_slot);
   *out = epoch_of(slot) > e_old ? nonce_combine(st->candidate, st->last_epoch_block) : st->epoch_nonce;
+  return PRAOS_OK;
+}
+
+int praos_tpraos_ticked_epoch_nonce(const praos_chain_state* st, const praos_epoch_info* ei, uint64_t slot,
+                                    const praos_nonce* extra_entropy, praos_nonce* out) {
+  if (!st || !ei || !out || ei->epoch_length == 0 || slot < ei->epoch_base_slot) return PRAOS_E_ARG;
+  auto epoch_of = [&](uint64_t s) {
+    return ei->epoch_base_no + (s < ei->epoch_base_slot ? 0 : (s - ei->epoch_base_slot) / ei->epoch_length);
+  };
+  const uint64_t e_old = st->last_slot_origin ? 0 : epoch_of(st->last_slot);
+  if (epoch_of(slot) > e_old) {        // TICKN: eta_c ⭒ eta_h ⭒ extraEntropy
+    *out = nonce_combine(st->candidate, st->last_epoch_block);
+    if (extra_entropy) *out = nonce_combine(*out, *extra_entropy);
+  } else {
+    *out = st->epoch_nonce;
+  }
   return PRAOS_OK;
 }
 

@@ -227,6 +227,8 @@ SIGNATURES = {
                                                             ctypes.POINTER(ctypes.c_size_t)]),
     "praos_ticked_epoch_nonce": (ctypes.c_int, [ctypes.POINTER(ChainState), ctypes.POINTER(EpochInfo), ctypes.c_uint64,
                                                 ctypes.POINTER(Nonce)]),
+    "praos_tpraos_ticked_epoch_nonce": (ctypes.c_int, [ctypes.POINTER(ChainState), ctypes.POINTER(EpochInfo),
+                                                       ctypes.c_uint64, ctypes.POINTER(Nonce), ctypes.POINTER(Nonce)]),
     "praos_group_open": (ctypes.c_void_p, [i32p, ctypes.c_int]),
     "praos_group_close": (None, [ctypes.c_void_p]),
     "praos_group_size": (ctypes.c_int, [ctypes.c_void_p]),
@@ -315,7 +317,7 @@ def ptr(a, t=u8p):
     return a.ctypes.data_as(t)
 
 
-OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP = 1, 2, 3, 4     # praos_set_option (include/praos_hip.h)
+OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP, OPT_PIPELINE = 1, 2, 3, 4, 5   # praos_set_option (praos_hip.h)
 
 
 class PraosError(RuntimeError):

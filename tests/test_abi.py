@@ -64,7 +64,8 @@ _STRUCTS = {"praos_params": "Params", "praos_pool": "Pool", "praos_headers": "He
             "praos_header_bytes": "HeaderBytes", "praos_out": "Out", "praos_nonce": "Nonce",
             "praos_chain_state": "ChainState", "praos_epoch_info": "EpochInfo", "praos_envelope": "Envelope",
             "praos_replay_stats": "ReplayStats", "praos_decoded": "Decoded", "praos_counters": "Counters",
-            "praos_synth_params": "SynthParams"}
+            "praos_synth_params": "SynthParams", "praos_tpraos_headers": "TPHeaders",
+            "praos_tpraos_out": "TPOut"}
 HASKELL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "haskell",
                        "Ouroboros", "Consensus", "Protocol", "Praos", "Batch.hs")
 

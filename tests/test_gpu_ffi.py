@@ -16,7 +16,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from test_gpu_replay import ENV, EPOCH_LEN, _genesis_state, _locate, chain  # noqa: F401  (fixture)
+from test_gpu_replay import ENV, EPOCH_LEN, _genesis_state, _locate, chain, tchain  # noqa: F401  (fixtures)
 
 pytestmark = pytest.mark.gpu
 
@@ -24,12 +24,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "integration", "c", "ffi_harness")
 
 
-def _epoch_file(path, chain):
+def _epoch_file(path, chain, tpraos_extra=None):
     p = chain["params"]
+    lv_major = ENV['lv_prot_major'] if tpraos_extra is None else 6
     lines = [f"eta0 {chain['cfg']['eta0'].hex()}",
              f"params {p.slots_per_kes_period} {p.max_kes_evo} {p.f_is_one} {p.vrf_check_output} {bytes(p.c_raw).hex()}",
              "epoch " + " ".join(str(x) for x in chain["epoch_info"]),
-             f"env {ENV['max_major_pv']} {ENV['lv_prot_major']} {ENV['max_header_size']} {ENV['max_body_size']}"]
+             f"env {ENV['max_major_pv']} {lv_major} {ENV['max_header_size']} {ENV['max_body_size']}"]
+    if tpraos_extra is not None:
+        lines.append(f"tpraos {tpraos_extra.hex()}")
     lines += [f"pool {h.hex()} {v.hex()} {int(s).to_bytes(16, 'little').hex()}" for h, v, s in chain["pools"]]
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
@@ -85,4 +88,38 @@ def test_ffi_sequence_stops_with_replay(ctx, chain, tmp_path):  # noqa: F811
     out = _run_harness(db, ef, threads=2)
     stats, cbor, tip = _python_replay(ctx, chain, db)
     assert (stats["stop_index"], stats["stop_verdict"]) == (k, abi.V_KES_SIG)
+    _agree(out, stats, cbor, tip)
+
+
+def test_ffi_tpraos_sequence_matches_replay(ctx, tchain, tmp_path):  # noqa: F811
+    """The TPraos call sequence (praos_tpraos_ticked_epoch_nonce -> praos_set_epoch ->
+    praos_verify_tpraos_header_bytes -> praos_tpraos_update_chain_dep_state, epoch by epoch)
+    and praos_replay_immutable_tpraos, from C, over the TPraos database: both end in the
+    Python TPraos replay's state and tip; with a damaged KES signature all three stop at
+    the same header."""
+    from praos_hip import abi
+    from test_gpu_replay import TP_EXTRA
+    ef = str(tmp_path / "epoch_tp.txt")
+    _epoch_file(ef, tchain, tpraos_extra=TP_EXTRA)
+
+    def py(db):
+        st, env = _genesis_state(tchain["cfg"]["eta0"]), dict(ENV, tip=None, lv_prot_major=6)
+        stats, _, _ = ctx.replay_immutable(db, tchain["pools"], tchain["params"], tchain["epoch_info"], st, env,
+                                           tpraos=True, extra_entropy=TP_EXTRA)
+        return stats, abi.state_encode(st).hex(), env["tip"]
+    out = _run_harness(tchain["path"], ef)
+    stats, cbor, tip = py(tchain["path"])
+    assert stats["validated"] == len(tchain["off"]) and out["binding"]["epochs"] == stats["epochs"] == 3
+    _agree(out, stats, cbor, tip)
+    assert "threads" not in out
+    k = int(np.nonzero(tchain["slots"] >= EPOCH_LEN)[0][11])
+    db = str(tmp_path / "bad_tp")
+    shutil.copytree(tchain["path"], db)
+    fname, pos = _locate(tchain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + int(tchain["len"][k]) - 200] ^= 0x01
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    out = _run_harness(db, ef, threads=2)
+    stats, cbor, tip = py(db)
+    assert (stats["stop_index"], stats["stop_verdict"]) == (k, abi.V_TPRAOS)
     _agree(out, stats, cbor, tip)

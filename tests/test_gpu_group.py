@@ -151,3 +151,28 @@ def _leader_decisions_invariant(o, pool_list, c_raw, band=1e-12):
     checked = (o["bits"][known] & 0x0F1F) == 0       # crypto-valid headers reach the leader test
     assert np.array_equal(gpu_leader[checked], rel[checked] > 0)
     assert float(np.min(np.abs(rel[checked]))) > band, float(np.min(np.abs(rel[checked])))
+
+
+@pytest.mark.parametrize("chunks", [2, 3, 8])
+def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
+    """praos_verify_header_bytes in K chunks (PRAOS_OPT_PIPELINE: H2D of chunk k+1 on the copy
+    stream beside the kernels of chunk k) gives every output and decoded field of the
+    one-batch path, including a header whose span lies outside the arena (DEC_RANGE)."""
+    from praos_hip import abi
+    cfg, H, pool_list, corrupted, p, arena, off, ln = c5_batch
+    off = off.copy()
+    off[5000] = len(arena) + 100                     # out of range
+    ctx.set_epoch(cfg["eta0"], pool_list, p)
+    try:
+        ctx.set_option(abi.OPT_PIPELINE, 1)
+        o1, D1 = ctx.verify_header_bytes(arena, off, ln, decoded=True)
+        ctx.set_option(abi.OPT_PIPELINE, chunks)
+        for _ in range(2):                            # the second call reuses the chunk batches
+            o2, D2 = ctx.verify_header_bytes(arena, off, ln, decoded=True)
+            for k in o1:
+                assert np.array_equal(o1[k], o2[k]), k
+            for k in D1:
+                assert np.array_equal(D1[k], D2[k]), k
+    finally:
+        ctx.set_option(abi.OPT_PIPELINE, 0)
+    assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT
