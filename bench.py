@@ -44,12 +44,12 @@ sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 # kernel schedules (tools/workmodel.py; DESIGN.md sec. 4 "Work model").
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  # noqa: E402
-                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES)
+                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES, W_VRF_V)
 # gfx950 VALU peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02g_traffic.json")   # tools/profile.sh r02g
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03b_traffic.json")   # tools/profile.sh r03b
 FEMUL_FILE = os.path.join(ROOT, "profiles", "r02", "femul_microbench.txt")  # tools/microbench/femul.hip
 
 
@@ -284,7 +284,7 @@ def load_traffic(kernel, workload):
     k = t.get("kernels", {}).get(kernel)
     if not k or t.get("workload") != workload:
         return None, None
-    return k.get("bytes_per_launch"), os.path.relpath(TRAFFIC_FILE, ROOT)
+    return k, os.path.relpath(TRAFFIC_FILE, ROOT)
 
 
 def make_input(ctx, args, cfg, rank, world=1):
@@ -344,6 +344,8 @@ def main():
     ap.add_argument("--concurrent", type=int, default=1, help="run OCert/KES/VRF kernels on 3 streams")
     ap.add_argument("--keycache", type=int, default=2,
                     help="min uses of a public key for the per-batch key cache (0 = off)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="chunks of the stored-bytes e2e pipeline (PRAOS_OPT_PIPELINE; 0 = auto)")
     ap.add_argument("--dedup", type=int, default=1,
                     help="verify each distinct OCert tuple once per batch (PRAOS_OPT_DEDUP; 0 = off)")
     args = ap.parse_args()
@@ -379,6 +381,7 @@ def main():
     if cfg["kernels"] != 7:
         args.dedup = 0
     ctx.set_option(abi.OPT_DEDUP, args.dedup)
+    ctx.set_option(abi.OPT_PIPELINE, args.pipeline)
     t0 = time.perf_counter()
     H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank, world)
     n = len(H["slot"])
@@ -392,12 +395,12 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kms = np.zeros(5)
+    kms = np.zeros(7)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.run(b)
         ctx.sync()                                     # per-step HIP-event kernel times
-        kms += [ctx.kernel_ms(k) for k in range(5)]
+        kms += [ctx.kernel_ms(k) for k in range(7)]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -409,11 +412,11 @@ def main():
     # per-kernel durations for the roofline: serial launches (HIP events on the
     # launch stream), untimed, after the timed region
     ctx.set_option(abi.OPT_CONCURRENT, 0)
-    kser = np.zeros(5)
+    kser = np.zeros(7)
     for _ in range(3):
         ctx.run(b)
         ctx.sync()
-        kser += [ctx.kernel_ms(k) for k in range(5)]
+        kser += [ctx.kernel_ms(k) for k in range(7)]
     kser /= 3
     ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
     kst = ctx.batch_stats(b)
@@ -529,7 +532,7 @@ def main():
     total = n * world if args.scaling == "weak" else (args.items or cfg["items"])
     value = total * steps / dt
     kms /= steps
-    per_kernel = {"ocert": kser[0], "kes": kser[1], "vrf": kser[2], "leader": kser[3]}
+    per_kernel = {"ocert": kser[0], "kes": kser[1], "vrf": kser[2], "leader": kser[3]}   # stream spans
     ran = [k for k in ("ocert", "kes", "vrf") if cfg["kernels"] & MASK[k]]
     # algorithmic work of one run (tools/workmodel.py): headers on cached keys
     # run the short chains, plus the per-key precomputation
@@ -542,13 +545,23 @@ def main():
             work["ocert"] = dds["ocert_unique"] * W_OCERT
     dominant = max(ran, key=lambda k: per_kernel[k])
     wk = work[dominant] / n
-    dom_achieved = work[dominant] / (per_kernel[dominant] * 1e-3)
+    dom_ms = per_kernel[dominant]
+    dom_work = work[dominant]
     w_pipe = (sum(work[k] for k in ran) + (n * W_LEADER if "vrf" in ran else 0)) / n
     pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
     # the dominant kernel as it runs: the key-cache variant when the cache is on
     dom_kernel = f"k_{dominant}_ck" if (args.keycache and kst.get(f"{'cold' if dominant == 'ocert' else dominant}_hits")) \
         else f"k_{dominant}"
-    traffic, traffic_src = load_traffic(dom_kernel, cfg["workload"])
+    if dominant == "vrf" and kser[6] > 0:
+        # the VRF runs in two kernels (k_vrf.hip): stage V (H, Gamma, V = [s]H - [c]Gamma) over
+        # every header is the largest single kernel of the step; price it alone, on the
+        # HIP events around its own launch (serial run, no other kernel on the GPU)
+        dom_kernel, dom_ms, dom_work, wk = "k_vrf_v", float(kser[6]), n * W_VRF_V, W_VRF_V
+    dom_achieved = dom_work / (dom_ms * 1e-3)
+    tk, traffic_src = load_traffic(dom_kernel, cfg["workload"])
+    traffic = tk.get("bytes_per_launch") if tk else None
+    # the same kernel's average duration in the committed rocprofv3 kernel trace (isolated launches)
+    rp_ms = tk.get("rocprof_isolated_avg_ms") if tk else None
     iw_peak, iw_cyc = issue_weighted_peak()
     line = {
         "metric": cfg["metric"],
@@ -566,7 +579,15 @@ def main():
                      "achieved": round(dom_achieved / 1e12, 3), "peak": round(PEAK_INT32 / 1e12, 2),
                      "unit": "T int32-ops/s", "frac": round(dom_achieved / PEAK_INT32, 4), "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": traffic_src,
-                     "work_per_unit": round(wk), "pipeline_achieved": round(pipe_achieved / 1e12, 3),
+                     "algorithmic_bytes_per_launch": n * (120 + 336) if dom_kernel == "k_vrf_v" else None,
+                     "algorithmic_bytes_basis": "per header: vrf_vk 32 + proof 80 + slot 8 read, the 336-byte "
+                                                "stage record (V, H, 8 Gamma, enc Gamma, flag) written"
+                                                if dom_kernel == "k_vrf_v" else None,
+                     "rocprof_isolated_avg_ms": rp_ms,
+                     "frac_rocprof": round(dom_work / (rp_ms * 1e-3) / PEAK_INT32, 4) if rp_ms else None,
+                     "work_per_unit": round(wk), "kernel_ms": round(dom_ms, 3),
+                     "kernel_ms_concurrent": round(float(kms[6]), 3) if dom_kernel == "k_vrf_v" else None,
+                     "pipeline_achieved": round(pipe_achieved / 1e12, 3),
                      "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": round(w_pipe),
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},
                      "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent),

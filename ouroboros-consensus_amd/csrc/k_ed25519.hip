@@ -63,9 +63,9 @@ __global__ void __launch_bounds__(NT, LB_ED) k_ocert_ck(const uint32_t* __restri
                                                         const uint32_t* __restrict__ kinfo,
                                                         const ge_niels* __restrict__ gbtab, OcertIn a) {
   const size_t items = *count;
-  if ((size_t)blockIdx.x * NT >= items) return;
+  if ((size_t)blockIdx.x * blockDim.x >= items) return;
   const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
-  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= items) return;
   const size_t i = list[t];
   const size_t e = (size_t)item_entry[i];
@@ -159,9 +159,9 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ kinfo,
                                                       const ge_niels* __restrict__ gbtab, KesIn a) {
   const size_t items = *count;
-  if ((size_t)blockIdx.x * NT >= items) return;
+  if ((size_t)blockIdx.x * blockDim.x >= items) return;
   const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
-  const size_t q = (size_t)blockIdx.x * NT + threadIdx.x;
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= items) return;
   const size_t i = list[q];
   const size_t e = (size_t)item_entry[i];

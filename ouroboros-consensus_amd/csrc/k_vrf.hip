@@ -1,56 +1,9 @@
 // k_vrf.hip -- ECVRF draft-03 verify + pool lookup + range extension kernel.
-#include "kcommon.hpp"
+#include "k_vrf.hpp"
 
 // ------------------------------------------------------------------ VRF
-// Header mode: issuer hash -> pool (binary search), VRF key hash, alpha =
-// mkInputVRF(slot, eta0), proof verify, beta, output check, leader/nonce values.
-// Plain mode (ok_out != null): alpha given per item; ok_out, beta only.
 // Items: i in [0, n) or list[0 .. *count) (key-cache partition, k_keys.hip):
 // k_vrf takes the misses, k_vrf_ck the hits (cached VRF key, short U chain).
-struct VrfIn {
-  const uint8_t* __restrict__ cold_vk;
-  const uint8_t* __restrict__ vrf_vk;
-  const uint8_t* __restrict__ vrf_out;
-  const uint8_t* __restrict__ vrf_proof;
-  const uint64_t* __restrict__ slot;
-  const uint32_t* __restrict__ eta0;     // eta_idx == null: the epoch nonce (8 words)
-  int eta0_neutral;
-  const uint8_t* __restrict__ eta_idx;   // several epochs per batch: header i uses entry eta_idx[i]
-                                         // of eta0 = table of 9-word entries (nonce, neutral flag)
-  const uint32_t* __restrict__ pool_hash;
-  const uint32_t* __restrict__ pool_vrf;
-  const int32_t* __restrict__ pool_map;
-  uint32_t npools;
-  int check_output;
-  const uint8_t* __restrict__ alpha_in;
-  uint16_t* __restrict__ bits;
-  int32_t* __restrict__ pool_idx;
-  int32_t* __restrict__ pool_sorted_idx;
-  uint8_t* __restrict__ beta_out;
-  uint8_t* __restrict__ leader_out;
-  uint8_t* __restrict__ nonce_out;
-  uint8_t* __restrict__ ok_out;
-  ge_cached* __restrict__ tabs;          // per-lane tables (LT_VRF entries per item)
-};
-
-// issuer pool: hashKey (Blake2b-224 of the cold vk, Praos.hs:552) -> sorted index or -1
-__device__ __forceinline__ int32_t pool_search(const uint32_t hk[8], const uint32_t* __restrict__ pool_hash,
-                                               uint32_t npools) {
-  int lo = 0, hi = (int)npools - 1;
-  while (lo <= hi) {
-    const int mid = (lo + hi) >> 1;
-    const uint32_t* ph = pool_hash + 7 * mid;
-    int c = 0;
-    for (int k = 0; k < 7 && c == 0; k++) {
-      const uint32_t x = __builtin_bswap32(ph[k]), q = __builtin_bswap32(hk[k]);   // byte order
-      c = x < q ? -1 : (x > q ? 1 : 0);
-    }
-    if (c == 0) return mid;
-    if (c < 0) lo = mid + 1; else hi = mid - 1;
-  }
-  return -1;
-}
-
 template <bool CACHED>
 __device__ __forceinline__ void vrf_item(const VrfIn& a, size_t i, const ge_niels* __restrict__ btab,
                                          const ge_cached* __restrict__ ktab, const uint32_t* __restrict__ kinfo) {
@@ -115,112 +68,6 @@ __device__ __forceinline__ void vrf_item(const VrfIn& a, size_t i, const ge_niel
   a.pool_idx[i] = sidx < 0 ? -1 : a.pool_map[sidx];
   a.pool_sorted_idx[i] = sidx;
   a.bits[i] = b;
-}
-
-// ---- two-stage form of the header mode (praos_core.hpp vrf_v_core / vrf_fin_core)
-// alpha = mkInputVRF(slot, eta) of header i (Praos/VRF.hs:55-69)
-__device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, size_t i) {
-  uint32_t e0[8];
-  const uint32_t* ep = a.eta_idx ? a.eta0 + 9 * (uint32_t)a.eta_idx[i] : a.eta0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) e0[k] = ep[k];
-  const bool neutral = a.eta_idx ? ep[8] != 0 : a.eta0_neutral != 0;
-  mk_input_vrf(alpha, a.slot[i], e0, neutral);
-}
-
-// stage V over every header of the batch: no dependence on the key cache
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_v(size_t n, VrfIn a, uint4* __restrict__ mid) {
-  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
-  if (i >= n) return;
-  uint32_t pk[8], pr[20], alpha[8];
-  load_words(pk, a.vrf_vk + 32 * i, 8);
-  load_words(pr, a.vrf_proof + 80 * i, 20);
-  header_alpha(alpha, a, i);
-  vrf_v_core(mid, n, i, pk, pr, pr + 8, pr + 12, alpha, lane_tab(a.tabs, i, LT_VRF));
-}
-
-// stage F: pool lookup and key hash (Praos.hs:533-541), U + challenge + beta, the output
-// check and the range extension -- the same results vrf_item writes in header mode
-template <bool CACHED>
-__device__ __forceinline__ void vrf_fin_item(const VrfIn& a, size_t i, size_t stride, const uint4* __restrict__ mid,
-                                             const ge_niels* __restrict__ btab, const ge_cached* __restrict__ ktab,
-                                             const uint32_t* __restrict__ kinfo) {
-  uint32_t pk[8], pr[20];
-  load_words(pk, a.vrf_vk + 32 * i, 8);
-  load_words(pr, a.vrf_proof + 80 * i, 20);
-  uint16_t b = 0;
-  int32_t sidx;
-  {
-    uint32_t cv[8], hk[8];
-    load_words(cv, a.cold_vk + 32 * i, 8);
-    blake2b_32(hk, cv, 28);
-    sidx = pool_search(hk, a.pool_hash, a.npools);
-    if (sidx < 0) {
-      b |= PRAOS_BIT_VRF_KEY_UNKNOWN;
-    } else {
-      uint32_t vh[8];
-      blake2b_32(vh, pk, 32);
-      bool same = true;
-#pragma unroll
-      for (int k = 0; k < 8; k++) same &= vh[k] == a.pool_vrf[8 * sidx + k];
-      if (!same) b |= PRAOS_BIT_VRF_KEY_WRONG;
-    }
-  }
-  uint32_t beta[16];
-  bool gamma_ok;
-  const bool proof_ok = vrf_fin_core<CACHED>(beta, gamma_ok, mid, stride, i, pk, pr + 8, pr + 12, btab,
-                                             lane_tab(a.tabs, i, LT_VRF), ktab, kinfo);
-  if (!gamma_ok) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) beta[k] = 0;
-  }
-  uint32_t out[16];
-  load_words(out, a.vrf_out + 64 * i, 16);
-  bool out_eq = true;
-#pragma unroll
-  for (int k = 0; k < 16; k++) out_eq &= out[k] == beta[k];
-  if (!proof_ok) b |= PRAOS_BIT_VRF_PROOF;
-  if (!out_eq && a.check_output) b |= PRAOS_BIT_VRF_OUTPUT;
-  uint32_t lv[8], nv[8], nn[8];
-  blake2b256_tag64(lv, 'L', out);
-  blake2b256_tag64(nv, 'N', out);
-  blake2b_32(nn, nv, 32);
-  store_words(a.leader_out + 32 * i, lv, 8);
-  store_words(a.nonce_out + 32 * i, nn, 8);
-  store_words(a.beta_out + 64 * i, beta, 16);
-  a.pool_idx[i] = sidx < 0 ? -1 : a.pool_map[sidx];
-  a.pool_sorted_idx[i] = sidx;
-  a.bits[i] = b;
-}
-
-// cached keys (the hit list): U from the key's tables and the radix-2^16 comb
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_fin(size_t stride, const uint32_t* __restrict__ list,
-                                                        const uint32_t* __restrict__ count,
-                                                        const int32_t* __restrict__ item_entry,
-                                                        const ge_cached* __restrict__ ktab,
-                                                        const uint32_t* __restrict__ kinfo,
-                                                        const ge_niels* __restrict__ comb, VrfIn a,
-                                                        const uint4* __restrict__ mid) {
-  const size_t items = *count;
-  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
-  if (t >= items) return;
-  const size_t i = list[t];
-  const size_t e = (size_t)item_entry[i];
-  vrf_fin_item<true>(a, i, stride, mid, comb, ktab + e * KT_STRIDE, kinfo + 9 * e);
-}
-
-// uncached keys (the miss list, or every header): U on a per-lane chain
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_fin_nc(size_t n, const uint32_t* __restrict__ list,
-                                                           const uint32_t* __restrict__ count,
-                                                           const ge_niels* __restrict__ gbtab, VrfIn a,
-                                                           const uint4* __restrict__ mid) {
-  const size_t items = list ? (size_t)*count : n;
-  if ((size_t)blockIdx.x * NT >= items) return;
-  __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
-  const size_t t = (size_t)blockIdx.x * NT + threadIdx.x;
-  if (t >= items) return;
-  vrf_fin_item<false>(a, list ? list[t] : t, n, mid, btab, nullptr, nullptr);
 }
 
 __global__ void __launch_bounds__(NT, LB_VRF) k_vrf(size_t n, const uint32_t* __restrict__ list,
@@ -370,38 +217,6 @@ void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
   VrfIn a{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, eta_idx, pool_hash, pool_vrf, pool_map, npools,
           check_output, alpha_in, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, ok_out, tabs};
   hipLaunchKernelGGL(k_vrf_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
-}
-static VrfIn vrf_in(const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
-                    const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx,
-                    const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools,
-                    int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
-                    uint8_t* leader_out, uint8_t* nonce_out, ge_cached* tabs) {
-  return VrfIn{cold_vk, vrf_vk, vrf_out, vrf_proof, slot, eta0, eta0_neutral, eta_idx, pool_hash, pool_vrf, pool_map,
-               npools, check_output, nullptr, bits, pool_idx, pool_sorted_idx, beta_out, leader_out, nonce_out, nullptr,
-               tabs};
-}
-void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
-                  const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid) {
-  const VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
-                         nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
-  hipLaunchKernelGGL(k_vrf_v, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, n, a, (uint4*)mid);
-}
-void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
-                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
-                    const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
-                    const uint8_t* vrf_proof, const uint32_t* pool_hash, const uint32_t* pool_vrf,
-                    const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx,
-                    int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out,
-                    ge_cached* tabs, const void* mid) {
-  const VrfIn a = vrf_in(cold_vk, vrf_vk, vrf_out, vrf_proof, nullptr, nullptr, 0, nullptr, pool_hash, pool_vrf,
-                         pool_map, npools, check_output, bits, pool_idx, pool_sorted_idx, beta_out, leader_out,
-                         nonce_out, tabs);
-  const dim3 g((unsigned)((n + NT - 1) / NT));
-  if (ktab)
-    hipLaunchKernelGGL(k_vrf_fin, g, dim3(NT), 0, stream, n, list, count, item_entry, ktab, kinfo, comb, a,
-                       (const uint4*)mid);
-  else
-    hipLaunchKernelGGL(k_vrf_fin_nc, g, dim3(NT), 0, stream, n, list, count, gbtab, a, (const uint4*)mid);
 }
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk,
                    const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out,

@@ -4,6 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+// Block size of the kernels without LDS tables (V / U / join of the VRF, the cached-key
+// Ed25519 chains).  1-wave blocks for small batches (so that 54k headers = 844 waves spread
+// over all 256 CUs instead of 211 four-wave blocks) measured slower (k_vrf_v 2.70 -> 2.98 ms
+// at 54k, profiles/r03/timeline_54k_wave_blocks.txt): 4-wave blocks everywhere.
+static inline unsigned lat_block(size_t n) { (void)n; return 256u; }
 struct ge_niels;
 struct ge_cached;
 void launch_ocert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
@@ -98,6 +103,16 @@ void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const ui
                     const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx,
                     int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out,
                     ge_cached* tabs, const void* mid);
+// three-kernel VRF: stage U (cached: ktab != null, k_vrf_u over the hit list; uncached: k_vrf_u_nc
+// over list[0 .. *count) or all n, 8-entry lane tables utabs) and the join over all n
+void launch_vrf_u(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
+                  const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const ge_niels* gbtab,
+                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid);
+void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const uint8_t* vrf_vk,
+                     const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
+                     const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
+                     uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
+                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid);
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs,
                    const int32_t* ovl_class, const uint32_t* gen, const uint8_t* eta_idx = nullptr);
 void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena, uint64_t arena_len,

@@ -12,7 +12,7 @@ static constexpr size_t BCOMB_TABLES = 32;         // fixed-base comb: 256^j B, 
 static constexpr size_t C16_TABLES = 16, C16_ENTRIES = 32768;   // radix-2^16 comb (scalarmult.hpp C16_T, C16_N)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
 static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
-static constexpr size_t VRF_MID_BYTES = 21 * 16;    // per-header record of the two-stage VRF (praos_core.hpp)
+static constexpr size_t VRF_MID_BYTES = 28 * 16;    // per-header records of the staged VRF (praos_core.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
 #include <algorithm>
@@ -101,6 +101,15 @@ struct praos_ctx {
   hipEvent_t mdone_ev[3] = {};
   hipStream_t vstream = nullptr;                       // VRF stage V (no key-cache dependence)
   hipEvent_t v_ev = nullptr;
+  hipEvent_t v0_ev = nullptr, v1_ev = nullptr;         // timing of k_vrf_v on its stream (kernel_ms[6])
+  hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
+  // second engine of the stored-bytes pipeline: its own streams and events, the parent's
+  // tables (btab, comb, epoch) borrowed, so consecutive chunks run concurrently
+  praos_ctx* twin = nullptr;
+  bool borrowed = false;
+  hipEvent_t pipe_ev = nullptr;                        // the twin's start: after the parent's queued work
+  int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
+                                                       // the three-kernel form below 300k headers (latency)
   // chunked stored-bytes pipeline (praos_verify_header_bytes): a copy stream, per-chunk
   // events and persistent chunk batches (reused while they are large enough)
   int pipeline = 0;                                    // PRAOS_OPT_PIPELINE (0 = auto)
@@ -116,8 +125,9 @@ struct praos_ctx {
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
-  float kernel_ms[6] = {0, 0, 0, 0, 0, 0};
+  float kernel_ms[7] = {0, 0, 0, 0, 0, 0, 0};
   bool last_from_bytes = false;
+  bool v_timed = false;                                // the last run launched k_vrf_v
   std::string err;
   ge_niels* btab = nullptr;
   ge_niels* bcomb16 = nullptr;                         // radix-2^16 comb of the cached-key chains (48 MB)
@@ -263,6 +273,7 @@ struct praos_batch {
   uint8_t *beta = nullptr, *leader = nullptr, *nonce = nullptr;
   // per-lane point tables of the three crypto kernels (kcommon.hpp lane_tab)
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
+  ge_cached* tab_vrfu = nullptr;   // 8-entry lane tables of stage U on uncached VRF keys
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
@@ -352,30 +363,23 @@ int praos_abi_version(void) { return PRAOS_ABI_VERSION; }
 
 const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
-praos_ctx* praos_open(int device) {
-  if (device == PRAOS_HOST_ONLY) {
-    praos_ctx* c = new praos_ctx();
-    c->device = -1;
-    return c;
-  }
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
-    fprintf(stderr, "praos_open: no HIP device %d (count %d)\n", device, ndev);
-    return nullptr;
-  }
-  praos_ctx* c = new praos_ctx();
-  c->device = device;
+// streams and events of a context (praos_open, and the pipeline's second engine)
+static bool open_streams(praos_ctx* c) {
   if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp) != 0;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->stream = nullptr;
-    praos_close(c);
-    return nullptr;
+    return false;
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   for (auto& e : c->side_ev) (void)hipEventCreate(&e);
   for (auto& e : c->miss_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->mdone_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->v_ev, hipEventDisableTiming);
+  (void)hipEventCreate(&c->v0_ev);
+  (void)hipEventCreateWithFlags(&c->u_ev, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->pipe_ev, hipEventDisableTiming);
+  if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
+  (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
@@ -400,6 +404,26 @@ praos_ctx* praos_open(int device) {
     // the VRF's stage V is the longest chain of a batch and starts at once: greatest priority
     (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, greatest);
     (void)hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
+  }
+  return true;
+}
+
+praos_ctx* praos_open(int device) {
+  if (device == PRAOS_HOST_ONLY) {
+    praos_ctx* c = new praos_ctx();
+    c->device = -1;
+    return c;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+    fprintf(stderr, "praos_open: no HIP device %d (count %d)\n", device, ndev);
+    return nullptr;
+  }
+  praos_ctx* c = new praos_ctx();
+  c->device = device;
+  if (!open_streams(c)) {
+    praos_close(c);
+    return nullptr;
   }
   if (hipMalloc(&c->btab, BCOMB_TABLES * BTAB_N * NIELS_BYTES) != hipSuccess) {
     c->btab = nullptr;
@@ -446,12 +470,15 @@ void praos_close(praos_ctx* c) {
   if (!c) return;
   if (c->device < 0) { delete c; return; }
   (void)hipSetDevice(c->device);
+  if (c->twin) praos_close(c->twin);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  free_epoch(c);
+  if (!c->borrowed) {
+    free_epoch(c);
+    (void)hipFree(c->d_gen);
+    (void)hipFree(c->btab);
+    (void)hipFree(c->bcomb16);
+  }
   free_spare(c);
-  (void)hipFree(c->d_gen);
-  (void)hipFree(c->btab);
-  (void)hipFree(c->bcomb16);
   c->pool.reset();
   for (int k = 0; k < 2; k++) {
     if (c->pin[k]) (void)hipHostFree(c->pin[k]);
@@ -465,6 +492,10 @@ void praos_close(praos_ctx* c) {
   for (auto& st : c->mside) if (st) (void)hipStreamDestroy(st);
   if (c->vstream) (void)hipStreamDestroy(c->vstream);
   if (c->v_ev) (void)hipEventDestroy(c->v_ev);
+  if (c->v0_ev) (void)hipEventDestroy(c->v0_ev);
+  if (c->u_ev) (void)hipEventDestroy(c->u_ev);
+  if (c->pipe_ev) (void)hipEventDestroy(c->pipe_ev);
+  if (c->v1_ev) (void)hipEventDestroy(c->v1_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (int k = 0; k < PIPE_MAX; k++) {
     if (c->pipe[k]) {
@@ -590,6 +621,7 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   ok &= dalloc(b, (uint8_t**)&b->tab_ocert, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_kes, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&b->tab_vrf, LT_VRF_B * n) == hipSuccess;
+  ok &= dalloc(b, (uint8_t**)&b->tab_vrfu, LT_ED_B * n) == hipSuccess;
   ok &= dalloc(b, &b->vrf_mid, VRF_MID_BYTES * n) == hipSuccess;
   ok &= dalloc(b, &b->kes_leaf, 32 * n) == hipSuccess;
   b->dd_cap = 256;
@@ -835,6 +867,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   uint16_t* bk = b->bits3 + n;
   uint16_t* bv = b->bits3 + 2 * n;
   const dim3 g(nblocks(n, NT)), blk(NT);
+  const dim3 gl(nblocks(n, lat_block(n))), bl(lat_block(n));     // kernels without LDS tables
   // The three crypto kernels are independent; run concurrently they fill each
   // other's tail waves (one launch of 432k headers is ~3.3 rounds of resident
   // waves).  Each writes its own bit array; k_leader joins and combines.
@@ -842,6 +875,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   hipStream_t sk = c->concurrent ? c->side[1] : c->stream;
   hipStream_t sv = c->concurrent ? c->side[2] : c->stream;
   c->last_from_bytes = b->from_bytes;
+  c->v_timed = false;
   if (b->from_bytes) {
     // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
@@ -921,7 +955,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                      b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
+      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, b->dd_ok);
     } else {
@@ -952,7 +986,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                      b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(g, blk, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
+      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, (uint8_t*)nullptr);
     } else {
@@ -978,7 +1012,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                  b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
                  bk, (uint8_t*)nullptr, b->tab_kes);
       keycache_precompute(k, b->kes_leaf, 0, sk);
-      launch_kes_ck(g, blk, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
+      launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                     P.slots_per_kes_period, bk);
     } else {
@@ -997,8 +1031,11 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
     hipStream_t sV = c->concurrent ? c->vstream : c->stream;
     if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
+    HIPCHK(c, hipEventRecord(c->v0_ev, sV));
     launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf, b->vrf_mid);
+    HIPCHK(c, hipEventRecord(c->v1_ev, sV));
     HIPCHK(c, hipEventRecord(c->v_ev, sV));
+    c->v_timed = true;
     auto after_v = [&](hipStream_t st) -> int {
       if (st != sV) HIPCHK(c, hipStreamWaitEvent(st, c->v_ev, 0));
       return PRAOS_OK;
@@ -1009,7 +1046,37 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                      c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx,
                      b->pool_sorted, b->beta, b->leader, b->nonce, b->tab_vrf, b->vrf_mid);
     };
-    if (kc) {
+    auto stage_u = [&](hipStream_t st, const uint32_t* list, const uint32_t* count, const praos_batch::KeyCache* k) {
+      launch_vrf_u(st, n, list, count, k ? k->item_entry : nullptr, k ? k->ktab : nullptr, k ? k->kinfo : nullptr,
+                   c->bcomb16, c->btab, b->vrf_vk, b->vrf_proof, b->tab_vrfu, b->vrf_mid);
+    };
+    auto join = [&](hipStream_t st) {
+      launch_vrf_join(st, n, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, c->d_pool_hash, c->d_pool_vrf,
+                      c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta,
+                      b->leader, b->nonce, b->vrf_mid);
+    };
+    if (c->vrf3 > 0 || (c->vrf3 < 0 && n < 300000)) {
+      // three kernels: U runs beside V (uncached keys at once on the miss stream, cached keys
+      // once their tables exist), the join after both
+      int r;
+      if (kc) {
+        praos_batch::KeyCache& k = b->kc[1];
+        r = keycache_lists(k, b->vrf_vk, sv);
+        if (r == PRAOS_OK) r = to_main(2, sv);
+        if (r != PRAOS_OK) return r;
+        stage_u(sm_[2], k.miss, k.counters + 2, nullptr);
+        if (sm_[2] != sv) {
+          HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
+        }
+        keycache_precompute(k, b->vrf_vk, 1, sv);
+        stage_u(sv, k.hit, k.counters + 1, &k);
+        if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
+      } else {
+        stage_u(sv, nullptr, nullptr, nullptr);
+      }
+      if ((r = after_v(sv)) != PRAOS_OK) return r;
+      join(sv);
+    } else if (kc) {
       praos_batch::KeyCache& k = b->kc[1];
       int r = keycache_lists(k, b->vrf_vk, sv);
       if (r == PRAOS_OK) r = to_main(2, sv);
@@ -1190,11 +1257,13 @@ int praos_batch_sync(praos_ctx* c) {
   c->kernel_ms[3] = all - (c->concurrent ? std::max(t[0], std::max(t[1], t[2])) : t[2]);
   c->kernel_ms[4] = all + dec;
   c->kernel_ms[5] = dec;
+  c->kernel_ms[6] = 0;
+  if (c->v_timed) (void)hipEventElapsedTime(&c->kernel_ms[6], c->v0_ev, c->v1_ev);
   return PRAOS_OK;
 }
 
 float praos_batch_kernel_ms(praos_ctx* c, int which) {
-  if (!c || which < 0 || which > 5) return -1.f;
+  if (!c || which < 0 || which > 6) return -1.f;
   return c->kernel_ms[which];
 }
 
@@ -1301,11 +1370,49 @@ int praos_decode_headers(praos_ctx* c, const praos_header_bytes* in, praos_decod
   return r;
 }
 
+// The pipeline's second engine: created on first use, then re-pointed at the parent's
+// current tables and options before each call (it is idle between calls).
+static praos_ctx* pipeline_twin(praos_ctx* c) {
+  if (!c->twin) {
+    praos_ctx* t = new praos_ctx();
+    t->device = c->device;
+    t->borrowed = true;
+    if (!open_streams(t)) {
+      praos_close(t);
+      return nullptr;
+    }
+    c->twin = t;
+  }
+  praos_ctx* t = c->twin;
+  t->btab = c->btab;
+  t->bcomb16 = c->bcomb16;
+  t->have_epoch = c->have_epoch;
+  t->params = c->params;
+  std::memcpy(t->eta0, c->eta0, 32);
+  t->eta0_neutral = c->eta0_neutral;
+  t->npools = c->npools;
+  t->d_pool_hash = c->d_pool_hash;
+  t->d_pool_vrf = c->d_pool_vrf;
+  t->d_pool_x = c->d_pool_x;
+  t->d_pool_map = c->d_pool_map;
+  t->d_eta0 = c->d_eta0;
+  t->concurrent = c->concurrent;
+  t->kernels = c->kernels;
+  t->keycache = c->keycache;
+  t->dedup = c->dedup;
+  t->vrf3 = c->vrf3;
+  t->key_wave_prio = c->key_wave_prio;
+  return t;
+}
+
 // Stored-bytes verification in K chunks (contiguous runs of headers): the arena slice of
 // chunk k+1 moves H2D on the copy stream (pinned staging, host threads) while the kernels
 // of chunk k run; chunk k's results come back D2H on the copy stream while later chunks
-// compute.  No stream synchronisation between the stages; one at the end.  The chunk
-// batches persist in the context (device buffers allocated once for a given size).
+// compute.  Chunks alternate between two engines (this context and its twin, each with its
+// own streams), so chunk k+1 starts as soon as its bytes have landed and fills the tail of
+// chunk k instead of queueing behind it.  No stream synchronisation between the stages; one
+// at the end.  The chunk batches persist in the context (device buffers allocated once for
+// a given size).
 static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec,
                                   int K) {
   HIPCHK(c, hipSetDevice(c->device));
@@ -1334,9 +1441,21 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
       p.off[i - p.lo] = in_range ? in->off[i] - p.base : UINT64_MAX / 2;
     }
   }
-  // launch: upload chunk k, then its decode + crypto behind the upload
+  // the comb the cached chains read is built on the parent before the twin borrows it
+  if (c->keycache > 0) {
+    const int rc = ensure_bcomb16(c);
+    if (rc != PRAOS_OK) return rc;
+  }
+  praos_ctx* eng[2] = {c, pipeline_twin(c)};
+  if (!eng[1]) eng[1] = c;
+  if (eng[1] != c) {
+    // the twin's streams start after everything already queued on the parent (the comb)
+    HIPCHK(c, hipEventRecord(c->pipe_ev, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(eng[1]->stream, c->pipe_ev, 0));
+  }
+  // device buffers of every chunk first (reused across calls while large enough)
   for (int k = 0; k < K; k++) {
-    Piece& p = P[k];
+    const Piece& p = P[k];
     const size_t m = p.hi - p.lo, bytes = p.end - p.base;
     if (!c->pipe[k] || c->pipe_n[k] < m || c->pipe_bytes[k] < bytes) {
       if (c->pipe[k]) {
@@ -1356,16 +1475,62 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
     b->arena_len = bytes;
     b->body_bytes_len = (size_t)b->signed_stride * m;
     b->decoded = false;
+  }
+  // Two host threads: this one stages the uploads (host copies into the pinned buffers are
+  // the long part), a launcher enqueues each chunk's kernels (~30 launches and memsets, 1.5-2.5
+  // ms of host time per chunk, profiles/r03/e2e_api_trace.txt) as soon as the chunk's upload is
+  // queued -- so neither waits for the other.  The kernels of chunk k wait on up_ev[k] on the GPU.
+  std::mutex mu;
+  std::condition_variable cv;
+  int queued = 0, failed = 0;
+  int run_rc = PRAOS_OK;
+  std::thread launcher([&] {
+    (void)hipSetDevice(c->device);
+    for (int k = 0; k < K; k++) {
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return queued > k || failed; });
+        if (queued <= k) return;                  // the upload side failed: nothing more to launch
+      }
+      praos_ctx* e = eng[k & 1];
+      int r = hipStreamWaitEvent(e->stream, c->up_ev[k], 0) == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
+      if (r == PRAOS_OK) r = praos_batch_run(e, c->pipe[k]);
+      if (r == PRAOS_OK && hipEventRecord(c->done_ev[k], e->stream) != hipSuccess) r = PRAOS_E_HIP;
+      if (r != PRAOS_OK) {
+        (void)hipStreamSynchronize(e->stream);
+        std::lock_guard<std::mutex> g(mu);
+        run_rc = r;
+        if (e != c) c->err = e->err;
+        return;
+      }
+    }
+  });
+  int up_rc = PRAOS_OK;
+  for (int k = 0; k < K && up_rc == PRAOS_OK; k++) {
+    const Piece& p = P[k];
+    const size_t m = p.hi - p.lo, bytes = p.end - p.base;
+    praos_batch* b = c->pipe[k];
     const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
-    HIPCHK(c, hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream));
-    if (bytes) HIPCHK(c, h2d_on(c, b->arena, in->bytes + p.base, bytes, c->cstream));
-    HIPCHK(c, hipMemcpyAsync(b->hoff, p.off.data(), 8 * m, hipMemcpyHostToDevice, c->cstream));
-    HIPCHK(c, hipMemcpyAsync(b->hlen, in->len + p.lo, 4 * m, hipMemcpyHostToDevice, c->cstream));
-    HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->up_ev[k], 0));
-    const int r = praos_batch_run(c, b);
-    if (r != PRAOS_OK) return r;
-    HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
+    bool ok = hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream) == hipSuccess;
+    if (ok && bytes) ok = h2d_on(c, b->arena, in->bytes + p.base, bytes, c->cstream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(b->hoff, p.off.data(), 8 * m, hipMemcpyHostToDevice, c->cstream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(b->hlen, in->len + p.lo, 4 * m, hipMemcpyHostToDevice, c->cstream) == hipSuccess;
+    ok = ok && hipEventRecord(c->up_ev[k], c->cstream) == hipSuccess;
+    std::lock_guard<std::mutex> g(mu);
+    if (ok) queued = k + 1;
+    else { up_rc = PRAOS_E_HIP; failed = 1; c->err = "pipeline upload failed"; }
+    cv.notify_one();
+  }
+  {
+    std::lock_guard<std::mutex> g(mu);
+    failed = 1;                                   // wakes the launcher if it waits for a chunk never queued
+    cv.notify_one();
+  }
+  launcher.join();
+  if (up_rc != PRAOS_OK || run_rc != PRAOS_OK) {
+    (void)hipStreamSynchronize(c->cstream);
+    for (praos_ctx* e : eng) (void)hipStreamSynchronize(e->stream);
+    return up_rc != PRAOS_OK ? up_rc : run_rc;
   }
   // results, chunk by chunk, as each finishes
   for (int k = 0; k < K; k++) {
@@ -1408,6 +1573,7 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   HIPCHK(c, hipStreamSynchronize(c->cstream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (eng[1] != c) HIPCHK(c, hipStreamSynchronize(eng[1]->stream));
   return PRAOS_OK;
 }
 

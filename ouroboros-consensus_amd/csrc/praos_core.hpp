@@ -440,21 +440,26 @@ FE_INLINE bool vrf_verify_core(uint32_t beta[16], bool& gamma_ok, const uint32_t
   return ok && gamma_ok && eq;
 }
 
-// ------------------------------------------------------------------ VRF verify in two stages
-// The same verification as vrf_verify_core, split at the only point where the public key's
-// precomputed tables are needed (k_vrf.hip): stage V (k_vrf_v) -- H = hash_to_curve,
-// Gamma decode, 8 Gamma, V = [s]H - [c]Gamma -- depends on the header alone and runs while
-// the key cache is being built; stage F (k_vrf_fin / k_vrf_fin_nc) -- U = [s]B - [c]Y from
-// the key's tables (or a per-lane chain), one batched inversion, the challenge hash, beta.
-// Stage V leaves a per-header record in SoA planes of uint4 (plane p of item i at
-// mid[p * stride + i], so a wave's access is one contiguous KB):
-//   planes 0-5 V (X, Y, Z), 6-11 H, 12-17 8 Gamma, 18-19 enc(Gamma), 20 flags (x: Gamma decoded)
-#define VRF_MID_PLANES 21
+// ------------------------------------------------------------------ VRF verify in stages
+// The same verification as vrf_verify_core, split into independent pieces (k_vrf.hip):
+// stage V (k_vrf_v) -- H = hash_to_curve, Gamma decode, 8 Gamma, V = [s]H - [c]Gamma --
+// depends on the header alone; stage U (k_vrf_u) -- U = [s]B - [c]Y from the key's tables
+// (k_keys.hip) or a per-lane chain -- depends on the key only; the two run concurrently
+// (U of a cached key once its tables exist, U of an uncached key at once).  The join
+// (k_vrf_join) -- one batched inversion, the challenge hash, beta -- reads both records.
+// (vrf_fin_core = U + join in one lane, the two-stage form, kept for comparison.)
+// Records in SoA planes of uint4 (plane p of item i at mid[p * stride + i], so a wave's
+// access is one contiguous KB):
+//   planes 0-5 V (X, Y, Z), 6-11 H, 12-17 8 Gamma, 18-19 enc(Gamma), 20 flags (x: Gamma
+//   decoded; written by stage V), 21-26 U (X, Y, Z), 27 key flag (x: vrf_validate_key; stage U)
+#define VRF_MID_PLANES 28
 #define VRF_MID_V 0
 #define VRF_MID_H 6
 #define VRF_MID_G8 12
 #define VRF_MID_GS 18
 #define VRF_MID_FLAGS 20
+#define VRF_MID_U 21
+#define VRF_MID_KEY 27
 
 FE_INLINE void mid_put(uint4* __restrict__ mid, size_t stride, size_t i, int plane, const uint32_t w[8]) {
   mid[(size_t)plane * stride + i] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -599,6 +604,90 @@ FE_INLINE bool vrf_fin_core(uint32_t beta[16], bool& gamma_ok, const uint4* __re
     ge_tobytes_zi(us, U.X, U.Y, zi);
     fe_mul(zi, inv, U.Z);             // 1/V.Z
     ge_tobytes_zi(vs, V.X, V.Y, zi);
+  }
+  mid_get(gs, mid, stride, i, VRF_MID_GS);
+  uint32_t cp[4];
+  vrf_hash_points(cp, hs, gs, us, vs);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < 4; k++) eq &= cp[k] == c4[k];
+  vrf_beta(beta, g8s);
+  return ok && gamma_ok && eq;
+}
+
+// Stage U: U = [s]B - [c]Y into planes VRF_MID_U.., vrf_validate_key into VRF_MID_KEY.
+// CACHED: kinfo / ktab of k_keys.hip and btab = the global radix-2^16 comb; otherwise Y is
+// decoded per lane ({1..8}(-Y) in the lane's 8-entry table vt) and btab = LDS {B, 2^128 B}.
+template <bool CACHED>
+FE_INLINE void vrf_u_core(uint4* __restrict__ mid, size_t stride, size_t i, const uint32_t pk[8], const uint32_t c4[4],
+                          const uint32_t s8[8], const ge_niels* __restrict__ btab, ge_cached* __restrict__ vt,
+                          const ge_cached* __restrict__ ktab, const uint32_t* __restrict__ kinfo) {
+  bool ok;
+  uint32_t sx[16], s[8], c[8], cw[8], sw[8];
+#pragma unroll
+  for (int k = 0; k < 16; k++) sx[k] = k < 8 ? s8[k] : 0u;
+  sc_reduce512(s, sx);
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[k] = k < 4 ? c4[k] : 0u;
+  sc_recode16(cw, c);
+  ge_p1p1 x;
+  if constexpr (CACHED) {
+    ok = (kinfo[0] & 1u) != 0;
+    sc_recode65536(sw, s);
+    straus_comb<8, true>(x, ktab, cw, btab, sw);
+  } else {
+    ge_p3 Y;
+    ok = !ge_has_small_order(pk);
+    ok = ge_frombytes(Y, pk, false) && ok;
+    fe_neg(Y.X, Y.X);
+    fe_neg(Y.T, Y.T);
+    build_cached_table(vt, Y);
+    sc_recode256(sw, s);
+    STRAUS<33, 33, 0, 16, true>(x, vt, cw, nullptr, nullptr, btab, sw);
+  }
+  ge_p2 U;
+  ge_p1p1_to_p2(U, x);
+  mid_put_xyz(mid, stride, i, VRF_MID_U, U.X, U.Y, U.Z);
+  mid[(size_t)VRF_MID_KEY * stride + i] = make_uint4(ok ? 1u : 0u, 0u, 0u, 0u);
+}
+
+// Join: the batched inversion of U.Z V.Z (8 Gamma).Z H.Z, the four encodings, the
+// challenge c' = SHA-512(0x04 || 0x02 || H || Gamma || U || V)[0..16) against c, beta.
+FE_INLINE bool vrf_join_core(uint32_t beta[16], bool& gamma_ok, const uint4* __restrict__ mid, size_t stride, size_t i,
+                             const uint32_t c4[4]) {
+  const bool ok = (mid[(size_t)VRF_MID_KEY * stride + i].x & 1u) != 0;
+  gamma_ok = (mid[(size_t)VRF_MID_FLAGS * stride + i].x & 1u) != 0;
+  fe z12, z123, z1234, inv, zi;
+  uint32_t hs[8], us[8], vs[8], gs[8], g8s[8];
+  {
+    fe UZ, VZ, G8Z, HZ;
+    mid_get(UZ.v, mid, stride, i, VRF_MID_U + 4);
+    mid_get(VZ.v, mid, stride, i, VRF_MID_V + 4);
+    mid_get(G8Z.v, mid, stride, i, VRF_MID_G8 + 4);
+    mid_get(HZ.v, mid, stride, i, VRF_MID_H + 4);
+    fe_mul(z12, UZ, VZ);
+    fe_mul(z123, z12, G8Z);
+    fe_mul(z1234, z123, HZ);
+    fe_invert_inl(inv, z1234);       // inline: no caller-saved registers around a call
+    fe_mul(zi, inv, z123);            // 1/H.Z
+    fe_mul(inv, inv, HZ);             // 1/(U.Z V.Z G8.Z)
+    fe X, Y;
+    mid_get(X.v, mid, stride, i, VRF_MID_H);
+    mid_get(Y.v, mid, stride, i, VRF_MID_H + 2);
+    ge_tobytes_zi(hs, X, Y, zi);
+    fe_mul(zi, inv, z12);             // 1/G8.Z
+    mid_get(X.v, mid, stride, i, VRF_MID_G8);
+    mid_get(Y.v, mid, stride, i, VRF_MID_G8 + 2);
+    ge_tobytes_zi(g8s, X, Y, zi);
+    fe_mul(inv, inv, G8Z);            // 1/(U.Z V.Z)
+    fe_mul(zi, inv, VZ);              // 1/U.Z
+    mid_get(X.v, mid, stride, i, VRF_MID_U);
+    mid_get(Y.v, mid, stride, i, VRF_MID_U + 2);
+    ge_tobytes_zi(us, X, Y, zi);
+    fe_mul(zi, inv, UZ);              // 1/V.Z
+    mid_get(X.v, mid, stride, i, VRF_MID_V);
+    mid_get(Y.v, mid, stride, i, VRF_MID_V + 2);
+    ge_tobytes_zi(vs, X, Y, zi);
   }
   mid_get(gs, mid, stride, i, VRF_MID_GS);
   uint32_t cp[4];

@@ -16,8 +16,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_ocert", "k_ocert_ck", "k_kes", "k_kes_ck", "k_kes_leafkeys", "k_vrf", "k_vrf_ck", "k_vrf_tp", "k_leader",
-           "k_key_precompute", "k_synth_headers")
+KERNELS = ("k_ocert", "k_ocert_ck", "k_kes", "k_kes_ck", "k_kes_leafkeys", "k_vrf", "k_vrf_ck", "k_vrf_v", "k_vrf_fin",
+           "k_vrf_fin_nc", "k_vrf_tp", "k_leader", "k_key_precompute", "k_key_tables", "k_decode_praos", "k_synth_headers")
 
 
 def short(name):
@@ -47,6 +47,7 @@ def main():
                     for r in csv.DictReader(f)]
         crypto = [r for r in rows if r[0] in KERNELS and not r[0].startswith("k_synth") and r[2] - r[1] > 100_000]
         iso, conc = defaultdict(list), defaultdict(list)
+        iso_avg = {}
         for k, s, e in crypto:
             overl = any(o is not None and o[1] < e and s < o[2] for o in crypto if o != (k, s, e))
             (conc if overl else iso)[k].append((e - s) / 1e6)
@@ -56,6 +57,8 @@ def main():
             a = iso.get(k, [])
             b = conc.get(k, [])
             lines.append(f"{k:16s} {len(a):10d} {sum(a)/max(1,len(a)):8.3f} {len(b):12d} {sum(b)/max(1,len(b)):8.3f}")
+            if a:
+                iso_avg[k] = sum(a) / len(a)
         lines.append("")
     bench = os.path.join(d, "kt_bench.json")
     if os.path.exists(bench):
@@ -108,12 +111,15 @@ def main():
         except (ValueError, KeyError, IndexError):
             workload = None
     traffic = {}
+    if not trace:
+        iso_avg = {}
     for k, o in out.items():
         if "FETCH_SIZE" in o and "WRITE_SIZE" in o:
             rd = 2 * 1024 * o["FETCH_SIZE"]["per_dispatch"]
             wr = 1024 * o["WRITE_SIZE"]["per_dispatch"]
             traffic[k] = {"bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-                          "items_per_launch": o["FETCH_SIZE"]["grid"], "bytes_per_item": (rd + wr) / o["FETCH_SIZE"]["grid"]}
+                          "items_per_launch": o["FETCH_SIZE"]["grid"], "bytes_per_item": (rd + wr) / o["FETCH_SIZE"]["grid"],
+                          "rocprof_isolated_avg_ms": iso_avg.get(k)}
     os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
     if traffic and workload:
         with open(os.path.join(root, "profiles", f"{tag}_traffic.json"), "w") as f:

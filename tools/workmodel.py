@@ -85,12 +85,22 @@ W_LEADER = 3000
 W_OCERT_CK = W_OCERT - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_comb(16, False)
 W_VRF_CK = W_VRF - DECODE - TABLE8 - straus(33, 33, 0, 32) + straus_comb(8, True)
 W_KES_CK = W_KES - DECODE - TABLE8 - straus(64, 64, 0, 32) + straus_comb(16, False)
+# two-stage VRF (praos_core.hpp vrf_v_core / vrf_fin_core, k_vrf.hip): what each kernel computes
+ELLIGATOR = SHA + (10 * M + 6 * S + 12 * A) + DECODE + (6 * M + 2 * S + 2 * A) + 3 * (DBL + TO_P3)
+W_VRF_V = (B2B                                        # alpha = mkInputVRF(slot, eta0)
+           + CANON + ELLIGATOR                        # canonical Y (no decode), H = hash_to_curve
+           + DECODE + 3 * (DBL + TO_P3)               # Gamma, 8 Gamma
+           + 2 * TABLE8 + SC_REDUCE + straus(64, 64, 33, 0) + TO_P2)   # V = [s]H - [c]Gamma
+_FIN = SC_REDUCE + TO_P2 + X + 10 * M + 4 * (2 * M + CANON) + 3 * SHA + 5 * B2B + 1000
+W_VRF_F_CK = _FIN + straus_comb(8, True)             # U from the cached key + comb; inversion, c', beta, L/N
+W_VRF_F = _FIN + DECODE + TABLE8 + straus(33, 33, 0, 32)
 W_KEY_COLD = key_precompute(16)
 W_KEY_KES = key_precompute(16)                       # leaf keys: same tables as cold keys
 W_KEY_VRF = key_precompute(9) + CANON
 
 if __name__ == "__main__":
     for k, v in (("ocert", W_OCERT), ("kes", W_KES), ("vrf", W_VRF), ("leader", W_LEADER),
-                 ("ocert_ck", W_OCERT_CK), ("vrf_ck", W_VRF_CK), ("kes_ck", W_KES_CK), ("key_cold", W_KEY_COLD), ("key_vrf", W_KEY_VRF)):
+                 ("ocert_ck", W_OCERT_CK), ("vrf_ck", W_VRF_CK), ("kes_ck", W_KES_CK), ("key_cold", W_KEY_COLD), ("key_vrf", W_KEY_VRF),
+                 ("vrf_v", W_VRF_V), ("vrf_f_ck", W_VRF_F_CK), ("vrf_f", W_VRF_F)):
         print(f"W_{k:7s} {v:>10,d} int32 ops / item")
     print(f"W_header  {W_OCERT + W_KES + W_VRF + W_LEADER:>10,d}")
