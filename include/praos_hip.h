@@ -201,10 +201,11 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * copied to every header carrying the same bytes; the KES-period checks stay per
  * header.  Verdicts are identical either way. */
 #define PRAOS_OPT_DEDUP 4
-/* PRAOS_OPT_PIPELINE (default 0 = auto): praos_verify_header_bytes runs a batch in this
- * many chunks (1 = one batch, up to 8), the stored bytes of chunk k+1 moving host ->
- * device on a copy stream while the kernels of chunk k run and chunk k-1's results move
- * back; auto = up to 4 chunks of at least 65,536 headers. */
+/* PRAOS_OPT_PIPELINE (default 0 = auto): praos_verify_header_bytes uploads a batch in
+ * this many chunks (1 = no pipeline, up to 8): the stored bytes of chunk k+1 move host ->
+ * device on a copy stream while chunk k is decoded and its VRF stage V runs; the rest of
+ * the batch runs once after the last chunk, and the VRF outputs move back while the KES
+ * checks finish; auto = up to 6 chunks of at least 65,536 headers. */
 #define PRAOS_OPT_PIPELINE 5
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):

@@ -156,11 +156,11 @@ struct DecOut {
   uint8_t *lead_out, *lead_proof;
 };
 
-__global__ void __launch_bounds__(NT) k_decode_praos(size_t n, const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                     const uint64_t* __restrict__ hoff,
+__global__ void __launch_bounds__(NT) k_decode_praos(size_t i0, size_t n, const uint8_t* __restrict__ arena,
+                                                     uint64_t arena_len, const uint64_t* __restrict__ hoff,
                                                      const uint32_t* __restrict__ hlen, DecOut o, int allow_tp,
                                                      uint32_t stride) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // headers [i0, n)
   if (i >= n) return;
   const uint64_t off = hoff[i], len = hlen[i];
   Rd r{arena, off, off + len, 0u, true};
@@ -304,9 +304,9 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
                          uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride, uint8_t* lead_out,
-                         uint8_t* lead_proof) {
+                         uint8_t* lead_proof, size_t i0) {
   DecOut o{slot,     cold_vk,   vrf_vk,      vrf_out,  vrf_proof, hot_vk,       ocert_sig, kes_sig,
            ocert_n,  ocert_c0,  body_off,    body_len, signed_body, block_no,   prev_hash, prev_genesis,
            body_size, body_hash, prot_major, prot_minor, header_hash, status, lead_out, lead_proof};
-  hipLaunchKernelGGL(k_decode_praos, grid, block, 0, stream, n, arena, arena_len, hoff, hlen, o, allow_tp, stride);
+  hipLaunchKernelGGL(k_decode_praos, grid, block, 0, stream, i0, n, arena, arena_len, hoff, hlen, o, allow_tp, stride);
 }

@@ -15,9 +15,9 @@ __device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, 
 }
 
 // stage V over every header of the batch: no dependence on the key cache
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_v(size_t n, VrfIn a, uint4* __restrict__ mid) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_v(size_t n, size_t i0, size_t i1, VrfIn a, uint4* __restrict__ mid) {
+  const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // headers [i0, i1), record stride n
+  if (i >= i1) return;
   uint32_t pk[8], pr[20], alpha[8];
   load_words(pk, a.vrf_vk + 32 * i, 8);
   load_words(pr, a.vrf_proof + 80 * i, 20);
@@ -205,11 +205,15 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_join(size_t n, VrfIn a, cons
 
 // ---- host launchers (kernels are only launchable from their own module)
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
-                  const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid) {
+                  const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
+                  size_t i0, size_t i1) {
   const VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
                          nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
   const unsigned bs = lat_block(n);
-  hipLaunchKernelGGL(k_vrf_v, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, a, (uint4*)mid);
+  i1 = i1 < n ? i1 : n;
+  if (i1 <= i0) return;
+  hipLaunchKernelGGL(k_vrf_v, dim3((unsigned)((i1 - i0 + bs - 1) / bs)), dim3(bs), 0, stream, n, i0, i1, a,
+                     (uint4*)mid);
 }
 void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,

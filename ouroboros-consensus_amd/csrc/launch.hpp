@@ -95,7 +95,8 @@ void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, u
 // record `mid` (VRF_MID_PLANES x 16 x n bytes); stage F over list[0 .. *count) (or all n when
 // list is null), cached (ktab != null: k_vrf_fin) or per-lane U (k_vrf_fin_nc)
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
-                  const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid);
+                  const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
+                  size_t i0 = 0, size_t i1 = SIZE_MAX);   // headers [i0, min(i1, n)); mid stride n
 void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
                     const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
@@ -121,7 +122,8 @@ void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
                          uint64_t* ocert_n, uint64_t* ocert_c0, uint64_t* body_off, uint32_t* body_len,
                          uint8_t* signed_body, uint64_t* block_no, uint8_t* prev_hash, uint8_t* prev_genesis,
                          uint32_t* body_size, uint8_t* body_hash, uint64_t* prot_major, uint64_t* prot_minor,
-                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride, uint8_t* lead_out = nullptr, uint8_t* lead_proof = nullptr);
+                         uint8_t* header_hash, uint16_t* status, int allow_tp, uint32_t stride, uint8_t* lead_out = nullptr, uint8_t* lead_proof = nullptr,
+                         size_t i0 = 0);   // headers [i0, n); grid covers n - i0
 void launch_block_split(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena,
                         uint64_t arena_len, uint64_t* off_io, uint32_t* len_io, uint64_t* seg_off, uint32_t* seg_len,
                         uint8_t* nseg, uint8_t* status);

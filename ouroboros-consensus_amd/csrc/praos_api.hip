@@ -91,6 +91,8 @@ class CopyPool {
 static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2 x 16 MB per context
 static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
 static constexpr size_t PIPE_MIN_CHUNK = 65536;     // headers per chunk at least (auto mode)
+static constexpr int PIPE_AUTO = 6;                 // chunks in auto mode (432k headers: 4 -> 21.9M, 6 -> 23.0M,
+                                                    // 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt)
 struct praos_batch;
 
 struct praos_ctx {
@@ -100,14 +102,10 @@ struct praos_ctx {
   hipStream_t mside[3] = {nullptr, nullptr, nullptr};  // their key-cache misses (uncached verifies)
   hipEvent_t mdone_ev[3] = {};
   hipStream_t vstream = nullptr;                       // VRF stage V (no key-cache dependence)
-  hipEvent_t v_ev = nullptr;
+  hipStream_t vstream2 = nullptr;                      // the odd chunks' stage V of the stored-bytes pipeline
+  hipEvent_t v_ev = nullptr, v2_ev = nullptr;
   hipEvent_t v0_ev = nullptr, v1_ev = nullptr;         // timing of k_vrf_v on its stream (kernel_ms[6])
   hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
-  // second engine of the stored-bytes pipeline: its own streams and events, the parent's
-  // tables (btab, comb, epoch) borrowed, so consecutive chunks run concurrently
-  praos_ctx* twin = nullptr;
-  bool borrowed = false;
-  hipEvent_t pipe_ev = nullptr;                        // the twin's start: after the parent's queued work
   int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
                                                        // the three-kernel form below 300k headers (latency)
   // chunked stored-bytes pipeline (praos_verify_header_bytes): a copy stream, per-chunk
@@ -163,7 +161,7 @@ struct praos_ctx {
   // allocation per 432k batch cost its page faults and its unmapping on every call)
   std::unique_ptr<uint8_t[]> h_arena;
   size_t h_arena_cap = 0;
-  std::vector<uint64_t> h_off;
+  std::vector<uint64_t> h_off, h_off2;
   std::vector<uint32_t> h_len;
 };
 
@@ -274,6 +272,7 @@ struct praos_batch {
   // per-lane point tables of the three crypto kernels (kcommon.hpp lane_tab)
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
   ge_cached* tab_vrfu = nullptr;   // 8-entry lane tables of stage U on uncached VRF keys
+  bool v_done = false;             // stage V already queued on ctx->vstream (stored-bytes pipeline)
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
@@ -375,9 +374,9 @@ static bool open_streams(praos_ctx* c) {
   for (auto& e : c->miss_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->mdone_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->v_ev, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->v2_ev, hipEventDisableTiming);
   (void)hipEventCreate(&c->v0_ev);
   (void)hipEventCreateWithFlags(&c->u_ev, hipEventDisableTiming);
-  (void)hipEventCreateWithFlags(&c->pipe_ev, hipEventDisableTiming);
   if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -403,6 +402,7 @@ static bool open_streams(praos_ctx* c) {
     }
     // the VRF's stage V is the longest chain of a batch and starts at once: greatest priority
     (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, greatest);
+    (void)hipStreamCreateWithPriority(&c->vstream2, hipStreamNonBlocking, greatest);
     (void)hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
   }
   return true;
@@ -470,14 +470,11 @@ void praos_close(praos_ctx* c) {
   if (!c) return;
   if (c->device < 0) { delete c; return; }
   (void)hipSetDevice(c->device);
-  if (c->twin) praos_close(c->twin);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (!c->borrowed) {
-    free_epoch(c);
-    (void)hipFree(c->d_gen);
-    (void)hipFree(c->btab);
-    (void)hipFree(c->bcomb16);
-  }
+  free_epoch(c);
+  (void)hipFree(c->d_gen);
+  (void)hipFree(c->btab);
+  (void)hipFree(c->bcomb16);
   free_spare(c);
   c->pool.reset();
   for (int k = 0; k < 2; k++) {
@@ -491,10 +488,11 @@ void praos_close(praos_ctx* c) {
   for (auto& st : c->side) if (st) (void)hipStreamDestroy(st);
   for (auto& st : c->mside) if (st) (void)hipStreamDestroy(st);
   if (c->vstream) (void)hipStreamDestroy(c->vstream);
+  if (c->vstream2) (void)hipStreamDestroy(c->vstream2);
+  if (c->v2_ev) (void)hipEventDestroy(c->v2_ev);
   if (c->v_ev) (void)hipEventDestroy(c->v_ev);
   if (c->v0_ev) (void)hipEventDestroy(c->v0_ev);
   if (c->u_ev) (void)hipEventDestroy(c->u_ev);
-  if (c->pipe_ev) (void)hipEventDestroy(c->pipe_ev);
   if (c->v1_ev) (void)hipEventDestroy(c->v1_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (int k = 0; k < PIPE_MAX; k++) {
@@ -1029,15 +1027,22 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     // needs no key); F after it -- the hits on sv once their key tables exist, the misses
     // on their miss stream (per-lane U)
     const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
-    hipStream_t sV = c->concurrent ? c->vstream : c->stream;
-    if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
-    HIPCHK(c, hipEventRecord(c->v0_ev, sV));
-    launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf, b->vrf_mid);
-    HIPCHK(c, hipEventRecord(c->v1_ev, sV));
+    // (stored-bytes pipeline: stage V was queued chunk by chunk on vstream while the later
+    // chunks were still uploading; b->v_done)
+    hipStream_t sV = (c->concurrent || b->v_done) ? c->vstream : c->stream;
+    if (!b->v_done) {
+      if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
+      HIPCHK(c, hipEventRecord(c->v0_ev, sV));
+      launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
+                   b->vrf_mid);
+      HIPCHK(c, hipEventRecord(c->v1_ev, sV));
+      c->v_timed = true;
+    }
     HIPCHK(c, hipEventRecord(c->v_ev, sV));
-    c->v_timed = true;
+    if (b->v_done) HIPCHK(c, hipEventRecord(c->v2_ev, c->vstream2));
     auto after_v = [&](hipStream_t st) -> int {
       if (st != sV) HIPCHK(c, hipStreamWaitEvent(st, c->v_ev, 0));
+      if (b->v_done) HIPCHK(c, hipStreamWaitEvent(st, c->v2_ev, 0));
       return PRAOS_OK;
     };
     auto fin = [&](hipStream_t st, const uint32_t* list, const uint32_t* count, const praos_batch::KeyCache* k) {
@@ -1370,211 +1375,125 @@ int praos_decode_headers(praos_ctx* c, const praos_header_bytes* in, praos_decod
   return r;
 }
 
-// The pipeline's second engine: created on first use, then re-pointed at the parent's
-// current tables and options before each call (it is idle between calls).
-static praos_ctx* pipeline_twin(praos_ctx* c) {
-  if (!c->twin) {
-    praos_ctx* t = new praos_ctx();
-    t->device = c->device;
-    t->borrowed = true;
-    if (!open_streams(t)) {
-      praos_close(t);
-      return nullptr;
-    }
-    c->twin = t;
-  }
-  praos_ctx* t = c->twin;
-  t->btab = c->btab;
-  t->bcomb16 = c->bcomb16;
-  t->have_epoch = c->have_epoch;
-  t->params = c->params;
-  std::memcpy(t->eta0, c->eta0, 32);
-  t->eta0_neutral = c->eta0_neutral;
-  t->npools = c->npools;
-  t->d_pool_hash = c->d_pool_hash;
-  t->d_pool_vrf = c->d_pool_vrf;
-  t->d_pool_x = c->d_pool_x;
-  t->d_pool_map = c->d_pool_map;
-  t->d_eta0 = c->d_eta0;
-  t->concurrent = c->concurrent;
-  t->kernels = c->kernels;
-  t->keycache = c->keycache;
-  t->dedup = c->dedup;
-  t->vrf3 = c->vrf3;
-  t->key_wave_prio = c->key_wave_prio;
-  return t;
-}
-
-// Stored-bytes verification in K chunks (contiguous runs of headers): the arena slice of
-// chunk k+1 moves H2D on the copy stream (pinned staging, host threads) while the kernels
-// of chunk k run; chunk k's results come back D2H on the copy stream while later chunks
-// compute.  Chunks alternate between two engines (this context and its twin, each with its
-// own streams), so chunk k+1 starts as soon as its bytes have landed and fills the tail of
-// chunk k instead of queueing behind it.  No stream synchronisation between the stages; one
-// at the end.  The chunk batches persist in the context (device buffers allocated once for
-// a given size).
+// Stored-bytes verification with the upload in K chunks (contiguous runs of headers) and
+// the batch's largest kernel run under it: chunk k's bytes move H2D on the copy stream
+// (pinned staging, host threads) while, on the GPU, chunk k-1 is decoded (ctx stream) and
+// its VRF stage V (H, Gamma, V = [s]H - [c]Gamma: over half of a header's work, and it needs
+// nothing but the header) runs on vstream.  After the last chunk the rest of the batch --
+// key caches, OCert, KES, U, the join, the leader test -- runs once over the whole batch, as
+// praos_batch_run does (full-batch key caches, no small-batch tails).  One batch for the whole
+// input, kept in the context (device buffers allocated once for a given size).
 static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec,
                                   int K) {
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = in->n;
-  struct Piece {
-    size_t lo, hi;
-    uint64_t base, end;
-    std::vector<uint64_t> off;
-  };
-  std::vector<Piece> P(K);
-  for (int k = 0; k < K; k++) {
-    Piece& p = P[k];
-    p.lo = n * k / K;
-    p.hi = n * (k + 1) / K;
-    p.base = UINT64_MAX;
-    p.end = 0;
-    for (size_t i = p.lo; i < p.hi; i++) {
-      if (in->off[i] > in->bytes_len || in->len[i] > in->bytes_len - in->off[i]) continue;
-      p.base = std::min<uint64_t>(p.base, in->off[i]);
-      p.end = std::max<uint64_t>(p.end, in->off[i] + in->len[i]);
-    }
-    if (p.base == UINT64_MAX) p.base = p.end = 0;
-    p.off.resize(p.hi - p.lo);
-    for (size_t i = p.lo; i < p.hi; i++) {   // rebased; a span outside the caller's arena stays outside
-      const bool in_range = in->off[i] <= in->bytes_len && in->len[i] <= in->bytes_len - in->off[i];
-      p.off[i - p.lo] = in_range ? in->off[i] - p.base : UINT64_MAX / 2;
-    }
+  // the arena span of the in-range headers, and offsets rebased to it
+  uint64_t base = UINT64_MAX, end = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (in->off[i] > in->bytes_len || in->len[i] > in->bytes_len - in->off[i]) continue;
+    base = std::min<uint64_t>(base, in->off[i]);
+    end = std::max<uint64_t>(end, in->off[i] + in->len[i]);
   }
-  // the comb the cached chains read is built on the parent before the twin borrows it
-  if (c->keycache > 0) {
+  if (base == UINT64_MAX) base = end = 0;
+  std::vector<uint64_t>& off = c->h_off2;
+  off.resize(n);
+  for (size_t i = 0; i < n; i++) {   // a span outside the caller's arena stays outside
+    const bool in_range = in->off[i] <= in->bytes_len && in->len[i] <= in->bytes_len - in->off[i];
+    off[i] = in_range ? in->off[i] - base : UINT64_MAX / 2;
+  }
+  // chunk k = headers [lo_k, hi_k) and the byte range [b0_k, b1_k) of the arena its headers
+  // need (relative to base); chunk k's upload covers what earlier chunks did not
+  std::vector<size_t> lo(K + 1);
+  std::vector<uint64_t> need(K);
+  for (int k = 0; k <= K; k++) lo[k] = n * k / K;
+  uint64_t hw = 0;
+  for (int k = 0; k < K; k++) {
+    for (size_t i = lo[k]; i < lo[k + 1]; i++)
+      if (off[i] != UINT64_MAX / 2) hw = std::max<uint64_t>(hw, off[i] + in->len[i]);
+    need[k] = hw;                                 // bytes [0, need[k]) cover chunks 0..k
+  }
+  const uint64_t bytes = end - base;
+  if (!c->pipe[0] || c->pipe_n[0] < n || c->pipe_bytes[0] < bytes) {
+    if (c->pipe[0]) {
+      HIPCHK(c, hipDeviceSynchronize());
+      for (void* q : c->pipe[0]->owned) (void)hipFree(q);
+      delete c->pipe[0];
+      c->pipe[0] = nullptr;
+    }
+    const size_t mc = n + n / 8 + 64, bc = bytes + bytes / 8 + 4096;   // headroom for the next call
+    c->pipe[0] = bytes_batch_alloc(c, mc, bc, false, nullptr);
+    if (!c->pipe[0]) return PRAOS_E_OOM;
+    c->pipe_n[0] = mc;
+    c->pipe_bytes[0] = bc;
+  }
+  praos_batch* b = c->pipe[0];
+  b->n = n;
+  b->arena_len = bytes;
+  b->body_bytes_len = (size_t)b->signed_stride * n;
+  const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
+  HIPCHK(c, hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream));
+  HIPCHK(c, hipMemcpyAsync(b->hoff, off.data(), 8 * n, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(c, hipMemcpyAsync(b->hlen, in->len, 4 * n, hipMemcpyHostToDevice, c->cstream));
+  if (c->keycache > 0 && n >= 2) {               // the comb the cached chains read (built once)
     const int rc = ensure_bcomb16(c);
     if (rc != PRAOS_OK) return rc;
   }
-  praos_ctx* eng[2] = {c, pipeline_twin(c)};
-  if (!eng[1]) eng[1] = c;
-  if (eng[1] != c) {
-    // the twin's streams start after everything already queued on the parent (the comb)
-    HIPCHK(c, hipEventRecord(c->pipe_ev, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(eng[1]->stream, c->pipe_ev, 0));
-  }
-  // device buffers of every chunk first (reused across calls while large enough)
+  const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
+  const bool vrf = (c->kernels & 4) != 0;
+  uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
-    const Piece& p = P[k];
-    const size_t m = p.hi - p.lo, bytes = p.end - p.base;
-    if (!c->pipe[k] || c->pipe_n[k] < m || c->pipe_bytes[k] < bytes) {
-      if (c->pipe[k]) {
-        HIPCHK(c, hipDeviceSynchronize());
-        for (void* q : c->pipe[k]->owned) (void)hipFree(q);
-        delete c->pipe[k];
-        c->pipe[k] = nullptr;
-      }
-      const size_t mc = m + m / 8 + 64, bc = bytes + bytes / 8 + 4096;   // headroom for the next call
-      c->pipe[k] = bytes_batch_alloc(c, mc, bc, false, nullptr);
-      if (!c->pipe[k]) return PRAOS_E_OOM;
-      c->pipe_n[k] = mc;
-      c->pipe_bytes[k] = bc;
+    if (need[k] > sent) {
+      HIPCHK(c, h2d_on(c, b->arena + sent, in->bytes + base + sent, need[k] - sent, c->cstream));
+      sent = need[k];
     }
-    praos_batch* b = c->pipe[k];
-    b->n = m;
-    b->arena_len = bytes;
-    b->body_bytes_len = (size_t)b->signed_stride * m;
-    b->decoded = false;
-  }
-  // Two host threads: this one stages the uploads (host copies into the pinned buffers are
-  // the long part), a launcher enqueues each chunk's kernels (~30 launches and memsets, 1.5-2.5
-  // ms of host time per chunk, profiles/r03/e2e_api_trace.txt) as soon as the chunk's upload is
-  // queued -- so neither waits for the other.  The kernels of chunk k wait on up_ev[k] on the GPU.
-  std::mutex mu;
-  std::condition_variable cv;
-  int queued = 0, failed = 0;
-  int run_rc = PRAOS_OK;
-  std::thread launcher([&] {
-    (void)hipSetDevice(c->device);
-    for (int k = 0; k < K; k++) {
-      {
-        std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return queued > k || failed; });
-        if (queued <= k) return;                  // the upload side failed: nothing more to launch
-      }
-      praos_ctx* e = eng[k & 1];
-      int r = hipStreamWaitEvent(e->stream, c->up_ev[k], 0) == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
-      if (r == PRAOS_OK) r = praos_batch_run(e, c->pipe[k]);
-      if (r == PRAOS_OK && hipEventRecord(c->done_ev[k], e->stream) != hipSuccess) r = PRAOS_E_HIP;
-      if (r != PRAOS_OK) {
-        (void)hipStreamSynchronize(e->stream);
-        std::lock_guard<std::mutex> g(mu);
-        run_rc = r;
-        if (e != c) c->err = e->err;
-        return;
-      }
+    HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->up_ev[k], 0));
+    const size_t m = lo[k + 1] - lo[k];
+    if (m == 0) continue;
+    launch_decode_praos(dim3(nblocks(m, NT)), dim3(NT), c->stream, lo[k + 1], b->arena, bytes, b->hoff, b->hlen,
+                        b->slot, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->hot_vk, b->ocert_sig, b->kes_sig,
+                        b->ocert_n, b->ocert_c0, b->body_off, b->body_len, b->body, b->block_no, b->prev_hash,
+                        b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor, b->header_hash,
+                        b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
+    HIPCHK(c, hipGetLastError());
+    if (vrf) {
+      HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
+      // the chunks' stage V alternate between two streams: on one they would queue behind
+      // each other (a chunk's V alone is latency-bound)
+      hipStream_t sv = (k & 1) ? c->vstream2 : c->vstream;
+      HIPCHK(c, hipStreamWaitEvent(sv, c->done_ev[k], 0));
+      launch_vrf_v(sv, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
+                   b->vrf_mid, lo[k], lo[k + 1]);
+      HIPCHK(c, hipGetLastError());
     }
-  });
-  int up_rc = PRAOS_OK;
-  for (int k = 0; k < K && up_rc == PRAOS_OK; k++) {
-    const Piece& p = P[k];
-    const size_t m = p.hi - p.lo, bytes = p.end - p.base;
-    praos_batch* b = c->pipe[k];
-    const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
-    bool ok = hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream) == hipSuccess;
-    if (ok && bytes) ok = h2d_on(c, b->arena, in->bytes + p.base, bytes, c->cstream) == hipSuccess;
-    ok = ok && hipMemcpyAsync(b->hoff, p.off.data(), 8 * m, hipMemcpyHostToDevice, c->cstream) == hipSuccess;
-    ok = ok && hipMemcpyAsync(b->hlen, in->len + p.lo, 4 * m, hipMemcpyHostToDevice, c->cstream) == hipSuccess;
-    ok = ok && hipEventRecord(c->up_ev[k], c->cstream) == hipSuccess;
-    std::lock_guard<std::mutex> g(mu);
-    if (ok) queued = k + 1;
-    else { up_rc = PRAOS_E_HIP; failed = 1; c->err = "pipeline upload failed"; }
-    cv.notify_one();
   }
-  {
-    std::lock_guard<std::mutex> g(mu);
-    failed = 1;                                   // wakes the launcher if it waits for a chunk never queued
-    cv.notify_one();
-  }
-  launcher.join();
-  if (up_rc != PRAOS_OK || run_rc != PRAOS_OK) {
-    (void)hipStreamSynchronize(c->cstream);
-    for (praos_ctx* e : eng) (void)hipStreamSynchronize(e->stream);
-    return up_rc != PRAOS_OK ? up_rc : run_rc;
-  }
-  // results, chunk by chunk, as each finishes
-  for (int k = 0; k < K; k++) {
-    const Piece& p = P[k];
-    praos_batch* b = c->pipe[k];
-    const size_t m = p.hi - p.lo, lo = p.lo;
-    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->done_ev[k], 0));
-    auto dn = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-      return dst && bytes ? d2h_on(c, dst, src, bytes, c->cstream) : hipSuccess;
+  b->decoded = true;
+  b->v_done = vrf;
+  int r = praos_batch_run(c, b);
+  b->decoded = false;
+  b->v_done = false;
+  // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
+  // header) are final once the VRF stream is done: they come back while KES still runs
+  if (r == PRAOS_OK && c->concurrent) {
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->side_ev[2], 0));
+    auto dn = [&](void* dst, const void* src, size_t nb) -> hipError_t {
+      return dst && nb ? d2h_on(c, dst, src, nb, c->cstream) : hipSuccess;
     };
-    HIPCHK(c, dn(out->bits + lo, b->bits, 2 * m));
-    HIPCHK(c, dn(out->pool_idx ? out->pool_idx + lo : nullptr, b->pool_idx, 4 * m));
-    HIPCHK(c, dn(out->beta ? out->beta + 64 * lo : nullptr, b->beta, 64 * m));
-    HIPCHK(c, dn(out->leader ? out->leader + 32 * lo : nullptr, b->leader, 32 * m));
-    HIPCHK(c, dn(out->nonce ? out->nonce + 32 * lo : nullptr, b->nonce, 32 * m));
-    if (dec) {
-      HIPCHK(c, dn(dec->status ? dec->status + lo : nullptr, b->dec_status, 2 * m));
-      HIPCHK(c, dn(dec->block_no ? dec->block_no + lo : nullptr, b->block_no, 8 * m));
-      HIPCHK(c, dn(dec->slot ? dec->slot + lo : nullptr, b->slot, 8 * m));
-      HIPCHK(c, dn(dec->prev_hash ? dec->prev_hash + 32 * lo : nullptr, b->prev_hash, 32 * m));
-      HIPCHK(c, dn(dec->prev_is_genesis ? dec->prev_is_genesis + lo : nullptr, b->prev_genesis, m));
-      HIPCHK(c, dn(dec->cold_vk ? dec->cold_vk + 32 * lo : nullptr, b->cold_vk, 32 * m));
-      HIPCHK(c, dn(dec->vrf_vk ? dec->vrf_vk + 32 * lo : nullptr, b->vrf_vk, 32 * m));
-      HIPCHK(c, dn(dec->vrf_out ? dec->vrf_out + 64 * lo : nullptr, b->vrf_out, 64 * m));
-      HIPCHK(c, dn(dec->vrf_proof ? dec->vrf_proof + 80 * lo : nullptr, b->vrf_proof, 80 * m));
-      HIPCHK(c, dn(dec->body_size ? dec->body_size + lo : nullptr, b->body_size, 4 * m));
-      HIPCHK(c, dn(dec->body_hash ? dec->body_hash + 32 * lo : nullptr, b->body_hash, 32 * m));
-      HIPCHK(c, dn(dec->hot_vk ? dec->hot_vk + 32 * lo : nullptr, b->hot_vk, 32 * m));
-      HIPCHK(c, dn(dec->ocert_n ? dec->ocert_n + lo : nullptr, b->ocert_n, 8 * m));
-      HIPCHK(c, dn(dec->ocert_c0 ? dec->ocert_c0 + lo : nullptr, b->ocert_c0, 8 * m));
-      HIPCHK(c, dn(dec->ocert_sig ? dec->ocert_sig + 64 * lo : nullptr, b->ocert_sig, 64 * m));
-      HIPCHK(c, dn(dec->prot_major ? dec->prot_major + lo : nullptr, b->prot_major, 8 * m));
-      HIPCHK(c, dn(dec->prot_minor ? dec->prot_minor + lo : nullptr, b->prot_minor, 8 * m));
-      HIPCHK(c, dn(dec->kes_sig ? dec->kes_sig + 448 * lo : nullptr, b->kes_sig, 448 * m));
-      HIPCHK(c, dn(dec->signed_len ? dec->signed_len + lo : nullptr, b->body_len, 4 * m));
-      HIPCHK(c, dn(dec->signed_body ? dec->signed_body + (size_t)PRAOS_SIGNED_STRIDE * lo : nullptr, b->body,
-                   (size_t)PRAOS_SIGNED_STRIDE * m));
-      HIPCHK(c, dn(dec->header_hash ? dec->header_hash + 32 * lo : nullptr, b->header_hash, 32 * m));
-    }
+    HIPCHK(c, dn(out->pool_idx, b->pool_idx, 4 * n));
+    HIPCHK(c, dn(out->beta, b->beta, 64 * n));
+    HIPCHK(c, dn(out->leader, b->leader, 32 * n));
+    HIPCHK(c, dn(out->nonce, b->nonce, 32 * n));
+    if (r == PRAOS_OK) r = praos_batch_sync(c);
+    if (r == PRAOS_OK) HIPCHK(c, d2h(c, out->bits, b->bits, 2 * n));
+  } else {
+    if (r == PRAOS_OK) r = praos_batch_sync(c);
+    if (r == PRAOS_OK) r = praos_batch_download(c, b, out);
   }
-  HIPCHK(c, hipStreamSynchronize(c->cstream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (eng[1] != c) HIPCHK(c, hipStreamSynchronize(eng[1]->stream));
-  return PRAOS_OK;
+  if (r == PRAOS_OK && dec) r = praos_batch_download_decoded(c, b, dec);
+  (void)hipStreamSynchronize(c->cstream);
+  (void)hipStreamSynchronize(c->vstream);
+  (void)hipStreamSynchronize(c->vstream2);
+  return r;
 }
 
 int praos_verify_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec) {
@@ -1585,7 +1504,7 @@ int praos_verify_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_
   {
     // chunked pipeline (PRAOS_OPT_PIPELINE: chunks; 0 = auto: up to 4 chunks of >= 64k headers)
     int K = c->pipeline;
-    if (K == 0) K = (int)std::min<size_t>(4, in->n / PIPE_MIN_CHUNK);
+    if (K == 0) K = (int)std::min<size_t>(PIPE_AUTO, in->n / PIPE_MIN_CHUNK);
     K = std::min<int>(K, (int)std::min<size_t>(PIPE_MAX, in->n));
     if (K >= 2 && c->device >= 0) return verify_bytes_pipelined(c, in, out, dec, K);
   }
