@@ -134,11 +134,17 @@ inline bool leader_x_raw(uint8_t x_le[16], const uint8_t sigma_fp[16], const uin
 inline praos_nonce nonce_combine(const praos_nonce& a, const praos_nonce& b) {
   if (a.neutral) return b;
   if (b.neutral) return a;
-  uint8_t m[64];
-  std::memcpy(m, a.hash, 32);
-  std::memcpy(m + 32, b.hash, 32);
-  praos_nonce r{};
-  blake2b(r.hash, 32, m, 64);
+  // Blake2b-256 of the 64-byte a || b: one compression, the block built in place
+  alignas(16) uint8_t blk[128];
+  std::memcpy(blk, a.hash, 32);
+  std::memcpy(blk + 32, b.hash, 32);
+  std::memset(blk + 64, 0, 64);
+  uint64_t h[8] = {0x6a09e667f3bcc908ULL ^ 0x01010020ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                   0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL,
+                   0x5be0cd19137e2179ULL};
+  blake2b_compress(h, blk, 64, true);
+  praos_nonce r;
+  std::memcpy(r.hash, h, 32);                        // little-endian host
   r.neutral = 0;
   return r;
 }

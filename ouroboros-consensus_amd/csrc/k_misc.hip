@@ -124,6 +124,33 @@ __global__ void __launch_bounds__(NT) k_leader(size_t n, const uint8_t* __restri
 }
 
 // ------------------------------------------------------------------ debug / self-test kernels
+// The header's nonce contribution from its CERTIFIED VRF output, before any verification
+// (the replay's nonce chain runs ahead of the crypto): Praos vrfNonceValue =
+// Blake2b-256(Blake2b-256("N" || output)) (Praos/VRF.hs:88-131), TPraos mkNonceFromOutputVRF =
+// Blake2b-256(output of the eta certificate).  The VRF join later writes the same values.
+__global__ void __launch_bounds__(NT) k_vrf_nonce(size_t n, const uint8_t* __restrict__ vrf_out, int tpraos,
+                                                   uint8_t* __restrict__ nonce_out) {
+  const size_t i = (size_t)blockIdx.x * NT + threadIdx.x;
+  if (i >= n) return;
+  uint32_t out[16], nn[8];
+  const uint4* q = (const uint4*)(vrf_out + 64 * i);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint4 v = q[k];
+    out[4 * k] = v.x; out[4 * k + 1] = v.y; out[4 * k + 2] = v.z; out[4 * k + 3] = v.w;
+  }
+  if (tpraos) {
+    blake2b256_of64(nn, out);
+  } else {
+    uint32_t nv[8];
+    blake2b256_tag64(nv, 'N', out);
+    blake2b_32(nn, nv, 32);
+  }
+  uint4* d = (uint4*)(nonce_out + 32 * i);
+  d[0] = make_uint4(nn[0], nn[1], nn[2], nn[3]);
+  d[1] = make_uint4(nn[4], nn[5], nn[6], nn[7]);
+}
+
 __global__ void k_debug_fe(int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -255,4 +282,8 @@ void launch_leader(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ui
   hipLaunchKernelGGL(k_leader, grid, block, 0, stream, n, leader_in, pool_sorted_idx, pool_x, x_item, f_is_one,
                      leader_words, b_ocert,
                      b_kes, b_vrf, bits, is_leader, iters, dec_status);
+}
+void launch_vrf_nonce(hipStream_t stream, size_t n, const uint8_t* vrf_out, int tpraos, uint8_t* nonce_out) {
+  if (n) hipLaunchKernelGGL(k_vrf_nonce, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, n, vrf_out, tpraos,
+                            nonce_out);
 }

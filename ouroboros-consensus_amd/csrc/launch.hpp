@@ -132,3 +132,5 @@ void launch_seg_hash(dim3 grid, dim3 block, hipStream_t stream, size_t n, const 
 void launch_block_join(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* nseg,
                        const uint8_t* split_status, const uint16_t* dec_status, const uint16_t* kes_bits,
                        const uint8_t* seg_hash, const uint8_t* body_hash, uint8_t* result, uint8_t* calc_hash);
+// replay: nonce contribution of each header's certified VRF output (k_misc.hip)
+void launch_vrf_nonce(hipStream_t stream, size_t n, const uint8_t* vrf_out, int tpraos, uint8_t* nonce_out);

@@ -4,6 +4,7 @@
 #include "praos_hip.h"
 #include "launch.hpp"
 #include "host_util.hpp"
+#include "replay_internal.hpp"
 
 static constexpr size_t NT = 256;                  // threads per block of the crypto kernels
 static constexpr size_t NIELS_BYTES = 3 * 32;      // sizeof(ge_niels)
@@ -112,6 +113,7 @@ struct praos_ctx {
   // events and persistent chunk batches (reused while they are large enough)
   int pipeline = 0;                                    // PRAOS_OPT_PIPELINE (0 = auto)
   hipStream_t cstream = nullptr;
+  hipStream_t dstream = nullptr;                       // replay: result downloads (rp_download_results)
   hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
   praos_batch* pipe[PIPE_MAX] = {};
   size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
@@ -318,6 +320,11 @@ struct praos_batch {
   std::vector<void*> owned;
   std::vector<size_t> owned_sz;
   praos_ctx* owner = nullptr;
+  // replay batches (rp_batch_alloc): capacity, decode / run events, pinned nonce table
+  size_t cap_n = 0, cap_bytes = 0;
+  hipEvent_t dec_ev = nullptr, run_ev = nullptr;
+  uint32_t* eta_h = nullptr;       // pinned: 9-word entries (nonce, neutral flag)
+  uint8_t* eidx_h = nullptr;       // pinned: per-header index
 };
 
 static constexpr size_t KT_BYTES = 16 * 8 * 4 * 32; // per cached key: 16 tables x 8 cached points
@@ -404,6 +411,7 @@ static bool open_streams(praos_ctx* c) {
     (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, greatest);
     (void)hipStreamCreateWithPriority(&c->vstream2, hipStreamNonBlocking, greatest);
     (void)hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking);
   }
   return true;
 }
@@ -504,6 +512,7 @@ void praos_close(praos_ctx* c) {
     if (c->done_ev[k]) (void)hipEventDestroy(c->done_ev[k]);
   }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->dstream) (void)hipStreamDestroy(c->dstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1375,6 +1384,153 @@ int praos_decode_headers(praos_ctx* c, const praos_header_bytes* in, praos_decod
   return r;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------- replay pipeline (internal, C++ linkage)
+praos_batch* rp_batch_alloc(praos_ctx* c, size_t n_cap, size_t bytes_cap, bool tpraos) {
+  if (!c || c->device < 0) return nullptr;
+  (void)hipSetDevice(c->device);
+  praos_batch* b = bytes_batch_alloc(c, std::max<size_t>(n_cap, 1), std::max<size_t>(bytes_cap, 8), tpraos, nullptr);
+  if (!b) return nullptr;
+  b->cap_n = std::max<size_t>(n_cap, 1);
+  b->cap_bytes = std::max<size_t>(bytes_cap, 8);
+  bool ok = dalloc(b, &b->eta_tab, 9 * 4 * 256) == hipSuccess && dalloc(b, &b->eta_idx, b->cap_n) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&b->dec_ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&b->run_ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&b->eta_h, 9 * 4 * 256, hipHostMallocDefault) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&b->eidx_h, b->cap_n, hipHostMallocDefault) == hipSuccess;
+  if (!ok) { rp_batch_destroy(c, b); return nullptr; }
+  return b;
+}
+
+void rp_batch_destroy(praos_ctx* c, praos_batch* b) {
+  if (!b) return;
+  if (c) (void)hipSetDevice(c->device);
+  if (b->dec_ev) (void)hipEventSynchronize(b->dec_ev);
+  if (b->run_ev) (void)hipEventSynchronize(b->run_ev);
+  if (b->dec_ev) (void)hipEventDestroy(b->dec_ev);
+  if (b->run_ev) (void)hipEventDestroy(b->run_ev);
+  if (b->eta_h) (void)hipHostFree(b->eta_h);
+  if (b->eidx_h) (void)hipHostFree(b->eidx_h);
+  for (void* p : b->owned) (void)hipFree(p);
+  delete b;
+}
+
+bool rp_batch_fits(const praos_batch* b, size_t n, size_t bytes) { return b && n <= b->cap_n && bytes <= b->cap_bytes; }
+
+// H2D of the concatenation of spans through the two pinned staging buffers: the pool's
+// threads gather each 16 MB piece (many small spans or a few large ones) while the DMA
+// engine moves the previous piece
+static hipError_t h2d_gather(praos_ctx* c, uint8_t* dst, const praos_span* sp, size_t ns, size_t total,
+                             hipStream_t st) {
+  if (!stage_init(c)) return hipErrorOutOfMemory;
+  std::vector<size_t> pre(ns + 1, 0);
+  for (size_t j = 0; j < ns; j++) pre[j + 1] = pre[j] + sp[j].len;
+  for (size_t off = 0, k = 0; off < total; off += STAGE_PIECE, k++) {
+    const size_t len = std::min(STAGE_PIECE, total - off);
+    hipError_t e = hipEventSynchronize(c->pin_ev[k & 1]);    // the DMA that last read this buffer
+    if (e != hipSuccess) return e;
+    uint8_t* pin = c->pin[k & 1];
+    const unsigned nt = c->pool->size();
+    c->pool->run([&](unsigned t) {
+      size_t a = off + len * t / nt;
+      const size_t b_ = off + len * (t + 1) / nt;
+      size_t j = (size_t)(std::upper_bound(pre.begin(), pre.end(), a) - pre.begin()) - 1;
+      while (a < b_ && j < ns) {
+        const size_t in = a - pre[j], m = std::min(b_ - a, sp[j].len - in);
+        std::memcpy(pin + (a - off), sp[j].p + in, m);
+        a += m;
+        j++;
+      }
+    });
+    e = hipMemcpyAsync(dst + off, pin, len, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(c->pin_ev[k & 1], st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+int rp_upload_decode(praos_ctx* c, praos_batch* b, size_t n, const praos_span* spans, size_t nspans,
+                     const uint64_t* hoff, const uint32_t* hlen) {
+  size_t bytes = 0;
+  for (size_t j = 0; j < nspans; j++) bytes += spans[j].len;
+  if (!c || !b || !rp_batch_fits(b, n, bytes) || (n && (!hoff || !hlen))) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  b->n = n;
+  b->arena_len = bytes;
+  b->body_bytes_len = (size_t)b->signed_stride * n;
+  b->decoded = true;                               // praos_batch_run skips the decode
+  const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
+  HIPCHK(c, hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream));
+  if (bytes) HIPCHK(c, h2d_gather(c, b->arena, spans, nspans, bytes, c->cstream));
+  if (n) {
+    HIPCHK(c, h2d_on(c, b->hoff, hoff, 8 * n, c->cstream));
+    HIPCHK(c, h2d_on(c, b->hlen, hlen, 4 * n, c->cstream));
+    launch_decode_praos(dim3(nblocks(n, NT)), dim3(NT), c->cstream, n, b->arena, bytes, b->hoff, b->hlen, b->slot,
+                        b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->hot_vk, b->ocert_sig, b->kes_sig,
+                        b->ocert_n, b->ocert_c0, b->body_off, b->body_len, b->body, b->block_no, b->prev_hash,
+                        b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor, b->header_hash,
+                        b->dec_status, b->tp_only ? 2 : 0, b->signed_stride, b->lead_out, b->lead_proof);
+    launch_vrf_nonce(c->cstream, n, b->vrf_out, b->tp_only ? 1 : 0, b->nonce);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipEventRecord(b->dec_ev, c->cstream));
+  return PRAOS_OK;
+}
+
+int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t* nonce) {
+  if (!c || !b || !d) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t n = b->n;
+  auto dn = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    return dst && bytes ? d2h_on(c, dst, src, bytes, c->cstream) : hipSuccess;
+  };
+  HIPCHK(c, dn(d->status, b->dec_status, 2 * n));
+  HIPCHK(c, dn(d->block_no, b->block_no, 8 * n));
+  HIPCHK(c, dn(d->slot, b->slot, 8 * n));
+  HIPCHK(c, dn(d->prev_hash, b->prev_hash, 32 * n));
+  HIPCHK(c, dn(d->prev_is_genesis, b->prev_genesis, n));
+  HIPCHK(c, dn(d->cold_vk, b->cold_vk, 32 * n));
+  HIPCHK(c, dn(d->body_size, b->body_size, 4 * n));
+  HIPCHK(c, dn(d->ocert_n, b->ocert_n, 8 * n));
+  HIPCHK(c, dn(d->header_hash, b->header_hash, 32 * n));
+  HIPCHK(c, dn(nonce, b->nonce, 32 * n));
+  return PRAOS_OK;
+}
+
+int rp_run(praos_ctx* c, praos_batch* b, const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx) {
+  if (!c || !b || (b->n && (!etas || !eta_idx)) || k == 0 || k > 256) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  for (uint32_t e = 0; e < k; e++) {
+    std::memset(b->eta_h + 9 * e, 0, 36);
+    if (!etas[e].neutral) std::memcpy(b->eta_h + 9 * e, etas[e].hash, 32);
+    b->eta_h[9 * e + 8] = etas[e].neutral ? 1u : 0u;
+  }
+  std::memcpy(b->eidx_h, eta_idx, b->n);
+  // the pinned host buffers are reused by the next batch on this slot only after this run
+  HIPCHK(c, hipStreamWaitEvent(c->stream, b->dec_ev, 0));
+  HIPCHK(c, hipMemcpyAsync(b->eta_tab, b->eta_h, 36 * (size_t)k, hipMemcpyHostToDevice, c->stream));
+  if (b->n) HIPCHK(c, hipMemcpyAsync(b->eta_idx, b->eidx_h, b->n, hipMemcpyHostToDevice, c->stream));
+  const int r = praos_batch_run(c, b);
+  if (r != PRAOS_OK) return r;
+  HIPCHK(c, hipEventRecord(b->run_ev, c->stream));
+  return PRAOS_OK;
+}
+
+int rp_download_results(praos_ctx* c, praos_batch* b, uint16_t* bits, int32_t* pool_idx) {
+  if (!c || !b || !bits) return PRAOS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamWaitEvent(c->dstream, b->run_ev, 0));
+  if (b->n) {
+    HIPCHK(c, hipMemcpyAsync(bits, b->bits, 2 * b->n, hipMemcpyDeviceToHost, c->dstream));
+    if (pool_idx) HIPCHK(c, hipMemcpyAsync(pool_idx, b->pool_idx, 4 * b->n, hipMemcpyDeviceToHost, c->dstream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->dstream));
+  return PRAOS_OK;
+}
+
+extern "C" {
+
 // Stored-bytes verification with the upload in K chunks (contiguous runs of headers) and
 // the batch's largest kernel run under it: chunk k's bytes move H2D on the copy stream
 // (pinned staging, host threads) while, on the GPU, chunk k-1 is decoded (ctx stream) and
@@ -1830,7 +1986,8 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
                      const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei,
                      praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed,
                      const praos_nonce* etas = nullptr, uint32_t netas = 0, const uint8_t* eta_idx = nullptr,
-                     bool tpraos = false, const praos_nonce* extra_entropy = nullptr, uint16_t* failures = nullptr) {
+                     bool tpraos = false, const praos_nonce* extra_entropy = nullptr, uint16_t* failures = nullptr,
+                     const praos_nonce* evol_after = nullptr) {
   if (!c || !h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash ||
       ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter)))
     return PRAOS_E_ARG;
@@ -1950,7 +2107,9 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     praos_nonce eta{};
     std::memcpy(eta.hash, crypto->nonce + 32 * i, 32);
     eta.neutral = 0;
-    W.evolving = nonce_combine(W.evolving, eta);
+    // evol_after (the replay's nonce chain, run ahead as if every header were valid) equals
+    // this chain up to the first invalid header; from there W skips the failed headers
+    W.evolving = (evol_after && !frozen) ? evol_after[i] : nonce_combine(W.evolving, eta);
     const uint64_t first_next = ei->epoch_base_slot + (e_new - ei->epoch_base_no + 1) * ei->epoch_length;
     if (slot + ei->stability_window < first_next) W.candidate = W.evolving;
     T.ctr[k] = n;
@@ -1989,6 +2148,16 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
   if (chain_stop) *chain_stop = std::min(stop, i);
   if (processed) *processed = i;
   return PRAOS_OK;
+}
+
+int rp_fold(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
+            const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei, praos_chain_state* st,
+            const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx, const praos_nonce* evolving_after,
+            bool tpraos, const praos_nonce* extra_entropy, uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
+            size_t* processed) {
+  if (!etas || !eta_idx || k == 0) return PRAOS_E_ARG;
+  return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, env, ei, st, verdict, chain_stop, processed, etas, k,
+                   eta_idx, tpraos, extra_entropy, failures, evolving_after);
 }
 
 extern "C" {

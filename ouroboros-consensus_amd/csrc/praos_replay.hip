@@ -1,19 +1,28 @@
 // praos_replay.hip -- db-analyser-style chain replay over an ImmutableDB directory
-// (SURVEY.md sec. 8 row N3): host C++ on top of the library's own C ABI.
+// (SURVEY.md sec. 8 row N3): host C++ on top of the library (its C ABI and the internal
+// pipeline entry points of replay_internal.hpp).
 //
 // Mirrors the reference's streaming loop (DBAnalyser/Analysis.hs:815-847,
 // processAllImmutableDB: ImmutableDB.streamAll, one iteratorNext per block) and its
 // header-validation pass (benchmarkLedgerOps, :479-607: tick, then validateHeader),
 // in batches: headers are read through the secondary index into batches of up to
-// batch_max headers (any number of epochs, up to 256), decoded on the device
-// (praos_batch_decode), given their epoch nonces -- the nonce tickChainDepState
-// (Praos.hs:407-431) reaches at each header, computed on the host from the certified
-// VRF outputs as if every header were valid -- crypto-checked under those nonces
-// (praos_batch_set_nonces + praos_batch_run) and folded on the host with
-// praos_validate_headers_nonces (envelope, then updateChainDepState), which accepts a
-// header only if the nonce its crypto ran with is the one the real fold ticks to.  One
-// ledger view (pools, parameters) for the whole replay.  Like the reference, the
-// replay ends at the first invalid header.
+// batch_max headers (any number of epochs, up to 256), decoded on the device, given their
+// epoch nonces -- the nonce tickChainDepState (Praos.hs:407-431) reaches at each header,
+// computed on the host from the certified VRF outputs as if every header were valid --
+// crypto-checked under those nonces, and folded on the host (envelope, then
+// updateChainDepState), which accepts a header only if the nonce its crypto ran with is the
+// one the real fold ticks to.  One ledger view (pools, parameters) for the whole replay.
+// Like the reference, the replay ends at the first invalid header.
+//
+// Three host threads, up to three batches in flight:
+//   reader (this thread): chunk files are memory-mapped; a batch's header bytes go straight
+//     from the mappings into the pinned staging buffers (coalesced spans, no host copy of
+//     the chunk), H2D on the copy stream, decode + the nonce value of every certified VRF
+//     output on the device (k_vrf_nonce), and back the decoded fields the chain needs;
+//   nonce chain: the evolving-nonce Blake2b chain in header order (the one sequential piece
+//     of work of the replay), the per-header epoch nonces, then the batch's crypto run;
+//   fold: waits for the crypto bits, folds envelope + updateChainDepState reusing the nonce
+//     chain's evolving nonces (no second Blake2b chain), writes the verdicts.
 //
 // On-disk format (ImmutableDB, Storage/ImmutableDB/Impl): NNNNN.chunk holds the
 // stored blocks back to back; NNNNN.secondary one 56-byte Entry per block
@@ -21,13 +30,25 @@
 // headerSize u16 BE, checksum u32 BE, headerHash 32 bytes, blockOrEBB (slot) u64 BE.
 // The primary index maps relative slots to entries and is not needed for a full
 // sequential replay.  Chunks are read from 00000 upwards until one is missing.
+#include <hip/hip_runtime.h>
+
 #include "praos_hip.h"
 #include "host_util.hpp"
+#include "replay_internal.hpp"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -58,40 +79,71 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// Streams (header bytes, slot) out of the chunk files, one chunk in memory at a time.
+// one chunk: its data file memory-mapped (read-only), its secondary index in memory
+struct Chunk {
+  const uint8_t* data = nullptr;
+  size_t len = 0;
+  void* map = nullptr;
+  std::vector<uint8_t> sec;
+  ~Chunk() {
+    if (map) munmap(map, len);
+  }
+};
+
+bool map_chunk(const std::string& path, Chunk& ch) {
+  const int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  struct stat st;
+  if (fstat(fd, &st) != 0) { close(fd); return false; }
+  ch.len = (size_t)st.st_size;
+  if (ch.len) {
+    void* m = mmap(nullptr, ch.len, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (m == MAP_FAILED) { close(fd); return false; }
+    ch.map = m;
+    ch.data = (const uint8_t*)m;
+  }
+  close(fd);
+  return true;
+}
+
+// Streams (header bytes, slot) out of the chunk files, one chunk mapped at a time (a batch
+// keeps the chunks it points into alive until its upload has read them).
 struct ChunkReader {
   std::string dir, err;
   int chunk = 0;
   bool done = false;
-  std::vector<uint8_t> data, sec;
+  std::shared_ptr<Chunk> cur;
   size_t entry = 0, nentries = 0;
   void load_next() {
     char name[32];
     std::snprintf(name, sizeof name, "/%05d.chunk", chunk);
-    if (!read_file(dir + name, data)) { done = true; return; }
+    auto ch = std::make_shared<Chunk>();
+    if (!map_chunk(dir + name, *ch)) { done = true; cur.reset(); return; }
     std::snprintf(name, sizeof name, "/%05d.secondary", chunk);
-    if (!read_file(dir + name, sec) || sec.size() % 56 != 0) {
+    if (!read_file(dir + name, ch->sec) || ch->sec.size() % 56 != 0) {
       err = std::string("missing or malformed secondary index ") + (name + 1);
       done = true;
+      cur.reset();
       return;
     }
+    cur = ch;
     chunk++;
     entry = 0;
-    nentries = sec.size() / 56;
+    nentries = cur->sec.size() / 56;
   }
   // the next entry, without consuming it; false at the end of the database
   bool peek(const uint8_t** hdr, uint32_t* len, uint64_t* slot, const uint8_t** hash = nullptr) {
     while (!done && entry >= nentries) load_next();
     if (done) return false;
-    const uint8_t* e = sec.data() + 56 * entry;
+    const uint8_t* e = cur->sec.data() + 56 * entry;
     const uint64_t boff = be(e, 8), hoff = be(e + 8, 2), hsz = be(e + 10, 2);
-    if (boff > data.size() || hoff + hsz > data.size() - boff) {
+    if (boff > cur->len || hoff + hsz > cur->len - boff) {
       err = "secondary index entry outside its chunk (chunk " + std::to_string(chunk - 1) + ", entry " +
             std::to_string(entry) + ")";
       done = true;
       return false;
     }
-    *hdr = data.data() + boff + hoff;
+    *hdr = cur->data + boff + hoff;
     *len = (uint32_t)hsz;
     *slot = be(e + 48, 8);
     if (hash) *hash = e + 16;
@@ -100,13 +152,16 @@ struct ChunkReader {
   void pop() { entry++; }
 };
 
+constexpr int SLOTS = 3;                      // batches in flight
+constexpr size_t SPAN_GAP = 4096;             // headers this close share one uploaded span
+
 }  // namespace
 
-// TPraos mode (eras Shelley..Alonzo, HFEras.hs:43-49; TPraos.hs:361-387): stored BHeaders
-// (praos_batch_upload_tpraos_bytes), the TPraos nonce rules -- the header's nonce is
-// mkNonceFromOutputVRF of its eta certificate (Blake2b-256 of the output, no range
-// extension) and TICKN adds the extra entropy (eta0 := eta_c ⭒ eta_h ⭒ extraEntropy) --
-// and the TPraos fold (PRTCL predicate-failure sets into failures[]).
+// TPraos mode (eras Shelley..Alonzo, HFEras.hs:43-49; TPraos.hs:361-387): stored BHeaders,
+// the TPraos nonce rules -- the header's nonce is mkNonceFromOutputVRF of its eta
+// certificate (Blake2b-256 of the output, no range extension) and TICKN adds the extra
+// entropy (eta0 := eta_c ⭒ eta_h ⭒ extraEntropy) -- and the TPraos fold (PRTCL
+// predicate-failure sets into failures[]).
 static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
                        const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                        praos_chain_state* st, size_t batch_max, uint8_t* verdicts, uint16_t* failures,
@@ -139,8 +194,8 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     }
   }
   // The ledger view (pools, parameters) is installed once; the epoch nonces travel
-  // with each batch (praos_batch_set_nonces), so a batch may span many epochs and stay
-  // large enough to fill the device even when epochs are short.
+  // with each batch, so a batch may span many epochs and stay large enough to fill the
+  // device even when epochs are short.
   {
     praos_nonce eta0{};
     uint32_t l;
@@ -155,22 +210,38 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     const int r = praos_set_epoch(ctx, eta0.neutral ? nullptr : eta0.hash, pools, npools, params);
     if (r != PRAOS_OK) return r;
   }
-  // Two batches in flight: while the host folds batch k, the device verifies batch k+1
-  // (its nonces come from the speculative nonce chain, which runs ahead of the fold).
-  struct Stage {
+  struct Slot {
     praos_batch* b = nullptr;
+    int state = 0;                            // 0 free, 1 decoded, 2 crypto queued
     size_t n = 0;
     uint64_t index0 = 0;
-    std::vector<uint8_t> arena;
+    std::vector<praos_span> spans;
+    std::vector<std::shared_ptr<Chunk>> chunks;
     std::vector<uint64_t> off, slot, block_no, ocn;
     std::vector<uint32_t> len, bsize;
-    std::vector<uint8_t> prev, gen, cold, hh, nonce, v, vout, eidx;
-    std::vector<uint16_t> dstat, bits, fails;
-    std::vector<int32_t> pidx;
-    std::vector<praos_nonce> etas;
+    std::vector<uint8_t> prev, gen, cold, hh, nonce, v, eidx;
+    std::vector<uint16_t> dstat, fails;
+    std::vector<praos_nonce> etas, evol;
+    uint16_t* bits = nullptr;                 // pinned
+    int32_t* pidx = nullptr;                  // pinned
+    size_t pin_cap = 0;
   };
-  Stage stage[2];
-  // the speculative nonce state (tick + reupdate as if every header were valid)
+  Slot S[SLOTS];
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<bool> stop{false};
+  int first_rc = PRAOS_OK;
+  uint64_t nbatches = UINT64_MAX;             // set by the reader at the end of the database
+  bool stopped = false;
+  auto fail = [&](int rc) {
+    std::lock_guard<std::mutex> g(mu);
+    if (first_rc == PRAOS_OK) first_rc = rc;
+    stop = true;
+    cv.notify_all();
+  };
+  double t_io = 0, t_dev = 0, t_wait = 0, t_nonce = 0, t_fold = 0;   // per thread: reader | fold
+  uint64_t epochs_seen = 0, batches = 0;
+  // ---- nonce chain (speculative tick + reupdate as if every header were valid)
   struct Spec {
     int32_t origin;
     uint64_t last;
@@ -180,203 +251,241 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
        st->last_epoch_block, false};
   praos_nonce last_eta{};
   bool have_last = false;
-  uint64_t next_index = 0;
-  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  // read, upload and decode the next batch, derive its nonces; false at the end
-  auto prepare = [&](Stage& S, int& rc) -> bool {
-    rc = PRAOS_OK;
-    auto t_io = std::chrono::steady_clock::now();
-    S.arena.clear();
-    S.off.clear();
-    S.len.clear();
+  uint64_t sp_epoch = sp.origin ? 0 : epoch_of(sp.last);
+  std::thread chain([&] {
+    for (uint64_t k = 0;; k++) {
+      Slot& C = S[k % SLOTS];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 1; });
+        if (stop || k >= nbatches) return;
+      }
+      auto t0 = std::chrono::steady_clock::now();
+      const size_t n = C.n;
+      C.etas.clear();
+      C.eidx.resize(n);
+      C.evol.resize(n);
+      // epoch bounds cached: a division per epoch, not per header (the loop is the replay's
+      // one sequential piece of work; one Blake2b compression per header is its floor)
+      uint64_t ep_lo = 1, ep_hi = 0, ep_no = 0, ep_cut = 0;     // [ep_lo, ep_hi): epoch ep_no
+      for (size_t i = 0; i < n; i++) {
+        const uint64_t slot_i = C.slot[i];
+        if (slot_i < ep_lo || slot_i >= ep_hi) {
+          ep_no = epoch_of(slot_i);
+          ep_lo = slot_i < ei->epoch_base_slot ? 0 : ei->epoch_base_slot + (ep_no - ei->epoch_base_no) * ei->epoch_length;
+          ep_hi = slot_i < ei->epoch_base_slot ? ei->epoch_base_slot : ep_lo + ei->epoch_length;
+          const uint64_t first_next = ei->epoch_base_slot + (ep_no - ei->epoch_base_no + 1) * ei->epoch_length;
+          ep_cut = first_next > ei->stability_window ? first_next - ei->stability_window : 0;
+        }
+        const uint64_t e_new = ep_no;
+        if (!sp.dead && e_new > (sp.origin ? 0 : sp_epoch)) {
+          sp.epoch_nonce = praos_host::nonce_combine(sp.candidate, sp.leb);
+          if (tpraos && extra_entropy) sp.epoch_nonce = praos_host::nonce_combine(sp.epoch_nonce, *extra_entropy);
+          sp.leb = sp.lab;
+        }
+        if (C.etas.empty() || !praos_host::nonce_eq(C.etas.back(), sp.epoch_nonce)) C.etas.push_back(sp.epoch_nonce);
+        C.eidx[i] = (uint8_t)std::min<size_t>(C.etas.size() - 1, 255);
+        if (sp.dead || (C.dstat[i] & PRAOS_DEC_FAILED)) { sp.dead = true; C.evol[i] = sp.evolving; continue; }
+        sp.origin = 0;
+        sp.last = slot_i;
+        sp_epoch = e_new;
+        sp.lab.neutral = C.gen[i] ? 1 : 0;
+        std::memset(sp.lab.hash, 0, 32);
+        if (!C.gen[i]) std::memcpy(sp.lab.hash, C.prev.data() + 32 * i, 32);
+        praos_nonce eta;
+        std::memcpy(eta.hash, C.nonce.data() + 32 * i, 32);
+        eta.neutral = 0;
+        sp.evolving = praos_host::nonce_combine(sp.evolving, eta);
+        C.evol[i] = sp.evolving;
+        if (slot_i < ep_cut) sp.candidate = sp.evolving;        // slot + window < first slot of the next epoch
+      }
+      if (C.etas.size() > 256) { praos_set_error_(ctx, "replay: > 256 epochs in a batch"); fail(PRAOS_E_STATE); return; }
+      for (const praos_nonce& e : C.etas)
+        if (!have_last || !praos_host::nonce_eq(e, last_eta)) { epochs_seen++; last_eta = e; have_last = true; }
+      t_nonce += ms_since(t0);
+      const int rc = rp_run(ctx, C.b, C.etas.data(), (uint32_t)C.etas.size(), C.eidx.data());
+      if (rc != PRAOS_OK) { fail(rc); return; }
+      std::lock_guard<std::mutex> g(mu);
+      C.state = 2;
+      batches++;
+      cv.notify_all();
+    }
+  });
+  // ---- fold (envelope + updateChainDepState over each verified batch, in order)
+  uint64_t validated = 0, headers_done = 0, stop_index = 0;
+  uint8_t stop_verdict = 0;
+  std::thread folder([&] {
+    for (uint64_t k = 0;; k++) {
+      Slot& C = S[k % SLOTS];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 2; });
+        if (stop || k >= nbatches) return;
+      }
+      auto t0 = std::chrono::steady_clock::now();
+      int rc = rp_download_results(ctx, C.b, C.bits, C.pidx);
+      if (rc != PRAOS_OK) { fail(rc); return; }
+      t_wait += ms_since(t0);
+      t0 = std::chrono::steady_clock::now();
+      const size_t n = C.n;
+      C.v.resize(n);
+      C.fails.resize(n);
+      praos_out out{C.bits, C.pidx, nullptr, nullptr, C.nonce.data()};
+      praos_headers h{};
+      h.n = n;
+      h.slot = C.slot.data();
+      h.cold_vk = C.cold.data();
+      h.ocert_n = C.ocn.data();
+      env->block_no = C.block_no.data();
+      env->header_hash = C.hh.data();
+      env->header_size = C.len.data();
+      env->body_size = C.bsize.data();
+      size_t stp = 0, done = 0;
+      rc = rp_fold(ctx, &h, C.prev.data(), C.gen.data(), &out, env, ei, st, C.etas.data(), (uint32_t)C.etas.size(),
+                   C.eidx.data(), C.evol.data(), tpraos, extra_entropy, C.v.data(), C.fails.data(), &stp, &done);
+      env->block_no = nullptr;
+      env->header_hash = nullptr;
+      env->header_size = nullptr;
+      env->body_size = nullptr;
+      t_fold += ms_since(t0);
+      if (rc != PRAOS_OK) { fail(rc); return; }
+      for (size_t j = 0; j < done && C.index0 + j < verdicts_cap; j++) {
+        verdicts[C.index0 + j] = C.v[j];
+        if (failures) failures[C.index0 + j] = tpraos ? C.fails[j] : 0;
+      }
+      std::lock_guard<std::mutex> g(mu);
+      if (stp < done) {          // the chain stops at the first invalid header
+        validated += stp;
+        stop_index = C.index0 + stp;
+        stop_verdict = C.v[stp];
+        headers_done = C.index0 + stp + 1;
+        stopped = true;
+        stop = true;
+      } else if (done < n) {     // every header valid so far, yet a nonce the fold disagrees with
+        praos_set_error_(ctx, "replay: epoch nonce of header " + std::to_string(C.index0 + done) + " diverged");
+        if (first_rc == PRAOS_OK) first_rc = PRAOS_E_STATE;
+        stop = true;
+      } else {
+        validated += n;
+        headers_done = C.index0 + n;
+      }
+      C.state = 0;
+      cv.notify_all();
+    }
+  });
+  // ---- reader (this thread): build, upload and decode batch k into slot k % SLOTS
+  uint64_t next_index = 0, built = 0;
+  for (uint64_t k = 0;; k++) {
+    Slot& C = S[k % SLOTS];
+    {
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait(g, [&] { return stop || C.state == 0; });
+      if (stop) break;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    C.spans.clear();
+    C.chunks.clear();
+    C.off.clear();
+    C.len.clear();
     const uint8_t* p;
     uint32_t l;
     uint64_t s, e_prev = 0;
     uint32_t nep = 0;
-    while (S.off.size() < batch_max && rd.peek(&p, &l, &s)) {
+    size_t arena = 0;
+    const Chunk* span_chunk = nullptr;
+    while (C.off.size() < batch_max && rd.peek(&p, &l, &s)) {
       const uint64_t e = epoch_of(s);
-      if (S.off.empty() || e != e_prev) {
+      if (C.off.empty() || e != e_prev) {
         if (nep == 256) break;
         nep++;
         e_prev = e;
       }
-      if (S.arena.capacity() < S.arena.size() + l) S.arena.reserve(2 * S.arena.size() + (size_t(1) << 20));
-      S.off.push_back(S.arena.size());
-      S.len.push_back(l);
-      S.arena.insert(S.arena.end(), p, p + l);
+      if (C.chunks.empty() || C.chunks.back() != rd.cur) C.chunks.push_back(rd.cur);
+      praos_span* last = C.spans.empty() ? nullptr : &C.spans.back();
+      if (last && span_chunk == rd.cur.get() && p >= last->p + last->len && p - (last->p + last->len) <= SPAN_GAP) {
+        const size_t ext = (size_t)(p + l - (last->p + last->len));
+        C.off.push_back(arena + (size_t)(p - (last->p + last->len)));
+        last->len += ext;
+        arena += ext;
+      } else {
+        C.spans.push_back({p, l});
+        span_chunk = rd.cur.get();
+        C.off.push_back(arena);
+        arena += l;
+      }
+      C.len.push_back(l);
       rd.pop();
     }
-    stats->ms_io += ms_since(t_io);
-    if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); rc = PRAOS_E_ARG; return false; }
-    if (S.off.empty()) return false;
-    const size_t n = S.n = S.off.size();
-    S.index0 = next_index;
+    t_io += ms_since(t0);
+    if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); fail(PRAOS_E_ARG); break; }
+    if (C.off.empty()) break;
+    t0 = std::chrono::steady_clock::now();
+    const size_t n = C.n = C.off.size();
+    C.index0 = next_index;
     next_index += n;
-    auto t_dev = std::chrono::steady_clock::now();
-    praos_header_bytes hb{n, S.arena.data(), S.arena.size(), S.off.data(), S.len.data()};
-    S.b = tpraos ? praos_batch_upload_tpraos_bytes(ctx, &hb) : praos_batch_upload_bytes(ctx, &hb);
-    if (!S.b) { rc = PRAOS_E_OOM; return false; }
-    S.dstat.resize(n); S.block_no.resize(n); S.slot.resize(n); S.ocn.resize(n); S.bsize.resize(n);
-    S.prev.resize(32 * n); S.gen.resize(n); S.cold.resize(32 * n); S.hh.resize(32 * n); S.vout.resize(64 * n);
-    S.bits.resize(n); S.pidx.resize(n); S.nonce.resize(32 * n); S.v.resize(n); S.eidx.resize(n); S.fails.resize(n);
-    praos_decoded dec{};
-    dec.status = S.dstat.data(); dec.block_no = S.block_no.data(); dec.slot = S.slot.data();
-    dec.prev_hash = S.prev.data(); dec.prev_is_genesis = S.gen.data(); dec.cold_vk = S.cold.data();
-    dec.body_size = S.bsize.data(); dec.ocert_n = S.ocn.data(); dec.header_hash = S.hh.data();
-    dec.vrf_out = S.vout.data();
-    rc = praos_batch_decode(ctx, S.b);
-    if (rc == PRAOS_OK) rc = praos_batch_download_decoded(ctx, S.b, &dec);
-    if (rc != PRAOS_OK) return false;
-    stats->ms_device += ms_since(t_dev);
-    // vrfNonceValue of every CERTIFIED output (Praos/VRF.hs:88-131), in parallel; then the
-    // nonce chain in order (tick at epoch changes, evolving ⭒ eta, candidate freeze)
-    auto t_nonce = std::chrono::steady_clock::now();
-    std::vector<praos_nonce> eta_of(n);
-    {
-      std::vector<std::thread> th;
-      for (unsigned t = 0; t < nthreads; t++)
-        th.emplace_back([&, t] {
-          for (size_t i = n * t / nthreads; i < n * (t + 1) / nthreads; i++) {
-            if (tpraos) {        // mkNonceFromOutputVRF (the eta certificate's output)
-              praos_host::blake2b(eta_of[i].hash, 32, S.vout.data() + 64 * i, 64);
-            } else {
-              uint8_t m[65], h1[32];
-              m[0] = 'N';
-              std::memcpy(m + 1, S.vout.data() + 64 * i, 64);
-              praos_host::blake2b(h1, 32, m, 65);
-              praos_host::blake2b(eta_of[i].hash, 32, h1, 32);
-            }
-            eta_of[i].neutral = 0;
-          }
-        });
-      for (auto& t : th) t.join();
+    if (!rp_batch_fits(C.b, n, arena)) {
+      rp_batch_destroy(ctx, C.b);
+      C.b = rp_batch_alloc(ctx, n + n / 8 + 64, arena + arena / 8 + 4096, tpraos);
+      if (!C.b) { fail(PRAOS_E_OOM); break; }
     }
-    S.etas.clear();
-    for (size_t i = 0; i < n; i++) {
-      const uint64_t e_new = epoch_of(S.slot[i]);
-      if (!sp.dead && e_new > (sp.origin ? 0 : epoch_of(sp.last))) {
-        sp.epoch_nonce = praos_host::nonce_combine(sp.candidate, sp.leb);
-        if (tpraos && extra_entropy) sp.epoch_nonce = praos_host::nonce_combine(sp.epoch_nonce, *extra_entropy);
-        sp.leb = sp.lab;
+    if (C.pin_cap < n) {
+      if (C.bits) (void)hipHostFree(C.bits);
+      if (C.pidx) (void)hipHostFree(C.pidx);
+      C.pin_cap = n + n / 8 + 64;
+      if (hipHostMalloc((void**)&C.bits, 2 * C.pin_cap, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc((void**)&C.pidx, 4 * C.pin_cap, hipHostMallocDefault) != hipSuccess) {
+        C.bits = nullptr;
+        C.pidx = nullptr;
+        C.pin_cap = 0;
+        fail(PRAOS_E_OOM);
+        break;
       }
-      if (S.etas.empty() || !praos_host::nonce_eq(S.etas.back(), sp.epoch_nonce)) S.etas.push_back(sp.epoch_nonce);
-      S.eidx[i] = (uint8_t)(S.etas.size() - 1);
-      if (sp.dead || (S.dstat[i] & PRAOS_DEC_FAILED)) { sp.dead = true; continue; }   // the chain stops here
-      sp.origin = 0;
-      sp.last = S.slot[i];
-      sp.lab.neutral = S.gen[i] ? 1 : 0;
-      std::memset(sp.lab.hash, 0, 32);
-      if (!S.gen[i]) std::memcpy(sp.lab.hash, S.prev.data() + 32 * i, 32);
-      sp.evolving = praos_host::nonce_combine(sp.evolving, eta_of[i]);
-      const uint64_t first_next = ei->epoch_base_slot + (e_new - ei->epoch_base_no + 1) * ei->epoch_length;
-      if (S.slot[i] + ei->stability_window < first_next) sp.candidate = sp.evolving;
     }
-    if (S.etas.size() > 256) { praos_set_error_(ctx, "replay: > 256 epochs in a batch"); rc = PRAOS_E_STATE; return false; }
-    for (const praos_nonce& e : S.etas)
-      if (!have_last || !praos_host::nonce_eq(e, last_eta)) { stats->epochs++; last_eta = e; have_last = true; }
-    stats->ms_nonce += ms_since(t_nonce);
-    rc = praos_batch_set_nonces(ctx, S.b, S.etas.data(), (uint32_t)S.etas.size(), S.eidx.data());
-    return rc == PRAOS_OK;
-  };
-  auto launch = [&](Stage& S) {
-    auto t = std::chrono::steady_clock::now();
-    const int r = praos_batch_run(ctx, S.b);   // async on the ctx stream
-    stats->ms_device += ms_since(t);
-    stats->batches++;
-    return r;
-  };
-  auto download = [&](Stage& S) {
-    auto t = std::chrono::steady_clock::now();
-    praos_out out{S.bits.data(), S.pidx.data(), nullptr, nullptr, S.nonce.data()};
-    const int r = praos_batch_download(ctx, S.b, &out);
-    stats->ms_device += ms_since(t);
-    return r;
-  };
-  // envelope + updateChainDepState over a verified batch; true when the chain stops
-  auto fold = [&](Stage& S, int& rc) -> bool {
-    auto t_fold = std::chrono::steady_clock::now();
-    const size_t n = S.n;
-    praos_out out{S.bits.data(), S.pidx.data(), nullptr, nullptr, S.nonce.data()};
-    praos_headers h{};
-    h.n = n;
-    h.slot = S.slot.data();
-    h.cold_vk = S.cold.data();
-    h.ocert_n = S.ocn.data();
-    env->block_no = S.block_no.data();
-    env->header_hash = S.hh.data();
-    env->header_size = S.len.data();
-    env->body_size = S.bsize.data();
-    size_t stop = 0, done = 0;
-    if (tpraos) {
-      praos_tpraos_headers th{};
-      th.h = h;
-      praos_tpraos_out to{S.bits.data(), S.pidx.data(), nullptr, nullptr, S.nonce.data()};
-      rc = praos_tpraos_validate_headers_nonces(ctx, &th, S.prev.data(), S.gen.data(), &to, env, ei, extra_entropy,
-                                                st, S.etas.data(), (uint32_t)S.etas.size(), S.eidx.data(),
-                                                S.v.data(), S.fails.data(), &stop, &done);
-    } else {
-      rc = praos_validate_headers_nonces(ctx, &h, S.prev.data(), S.gen.data(), &out, env, ei, st, S.etas.data(),
-                                         (uint32_t)S.etas.size(), S.eidx.data(), S.v.data(), &stop, &done);
-    }
-    env->block_no = nullptr;
-    env->header_hash = nullptr;
-    env->header_size = nullptr;
-    env->body_size = nullptr;
-    stats->ms_fold += ms_since(t_fold);
-    if (rc != PRAOS_OK) return true;
-    for (size_t k = 0; k < done && S.index0 + k < verdicts_cap; k++) {
-      verdicts[S.index0 + k] = S.v[k];
-      if (failures) failures[S.index0 + k] = tpraos ? S.fails[k] : 0;
-    }
-    if (stop < done) {          // the chain stops at the first invalid header
-      stats->validated += stop;
-      stats->stop_index = S.index0 + stop;
-      stats->stop_verdict = S.v[stop];
-      stats->headers = S.index0 + stop + 1;
-      return true;
-    }
-    if (done < n) {             // every header valid so far, yet a nonce the fold disagrees with
-      praos_set_error_(ctx, "replay: epoch nonce of header " + std::to_string(S.index0 + done) + " diverged");
-      rc = PRAOS_E_STATE;
-      return true;
-    }
-    stats->validated += n;
-    stats->headers = S.index0 + n;
-    return false;
-  };
-  auto release = [&](Stage& S) {
-    if (S.b) praos_batch_free(ctx, S.b);
-    S.b = nullptr;
-  };
-  bool stopped = false;
-  int rc = PRAOS_OK;
-  int cur = 0;
-  bool have_cur = prepare(stage[cur], rc);
-  if (rc == PRAOS_OK && have_cur) rc = launch(stage[cur]);
-  while (rc == PRAOS_OK && have_cur) {
-    Stage& C = stage[cur];
-    Stage& N = stage[cur ^ 1];
-    // the next batch is read and decoded while C's crypto runs; its decode queues behind it
-    const bool have_next = !sp.dead && prepare(N, rc);
-    if (rc != PRAOS_OK) break;
-    rc = download(C);
-    if (rc != PRAOS_OK) break;
-    if (have_next) {
-      rc = launch(N);           // N's crypto overlaps C's fold
-      if (rc != PRAOS_OK) break;
-    }
-    stopped = fold(C, rc);
-    release(C);
-    if (stopped || rc != PRAOS_OK) break;
-    have_cur = have_next;
-    cur ^= 1;
+    int rc = rp_upload_decode(ctx, C.b, n, C.spans.data(), C.spans.size(), C.off.data(), C.len.data());
+    C.chunks.clear();                         // the mappings have been read (except the reader's current one)
+    C.dstat.resize(n); C.block_no.resize(n); C.slot.resize(n); C.ocn.resize(n); C.bsize.resize(n);
+    C.prev.resize(32 * n); C.gen.resize(n); C.cold.resize(32 * n); C.hh.resize(32 * n); C.nonce.resize(32 * n);
+    praos_decoded dec{};
+    dec.status = C.dstat.data(); dec.block_no = C.block_no.data(); dec.slot = C.slot.data();
+    dec.prev_hash = C.prev.data(); dec.prev_is_genesis = C.gen.data(); dec.cold_vk = C.cold.data();
+    dec.body_size = C.bsize.data(); dec.ocert_n = C.ocn.data(); dec.header_hash = C.hh.data();
+    if (rc == PRAOS_OK) rc = rp_download_decoded(ctx, C.b, &dec, C.nonce.data());
+    t_dev += ms_since(t0);
+    if (rc != PRAOS_OK) { fail(rc); break; }
+    std::lock_guard<std::mutex> g(mu);
+    C.state = 1;
+    built = k + 1;
+    cv.notify_all();
   }
-  release(stage[0]);
-  release(stage[1]);
-  if (rc != PRAOS_OK) return rc;
-  const uint64_t index0 = stopped ? stats->headers : next_index;
-  if (!stopped) stats->stop_index = index0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    nbatches = built;                         // the chain and the fold finish what was handed on
+    cv.notify_all();
+  }
+  chain.join();
+  folder.join();
+  for (Slot& C : S) {
+    rp_batch_destroy(ctx, C.b);
+    if (C.bits) (void)hipHostFree(C.bits);
+    if (C.pidx) (void)hipHostFree(C.pidx);
+  }
+  stats->ms_io = t_io;
+  stats->ms_device = t_dev + t_wait;
+  stats->ms_nonce = t_nonce;
+  stats->ms_fold = t_fold;
+  stats->epochs = (uint32_t)epochs_seen;
+  stats->batches = (uint32_t)batches;
   stats->chunks = (uint32_t)rd.chunk;
+  stats->validated = validated;
+  if (first_rc != PRAOS_OK) return first_rc;
+  if (stopped) {
+    stats->stop_index = stop_index;
+    stats->stop_verdict = stop_verdict;
+    stats->headers = headers_done;
+  } else {
+    stats->headers = next_index;
+    stats->stop_index = next_index;
+  }
   return PRAOS_OK;
 }
 

@@ -1,0 +1,37 @@
+#pragma once
+// replay_internal.hpp -- entry points of libpraos_hip used by the replay driver
+// (praos_replay.hip) for its threaded pipeline; C++ linkage, not part of the C ABI.
+#include "praos_hip.h"
+#include <cstddef>
+#include <cstdint>
+
+struct praos_span {           // a run of stored bytes in host memory (e.g. an mmapped chunk file)
+  const uint8_t* p;
+  size_t len;
+};
+
+// A persistent from-bytes batch with room for n_cap headers over bytes_cap stored bytes, its
+// own events and pinned host buffers for the nonce table.
+praos_batch* rp_batch_alloc(praos_ctx* c, size_t n_cap, size_t bytes_cap, bool tpraos);
+void rp_batch_destroy(praos_ctx* c, praos_batch* b);
+bool rp_batch_fits(const praos_batch* b, size_t n, size_t bytes);
+// Copy stream: the spans' concatenation (the arena) and the per-header (offset, length) go
+// H2D through the pinned staging buffers, then decode and the nonce value of each header's
+// certified VRF output (k_vrf_nonce).  Returns once the host side is queued.
+int rp_upload_decode(praos_ctx* c, praos_batch* b, size_t n, const praos_span* spans, size_t nspans,
+                     const uint64_t* hoff, const uint32_t* hlen);
+// D2H of the decoded fields the nonce chain and the fold read, and the nonce values
+// (copy stream; returns when they are in host memory).
+int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t* nonce);
+// The crypto run under per-header epoch nonces (etas[eta_idx[i]]), queued after the decode;
+// the host arrays are copied before return.
+int rp_run(praos_ctx* c, praos_batch* b, const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx);
+// Waits for the run and copies its bits and pool indices out (download stream).
+int rp_download_results(praos_ctx* c, praos_batch* b, uint16_t* bits, int32_t* pool_idx);
+// praos_validate_headers_nonces / praos_tpraos_validate_headers_nonces with the evolving nonce
+// after each header precomputed by the caller's nonce chain (used until the first invalid header).
+int rp_fold(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
+            const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei, praos_chain_state* st,
+            const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx, const praos_nonce* evolving_after,
+            bool tpraos, const praos_nonce* extra_entropy, uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
+            size_t* processed);

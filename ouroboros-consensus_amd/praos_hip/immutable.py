@@ -82,7 +82,8 @@ def _combine(a, b):
     return hashlib.blake2b(a + b, digest_size=32).digest()
 
 
-def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpraos=False, extra_entropy=None):
+def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpraos=False, extra_entropy=None,
+                           progress=None):
     """A linked chain over `epochs` epochs of `epoch_length` slots from slot 0 (Origin,
     GenesisHash, epoch 0 nonce = cfg["eta0"]).  Returns dict(arena, off, len, slots,
     header_hash, pools, params, nonces (per epoch), state (after the last
@@ -103,10 +104,18 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
             if tpraos:
                 eta = _combine(eta, extra_entropy)          # TICKN
         nonces.append(eta)
-        lead = ctx.leader_schedule(cfg["seed"], sig, p, eta, e * epoch_length, epoch_length, tpraos=tpraos)
-        idx = np.nonzero(lead >= 0)[0]
-        sl = (e * epoch_length + idx).astype(np.uint64)
-        pl = lead[idx].astype(np.uint32)
+        if cfg.get("round_robin"):
+            # f = 1 (every pool a leader in every slot, checkLeaderNatValue's f == 1 case):
+            # a block in every slot, forged by the pools in turn -- a dense chain of the C5
+            # shape (432k headers per 432k-slot epoch) without the 26e9-evaluation search
+            assert cfg["f"] == 1, "round_robin schedules are leader-valid only for f = 1"
+            sl = np.arange(e * epoch_length, (e + 1) * epoch_length, dtype=np.uint64)
+            pl = (sl % cfg["npools"]).astype(np.uint32)
+        else:
+            lead = ctx.leader_schedule(cfg["seed"], sig, p, eta, e * epoch_length, epoch_length, tpraos=tpraos)
+            idx = np.nonzero(lead >= 0)[0]
+            sl = (e * epoch_length + idx).astype(np.uint64)
+            pl = lead[idx].astype(np.uint32)
         n = len(sl)
         H, keys, _ = ctx.synthesize(n, cfg["npools"], p, eta, cfg["seed"], body_len=0, schedule=(sl, pl),
                                     block_no0=block_no, link=True, prev0=prev, tpraos=tpraos)
@@ -133,6 +142,8 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
         hh_all.append(H["header_hash"])
         prev = bytes(H["header_hash"][-1])
         block_no += n
+        if progress:
+            progress(e, n)
     # one stored-bytes arena over all epochs
     arenas, offs, lens, base = [], [], [], 0
     for H in parts:

@@ -30,16 +30,25 @@ def main():
     ap.add_argument("--chunk-slots", type=int, default=21_600)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch-sizes", default="16384,32768,65536,1048576")
+    ap.add_argument("--round-robin", action="store_true",
+                    help="f = 1 and a block in every slot, pools in turn (the C5 shape: 432k headers per "
+                         "432k-slot epoch, 3000 pools, without the leader-schedule search)")
+    ap.add_argument("--window", type=int, default=None, help="stability window in slots (default 4k/f, k = 2160)")
     args = ap.parse_args()
     import hashlib
     import praos_hip
     from praos_hip import immutable
     ctx = praos_hip.Context(0)
-    cfg = dict(npools=args.pools, stake_offset=10, f=Fraction(1, 20), slots_per_kes_period=129600, max_kes_evo=62,
-               eta0=hashlib.blake2b(b"replay-bench", digest_size=32).digest(), seed=b"RB" + b"\x5b" * 30)
-    window = 4 * 2160 * 20                    # 4k/f with k = 2160: the Babbage stability window
+    f = Fraction(1) if args.round_robin else Fraction(1, 20)
+    cfg = dict(npools=args.pools, stake_offset=10, f=f, slots_per_kes_period=129600, max_kes_evo=62,
+               eta0=hashlib.blake2b(b"replay-bench", digest_size=32).digest(), seed=b"RB" + b"\x5b" * 30,
+               round_robin=args.round_robin)
+    window = args.window or int(4 * 2160 / f)   # 4k/f with k = 2160: the Babbage stability window
     t0 = time.perf_counter()
-    data = immutable.make_multi_epoch_chain(ctx, cfg, args.epochs, args.epoch_length, window)
+    data = immutable.make_multi_epoch_chain(
+        ctx, cfg, args.epochs, args.epoch_length, window,
+        progress=lambda e, n: print(f"epoch {e}: {n} blocks signed and linked ({time.perf_counter() - t0:.0f}s)",
+                                    file=sys.stderr, flush=True))
     t_gen = time.perf_counter() - t0
     n = len(data["off"])
     env_limits = {"max_major_pv": 9, "lv_prot_major": 8, "max_header_size": 1100, "max_body_size": 90_112}
@@ -65,6 +74,7 @@ def main():
                     "value": round(n / (best["wall_ms"] * 1e-3), 1), "unit": "headers/s", "headers": n,
                     "epochs": args.epochs, "blocks_per_epoch": round(n / args.epochs), "chunks": nch,
                     "pools": args.pools, "wall_ms": round(best["wall_ms"], 2),
+                    "schedule": "round-robin, f = 1" if args.round_robin else "first-leader-wins, f = 1/20",
                     "stages_ms": {k: round(best[k], 2) for k in ("ms_io", "ms_device", "ms_nonce", "ms_fold")},
                     "batch_max": batch_max, "batches": best["batches"], "epoch_nonces": best["epochs"],
                     "generate_s": round(t_gen, 1), "reps": args.reps,
