@@ -347,24 +347,57 @@ __global__ void __launch_bounds__(NT) k_synth_headers(
   }
 }
 
-// Chain linking (one lane, sequential): prevHash of header i := headerHash of header i-1
+// Per KES leaf key, for the linker: the clamped scalar a, a fixed signing nonce r =
+// SHA-512(prefix) mod L (the RFC 8032 nonce of the empty message) and R = [r]B.  Any r gives
+// a valid Ed25519 signature (verification never sees how r was chosen), so the sequential
+// re-signing of a linked chain needs no scalar multiplication per block.
+__global__ void __launch_bounds__(NT) k_synth_link_keys(uint32_t nleaves, const ge_niels* __restrict__ gbtab,
+                                                        const uint32_t* __restrict__ leaf_seed,
+                                                        uint32_t* __restrict__ keys) {
+  __shared__ ge_niels sbtab[2 * BTAB_N];
+  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
+  const uint32_t li = blockIdx.x * NT + threadIdx.x;
+  if (li >= nleaves) return;
+  uint32_t seed[8], az[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) seed[k] = leaf_seed[8 * (size_t)li + k];
+  ed25519_expand(az, seed);
+  uint32_t S[9], d[16], r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) S[k] = az[8 + k];
+  S[8] = 0x80u;
+  sha512_regs<9, 32>(d, S);
+  sc_reduce512(r, d);
+  ge_p3 R;
+  ge_scalarmult_base(R, r, btab);
+  uint32_t rs[8];
+  ge_tobytes(rs, R.X, R.Y, R.Z);
+  uint32_t* o = keys + 24 * (size_t)li;
+#pragma unroll
+  for (int k = 0; k < 8; k++) { o[k] = az[k]; o[8 + k] = r[k]; o[16 + k] = rs[k]; }
+}
+
+// Chain linking (sequential): prevHash of header i := headerHash of header i-1
 // (HeaderValidation.hs:308-309 checks exactly that), so every KES signature has to be
 // redone in order -- the body, and with it the header hash, changes.  Header 0 gets
 // prev0, or GenesisHash (CBOR null, the body shrinks by 33 bytes) when prev0 is null.
 // headerHash = Blake2b-256 of the stored header [body, kesSig] (Praos/Header.hs:147-151).
-__global__ void __launch_bounds__(64) k_synth_link(size_t n, const ge_niels* gbtab, const uint8_t* __restrict__ prev0,
-                                                   const uint32_t* __restrict__ leaf_seed,
+// One wave: lane 0 signs and hashes from an LDS copy of the header that the wave builds
+// (byte loops over global memory in one lane cost ~1 ms per block); the leaf keys' a, r, R
+// come from k_synth_link_keys.
+__global__ void __launch_bounds__(64) k_synth_link(size_t n, const uint8_t* __restrict__ prev0,
+                                                   const uint32_t* __restrict__ lkeys,
                                                    const uint32_t* __restrict__ tree, const uint32_t* __restrict__ leaf_of,
                                                    uint8_t* __restrict__ body_bytes, const uint64_t* __restrict__ body_off,
                                                    uint32_t* __restrict__ body_len, uint8_t* __restrict__ kes_sig,
-                                                   uint8_t* __restrict__ hdr_scratch, uint8_t* __restrict__ header_hash,
-                                                   uint32_t stride) {
-  __shared__ ge_niels sbtab[2 * BTAB_N];
-  const ge_niels* btab = stage_btab<5>(gbtab, sbtab);
-  if (threadIdx.x != 0) return;
-  uint32_t prev[8];
+                                                   uint8_t* __restrict__ header_hash, uint32_t stride) {
+  __shared__ __attribute__((aligned(16))) uint8_t body_s[640];  // the signed body (8-aligned for SHA-512)
+  __shared__ __attribute__((aligned(16))) uint8_t hdr[1152];    // 0x82 | body | 59 01 c0 | kesSig 448 | pad
+  __shared__ uint32_t prev_s[8];
+  __shared__ uint32_t bl_s;
+  const unsigned lane = threadIdx.x;
   bool genesis = prev0 == nullptr;
-  if (!genesis) load_words(prev, prev0, 8);
+  if (lane == 0 && !genesis) load_words(prev_s, prev0, 8);
   auto ulen = [](uint32_t ib) -> uint32_t {
     const uint32_t ai = ib & 31u;
     return ai < 24 ? 1u : ai == 24 ? 2u : ai == 25 ? 3u : ai == 26 ? 5u : 9u;
@@ -372,43 +405,72 @@ __global__ void __launch_bounds__(64) k_synth_link(size_t n, const ge_niels* gbt
   for (size_t i = 0; i < n; i++) {
     uint8_t* b = body_bytes + body_off[i];
     uint32_t bl = body_len[i];
-    uint32_t q = 1;
-    q += ulen(b[q]);                              // blockNo
-    q += ulen(b[q]);                              // slotNo; b[q] = 0x58 (bytes(32)) or 0xf6 (null)
-    if (genesis) {
-      if (b[q] == 0x58) {                         // bytes(32) -> null: shift the tail left by 33
-        for (uint32_t k = q + 1; k + 33 < bl; k++) b[k] = b[k + 33];
-        b[q] = 0xf6;
-        bl -= 33;
-        for (uint32_t k = bl; k < ((bl + 7) & ~7u) + 8 && k < stride; k++) b[k] = 0;
-        body_len[i] = bl;
+    for (uint32_t k = lane; k < 640; k += 64) body_s[k] = k < bl && k < stride ? b[k] : 0;
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t q = 1;
+      q += ulen(body_s[q]);                       // blockNo
+      q += ulen(body_s[q]);                       // slotNo; body_s[q] = 0x58 (bytes(32)) or 0xf6 (null)
+      bool ok = true;
+      if (genesis) {
+        if (body_s[q] == 0x58) {                  // bytes(32) -> null: shift the tail left by 33
+          for (uint32_t k = q + 1; k + 33 < bl; k++) body_s[k] = body_s[k + 33];
+          body_s[q] = 0xf6;
+          bl -= 33;
+          for (uint32_t k = bl; k < 640; k++) body_s[k] = 0;
+          body_len[i] = bl;
+        }
+      } else if (body_s[q] != 0x58) {
+        ok = false;                               // not produced by k_synth_headers
+      } else {
+        for (int k = 0; k < 32; k++) body_s[q + 2 + k] = (uint8_t)(prev_s[k / 4] >> (8 * (k % 4)));
       }
-    } else {
-      if (b[q] != 0x58) return;                   // not produced by k_synth_headers
-      for (int k = 0; k < 32; k++) b[q + 2 + k] = (uint8_t)(prev[k / 4] >> (8 * (k % 4)));
+      bl_s = ok ? bl : 0xffffffffu;
+      if (ok) {
+        // KES leaf signature over the new body with the leaf's fixed nonce; the Merkle path
+        // of the signature is unchanged
+        const uint32_t li = leaf_of[i];
+        const uint32_t* T = tree + (size_t)(li / 64u) * 128 * 8;
+        const uint32_t* lk = lkeys + 24 * (size_t)li;
+        uint32_t pre[16], d[16], h[8], a[8], r[8], S[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          pre[k] = lk[16 + k];                    // R
+          pre[8 + k] = T[(64 + li % 64u) * 8 + k];  // A (the leaf's public key)
+          a[k] = lk[k];
+          r[k] = lk[8 + k];
+        }
+        sha512_stream(d, pre, 64, body_s, bl);
+        sc_reduce512(h, d);
+        sc_muladd(S, h, a, r);
+        uint32_t sig[16];
+#pragma unroll
+        for (int k = 0; k < 8; k++) { sig[k] = pre[k]; sig[8 + k] = S[k]; }
+        store_words(kes_sig + 448 * i, sig, 16);
+        hdr[0] = 0x82;
+        hdr[1 + bl] = 0x59; hdr[2 + bl] = 0x01; hdr[3 + bl] = 0xc0;
+        for (int k = 0; k < 64; k++) hdr[4 + bl + k] = (uint8_t)(sig[k / 4] >> (8 * (k % 4)));
+      }
     }
-    // KES leaf signature over the new body (the Merkle path of the signature is unchanged)
-    const uint32_t li = leaf_of[i];
-    const uint32_t* T = tree + (size_t)(li / 64u) * 128 * 8;
-    uint32_t seed[8], lpk[8], az[16], sig[16];
+    __syncthreads();
+    if (bl_s == 0xffffffffu) return;
+    bl = bl_s;
+    // header bytes in LDS: body, the Merkle path (unchanged) after the new leaf signature,
+    // zero pad; the new body back to global memory
+    for (uint32_t k = lane; k < bl; k += 64) hdr[1 + k] = body_s[k];
+    for (uint32_t k = 64 + lane; k < 448; k += 64) hdr[4 + bl + k] = kes_sig[448 * i + k];
+    for (uint32_t k = 4 + bl + 448 + lane; k < 1152; k += 64) hdr[k] = 0;
+    for (uint32_t k = lane; k < ((bl + 7) & ~7u) + 8 && k < stride; k += 64) b[k] = body_s[k];
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t hh[8];
+      b2b256_range(hh, hdr, 0, 4 + bl + 448);
+      if (header_hash) store_words(header_hash + 32 * i, hh, 8);
 #pragma unroll
-    for (int k = 0; k < 8; k++) { seed[k] = leaf_seed[8 * (size_t)li + k]; lpk[k] = T[(64 + li % 64u) * 8 + k]; }
-    ed25519_expand(az, seed);
-    ed25519_sign_core(sig, az, lpk, b, bl, btab);
-    uint8_t* ks = kes_sig + 448 * i;
-    store_words(ks, sig, 16);
-    // header bytes [body, kesSig] -> Blake2b-256
-    uint8_t* h = hdr_scratch;
-    h[0] = 0x82;
-    for (uint32_t k = 0; k < bl; k++) h[1 + k] = b[k];
-    h[1 + bl] = 0x59; h[2 + bl] = 0x01; h[3 + bl] = 0xc0;
-    for (uint32_t k = 0; k < 448; k++) h[4 + bl + k] = ks[k];
-    uint32_t hh[8];
-    b2b256_range(hh, h, 0, 4 + bl + 448);
-    if (header_hash) store_words(header_hash + 32 * i, hh, 8);
-#pragma unroll
-    for (int k = 0; k < 8; k++) prev[k] = hh[k];
+      for (int k = 0; k < 8; k++) prev_s[k] = hh[k];
+    }
     genesis = false;
+    __syncthreads();
   }
 }
 
@@ -534,12 +596,14 @@ void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
                      ocert_c0, ocert_sig, kes_sig, body_off, body_len, body_bytes, tpraos, l_out, l_proof,
                      body_hash_in, sched_slot, sched_pool, block_no0, leaf_of);
 }
-void launch_synth_link(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
-                       const uint32_t* leaf_seed, const uint32_t* tree, const uint32_t* leaf_of, uint8_t* body_bytes,
-                       const uint64_t* body_off, uint32_t* body_len, uint8_t* kes_sig, uint8_t* hdr_scratch,
-                       uint8_t* header_hash, uint32_t stride) {
-  hipLaunchKernelGGL(k_synth_link, grid, block, 0, stream, n, gbtab, prev0, leaf_seed, tree, leaf_of, body_bytes,
-                     body_off, body_len, kes_sig, hdr_scratch, header_hash, stride);
+void launch_synth_link(hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
+                       const uint32_t* leaf_seed, uint32_t nleaves, uint32_t* lkeys, const uint32_t* tree,
+                       const uint32_t* leaf_of, uint8_t* body_bytes, const uint64_t* body_off, uint32_t* body_len,
+                       uint8_t* kes_sig, uint8_t* header_hash, uint32_t stride) {
+  hipLaunchKernelGGL(k_synth_link_keys, dim3((nleaves + NT - 1) / NT), dim3(NT), 0, stream, nleaves, gbtab, leaf_seed,
+                     lkeys);
+  hipLaunchKernelGGL(k_synth_link, dim3(1), dim3(64), 0, stream, n, prev0, lkeys, tree, leaf_of, body_bytes, body_off,
+                     body_len, kes_sig, header_hash, stride);
 }
 void launch_synth_vrf_scalar(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const uint32_t* vrf_seed,
                              uint32_t* vrf_x) {

@@ -80,10 +80,10 @@ void launch_synth_pools(dim3 grid, dim3 block, hipStream_t stream, uint32_t npoo
 void launch_synth_kes_leaves(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const ge_niels* gbtab, const uint32_t* kes_seed, uint32_t* leaf_seed, uint32_t* tree);
 void launch_synth_kes_tree(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, uint32_t* tree);
 void launch_synth_headers(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, uint32_t npools, uint32_t nkes, uint64_t first_slot, uint64_t slot_stride, uint64_t slots_per_kes_period, uint32_t blen, uint64_t salt, const uint32_t* eta0, int eta0_neutral, const uint32_t* cold_seed, const uint32_t* cold_pk, const uint32_t* vrf_seed, const uint32_t* vrf_pk, const uint32_t* leaf_seed, const uint32_t* tree, uint8_t* msg_scratch, uint64_t* slot, uint8_t* cold_vk, uint8_t* vrf_vk, uint8_t* vrf_out, uint8_t* vrf_proof, uint8_t* hot_vk, uint64_t* ocert_n, uint64_t* ocert_c0, uint8_t* ocert_sig, uint8_t* kes_sig, uint64_t* body_off, uint32_t* body_len, uint8_t* body_bytes, int tpraos, uint8_t* l_out, uint8_t* l_proof, const uint8_t* body_hash_in, const uint64_t* sched_slot, const uint32_t* sched_pool, uint64_t block_no0, uint32_t* leaf_of);
-void launch_synth_link(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
-                       const uint32_t* leaf_seed, const uint32_t* tree, const uint32_t* leaf_of, uint8_t* body_bytes,
-                       const uint64_t* body_off, uint32_t* body_len, uint8_t* kes_sig, uint8_t* hdr_scratch,
-                       uint8_t* header_hash, uint32_t stride);
+void launch_synth_link(hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* prev0,
+                       const uint32_t* leaf_seed, uint32_t nleaves, uint32_t* lkeys, const uint32_t* tree,
+                       const uint32_t* leaf_of, uint8_t* body_bytes, const uint64_t* body_off, uint32_t* body_len,
+                       uint8_t* kes_sig, uint8_t* header_hash, uint32_t stride);
 void launch_synth_vrf_scalar(dim3 grid, dim3 block, hipStream_t stream, uint32_t npools, const uint32_t* vrf_seed,
                              uint32_t* vrf_x);
 void launch_synth_leader_search(dim3 grid, dim3 block, hipStream_t stream, uint64_t first_slot, uint64_t nslots,

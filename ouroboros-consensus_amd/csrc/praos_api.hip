@@ -2397,7 +2397,7 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
   if (link && sp->body_len != 0) { c->err = "link_prev needs CBOR bodies (body_len 0)"; return PRAOS_E_ARG; }
   auto dleaf = s.zeros<uint32_t>(4 * n);
   auto dprev0 = link && sp->prev0 ? s.up(sp->prev0, 32) : nullptr;
-  auto dhscr = s.zeros<uint8_t>(link ? 1100 : 16);     // [body <= 598 B, kesSig 448 B] + heads
+  auto dlkeys = s.zeros<uint32_t>(link ? 4 * 24 * (size_t)nk * 64 : 16);   // per KES leaf: a, r, R (k_synth_link_keys)
   auto dhh = s.zeros<uint8_t>(link ? 32 * n : 16);
   if (!s.ok) { c->err = "alloc"; return PRAOS_E_OOM; }
   uint64_t salt = 0;
@@ -2414,8 +2414,8 @@ static int synthesize_impl(praos_ctx* c, const praos_synth_params* sp, const pra
                        dvrfvk, dvout, dproof, dhot, dn, dc0, dosig, dksig, doff, dlen, dbody, tpraos, dlout, dlproof,
                        sp->body_len == 0 ? dbh : nullptr, dss, dsp, sp->block_no0, dleaf);
     if (link)
-      launch_synth_link(dim3(1), dim3(64), c->stream, n, c->btab, dprev0, leaf_seed, tree, dleaf, dbody, doff, dlen,
-                        dksig, dhscr, dhh, (uint32_t)bstride);
+      launch_synth_link(c->stream, n, c->btab, dprev0, leaf_seed, (uint32_t)(nk * 64), dlkeys, tree, dleaf, dbody, doff,
+                        dlen, dksig, dhh, (uint32_t)bstride);
     launch_synth_corrupt(dim3(nblocks(n, 256)), dim3(256), c->stream, n, sp->corrupt_per_10000,
                        salt, dosig, dksig, dproof, dvout, dbody, doff, dlen, dcor, tpraos ? dlproof : nullptr,
                        sp->body_len == 0 ? (tpraos ? 2 : 1) : 0, sp->corrupt_fields ? sp->corrupt_fields : 0x1fu, dcold, dhot, dn,

@@ -45,10 +45,20 @@ def main():
                round_robin=args.round_robin)
     window = args.window or int(4 * 2160 / f)   # 4k/f with k = 2160: the Babbage stability window
     t0 = time.perf_counter()
+    # heartbeat while the chain is generated (the linked re-signing is sequential: minutes
+    # for 432k-block epochs)
+    import threading
+    gen_done = threading.Event()
+
+    def beat():
+        while not gen_done.wait(30):
+            print(f"generating... {time.perf_counter() - t0:.0f}s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     data = immutable.make_multi_epoch_chain(
         ctx, cfg, args.epochs, args.epoch_length, window,
         progress=lambda e, n: print(f"epoch {e}: {n} blocks signed and linked ({time.perf_counter() - t0:.0f}s)",
                                     file=sys.stderr, flush=True))
+    gen_done.set()
     t_gen = time.perf_counter() - t0
     n = len(data["off"])
     env_limits = {"max_major_pv": 9, "lv_prot_major": 8, "max_header_size": 1100, "max_body_size": 90_112}
