@@ -471,9 +471,12 @@ def main():
             from praos_hip.chunk import pack_chunk
             arena, off_, ln_ = pack_chunk(H)
             ob = ctx.verify_header_bytes(arena, off_, ln_)            # warm (chunk batches allocated)
-            te = time.perf_counter()
-            ob = ctx.verify_header_bytes(arena, off_, ln_)
-            te = time.perf_counter() - te
+            te = []
+            for _ in range(3):                                         # best of 3 calls
+                t_ = time.perf_counter()
+                ob = ctx.verify_header_bytes(arena, off_, ln_)
+                te.append(time.perf_counter() - t_)
+            te = min(te)
             # a corrupted body byte (corruption kind 5) makes the stored CBOR itself
             # malformed or different, so the byte path rejects that header at decode
             # (PRAOS_BIT_DECODE) where the SoA path rejects it at the KES check: those
@@ -484,10 +487,10 @@ def main():
                    "accept_equal_all": bool(((ob["bits"] == 0) == (out["bits"] == 0)).all()),
                    "body_corrupted_excluded": int((~cmp).sum()),
                    "input_bytes": int(len(arena)), "h2d_GBps_equiv": round(len(arena) / te / 1e9, 1),
-                   "path": "praos_verify_header_bytes: stored header bytes (pageable host arena) -> chunked "
-                           "(4 x 108k headers) H2D through pinned staging on a copy stream overlapping the "
-                           "device decode + crypto of the previous chunk -> D2H of each chunk's results while "
-                           "later chunks compute"}
+                   "path": "praos_verify_header_bytes: stored header bytes (pageable host arena) -> H2D in "
+                           "6 chunks through pinned staging on a copy stream, each landed chunk decoded and its "
+                           "VRF stage V run while later chunks upload -> the rest of the batch once -> VRF "
+                           "outputs D2H while the KES checks finish (best of 3 calls)"}
         # the host-SoA entry point (every decoded field from the host, 1,236 B per header)
         oe = ctx.verify_headers(H)
         te = time.perf_counter()

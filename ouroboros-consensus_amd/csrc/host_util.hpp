@@ -29,12 +29,13 @@ inline uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
   PH_G(v0, v5, v10, v15, M[s8], M[s9]) PH_G(v1, v6, v11, v12, M[s10], M[s11])      \
   PH_G(v2, v7, v8, v13, M[s12], M[s13]) PH_G(v3, v4, v9, v14, M[s14], M[s15])
 
-inline void blake2b_compress(uint64_t h[8], const uint8_t blk[128], uint64_t t, bool last) {
+// compression over message words M (inlined into its callers: where M's words are known
+// constants -- the zero half of a 64-byte message -- the compiler drops their additions)
+__attribute__((always_inline)) inline void blake2b_compress_words(uint64_t h[8], const uint64_t M[16], uint64_t t,
+                                                                  bool last) {
   static constexpr uint64_t IV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                                      0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
                                      0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
-  uint64_t M[16];
-  std::memcpy(M, blk, 128);                          // little-endian host
   uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3], v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
   uint64_t v8 = IV[0], v9 = IV[1], v10 = IV[2], v11 = IV[3], v12 = IV[4] ^ t, v13 = IV[5];
   uint64_t v14 = last ? ~IV[6] : IV[6], v15 = IV[7];
@@ -52,6 +53,12 @@ inline void blake2b_compress(uint64_t h[8], const uint8_t blk[128], uint64_t t, 
   PH_ROUND(14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3)
   h[0] ^= v0 ^ v8; h[1] ^= v1 ^ v9; h[2] ^= v2 ^ v10; h[3] ^= v3 ^ v11;
   h[4] ^= v4 ^ v12; h[5] ^= v5 ^ v13; h[6] ^= v6 ^ v14; h[7] ^= v7 ^ v15;
+}
+
+inline void blake2b_compress(uint64_t h[8], const uint8_t blk[128], uint64_t t, bool last) {
+  uint64_t M[16];
+  std::memcpy(M, blk, 128);                          // little-endian host
+  blake2b_compress_words(h, M, t, last);
 }
 #undef PH_ROUND
 #undef PH_G
@@ -134,15 +141,15 @@ inline bool leader_x_raw(uint8_t x_le[16], const uint8_t sigma_fp[16], const uin
 inline praos_nonce nonce_combine(const praos_nonce& a, const praos_nonce& b) {
   if (a.neutral) return b;
   if (b.neutral) return a;
-  // Blake2b-256 of the 64-byte a || b: one compression, the block built in place
-  alignas(16) uint8_t blk[128];
-  std::memcpy(blk, a.hash, 32);
-  std::memcpy(blk + 32, b.hash, 32);
-  std::memset(blk + 64, 0, 64);
+  // Blake2b-256 of the 64-byte a || b: one compression whose second message half is the
+  // constant zero padding (the fold's and the replay's nonce chains are one of these per header)
+  uint64_t M[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  std::memcpy(M, a.hash, 32);
+  std::memcpy(M + 4, b.hash, 32);
   uint64_t h[8] = {0x6a09e667f3bcc908ULL ^ 0x01010020ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
                    0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL,
                    0x5be0cd19137e2179ULL};
-  blake2b_compress(h, blk, 64, true);
+  blake2b_compress_words(h, M, 64, true);
   praos_nonce r;
   std::memcpy(r.hash, h, 32);                        // little-endian host
   r.neutral = 0;

@@ -114,6 +114,7 @@ struct praos_ctx {
   int pipeline = 0;                                    // PRAOS_OPT_PIPELINE (0 = auto)
   hipStream_t cstream = nullptr;
   hipStream_t dstream = nullptr;                       // replay: result downloads (rp_download_results)
+  praos_batch* rp_keep[RP_SLOTS] = {};                 // replay batches kept between calls
   hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
   praos_batch* pipe[PIPE_MAX] = {};
   size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
@@ -503,6 +504,7 @@ void praos_close(praos_ctx* c) {
   if (c->u_ev) (void)hipEventDestroy(c->u_ev);
   if (c->v1_ev) (void)hipEventDestroy(c->v1_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+  for (int k = 0; k < RP_SLOTS; k++) rp_batch_destroy(c, c->rp_keep[k]);
   for (int k = 0; k < PIPE_MAX; k++) {
     if (c->pipe[k]) {
       for (void* p : c->pipe[k]->owned) (void)hipFree(p);
@@ -1417,6 +1419,21 @@ void rp_batch_destroy(praos_ctx* c, praos_batch* b) {
 }
 
 bool rp_batch_fits(const praos_batch* b, size_t n, size_t bytes) { return b && n <= b->cap_n && bytes <= b->cap_bytes; }
+
+praos_batch* rp_batch_take(praos_ctx* c, int k, size_t n, size_t bytes, bool tpraos) {
+  if (!c || k < 0 || k >= RP_SLOTS) return nullptr;
+  praos_batch* b = c->rp_keep[k];
+  c->rp_keep[k] = nullptr;
+  if (b && rp_batch_fits(b, n, bytes) && b->tp_only == tpraos) return b;
+  rp_batch_destroy(c, b);
+  return rp_batch_alloc(c, n + n / 8 + 64, bytes + bytes / 8 + 4096, tpraos);
+}
+
+void rp_batch_keep(praos_ctx* c, int k, praos_batch* b) {
+  if (!c || k < 0 || k >= RP_SLOTS) { rp_batch_destroy(c, b); return; }
+  if (c->rp_keep[k] && c->rp_keep[k] != b) rp_batch_destroy(c, c->rp_keep[k]);
+  c->rp_keep[k] = b;
+}
 
 // H2D of the concatenation of spans through the two pinned staging buffers: the pool's
 // threads gather each 16 MB piece (many small spans or a few large ones) while the DMA

@@ -152,7 +152,7 @@ struct ChunkReader {
   void pop() { entry++; }
 };
 
-constexpr int SLOTS = 3;                      // batches in flight
+constexpr int SLOTS = RP_SLOTS;               // batches in flight (kept by the context between calls)
 constexpr size_t SPAN_GAP = 4096;             // headers this close share one uploaded span
 
 }  // namespace
@@ -212,7 +212,7 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
   }
   struct Slot {
     praos_batch* b = nullptr;
-    int state = 0;                            // 0 free, 1 decoded, 2 crypto queued
+    int state = 0;                            // 0 free, 1 decoded, 2 nonces known, 3 crypto queued
     size_t n = 0;
     uint64_t index0 = 0;
     std::vector<praos_span> spans;
@@ -268,6 +268,14 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
       // epoch bounds cached: a division per epoch, not per header (the loop is the replay's
       // one sequential piece of work; one Blake2b compression per header is its floor)
       uint64_t ep_lo = 1, ep_hi = 0, ep_no = 0, ep_cut = 0;     // [ep_lo, ep_hi): epoch ep_no
+      size_t lab_i = SIZE_MAX, cand_i = SIZE_MAX;   // headers whose prev hash / evolving nonce are the
+                                                    // current labNonce / candidate (copied when needed)
+      bool fresh = true;
+      auto set_lab = [&](size_t j) {
+        sp.lab.neutral = C.gen[j] ? 1 : 0;
+        std::memset(sp.lab.hash, 0, 32);
+        if (!C.gen[j]) std::memcpy(sp.lab.hash, C.prev.data() + 32 * j, 32);
+      };
       for (size_t i = 0; i < n; i++) {
         const uint64_t slot_i = C.slot[i];
         if (slot_i < ep_lo || slot_i >= ep_hi) {
@@ -279,34 +287,57 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
         }
         const uint64_t e_new = ep_no;
         if (!sp.dead && e_new > (sp.origin ? 0 : sp_epoch)) {
+          if (lab_i != SIZE_MAX) set_lab(lab_i);
+          lab_i = SIZE_MAX;
+          if (cand_i != SIZE_MAX) sp.candidate = C.evol[cand_i];
+          cand_i = SIZE_MAX;
           sp.epoch_nonce = praos_host::nonce_combine(sp.candidate, sp.leb);
           if (tpraos && extra_entropy) sp.epoch_nonce = praos_host::nonce_combine(sp.epoch_nonce, *extra_entropy);
           sp.leb = sp.lab;
+          fresh = true;
         }
-        if (C.etas.empty() || !praos_host::nonce_eq(C.etas.back(), sp.epoch_nonce)) C.etas.push_back(sp.epoch_nonce);
+        if (fresh) {                              // the epoch nonce changes only at a tick
+          if (C.etas.empty() || !praos_host::nonce_eq(C.etas.back(), sp.epoch_nonce)) C.etas.push_back(sp.epoch_nonce);
+          fresh = false;
+        }
         C.eidx[i] = (uint8_t)std::min<size_t>(C.etas.size() - 1, 255);
         if (sp.dead || (C.dstat[i] & PRAOS_DEC_FAILED)) { sp.dead = true; C.evol[i] = sp.evolving; continue; }
         sp.origin = 0;
         sp.last = slot_i;
         sp_epoch = e_new;
-        sp.lab.neutral = C.gen[i] ? 1 : 0;
-        std::memset(sp.lab.hash, 0, 32);
-        if (!C.gen[i]) std::memcpy(sp.lab.hash, C.prev.data() + 32 * i, 32);
+        lab_i = i;                                // labNonce: the prev hash of this header (copied when needed)
         praos_nonce eta;
         std::memcpy(eta.hash, C.nonce.data() + 32 * i, 32);
         eta.neutral = 0;
         sp.evolving = praos_host::nonce_combine(sp.evolving, eta);
         C.evol[i] = sp.evolving;
-        if (slot_i < ep_cut) sp.candidate = sp.evolving;        // slot + window < first slot of the next epoch
+        if (slot_i < ep_cut) cand_i = i;          // slot + window < first slot of the next epoch: candidate := evolving
       }
+      if (lab_i != SIZE_MAX) set_lab(lab_i);
+      if (cand_i != SIZE_MAX) sp.candidate = C.evol[cand_i];
       if (C.etas.size() > 256) { praos_set_error_(ctx, "replay: > 256 epochs in a batch"); fail(PRAOS_E_STATE); return; }
       for (const praos_nonce& e : C.etas)
         if (!have_last || !praos_host::nonce_eq(e, last_eta)) { epochs_seen++; last_eta = e; have_last = true; }
       t_nonce += ms_since(t0);
+      std::lock_guard<std::mutex> g(mu);
+      C.state = 2;
+      cv.notify_all();
+    }
+  });
+  // ---- launcher: queues each batch's crypto (~30 launches: 1-2 ms of host time per batch,
+  // kept off the nonce chain's thread)
+  std::thread launcher([&] {
+    for (uint64_t k = 0;; k++) {
+      Slot& C = S[k % SLOTS];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 2; });
+        if (stop || k >= nbatches) return;
+      }
       const int rc = rp_run(ctx, C.b, C.etas.data(), (uint32_t)C.etas.size(), C.eidx.data());
       if (rc != PRAOS_OK) { fail(rc); return; }
       std::lock_guard<std::mutex> g(mu);
-      C.state = 2;
+      C.state = 3;
       batches++;
       cv.notify_all();
     }
@@ -319,7 +350,7 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
       Slot& C = S[k % SLOTS];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 2; });
+        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 3; });
         if (stop || k >= nbatches) return;
       }
       auto t0 = std::chrono::steady_clock::now();
@@ -393,7 +424,10 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     uint32_t nep = 0;
     size_t arena = 0;
     const Chunk* span_chunk = nullptr;
-    while (C.off.size() < batch_max && rd.peek(&p, &l, &s)) {
+    // the first batch is a quarter of the others: the nonce chain (the replay's sequential
+    // part) starts as soon as possible
+    const size_t cap = k == 0 ? std::max<size_t>(1, batch_max / 4) : batch_max;
+    while (C.off.size() < cap && rd.peek(&p, &l, &s)) {
       const uint64_t e = epoch_of(s);
       if (C.off.empty() || e != e_prev) {
         if (nep == 256) break;
@@ -424,8 +458,8 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     C.index0 = next_index;
     next_index += n;
     if (!rp_batch_fits(C.b, n, arena)) {
-      rp_batch_destroy(ctx, C.b);
-      C.b = rp_batch_alloc(ctx, n + n / 8 + 64, arena + arena / 8 + 4096, tpraos);
+      if (C.b) rp_batch_destroy(ctx, C.b);
+      C.b = rp_batch_take(ctx, (int)(k % SLOTS), n, arena, tpraos);
       if (!C.b) { fail(PRAOS_E_OOM); break; }
     }
     if (C.pin_cap < n) {
@@ -463,9 +497,11 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     cv.notify_all();
   }
   chain.join();
+  launcher.join();
   folder.join();
-  for (Slot& C : S) {
-    rp_batch_destroy(ctx, C.b);
+  for (int k = 0; k < SLOTS; k++) {
+    Slot& C = S[k];
+    if (C.b) rp_batch_keep(ctx, k, C.b);
     if (C.bits) (void)hipHostFree(C.bits);
     if (C.pidx) (void)hipHostFree(C.pidx);
   }

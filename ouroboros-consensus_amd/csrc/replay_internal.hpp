@@ -15,6 +15,12 @@ struct praos_span {           // a run of stored bytes in host memory (e.g. an m
 praos_batch* rp_batch_alloc(praos_ctx* c, size_t n_cap, size_t bytes_cap, bool tpraos);
 void rp_batch_destroy(praos_ctx* c, praos_batch* b);
 bool rp_batch_fits(const praos_batch* b, size_t n, size_t bytes);
+// The context keeps the replay's batches between calls (RP_SLOTS of them, freed by praos_close):
+// rp_batch_take returns slot k's batch when it fits n headers over `bytes` (else a new one),
+// rp_batch_keep hands it back.
+constexpr int RP_SLOTS = 3;
+praos_batch* rp_batch_take(praos_ctx* c, int k, size_t n, size_t bytes, bool tpraos);
+void rp_batch_keep(praos_ctx* c, int k, praos_batch* b);
 // Copy stream: the spans' concatenation (the arena) and the per-header (offset, length) go
 // H2D through the pinned staging buffers, then decode and the nonce value of each header's
 // certified VRF output (k_vrf_nonce).  Returns once the host side is queued.
