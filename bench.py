@@ -44,7 +44,7 @@ sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 # kernel schedules (tools/workmodel.py; DESIGN.md sec. 4 "Work model").
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  # noqa: E402
-                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES, W_VRF_V)
+                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES, W_VRF_V, W_VRF_TP, W_TP_HEADER)
 # gfx950 VALU peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
@@ -80,6 +80,9 @@ CONFIGS = {
     "c4": dict(items=1_000_000, pools=3000, kernels=2, nkes=0, metric="Sum6KES verifications/sec",
                workload="configs[3]: 1M Sum6KES verifies (depth-6 Blake2b-256 Merkle path + Ed25519 leaf), "
                         "397-byte messages, 1% corrupted"),
+    "tp": dict(items=432_000, pools=3000, kernels=7, metric="TPraos headers validated/sec (2 VRF+KES+OCert+leader)",
+               workload="TPraos (Shelley..Alonzo) headers from stored bytes: 432k BHeaders decoded on the device, "
+                        "3000 pools forging in turn (f = 1), single eta0, 1% corrupted"),
     "c5": dict(items=432_000, kernels=7, metric="Praos headers validated/sec (VRF+KES+OCert+leader)",
                workload="configs[4]: mainnet-shaped epoch replay, the first 432k blocks of a first-leader-wins "
                         "Praos chain per GPU, 3000-pool stake distribution, single eta0, 1% corrupted"),
@@ -307,6 +310,22 @@ def make_input(ctx, args, cfg, rank, world=1):
                                                        corrupt_per_10000=args.corrupt_per_10000)
         return (H, pool_list, corrupted, p, ccfg["eta0"], fixed.active_slot_log(ccfg["f"]),
                 ccfg["slots_per_kes_period"], ccfg["max_kes_evo"])
+    if args.config == "tp":
+        # TPraos headers (two VRF certificates, the 2^512 leader bound): f = 1 and the pools in
+        # turn, so every header is leader-valid without a schedule search (checkLeaderNatValue's
+        # f = 1 case); stored as BHeader bytes and decoded on the device in every run
+        from fractions import Fraction
+        n = args.items or cfg["items"]
+        ccfg = dict(npools=cfg["pools"], stake_offset=10, f=Fraction(1), slots_per_kes_period=129600,
+                    max_kes_evo=62, eta0=hashlib.blake2b(b"bench-tpraos-nonce", digest_size=32).digest())
+        p = chains.params(ccfg)
+        sl = np.arange(rank * n, (rank + 1) * n, dtype=np.uint64)
+        pl = (sl % cfg["pools"]).astype(np.uint32)
+        H, keys, corrupted = ctx.synthesize(n, cfg["pools"], p, ccfg["eta0"], b"TP" + b"\x5c" * 26 + rank.to_bytes(4, "little"),
+                                            body_len=0, schedule=(sl, pl), tpraos=True,
+                                            corrupt_per_10000=args.corrupt_per_10000)
+        pool_list = [(h, v, s_) for (h, v), s_ in zip(keys, chains.stake(cfg["pools"], 10))]
+        return H, pool_list, corrupted, p, ccfg["eta0"], 0, 129600, 62
     # single-primitive configs: evenly spaced slots, pools by hash (not a leader-valid chain)
     n = args.items or cfg["items"]
     npools = cfg["pools"] or n
@@ -378,7 +397,7 @@ def main():
     ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
     # the dedup belongs to the header pipeline (c1/c5: a chain repeats each pool's OCert);
     # the single-primitive configs measure every signature on its own
-    if cfg["kernels"] != 7:
+    if cfg["kernels"] != 7 or args.config == "tp":
         args.dedup = 0
     ctx.set_option(abi.OPT_DEDUP, args.dedup)
     ctx.set_option(abi.OPT_PIPELINE, args.pipeline)
@@ -386,7 +405,12 @@ def main():
     H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank, world)
     n = len(H["slot"])
     ctx.set_epoch(eta0, pool_list, p)
-    b = ctx.upload(H)
+    if args.config == "tp":
+        from praos_hip.chunk import pack_chunk
+        tp_arena, tp_off, tp_len = pack_chunk(H, era_tag=5)
+        b = ctx.upload_tpraos_bytes(tp_arena, tp_off, tp_len)
+    else:
+        b = ctx.upload(H)
     log(f"[rank {rank}] {args.config}: synthesised + uploaded {n} items in {time.perf_counter() - t0:.1f}s")
 
     for _ in range(args.warmup):
@@ -438,7 +462,7 @@ def main():
         ctx.set_option(abi.OPT_DEDUP, args.dedup)
         ctx.run(b)
         ctx.sync()
-    out = ctx.download(b, n)
+    out = ctx.download_tpraos(b, n) if args.config == "tp" else ctx.download(b, n)
     ctx.free(b)
     # one-GPU proxy of strong scaling: the rate of a 1/k shard of this batch (rank 0's
     # contiguous slot range at N = k), timed like the headline after one warm-up pass
@@ -462,7 +486,7 @@ def main():
     # end to end through the blocking entry point: host SoA in, H2D, all kernels,
     # D2H of bits/beta/leader/nonce (never the headline value)
     e2e = None
-    if not args.no_e2e and rank == 0:
+    if not args.no_e2e and rank == 0 and args.config != "tp":
         e2e = {}
         if args.config in ("c1", "c5"):
             # stored header bytes (what an ImmutableDB chunk holds, ~860 B per header) ->
@@ -560,6 +584,13 @@ def main():
         # every header is the largest single kernel of the step; price it alone, on the
         # HIP events around its own launch (serial run, no other kernel on the GPU)
         dom_kernel, dom_ms, dom_work, wk = "k_vrf_v", float(kser[6]), n * W_VRF_V, W_VRF_V
+    if args.config == "tp":
+        # the TPraos batch runs decode, k_ocert, k_kes, k_vrf_tp (two uncached certificates per
+        # lane) and k_leader; priced as one pipeline over the step
+        w_pipe = W_TP_HEADER
+        pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
+        dom_kernel, dom_ms, dom_work, wk = "tpraos pipeline (k_ocert | k_kes | k_vrf_tp, k_leader)", float(kms[4]), \
+            n * W_TP_HEADER, W_TP_HEADER
     dom_achieved = dom_work / (dom_ms * 1e-3)
     tk, traffic_src = load_traffic(dom_kernel, cfg["workload"])
     traffic = tk.get("bytes_per_launch") if tk else None
@@ -616,7 +647,7 @@ def main():
         line["strong_proxy"] = dict(proxy, note="one GPU validating only the first 1/k of the batch (rank 0's "
                                                 "shard of a strong-scaling run at N = k); per_gpu_vs_full = its "
                                                 "rate / this line's value")
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and args.config != "tp":   # (the CPU twin has no TPraos path)
         usable, _, _ = host_cores()
         threads = max(1, min(args.cpu_workers, usable))
         kind, per_item, mask = {7: ("header", 2.5e-4, 0x1F1F), 1: ("ocert", 5e-5, 0x0004),

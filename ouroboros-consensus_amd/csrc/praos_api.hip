@@ -12,7 +12,7 @@ static constexpr size_t BTAB_N = 128;              // entries per fixed-base tab
 static constexpr size_t BCOMB_TABLES = 32;         // fixed-base comb: 256^j B, j < 32 (scalarmult.hpp BCOMB_T)
 static constexpr size_t C16_TABLES = 16, C16_ENTRIES = 32768;   // radix-2^16 comb (scalarmult.hpp C16_T, C16_N)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
-static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
+static constexpr size_t LT_ED_N = 8, LT_ED_B = LT_ED_N * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
 static constexpr size_t VRF_MID_BYTES = 28 * 16;    // per-header records of the staged VRF (praos_core.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
@@ -115,7 +115,7 @@ struct praos_ctx {
   hipStream_t cstream = nullptr;
   hipStream_t dstream = nullptr;                       // replay: result downloads (rp_download_results)
   praos_batch* rp_keep[RP_SLOTS] = {};                 // replay batches kept between calls
-  hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
+  hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {}, kes_ev[PIPE_MAX] = {};
   praos_batch* pipe[PIPE_MAX] = {};
   size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
@@ -276,6 +276,7 @@ struct praos_batch {
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
   ge_cached* tab_vrfu = nullptr;   // 8-entry lane tables of stage U on uncached VRF keys
   bool v_done = false;             // stage V already queued on ctx->vstream (stored-bytes pipeline)
+  bool kes_done = false;           // the KES checks already queued chunk by chunk (stored-bytes pipeline)
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
@@ -285,6 +286,8 @@ struct praos_batch {
     uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
     ge_cached* ktab = nullptr;
   } kc[3];                       // [2] KES leaf keys
+  std::vector<KeyCache> kc_chunk;  // the stored-bytes pipeline's per-chunk KES leaf-key caches
+  size_t kc_chunk_n = 0;
   uint8_t* kes_leaf = nullptr;   // n*32: the leaf key of each header's KES signature
   bool kc_used = false;
   // OCert dedup (k_keys.hip k_ocert_dedup): hash set over the 144-byte OCert tuple,
@@ -389,6 +392,7 @@ static bool open_streams(praos_ctx* c) {
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : c->kes_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
@@ -512,6 +516,7 @@ void praos_close(praos_ctx* c) {
     }
     if (c->up_ev[k]) (void)hipEventDestroy(c->up_ev[k]);
     if (c->done_ev[k]) (void)hipEventDestroy(c->done_ev[k]);
+    if (c->kes_ev[k]) (void)hipEventDestroy(c->kes_ev[k]);
   }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->dstream) (void)hipStreamDestroy(c->dstream);
@@ -604,6 +609,27 @@ void praos_batch_free(praos_ctx* c, praos_batch* b) {
   delete b;
 }
 
+// one public-key cache (k_keys.hip) for batches of up to n items
+static bool alloc_keycache(praos_batch* b, praos_batch::KeyCache& k, size_t n) {
+  bool ok = true;
+  k.cap = 256;
+  while (k.cap < 2 * n) k.cap <<= 1;
+  k.max_entries = (uint32_t)std::min<size_t>(n / 2 + 1, KC_MAX_ENTRIES);
+  ok &= dalloc(b, &k.slot_rep, 4 * (size_t)k.cap) == hipSuccess;
+  ok &= dalloc(b, &k.slot_cnt, 4 * (size_t)k.cap) == hipSuccess;
+  ok &= dalloc(b, &k.slot_entry, 4 * (size_t)k.cap) == hipSuccess;
+  ok &= dalloc(b, &k.item_slot, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &k.item_entry, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &k.hit, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &k.miss, 4 * n) == hipSuccess;
+  ok &= dalloc(b, &k.counters, 16) == hipSuccess;
+  ok &= dalloc(b, &k.entry_rep, 4 * (size_t)k.max_entries) == hipSuccess;
+  ok &= dalloc(b, &k.entry_pos, 4 * (size_t)k.max_entries) == hipSuccess;
+  ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
+  ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
+  return ok;
+}
+
 // device buffers of a batch: header SoA, body arena, outputs, key caches
 static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   bool ok = true;
@@ -640,23 +666,7 @@ static bool alloc_soa(praos_batch* b, size_t n, size_t body_arena_bytes) {
   ok &= dalloc(b, &b->dd_reps, 4 * n) == hipSuccess;
   ok &= dalloc(b, &b->dd_counters, 16) == hipSuccess;
   ok &= dalloc(b, &b->dd_ok, n) == hipSuccess;
-  for (auto& k : b->kc) {
-    k.cap = 256;
-    while (k.cap < 2 * n) k.cap <<= 1;
-    k.max_entries = (uint32_t)std::min<size_t>(n / 2 + 1, KC_MAX_ENTRIES);
-    ok &= dalloc(b, &k.slot_rep, 4 * (size_t)k.cap) == hipSuccess;
-    ok &= dalloc(b, &k.slot_cnt, 4 * (size_t)k.cap) == hipSuccess;
-    ok &= dalloc(b, &k.slot_entry, 4 * (size_t)k.cap) == hipSuccess;
-    ok &= dalloc(b, &k.item_slot, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.item_entry, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.hit, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.miss, 4 * n) == hipSuccess;
-    ok &= dalloc(b, &k.counters, 16) == hipSuccess;
-    ok &= dalloc(b, &k.entry_rep, 4 * (size_t)k.max_entries) == hipSuccess;
-    ok &= dalloc(b, &k.entry_pos, 4 * (size_t)k.max_entries) == hipSuccess;
-    ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
-    ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
-  }
+  for (auto& k : b->kc) ok &= alloc_keycache(b, k, n);
   return ok;
 }
 
@@ -869,6 +879,55 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
   return r;
 }
 
+// key cache prepass over items [0, n) (or list[0 .. *count)): hash set, entries, hit/miss lists
+static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint8_t* keys, hipStream_t st,
+                    const uint32_t* list = nullptr, const uint32_t* count = nullptr) {
+  const dim3 g(nblocks(n, NT)), blk(NT);
+  HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
+  HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
+  HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
+  launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
+  launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)c->keycache,
+                    k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
+  launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit, k.miss,
+                       k.counters);
+  return PRAOS_OK;
+}
+static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
+  launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries, k.entry_rep,
+                        keys, k.ktab, k.kinfo, c->key_wave_prio);
+}
+
+// The KES checks of headers [lo, hi) of a batch with the chunk's own leaf-key cache k: leaf
+// keys, cache lists, the misses on stream sm (after ev: the partition is known), the key
+// tables and the cached chains on st.  Writes the KES bits of those headers.
+static int kes_range(praos_ctx* c, praos_batch* b, praos_batch::KeyCache& k, size_t lo, size_t hi, hipStream_t st,
+                     hipStream_t sm, hipEvent_t ev) {
+  const size_t m = hi - lo;
+  if (m == 0) return PRAOS_OK;
+  const dim3 g(nblocks(m, NT)), blk(NT);
+  const praos_params& P = c->params;
+  uint16_t* bk = b->bits3 + b->n + lo;
+  uint8_t* leaf = b->kes_leaf + 32 * lo;
+  launch_kes_leafkeys(g, blk, st, m, b->kes_sig + 448 * lo, b->slot + lo, b->ocert_c0 + lo, P.slots_per_kes_period,
+                      leaf);
+  int r = kc_lists(c, k, m, leaf, st);
+  if (r != PRAOS_OK) return r;
+  if (sm != st) {
+    HIPCHK(c, hipEventRecord(ev, st));
+    HIPCHK(c, hipStreamWaitEvent(sm, ev, 0));
+  }
+  launch_kes(g, blk, sm, m, k.miss, k.counters + 2, c->btab, b->hot_vk + 32 * lo, b->kes_sig + 448 * lo,
+             b->body_off + lo, b->body_len + lo, b->body, b->body_bytes_len, b->slot + lo, b->ocert_c0 + lo,
+             P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, (ge_cached*)((uint8_t*)b->tab_kes + LT_ED_B * lo));
+  kc_precompute(c, k, leaf, 0, st);
+  launch_kes_ck(g, blk, st, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk + 32 * lo,
+                b->kes_sig + 448 * lo, b->body_off + lo, b->body_len + lo, b->body, b->body_bytes_len, b->slot + lo,
+                b->ocert_c0 + lo, P.slots_per_kes_period, bk);
+  HIPCHK(c, hipGetLastError());
+  return PRAOS_OK;
+}
+
 static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   const size_t n = b->n;
   const praos_params& P = c->params;
@@ -931,19 +990,10 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   };
   auto keycache_lists = [&](praos_batch::KeyCache& k, const uint8_t* keys, hipStream_t st,
                             const uint32_t* list = nullptr, const uint32_t* count = nullptr) -> int {
-    HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
-    HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
-    HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
-    launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
-    launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)c->keycache,
-                      k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
-    launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit,
-                         k.miss, k.counters);
-    return PRAOS_OK;
+    return kc_lists(c, k, n, keys, st, list, count);
   };
   auto keycache_precompute = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
-    launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries,
-                          k.entry_rep, keys, k.ktab, k.kinfo, c->key_wave_prio);
+    kc_precompute(c, k, keys, kind, st);
   };
   b->dd_used = false;
   std::function<void()> ocert_miss;
@@ -1008,7 +1058,10 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   }
   if (ocert_miss) ocert_miss();
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
-  if (c->kernels & 2) {
+  if (b->kes_done) {
+    // queued chunk by chunk by the stored-bytes pipeline (on side[1] / side[0] and their miss
+    // streams, all joined below)
+  } else if (c->kernels & 2) {
     if (kc) {
       // leaf-key cache: the Ed25519 key a Sum6KES signature ends on repeats for every
       // header a pool signs in one KES period
@@ -1613,6 +1666,19 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
   const bool vrf = (c->kernels & 4) != 0;
+  // the KES checks also run chunk by chunk under the upload, each chunk with its own leaf-key
+  // cache (a leaf key is one pool's key for one KES period: the chunks of a slot range share few)
+  const bool kes = (c->kernels & 2) && c->keycache > 0 && c->concurrent;
+  if (kes) {
+    const size_t mmax = n / K + 64;
+    if ((int)b->kc_chunk.size() < K || b->kc_chunk_n < mmax) {
+      b->kc_chunk.assign(K, praos_batch::KeyCache{});
+      bool ok = true;
+      for (auto& k : b->kc_chunk) ok &= alloc_keycache(b, k, mmax + mmax / 8);
+      if (!ok) { c->err = "device allocation failed"; return PRAOS_E_OOM; }
+      b->kc_chunk_n = mmax + mmax / 8;
+    }
+  }
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
@@ -1629,8 +1695,16 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
                         b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor, b->header_hash,
                         b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
+    if (kes) {
+      // consecutive chunks alternate between two stream pairs (the OCert stream is idle until
+      // the batch run): one chunk's KES is a latency-bound chain and would queue behind another
+      hipStream_t st = (k & 1) ? c->side[0] : c->side[1], sm = (k & 1) ? c->mside[0] : c->mside[1];
+      HIPCHK(c, hipStreamWaitEvent(st, c->done_ev[k], 0));
+      const int rk = kes_range(c, b, b->kc_chunk[k], lo[k], lo[k + 1], st, sm, c->kes_ev[k]);
+      if (rk != PRAOS_OK) return rk;
+    }
     if (vrf) {
-      HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
       // the chunks' stage V alternate between two streams: on one they would queue behind
       // each other (a chunk's V alone is latency-bound)
       hipStream_t sv = (k & 1) ? c->vstream2 : c->vstream;
@@ -1642,9 +1716,11 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   b->decoded = true;
   b->v_done = vrf;
+  b->kes_done = kes;
   int r = praos_batch_run(c, b);
   b->decoded = false;
   b->v_done = false;
+  b->kes_done = false;
   // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
   // header) are final once the VRF stream is done: they come back while KES still runs
   if (r == PRAOS_OK && c->concurrent) {
@@ -2630,15 +2706,30 @@ static int tpraos_run(praos_ctx* c, praos_batch* b, const uint8_t* dlout, const 
   uint16_t* bo = b->bits3;
   uint16_t* bk = b->bits3 + n;
   uint16_t* bv = b->bits3 + 2 * n;
-  launch_ocert(g, blk, c->stream, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
+  // OCert, KES and the two-certificate VRF on the three side streams (the VRF one at the
+  // greatest priority), joined before the leader test -- as the Praos pipeline runs them
+  hipStream_t so = c->concurrent ? c->side[0] : c->stream;
+  hipStream_t sk = c->concurrent ? c->side[1] : c->stream;
+  hipStream_t sv = c->concurrent ? c->side[2] : c->stream;
+  if (c->concurrent) {
+    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+    for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[1], 0));
+  }
+  launch_ocert(g, blk, so, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
                b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
-  launch_kes(g, blk, c->stream, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
+  launch_kes(g, blk, sk, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
              b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
              (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
-  launch_vrf_tp(g, blk, c->stream, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
+  launch_vrf_tp(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
                 b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
                 c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l,
                 b->nonce, b->tab_vrf, dcls, c->d_gen, b->eta_idx);
+  if (c->concurrent) {
+    for (int k = 0; k < 3; k++) {
+      HIPCHK(c, hipEventRecord(c->side_ev[k], c->side[k]));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
+    }
+  }
   launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr, (int)P.f_is_one,
                 16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
                 b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);

@@ -641,6 +641,26 @@ class Context:
             self.check(-3)
         return b
 
+    def upload_tpraos_bytes(self, arena, off, length):
+        """Stored TPraos headers (BHeader) as a resident batch (praos_batch_upload_tpraos_bytes);
+        every praos_batch_run decodes them on the device and runs the TPraos kernels."""
+        arena, off, length = self._chunk(arena, off, length)
+        hb = self.header_bytes_struct(arena, off, length)
+        b = self.L.praos_batch_upload_tpraos_bytes(self.h, ctypes.byref(hb))
+        if not b:
+            self.check(-3)
+        return b
+
+    def download_tpraos(self, b, n):
+        o = {"bits": np.zeros(n, np.uint16), "pool_idx": np.zeros(n, np.int32),
+             "beta_eta": np.zeros((n, 64), np.uint8), "beta_leader": np.zeros((n, 64), np.uint8),
+             "nonce": np.zeros((n, 32), np.uint8)}
+        to = TPOut()
+        to.bits, to.pool_idx = ptr(o["bits"], u16p), ptr(o["pool_idx"], i32p)
+        to.beta_eta, to.beta_leader, to.nonce = ptr(o["beta_eta"]), ptr(o["beta_leader"]), ptr(o["nonce"])
+        self.check(self.L.praos_batch_download_tpraos(self.h, b, ctypes.byref(to)))
+        return o
+
     def batch_decode(self, b):
         self.check(self.L.praos_batch_decode(self.h, b))
 

@@ -94,6 +94,12 @@ W_VRF_V = (B2B                                        # alpha = mkInputVRF(slot,
 _FIN = SC_REDUCE + TO_P2 + X + 10 * M + 4 * (2 * M + CANON) + 3 * SHA + 5 * B2B + 1000
 W_VRF_F_CK = _FIN + straus_comb(8, True)             # U from the cached key + comb; inversion, c', beta, L/N
 W_VRF_F = _FIN + DECODE + TABLE8 + straus(33, 33, 0, 32)
+# TPraos header (TPraos.hs:361-387, k_vrf_tp): two certificates (eta, L) per header, each a full
+# uncached draft-03 verify with its mkSeed input (2 Blake2b), issuer + VRF-key hashes, the
+# eta nonce hash; the leader test against 2^512
+W_VRF_TP = 2 * (vrf_verify() + 2 * B2B) + 3 * B2B + 1000
+W_LEADER_TP = 6000
+W_TP_HEADER = W_OCERT + W_KES + W_VRF_TP + W_LEADER_TP
 W_KEY_COLD = key_precompute(16)
 W_KEY_KES = key_precompute(16)                       # leaf keys: same tables as cold keys
 W_KEY_VRF = key_precompute(9) + CANON
@@ -101,6 +107,7 @@ W_KEY_VRF = key_precompute(9) + CANON
 if __name__ == "__main__":
     for k, v in (("ocert", W_OCERT), ("kes", W_KES), ("vrf", W_VRF), ("leader", W_LEADER),
                  ("ocert_ck", W_OCERT_CK), ("vrf_ck", W_VRF_CK), ("kes_ck", W_KES_CK), ("key_cold", W_KEY_COLD), ("key_vrf", W_KEY_VRF),
-                 ("vrf_v", W_VRF_V), ("vrf_f_ck", W_VRF_F_CK), ("vrf_f", W_VRF_F)):
+                 ("vrf_v", W_VRF_V), ("vrf_f_ck", W_VRF_F_CK), ("vrf_f", W_VRF_F), ("vrf_tp", W_VRF_TP),
+                 ("tp_hdr", W_TP_HEADER)):
         print(f"W_{k:7s} {v:>10,d} int32 ops / item")
     print(f"W_header  {W_OCERT + W_KES + W_VRF + W_LEADER:>10,d}")
