@@ -12,7 +12,7 @@ static constexpr size_t BTAB_N = 128;              // entries per fixed-base tab
 static constexpr size_t BCOMB_TABLES = 32;         // fixed-base comb: 256^j B, j < 32 (scalarmult.hpp BCOMB_T)
 static constexpr size_t C16_TABLES = 16, C16_ENTRIES = 32768;   // radix-2^16 comb (scalarmult.hpp C16_T, C16_N)
 static constexpr size_t CACHED_BYTES = 4 * 32;     // sizeof(ge_cached)
-static constexpr size_t LT_ED_N = 8, LT_ED_B = LT_ED_N * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
+static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES;   // per-lane tables (kcommon.hpp)
 static constexpr size_t VRF_MID_BYTES = 28 * 16;    // per-header records of the staged VRF (praos_core.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
@@ -115,7 +115,7 @@ struct praos_ctx {
   hipStream_t cstream = nullptr;
   hipStream_t dstream = nullptr;                       // replay: result downloads (rp_download_results)
   praos_batch* rp_keep[RP_SLOTS] = {};                 // replay batches kept between calls
-  hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {}, kes_ev[PIPE_MAX] = {};
+  hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
   praos_batch* pipe[PIPE_MAX] = {};
   size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
@@ -276,7 +276,6 @@ struct praos_batch {
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
   ge_cached* tab_vrfu = nullptr;   // 8-entry lane tables of stage U on uncached VRF keys
   bool v_done = false;             // stage V already queued on ctx->vstream (stored-bytes pipeline)
-  bool kes_done = false;           // the KES checks already queued chunk by chunk (stored-bytes pipeline)
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
@@ -286,8 +285,6 @@ struct praos_batch {
     uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
     ge_cached* ktab = nullptr;
   } kc[3];                       // [2] KES leaf keys
-  std::vector<KeyCache> kc_chunk;  // the stored-bytes pipeline's per-chunk KES leaf-key caches
-  size_t kc_chunk_n = 0;
   uint8_t* kes_leaf = nullptr;   // n*32: the leaf key of each header's KES signature
   bool kc_used = false;
   // OCert dedup (k_keys.hip k_ocert_dedup): hash set over the 144-byte OCert tuple,
@@ -392,7 +389,6 @@ static bool open_streams(praos_ctx* c) {
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  for (auto& e : c->kes_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
@@ -516,7 +512,6 @@ void praos_close(praos_ctx* c) {
     }
     if (c->up_ev[k]) (void)hipEventDestroy(c->up_ev[k]);
     if (c->done_ev[k]) (void)hipEventDestroy(c->done_ev[k]);
-    if (c->kes_ev[k]) (void)hipEventDestroy(c->kes_ev[k]);
   }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->dstream) (void)hipStreamDestroy(c->dstream);
@@ -898,36 +893,6 @@ static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t*
                         keys, k.ktab, k.kinfo, c->key_wave_prio);
 }
 
-// The KES checks of headers [lo, hi) of a batch with the chunk's own leaf-key cache k: leaf
-// keys, cache lists, the misses on stream sm (after ev: the partition is known), the key
-// tables and the cached chains on st.  Writes the KES bits of those headers.
-static int kes_range(praos_ctx* c, praos_batch* b, praos_batch::KeyCache& k, size_t lo, size_t hi, hipStream_t st,
-                     hipStream_t sm, hipEvent_t ev) {
-  const size_t m = hi - lo;
-  if (m == 0) return PRAOS_OK;
-  const dim3 g(nblocks(m, NT)), blk(NT);
-  const praos_params& P = c->params;
-  uint16_t* bk = b->bits3 + b->n + lo;
-  uint8_t* leaf = b->kes_leaf + 32 * lo;
-  launch_kes_leafkeys(g, blk, st, m, b->kes_sig + 448 * lo, b->slot + lo, b->ocert_c0 + lo, P.slots_per_kes_period,
-                      leaf);
-  int r = kc_lists(c, k, m, leaf, st);
-  if (r != PRAOS_OK) return r;
-  if (sm != st) {
-    HIPCHK(c, hipEventRecord(ev, st));
-    HIPCHK(c, hipStreamWaitEvent(sm, ev, 0));
-  }
-  launch_kes(g, blk, sm, m, k.miss, k.counters + 2, c->btab, b->hot_vk + 32 * lo, b->kes_sig + 448 * lo,
-             b->body_off + lo, b->body_len + lo, b->body, b->body_bytes_len, b->slot + lo, b->ocert_c0 + lo,
-             P.slots_per_kes_period, (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, (ge_cached*)((uint8_t*)b->tab_kes + LT_ED_B * lo));
-  kc_precompute(c, k, leaf, 0, st);
-  launch_kes_ck(g, blk, st, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk + 32 * lo,
-                b->kes_sig + 448 * lo, b->body_off + lo, b->body_len + lo, b->body, b->body_bytes_len, b->slot + lo,
-                b->ocert_c0 + lo, P.slots_per_kes_period, bk);
-  HIPCHK(c, hipGetLastError());
-  return PRAOS_OK;
-}
-
 static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   const size_t n = b->n;
   const praos_params& P = c->params;
@@ -1058,10 +1023,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   }
   if (ocert_miss) ocert_miss();
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
-  if (b->kes_done) {
-    // queued chunk by chunk by the stored-bytes pipeline (on side[1] / side[0] and their miss
-    // streams, all joined below)
-  } else if (c->kernels & 2) {
+  if (c->kernels & 2) {
     if (kc) {
       // leaf-key cache: the Ed25519 key a Sum6KES signature ends on repeats for every
       // header a pool signs in one KES period
@@ -1666,19 +1628,6 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
   const bool vrf = (c->kernels & 4) != 0;
-  // the KES checks also run chunk by chunk under the upload, each chunk with its own leaf-key
-  // cache (a leaf key is one pool's key for one KES period: the chunks of a slot range share few)
-  const bool kes = (c->kernels & 2) && c->keycache > 0 && c->concurrent;
-  if (kes) {
-    const size_t mmax = n / K + 64;
-    if ((int)b->kc_chunk.size() < K || b->kc_chunk_n < mmax) {
-      b->kc_chunk.assign(K, praos_batch::KeyCache{});
-      bool ok = true;
-      for (auto& k : b->kc_chunk) ok &= alloc_keycache(b, k, mmax + mmax / 8);
-      if (!ok) { c->err = "device allocation failed"; return PRAOS_E_OOM; }
-      b->kc_chunk_n = mmax + mmax / 8;
-    }
-  }
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
@@ -1696,14 +1645,6 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
                         b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
-    if (kes) {
-      // consecutive chunks alternate between two stream pairs (the OCert stream is idle until
-      // the batch run): one chunk's KES is a latency-bound chain and would queue behind another
-      hipStream_t st = (k & 1) ? c->side[0] : c->side[1], sm = (k & 1) ? c->mside[0] : c->mside[1];
-      HIPCHK(c, hipStreamWaitEvent(st, c->done_ev[k], 0));
-      const int rk = kes_range(c, b, b->kc_chunk[k], lo[k], lo[k + 1], st, sm, c->kes_ev[k]);
-      if (rk != PRAOS_OK) return rk;
-    }
     if (vrf) {
       // the chunks' stage V alternate between two streams: on one they would queue behind
       // each other (a chunk's V alone is latency-bound)
@@ -1716,11 +1657,9 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   b->decoded = true;
   b->v_done = vrf;
-  b->kes_done = kes;
   int r = praos_batch_run(c, b);
   b->decoded = false;
   b->v_done = false;
-  b->kes_done = false;
   // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
   // header) are final once the VRF stream is done: they come back while KES still runs
   if (r == PRAOS_OK && c->concurrent) {
