@@ -494,13 +494,25 @@ def main():
             # kernels, D2H of each chunk's results while later chunks compute
             from praos_hip.chunk import pack_chunk
             arena, off_, ln_ = pack_chunk(H)
-            ob = ctx.verify_header_bytes(arena, off_, ln_)            # warm (chunk batches allocated)
-            te = []
-            for _ in range(3):                                         # best of 3 calls
-                t_ = time.perf_counter()
-                ob = ctx.verify_header_bytes(arena, off_, ln_)
-                te.append(time.perf_counter() - t_)
-            te = min(te)
+            ob = ctx.alloc_out(n)                                      # caller-owned outputs, reused
+
+            def best_of_3():
+                ctx.verify_header_bytes(arena, off_, ln_, out=ob)      # warm (chunk batches allocated)
+                ts = []
+                for _ in range(3):
+                    t_ = time.perf_counter()
+                    ctx.verify_header_bytes(arena, off_, ln_, out=ob)
+                    ts.append(time.perf_counter() - t_)
+                return min(ts)
+            te_pageable = best_of_3()
+            # the same with the host arena and the output arrays page-locked once
+            # (praos_host_register, as a replay reader locks its chunk buffers): direct DMA
+            bufs = [arena] + [v for v in ob.values() if v.nbytes >= (4 << 20)]
+            for a in bufs:
+                ctx.host_register(a)
+            te = best_of_3()
+            for a in bufs:
+                ctx.host_unregister(a)
             # a corrupted body byte (corruption kind 5) makes the stored CBOR itself
             # malformed or different, so the byte path rejects that header at decode
             # (PRAOS_BIT_DECODE) where the SoA path rejects it at the KES check: those
@@ -511,10 +523,13 @@ def main():
                    "accept_equal_all": bool(((ob["bits"] == 0) == (out["bits"] == 0)).all()),
                    "body_corrupted_excluded": int((~cmp).sum()),
                    "input_bytes": int(len(arena)), "h2d_GBps_equiv": round(len(arena) / te / 1e9, 1),
-                   "path": "praos_verify_header_bytes: stored header bytes (pageable host arena) -> H2D in "
-                           "6 chunks through pinned staging on a copy stream, each landed chunk decoded and its "
-                           "VRF stage V run while later chunks upload -> the rest of the batch once -> VRF "
-                           "outputs D2H while the KES checks finish (best of 3 calls)"}
+                   "pageable": {"value": round(n / te_pageable, 1), "ms": round(te_pageable * 1e3, 2),
+                                "note": "the same calls with the arena and outputs in pageable memory: "
+                                        "uploads staged through the library's pinned buffers by 16 host threads"},
+                   "path": "praos_verify_header_bytes: stored header bytes (host arena page-locked once with "
+                           "praos_host_register) -> H2D in 6 chunks on a copy stream, each landed chunk decoded "
+                           "and its VRF stage V run while later chunks upload -> the rest of the batch once -> "
+                           "VRF outputs D2H while the KES checks finish (best of 3 calls)"}
         # the host-SoA entry point (every decoded field from the host, 1,236 B per header)
         oe = ctx.verify_headers(H)
         te = time.perf_counter()

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 10
+#define PRAOS_ABI_VERSION 11
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -222,6 +222,14 @@ int praos_batch_dedup_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[2]);
  * kernel k_vrf_v alone (events around its launch on its own stream).  With concurrent
  * streams, 0-2 are measured from the common start to each kernel's end. */
 float praos_batch_kernel_ms(praos_ctx* ctx, int which);
+
+/* Page-locks [p, p + len) of caller memory (hipHostRegister) for the context's device, e.g.
+ * a replay reader's chunk buffer or a Haskell pinned ByteString that lives across many calls;
+ * uploads whose source lies inside a registered range move by direct DMA instead of through
+ * the library's pinned staging buffers and host copy threads.  Returns 0, or PRAOS_E_HIP.
+ * Unregister before freeing the memory. */
+int praos_host_register(praos_ctx* ctx, void* p, size_t len);
+int praos_host_unregister(praos_ctx* ctx, void* p);
 
 /* ---- stored headers: decode on the GPU ----
  * Input: a byte arena (e.g. an ImmutableDB chunk file as read) and per header

@@ -152,6 +152,9 @@ struct praos_ctx {
   std::vector<praos_gen_deleg> gen_delegs;
   std::set<std::string> gen_delegate_hashes;
   uint32_t* d_gen = nullptr;
+  // caller ranges page-locked with praos_host_register: uploads from them skip the staging
+  std::mutex reg_mu;
+  std::vector<std::pair<uintptr_t, size_t>> registered;
   // host <-> device staging for large transfers from pageable caller memory
   uint8_t* pin[2] = {nullptr, nullptr};
   hipEvent_t pin_ev[2] = {};
@@ -189,8 +192,17 @@ static bool stage_init(praos_ctx* c) {
   return true;
 }
 
+static bool is_registered(praos_ctx* c, const void* p, size_t len) {
+  std::lock_guard<std::mutex> g(c->reg_mu);
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto& r : c->registered)
+    if (a >= r.first && len <= r.second && a - r.first <= r.second - len) return true;
+  return false;
+}
+
 static hipError_t h2d_on(praos_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
-  if (bytes < (4u << 20) || !stage_init(c)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+  if (bytes < (4u << 20) || is_registered(c, src, bytes) || !stage_init(c))
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);   // registered memory: direct DMA
   for (size_t off = 0, k = 0; off < bytes; off += STAGE_PIECE, k++) {
     const size_t len = std::min(STAGE_PIECE, bytes - off);
     hipError_t e = hipEventSynchronize(c->pin_ev[k & 1]);    // the DMA that last used this buffer
@@ -205,7 +217,7 @@ static hipError_t h2d_on(praos_ctx* c, void* dst, const void* src, size_t bytes,
 // D2H on stream st, whose producers the caller has ordered before (an event wait); returns
 // when the bytes are in dst
 static hipError_t d2h_on(praos_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
-  if (bytes < (4u << 20) || !stage_init(c)) {
+  if (bytes < (4u << 20) || is_registered(c, dst, bytes) || !stage_init(c)) {
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
     return e == hipSuccess ? hipStreamSynchronize(st) : e;
   }
@@ -367,6 +379,30 @@ static hipError_t dalloc(praos_batch* b, T** p, size_t bytes) {
 extern "C" {
 
 int praos_abi_version(void) { return PRAOS_ABI_VERSION; }
+
+int praos_host_register(praos_ctx* c, void* p, size_t len) {
+  if (!c || !p || len == 0) return PRAOS_E_ARG;
+  if (c->device < 0) return PRAOS_E_STATE;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipHostRegister(p, len, hipHostRegisterDefault));
+  std::lock_guard<std::mutex> g(c->reg_mu);
+  c->registered.emplace_back((uintptr_t)p, len);
+  return PRAOS_OK;
+}
+
+int praos_host_unregister(praos_ctx* c, void* p) {
+  if (!c || !p) return PRAOS_E_ARG;
+  {
+    std::lock_guard<std::mutex> g(c->reg_mu);
+    auto it = std::find_if(c->registered.begin(), c->registered.end(),
+                           [&](const std::pair<uintptr_t, size_t>& r) { return r.first == (uintptr_t)p; });
+    if (it == c->registered.end()) return PRAOS_E_ARG;
+    c->registered.erase(it);
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipHostUnregister(p));
+  return PRAOS_OK;
+}
 
 const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
@@ -846,9 +882,8 @@ static int batch_decode(praos_ctx* c, praos_batch* b) {
   return hipGetLastError() == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
 }
 
+static int32_t overlay_class(const praos_ctx* c, uint64_t slot);
 static int batch_run_impl(praos_ctx* c, praos_batch* b);
-static int tpraos_run(praos_ctx* c, praos_batch* b, const uint8_t* dlout, const uint8_t* dlproof, uint8_t* dbeta_l,
-                      const uint64_t* host_slots);
 static int tpraos_download(praos_ctx* c, praos_batch* b, const uint8_t* dbeta_l, praos_tpraos_out* out);
 
 int praos_batch_run(praos_ctx* c, praos_batch* b) {
@@ -921,19 +956,18 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     const int rc = ensure_bcomb16(c);
     if (rc != PRAOS_OK) return rc;
   }
-  if (b->tp_only) {          // TPraos headers from stored bytes: the TPraos kernels, in order
-    std::vector<uint64_t> slots;
-    if (c->ovl_on) {         // the overlay schedule is classified on the host from the decoded slots
-      slots.resize(n);
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipMemcpy(slots.data(), b->slot, 8 * n, hipMemcpyDeviceToHost));
-    }
-    HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-    for (int k = 0; k < 3; k++) HIPCHK(c, hipEventRecord(c->side_ev[k], c->stream));
-    const int r = tpraos_run(c, b, b->lead_out, b->lead_proof, b->beta_l, slots.data());
-    if (r != PRAOS_OK) return r;
-    HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
-    return PRAOS_OK;
+  // TPraos (b->tp_only): the same OCert and KES passes (dedup, key caches, side streams); the
+  // VRF pass is the two-certificate k_vrf_tp (overlay classes from the host slots when
+  // praos_set_overlay is on) and the leader test takes the certified L output, 2^512 bound
+  int32_t* dcls = nullptr;
+  if (b->tp_only && c->ovl_on) {
+    std::vector<uint64_t> slots(n);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(slots.data(), b->slot, 8 * n, hipMemcpyDeviceToHost));
+    std::vector<int32_t> cls(n);
+    for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, slots[i]);
+    if (dalloc(b, &dcls, 4 * n) != hipSuccess) return PRAOS_E_OOM;
+    HIPCHK(c, hipMemcpy(dcls, cls.data(), 4 * n, hipMemcpyHostToDevice));
   }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
@@ -1048,7 +1082,12 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
   const bool do_vrf = (c->kernels & 4) != 0;
-  if (do_vrf) {
+  if (do_vrf && b->tp_only) {
+    launch_vrf_tp(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->lead_out, b->lead_proof,
+                  b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
+                  c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, b->beta_l,
+                  b->nonce, b->tab_vrf, dcls, c->d_gen, b->eta_idx);
+  } else if (do_vrf) {
     // two stages (k_vrf.hip): V over every header on its own stream, from ev[0] on (it
     // needs no key); F after it -- the hits on sv once their key tables exist, the misses
     // on their miss stream (per-lane U)
@@ -1135,9 +1174,9 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->mdone_ev[k], 0));
     }
   }
-  launch_leader(g, blk, c->stream, n, b->leader, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr,
-                (int)P.f_is_one, 8, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
-                b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
+  launch_leader(g, blk, c->stream, n, b->tp_only ? b->lead_out : b->leader, b->pool_sorted, c->d_pool_x,
+                (const uint32_t*)nullptr, (int)P.f_is_one, b->tp_only ? 16 : 8, bo, bk, bv, b->bits, (uint8_t*)nullptr,
+                (int32_t*)nullptr, b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
   HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
   HIPCHK(c, hipGetLastError());
   return PRAOS_OK;
@@ -2625,57 +2664,6 @@ int praos_overlay_classify(praos_ctx* c, size_t n, const uint64_t* slots, int32_
   return PRAOS_OK;
 }
 
-// TPraos batch: OCert + KES kernels are shared with Praos; VRF checks use the
-// two-certificate kernel and the leader test the 2^512 bound.
-// TPraos crypto over a batch whose SoA is on the device (uploaded from host arrays, or
-// decoded from stored bytes): OCERT, KES, OVERLAY praosVrfChecks (k_vrf_tp) and the
-// 2^512 leader test; overlay classes from the host slots (praos_set_overlay).
-static int tpraos_run(praos_ctx* c, praos_batch* b, const uint8_t* dlout, const uint8_t* dlproof, uint8_t* dbeta_l,
-                      const uint64_t* host_slots) {
-  const size_t n = b->n;
-  int32_t* dcls = nullptr;
-  if (c->ovl_on) {
-    if (dalloc(b, &dcls, 4 * n) != hipSuccess) return PRAOS_E_OOM;
-    std::vector<int32_t> cls(n);
-    for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, host_slots[i]);
-    HIPCHK(c, hipMemcpy(dcls, cls.data(), 4 * n, hipMemcpyHostToDevice));
-  }
-  const praos_params& P = c->params;
-  const dim3 g(nblocks(n, NT)), blk(NT);
-  uint16_t* bo = b->bits3;
-  uint16_t* bk = b->bits3 + n;
-  uint16_t* bv = b->bits3 + 2 * n;
-  // OCert, KES and the two-certificate VRF on the three side streams (the VRF one at the
-  // greatest priority), joined before the leader test -- as the Praos pipeline runs them
-  hipStream_t so = c->concurrent ? c->side[0] : c->stream;
-  hipStream_t sk = c->concurrent ? c->side[1] : c->stream;
-  hipStream_t sv = c->concurrent ? c->side[2] : c->stream;
-  if (c->concurrent) {
-    HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
-    for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[1], 0));
-  }
-  launch_ocert(g, blk, so, n, nullptr, nullptr, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-               b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr, b->tab_ocert);
-  launch_kes(g, blk, sk, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
-             b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
-             (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
-  launch_vrf_tp(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, dlout, dlproof,
-                b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
-                c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, dbeta_l,
-                b->nonce, b->tab_vrf, dcls, c->d_gen, b->eta_idx);
-  if (c->concurrent) {
-    for (int k = 0; k < 3; k++) {
-      HIPCHK(c, hipEventRecord(c->side_ev[k], c->side[k]));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
-    }
-  }
-  launch_leader(g, blk, c->stream, n, dlout, b->pool_sorted, c->d_pool_x, (const uint32_t*)nullptr, (int)P.f_is_one,
-                16, bo, bk, bv, b->bits, (uint8_t*)nullptr, (int32_t*)nullptr,
-                b->from_bytes ? b->dec_status : (const uint16_t*)nullptr);
-  HIPCHK(c, hipGetLastError());
-  return PRAOS_OK;
-}
-
 static int tpraos_download(praos_ctx* c, praos_batch* b, const uint8_t* dbeta_l, praos_tpraos_out* out) {
   const size_t n = b->n;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2704,7 +2692,11 @@ int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, pr
   auto body = [&]() -> int {
     HIPCHK(c, hipMemcpy(dlout, th->leader_out, 64 * n, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(dlproof, th->leader_proof, 80 * n, hipMemcpyHostToDevice));
-    const int r = tpraos_run(c, b, dlout, dlproof, dbeta_l, th->h.slot);
+    b->tp_only = true;
+    b->lead_out = dlout;
+    b->lead_proof = dlproof;
+    b->beta_l = dbeta_l;
+    const int r = praos_batch_run(c, b);
     return r == PRAOS_OK ? tpraos_download(c, b, dbeta_l, out) : r;
   };
   rc = body();
@@ -2748,15 +2740,7 @@ int praos_verify_tpraos_header_bytes(praos_ctx* c, const praos_header_bytes* in,
   praos_batch* b = upload_bytes_impl(c, in, true);
   if (!b) return PRAOS_E_OOM;
   auto body = [&]() -> int {
-    const int rd = batch_decode(c, b);
-    if (rd != PRAOS_OK) { c->err = "decode launch failed"; return rd; }
-    std::vector<uint64_t> slots;
-    if (c->ovl_on) {             // the overlay schedule is classified on the host from the decoded slots
-      slots.resize(n);
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipMemcpy(slots.data(), b->slot, 8 * n, hipMemcpyDeviceToHost));
-    }
-    int r = tpraos_run(c, b, b->lead_out, b->lead_proof, b->beta_l, slots.data());
+    int r = praos_batch_run(c, b);             // decode, then the TPraos passes
     if (r == PRAOS_OK) r = tpraos_download(c, b, b->beta_l, out);
     if (r == PRAOS_OK && dec) r = praos_batch_download_decoded(c, b, dec);
     if (r == PRAOS_OK && leader_out) HIPCHK(c, d2h(c, leader_out, b->lead_out, 64 * n));

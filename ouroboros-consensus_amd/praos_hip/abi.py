@@ -173,6 +173,8 @@ TP_SIGNED_STRIDE = 640
 # every entry point declared in include/praos_hip.h: name -> (restype, argtypes)
 SIGNATURES = {
     "praos_abi_version": (ctypes.c_int, []),
+    "praos_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "praos_host_unregister": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "praos_open": (ctypes.c_void_p, [ctypes.c_int]),
     "praos_close": (None, [ctypes.c_void_p]),
     "praos_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
@@ -567,11 +569,12 @@ class Context:
         self.check(self.L.praos_decode_headers(self.h, ctypes.byref(hb), ctypes.byref(d)))
         return D
 
-    def verify_header_bytes(self, arena, off, length, decoded=False):
+    def verify_header_bytes(self, arena, off, length, decoded=False, out=None):
+        """out: caller-owned output arrays (alloc_out) reused across calls."""
         arena, off, length = self._chunk(arena, off, length)
         n = len(off)
         hb = self.header_bytes_struct(arena, off, length)
-        o = self.alloc_out(n)
+        o = self.alloc_out(n) if out is None else out
         os_ = self.out_struct(o)
         D, d = self.alloc_decoded(n) if decoded else (None, None)
         self.check(self.L.praos_verify_header_bytes(self.h, ctypes.byref(hb), ctypes.byref(os_),
@@ -640,6 +643,14 @@ class Context:
         if not b:
             self.check(-3)
         return b
+
+    def host_register(self, arr):
+        """Page-locks a numpy array's memory for this context (praos_host_register): uploads
+        from it move by direct DMA.  Keep the array alive until host_unregister."""
+        self.check(self.L.praos_host_register(self.h, arr.ctypes.data, arr.nbytes))
+
+    def host_unregister(self, arr):
+        self.check(self.L.praos_host_unregister(self.h, arr.ctypes.data))
 
     def upload_tpraos_bytes(self, arena, off, length):
         """Stored TPraos headers (BHeader) as a resident batch (praos_batch_upload_tpraos_bytes);
