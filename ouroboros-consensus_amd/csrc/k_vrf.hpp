@@ -30,6 +30,7 @@ struct VrfIn {
   uint8_t* __restrict__ nonce_out;
   uint8_t* __restrict__ ok_out;
   ge_cached* __restrict__ tabs;          // per-lane tables (LT_VRF entries per item)
+  int wave_prio;                         // stage V / join waves at s_setprio 3 (small batches)
 };
 
 // issuer pool: hashKey (Blake2b-224 of the cold vk, Praos.hs:552) -> sorted index or -1

@@ -18,6 +18,7 @@ __device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, 
 __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_v(size_t n, size_t i0, size_t i1, VrfIn a, uint4* __restrict__ mid) {
   const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // headers [i0, i1), record stride n
   if (i >= i1) return;
+  if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
   uint32_t pk[8], pr[20], alpha[8];
   load_words(pk, a.vrf_vk + 32 * i, 8);
   load_words(pr, a.vrf_proof + 80 * i, 20);
@@ -153,6 +154,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_u_nc(size_t n, const uint32_
 __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
   uint16_t b = 0;
   int32_t sidx;
   {
@@ -206,9 +208,10 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_join(size_t n, VrfIn a, cons
 // ---- host launchers (kernels are only launchable from their own module)
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
                   const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
-                  size_t i0, size_t i1) {
-  const VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
-                         nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
+                  size_t i0, size_t i1, int wave_prio) {
+  VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
+                   nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
+  a.wave_prio = wave_prio;
   const unsigned bs = lat_block(n);
   i1 = i1 < n ? i1 : n;
   if (i1 <= i0) return;
@@ -248,10 +251,11 @@ void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const
                      const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                      uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
-                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid) {
-  const VrfIn a = vrf_in(cold_vk, vrf_vk, vrf_out, vrf_proof, nullptr, nullptr, 0, nullptr, pool_hash, pool_vrf,
-                         pool_map, npools, check_output, bits, pool_idx, pool_sorted_idx, beta_out, leader_out,
-                         nonce_out, nullptr);
+                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio) {
+  VrfIn a = vrf_in(cold_vk, vrf_vk, vrf_out, vrf_proof, nullptr, nullptr, 0, nullptr, pool_hash, pool_vrf,
+                   pool_map, npools, check_output, bits, pool_idx, pool_sorted_idx, beta_out, leader_out,
+                   nonce_out, nullptr);
+  a.wave_prio = wave_prio;
   const unsigned bs = lat_block(n);
   hipLaunchKernelGGL(k_vrf_join, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, a, (const uint4*)mid);
 }

@@ -96,7 +96,8 @@ void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, u
 // list is null), cached (ktab != null: k_vrf_fin) or per-lane U (k_vrf_fin_nc)
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
                   const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
-                  size_t i0 = 0, size_t i1 = SIZE_MAX);   // headers [i0, min(i1, n)); mid stride n
+                  size_t i0 = 0, size_t i1 = SIZE_MAX,    // headers [i0, min(i1, n)); mid stride n
+                  int wave_prio = 0);                      // waves at s_setprio 3
 void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
                     const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
@@ -113,7 +114,7 @@ void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const
                      const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                      uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
-                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid);
+                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio = 0);
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs,
                    const int32_t* ovl_class, const uint32_t* gen, const uint8_t* eta_idx = nullptr);
 void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena, uint64_t arena_len,

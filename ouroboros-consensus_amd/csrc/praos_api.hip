@@ -107,6 +107,7 @@ struct praos_ctx {
   hipEvent_t v_ev = nullptr, v2_ev = nullptr;
   hipEvent_t v0_ev = nullptr, v1_ev = nullptr;         // timing of k_vrf_v on its stream (kernel_ms[6])
   hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
+  int vrf_prio = 0;                                   // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO; -1: small batches)
   int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
                                                        // the three-kernel form below 300k headers (latency)
   // chunked stored-bytes pipeline (praos_verify_header_bytes): a copy stream, per-chunk
@@ -422,6 +423,7 @@ static bool open_streams(praos_ctx* c) {
   (void)hipEventCreate(&c->v0_ev);
   (void)hipEventCreateWithFlags(&c->u_ev, hipEventDisableTiming);
   if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PRAOS_VRF_PRIO")) c->vrf_prio = std::atoi(e);
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -1095,11 +1097,12 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     // (stored-bytes pipeline: stage V was queued chunk by chunk on vstream while the later
     // chunks were still uploading; b->v_done)
     hipStream_t sV = (c->concurrent || b->v_done) ? c->vstream : c->stream;
+    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < 300000);
     if (!b->v_done) {
       if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
       HIPCHK(c, hipEventRecord(c->v0_ev, sV));
       launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
-                   b->vrf_mid);
+                   b->vrf_mid, 0, SIZE_MAX, wprio);
       HIPCHK(c, hipEventRecord(c->v1_ev, sV));
       c->v_timed = true;
     }
@@ -1123,7 +1126,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     auto join = [&](hipStream_t st) {
       launch_vrf_join(st, n, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, c->d_pool_hash, c->d_pool_vrf,
                       c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta,
-                      b->leader, b->nonce, b->vrf_mid);
+                      b->leader, b->nonce, b->vrf_mid, wprio);
     };
     if (c->vrf3 > 0 || (c->vrf3 < 0 && n < 300000)) {
       // three kernels: U runs beside V (uncached keys at once on the miss stream, cached keys
