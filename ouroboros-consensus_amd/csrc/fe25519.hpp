@@ -407,8 +407,13 @@ FE_INLINE void fe_chi_inl(fe& r, const fe& z) {
 __device__ __noinline__ fe fe_invert_v(fe z) { fe r; fe_invert_inl(r, z); return r; }
 __device__ __noinline__ fe fe_pow22523_v(fe z) { fe r; fe_pow22523_inl(r, z); return r; }
 __device__ __noinline__ fe fe_chi_v(fe z) { fe r; fe_chi_inl(r, z); return r; }
+#if FE_POW_INLINE   // a module whose kernels keep values live across the chain (no call spills)
+FE_INLINE void fe_invert(fe& r, const fe& z) { fe_invert_inl(r, z); }
+FE_INLINE void fe_pow22523(fe& r, const fe& z) { fe_pow22523_inl(r, z); }
+#else
 FE_INLINE void fe_invert(fe& r, const fe& z) { r = fe_invert_v(z); }
 FE_INLINE void fe_pow22523(fe& r, const fe& z) { r = fe_pow22523_v(z); }
+#endif
 FE_INLINE void fe_chi(fe& r, const fe& z) { r = fe_chi_v(z); }
 
 __device__ __constant__ static const uint32_t FE_D[8] = {0x135978a3u, 0x75eb4dcau, 0x4141d8abu, 0x00700a4du,

@@ -3,6 +3,15 @@
 // kept for A/B (PRAOS_VRF3=0).
 #include "k_vrf.hpp"
 
+// waves per SIMD the launch bounds ask for: stage V (the largest kernel, 168 VGPRs at 3) and
+// the U / join kernels (at 3 they spill SHA-512 and point state to scratch)
+#ifndef LB_VRF_V
+#define LB_VRF_V LB_VRF
+#endif
+#ifndef LB_VRF_F
+#define LB_VRF_F LB_VRF
+#endif
+
 // ---- two-stage form of the header mode (praos_core.hpp vrf_v_core / vrf_fin_core)
 // alpha = mkInputVRF(slot, eta) of header i (Praos/VRF.hs:55-69)
 __device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, size_t i) {
@@ -15,7 +24,7 @@ __device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, 
 }
 
 // stage V over every header of the batch: no dependence on the key cache
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_v(size_t n, size_t i0, size_t i1, VrfIn a, uint4* __restrict__ mid) {
+__global__ void __launch_bounds__(NT, LB_VRF_V) k_vrf_v(size_t n, size_t i0, size_t i1, VrfIn a, uint4* __restrict__ mid) {
   const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // headers [i0, i1), record stride n
   if (i >= i1) return;
   if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
@@ -81,7 +90,7 @@ __device__ __forceinline__ void vrf_fin_item(const VrfIn& a, size_t i, size_t st
 }
 
 // cached keys (the hit list): U from the key's tables and the radix-2^16 comb
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_fin(size_t stride, const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_fin(size_t stride, const uint32_t* __restrict__ list,
                                                         const uint32_t* __restrict__ count,
                                                         const int32_t* __restrict__ item_entry,
                                                         const ge_cached* __restrict__ ktab,
@@ -97,7 +106,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_fin(size_t stride, const uin
 }
 
 // uncached keys (the miss list, or every header): U on a per-lane chain
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_fin_nc(size_t n, const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_fin_nc(size_t n, const uint32_t* __restrict__ list,
                                                            const uint32_t* __restrict__ count,
                                                            const ge_niels* __restrict__ gbtab, VrfIn a,
                                                            const uint4* __restrict__ mid) {
@@ -112,7 +121,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_fin_nc(size_t n, const uint3
 
 // ---- three-kernel form (praos_core.hpp vrf_u_core / vrf_join_core): U apart from V
 // U of a cached key (the hit list): the key's tables and the radix-2^16 comb
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_u(size_t stride, const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_u(size_t stride, const uint32_t* __restrict__ list,
                                                       const uint32_t* __restrict__ count,
                                                       const int32_t* __restrict__ item_entry,
                                                       const ge_cached* __restrict__ ktab,
@@ -130,7 +139,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_u(size_t stride, const uint3
 
 // U of an uncached key (the miss list, or every header): a per-lane chain; vt = an 8-entry
 // lane table region of its own (stage V runs at the same time on the 16-entry one)
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_u_nc(size_t n, const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_u_nc(size_t n, const uint32_t* __restrict__ list,
                                                          const uint32_t* __restrict__ count,
                                                          const ge_niels* __restrict__ gbtab,
                                                          const uint8_t* __restrict__ vrf_vk,
@@ -151,7 +160,7 @@ __global__ void __launch_bounds__(NT, LB_VRF) k_vrf_u_nc(size_t n, const uint32_
 
 // join over every header: pool lookup and key hash (Praos.hs:533-541), the batched
 // inversion, the challenge, beta, the output check and the range extension
-__global__ void __launch_bounds__(NT, LB_VRF) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
+__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
