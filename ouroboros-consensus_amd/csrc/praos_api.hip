@@ -447,8 +447,11 @@ static bool open_streams(praos_ctx* c) {
       (void)hipStreamCreateWithPriority(&c->mside[k], hipStreamNonBlocking, hi ? greatest : least);
     }
     // the VRF's stage V is the longest chain of a batch and starts at once: greatest priority
-    (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, greatest);
-    (void)hipStreamCreateWithPriority(&c->vstream2, hipStreamNonBlocking, greatest);
+    // (PRAOS_V_PRIO=0: least, an A/B knob)
+    const char* vp = std::getenv("PRAOS_V_PRIO");
+    const int vprio = (vp && std::atoi(vp) == 0) ? least : greatest;
+    (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, vprio);
+    (void)hipStreamCreateWithPriority(&c->vstream2, hipStreamNonBlocking, vprio);
     (void)hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
     (void)hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking);
   }
