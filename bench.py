@@ -44,7 +44,7 @@ sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 # kernel schedules (tools/workmodel.py; DESIGN.md sec. 4 "Work model").
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  # noqa: E402
-                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES, W_VRF_V, W_VRF_TP, W_TP_HEADER)
+                       W_KES_CK, W_KEY_COLD, W_KEY_VRF, W_KEY_KES, W_VRF_V, W_VRF_TP, W_LEADER_TP)
 # gfx950 VALU peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
@@ -600,12 +600,19 @@ def main():
         # HIP events around its own launch (serial run, no other kernel on the GPU)
         dom_kernel, dom_ms, dom_work, wk = "k_vrf_v", float(kser[6]), n * W_VRF_V, W_VRF_V
     if args.config == "tp":
-        # the TPraos batch runs decode, k_ocert, k_kes, k_vrf_tp (two uncached certificates per
-        # lane) and k_leader; priced as one pipeline over the step
-        w_pipe = W_TP_HEADER
+        # the TPraos batch runs decode, the OCert / KES passes of the Praos step (dedup, key
+        # caches) and both VRF certificates through the staged kernels against the VRF key
+        # cache (k_vrf_v per certificate, U cached or per lane, k_vrf_join_tp; each priced as
+        # a Praos VRF verify), or with PRAOS_TP_STAGED=0 the one-kernel k_vrf_tp (two uncached
+        # certificates per lane, W_VRF_TP); priced as one pipeline over the step
+        w_vrf = (2 * (kst["vrf_hits"] * W_VRF_CK + kst["vrf_misses"] * W_VRF) + kst["vrf_keys"] * W_KEY_VRF
+                 if kst["vrf_keys"] else n * W_VRF_TP)
+        w_pipe = (work["ocert"] + work["kes"] + w_vrf) / n + W_LEADER_TP
         pipe_achieved = n * w_pipe / (kms[4] * 1e-3)
-        dom_kernel, dom_ms, dom_work, wk = "tpraos pipeline (k_ocert | k_kes | k_vrf_tp, k_leader)", float(kms[4]), \
-            n * W_TP_HEADER, W_TP_HEADER
+        dom_kernel, dom_ms, dom_work, wk = ("tpraos pipeline (OCert | KES | VRF V/U/join x 2 certificates, k_leader)"
+                                            if kst["vrf_keys"] else
+                                            "tpraos pipeline (OCert | KES | k_vrf_tp, k_leader)"), float(kms[4]), \
+            n * w_pipe, w_pipe
     dom_achieved = dom_work / (dom_ms * 1e-3)
     tk, traffic_src = load_traffic(dom_kernel, cfg["workload"])
     traffic = tk.get("bytes_per_launch") if tk else None

@@ -31,6 +31,8 @@ struct VrfIn {
   uint8_t* __restrict__ ok_out;
   ge_cached* __restrict__ tabs;          // per-lane tables (LT_VRF entries per item)
   int wave_prio;                         // stage V / join waves at s_setprio 3 (small batches)
+  int tp_seed;                           // stage V alpha: 0 Praos mkInputVRF; 1 + k TPraos mkSeed
+                                         // with ucNonce k (0 seedEta, 1 seedL)
 };
 
 // issuer pool: hashKey (Blake2b-224 of the cold vk, Praos.hs:552) -> sorted index or -1

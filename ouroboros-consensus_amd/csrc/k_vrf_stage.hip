@@ -13,14 +13,16 @@
 #endif
 
 // ---- two-stage form of the header mode (praos_core.hpp vrf_v_core / vrf_fin_core)
-// alpha = mkInputVRF(slot, eta) of header i (Praos/VRF.hs:55-69)
+// alpha = mkInputVRF(slot, eta) of header i (Praos/VRF.hs:55-69), or for a TPraos
+// certificate mkSeed(ucNonce, slot, eta) (TPraos.hs:378-387 -> BHeader.mkSeed)
 __device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, size_t i) {
   uint32_t e0[8];
   const uint32_t* ep = a.eta_idx ? a.eta0 + 9 * (uint32_t)a.eta_idx[i] : a.eta0;
 #pragma unroll
   for (int k = 0; k < 8; k++) e0[k] = ep[k];
   const bool neutral = a.eta_idx ? ep[8] != 0 : a.eta0_neutral != 0;
-  mk_input_vrf(alpha, a.slot[i], e0, neutral);
+  if (a.tp_seed) tpraos_seed(alpha, a.slot[i], e0, neutral, (uint64_t)(a.tp_seed - 1));
+  else mk_input_vrf(alpha, a.slot[i], e0, neutral);
 }
 
 // stage V over every header of the batch: no dependence on the key cache
@@ -214,13 +216,92 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join(size_t n, VrfIn a, co
   a.bits[i] = b;
 }
 
+// TPraos join of certificate `cert` (0: eta / nonce cert, 1: leader cert), the staged form of
+// k_vrf_tp: cert 0 classifies the slot (overlay classes from praos_set_overlay: -2 not
+// active, >= 0 a genesis delegate's slot checked against gen; else the pool lookup and VRF
+// key hash, Praos.hs:533-541 as TPraos.hs:304-387 uses them) and writes beta_eta + the nonce
+// (mkNonceFromOutputVRF of the stated output); cert 1 adds its bit to bits[i] and writes beta_l.
+// Runs after cert 0's join on the same stream (bits read-modify-write).
+__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join_tp(size_t n, int cert, VrfIn a,
+                                                            const uint4* __restrict__ mid,
+                                                            const int32_t* __restrict__ ovl_class,
+                                                            const uint32_t* __restrict__ gen) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t cls = ovl_class ? ovl_class[i] : -1;
+  uint16_t b = 0;
+  if (cert == 0) {
+    uint32_t pk[8], cv[8], hk[8];
+    load_words(cv, a.cold_vk + 32 * i, 8);
+    blake2b_32(hk, cv, 28);
+    load_words(pk, a.vrf_vk + 32 * i, 8);
+    int32_t sidx = -1;
+    if (cls == -2) {
+      b |= PRAOS_BIT_TP_NOT_ACTIVE;                  // NotActiveSlotOVERLAY
+    } else if (cls >= 0) {                           // pbftVrfChecks vs the genesis delegate
+      b |= PRAOS_BIT_TP_OVERLAY;
+      const uint32_t* gd = gen + 16 * cls;
+      bool cold_ok = true, vrf_ok = true;
+#pragma unroll
+      for (int k = 0; k < 7; k++) cold_ok &= hk[k] == gd[k];
+      uint32_t vh[8];
+      blake2b_32(vh, pk, 32);
+#pragma unroll
+      for (int k = 0; k < 8; k++) vrf_ok &= vh[k] == gd[8 + k];
+      if (!cold_ok) b |= PRAOS_BIT_TP_GEN_COLD;
+      if (!vrf_ok) b |= PRAOS_BIT_TP_GEN_VRF;
+    } else {
+      sidx = pool_search(hk, a.pool_hash, a.npools);
+      if (sidx < 0) {
+        b |= PRAOS_BIT_VRF_KEY_UNKNOWN;
+      } else {
+        uint32_t vh[8];
+        blake2b_32(vh, pk, 32);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < 8; k++) same &= vh[k] == a.pool_vrf[8 * sidx + k];
+        if (!same) b |= PRAOS_BIT_VRF_KEY_WRONG;
+      }
+    }
+    a.pool_idx[i] = sidx < 0 ? -1 : a.pool_map[sidx];
+    a.pool_sorted_idx[i] = sidx;
+  } else {
+    b = a.bits[i];
+  }
+  uint32_t c4[4];
+  {
+    const uint4 q = *(const uint4*)(a.vrf_proof + 80 * i + 32);
+    c4[0] = q.x; c4[1] = q.y; c4[2] = q.z; c4[3] = q.w;
+  }
+  uint32_t beta[16], out[16];
+  bool gamma_ok;
+  const bool ok = vrf_join_core(beta, gamma_ok, mid, n, i, c4);
+  if (!gamma_ok) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) beta[k] = 0;
+  }
+  load_words(out, a.vrf_out + 64 * i, 16);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < 16; k++) eq &= beta[k] == out[k];
+  if ((!ok || (a.check_output && !eq)) && cls != -2) b |= cert ? PRAOS_BIT_TP_VRF_LEADER : PRAOS_BIT_TP_VRF_NONCE;
+  store_words(a.beta_out + 64 * i, beta, 16);
+  if (cert == 0) {
+    uint32_t nn[8];
+    blake2b256_of64(nn, out);                        // mkNonceFromOutputVRF
+    store_words(a.nonce_out + 32 * i, nn, 8);
+  }
+  a.bits[i] = b;
+}
+
 // ---- host launchers (kernels are only launchable from their own module)
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
                   const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
-                  size_t i0, size_t i1, int wave_prio) {
+                  size_t i0, size_t i1, int wave_prio, int tp_seed) {
   VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
                    nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
   a.wave_prio = wave_prio;
+  a.tp_seed = tp_seed;
   const unsigned bs = lat_block(n);
   i1 = i1 < n ? i1 : n;
   if (i1 <= i0) return;
@@ -267,4 +348,16 @@ void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const
   a.wave_prio = wave_prio;
   const unsigned bs = lat_block(n);
   hipLaunchKernelGGL(k_vrf_join, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, a, (const uint4*)mid);
+}
+void launch_vrf_join_tp(hipStream_t stream, size_t n, int cert, const uint8_t* cold_vk, const uint8_t* vrf_vk,
+                        const uint8_t* cert_out, const uint8_t* cert_proof, const uint32_t* pool_hash,
+                        const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
+                        uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
+                        uint8_t* nonce_out, const void* mid, const int32_t* ovl_class, const uint32_t* gen) {
+  const VrfIn a = vrf_in(cold_vk, vrf_vk, cert_out, cert_proof, nullptr, nullptr, 0, nullptr, pool_hash, pool_vrf,
+                         pool_map, npools, check_output, bits, pool_idx, pool_sorted_idx, beta_out, nullptr,
+                         nonce_out, nullptr);
+  const unsigned bs = lat_block(n);
+  hipLaunchKernelGGL(k_vrf_join_tp, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, cert, a,
+                     (const uint4*)mid, ovl_class, gen);
 }

@@ -97,7 +97,8 @@ void launch_synth_corrupt(dim3 grid, dim3 block, hipStream_t stream, size_t n, u
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
                   const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
                   size_t i0 = 0, size_t i1 = SIZE_MAX,    // headers [i0, min(i1, n)); mid stride n
-                  int wave_prio = 0);                      // waves at s_setprio 3
+                  int wave_prio = 0,                       // waves at s_setprio 3
+                  int tp_seed = 0);                        // 1 + k: TPraos mkSeed alpha, ucNonce k
 void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
                     const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
@@ -115,6 +116,13 @@ void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                      uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
                      uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio = 0);
+// TPraos join of certificate cert (0: eta, 1: leader; k_vrf_stage.hip k_vrf_join_tp), after
+// stage V (tp_seed 1 + cert) and U of that certificate into `mid`
+void launch_vrf_join_tp(hipStream_t stream, size_t n, int cert, const uint8_t* cold_vk, const uint8_t* vrf_vk,
+                        const uint8_t* cert_out, const uint8_t* cert_proof, const uint32_t* pool_hash,
+                        const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
+                        uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
+                        uint8_t* nonce_out, const void* mid, const int32_t* ovl_class, const uint32_t* gen);
 void launch_vrf_tp(dim3 grid, dim3 block, hipStream_t stream, size_t n, const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* eta_out, const uint8_t* eta_proof, const uint8_t* l_out, const uint8_t* l_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint32_t* pool_hash, const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output, uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_eta, uint8_t* beta_l, uint8_t* nonce_out, ge_cached* tabs,
                    const int32_t* ovl_class, const uint32_t* gen, const uint8_t* eta_idx = nullptr);
 void launch_decode_praos(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* arena, uint64_t arena_len,

@@ -107,6 +107,8 @@ struct praos_ctx {
   hipEvent_t v_ev = nullptr, v2_ev = nullptr;
   hipEvent_t v0_ev = nullptr, v1_ev = nullptr;         // timing of k_vrf_v on its stream (kernel_ms[6])
   hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
+  int tp_staged = 1;                                  // TPraos VRF through the staged kernels + VRF key cache
+                                                       // (PRAOS_TP_STAGED=0: the one-kernel k_vrf_tp)
   int vrf_prio = 0;                                   // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO; -1: small batches)
   int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
                                                        // the three-kernel form below 300k headers (latency)
@@ -290,6 +292,8 @@ struct praos_batch {
   ge_cached* tab_vrfu = nullptr;   // 8-entry lane tables of stage U on uncached VRF keys
   bool v_done = false;             // stage V already queued on ctx->vstream (stored-bytes pipeline)
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
+  uint8_t* vrf_mid2 = nullptr;  // TPraos: the leader certificate's record (allocated on first use)
+  size_t vrf_mid2_n = 0;
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
     uint32_t cap = 0, max_entries = 0;
@@ -424,6 +428,7 @@ static bool open_streams(praos_ctx* c) {
   (void)hipEventCreateWithFlags(&c->u_ev, hipEventDisableTiming);
   if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_VRF_PRIO")) c->vrf_prio = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -1087,7 +1092,55 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
   const bool do_vrf = (c->kernels & 4) != 0;
-  if (do_vrf && b->tp_only) {
+  if (do_vrf && b->tp_only && c->tp_staged) {
+    // TPraos, staged: stage V of both certificates (mkSeed alphas) on the V stream from ev[0]
+    // on, U of both against the VRF key cache (misses on the miss stream at once, hits after
+    // the key tables), then the two joins in order on the VRF stream
+    const size_t cap = std::max(n, b->cap_n);
+    if (!b->vrf_mid2 || b->vrf_mid2_n < n) {
+      if (dalloc(b, &b->vrf_mid2, VRF_MID_BYTES * cap) != hipSuccess) return PRAOS_E_OOM;
+      b->vrf_mid2_n = cap;
+    }
+    const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
+    const uint8_t* proof[2] = {b->vrf_proof, b->lead_proof};
+    const uint8_t* outv[2] = {b->vrf_out, b->lead_out};
+    uint8_t* mid[2] = {b->vrf_mid, b->vrf_mid2};
+    uint8_t* beta[2] = {b->beta, b->beta_l};
+    hipStream_t sV = c->concurrent ? c->vstream : c->stream;
+    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < 300000);
+    if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
+    HIPCHK(c, hipEventRecord(c->v0_ev, sV));
+    for (int k = 0; k < 2; k++)
+      launch_vrf_v(sV, n, b->vrf_vk, proof[k], b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf, mid[k], 0,
+                   SIZE_MAX, wprio, 1 + k);
+    HIPCHK(c, hipEventRecord(c->v1_ev, sV));
+    c->v_timed = true;
+    HIPCHK(c, hipEventRecord(c->v_ev, sV));
+    if (kc) {
+      praos_batch::KeyCache& k = b->kc[1];
+      int r = keycache_lists(k, b->vrf_vk, sv);
+      if (r == PRAOS_OK) r = to_main(2, sv);
+      if (r != PRAOS_OK) return r;
+      for (int q = 0; q < 2; q++)
+        launch_vrf_u(sm_[2], n, k.miss, k.counters + 2, nullptr, nullptr, nullptr, c->bcomb16, c->btab, b->vrf_vk,
+                     proof[q], b->tab_vrfu, mid[q]);
+      if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
+      keycache_precompute(k, b->vrf_vk, 1, sv);
+      for (int q = 0; q < 2; q++)
+        launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, c->btab, b->vrf_vk,
+                     proof[q], b->tab_vrfu, mid[q]);
+      if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
+    } else {
+      for (int q = 0; q < 2; q++)
+        launch_vrf_u(sv, n, nullptr, nullptr, nullptr, nullptr, nullptr, c->bcomb16, c->btab, b->vrf_vk, proof[q],
+                     b->tab_vrfu, mid[q]);
+    }
+    if (sv != sV) HIPCHK(c, hipStreamWaitEvent(sv, c->v_ev, 0));
+    for (int q = 0; q < 2; q++)
+      launch_vrf_join_tp(sv, n, q, b->cold_vk, b->vrf_vk, outv[q], proof[q], c->d_pool_hash, c->d_pool_vrf,
+                         c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, beta[q],
+                         b->nonce, mid[q], dcls, c->d_gen);
+  } else if (do_vrf && b->tp_only) {
     launch_vrf_tp(g, blk, sv, n, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->lead_out, b->lead_proof,
                   b->slot, b->eta_tab ? b->eta_tab : c->d_eta0, c->eta0_neutral, c->d_pool_hash, c->d_pool_vrf,
                   c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, b->beta_l,

@@ -53,6 +53,37 @@ def test_tpraos_synth_chain_parity(ctx, oracle):
     assert 0 < sum(1 for i in clean if not int(o["bits"][i]) & 0x1000) < len(clean)
 
 
+def test_tpraos_staged_equals_one_kernel(ctx):
+    """The staged TPraos VRF (stage V per certificate with its mkSeed input, U against the VRF
+    key cache -- hits and per-lane misses --, k_vrf_join_tp) against the one-kernel k_vrf_tp
+    (PRAOS_TP_STAGED=0, two uncached certificates per lane) on the same corrupted chain:
+    every output bit for bit."""
+    import praos_hip
+    from praos_hip import fixed
+    p, c_raw = _params(Fraction(1, 2))
+    eta0 = b2b(b"tpraos-staged")
+    n, npools = 3000, 1500          # ~2 headers per VRF key: about a quarter used once (cache misses)
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, b"\x35" * 32, first_slot=9000, slot_stride=2,
+                                         corrupt_per_10000=1200, tpraos=True)
+    pool_list = [(h, v, fixed.from_rational(Fraction(1, npools))) for (h, v) in pools]
+    ctx.set_epoch(eta0, pool_list, p)
+    o = ctx.verify_tpraos_headers(H)
+    os.environ["PRAOS_TP_STAGED"] = "0"
+    try:
+        c2 = praos_hip.Context(0)
+    finally:
+        del os.environ["PRAOS_TP_STAGED"]
+    try:
+        c2.set_epoch(eta0, pool_list, p)
+        o2 = c2.verify_tpraos_headers(H)
+    finally:
+        c2.close()
+    assert set(o) == set(o2)
+    for k in o:
+        assert np.array_equal(np.asarray(o[k]), np.asarray(o2[k])), k
+    assert np.count_nonzero(corrupted) and any(int(x) & (0x0400 | 0x0800) for x in o["bits"])
+
+
 def test_tpraos_golden_blocks(ctx):
     """The golden TPraos blocks: OCert and KES verify, both certificates' proof_to_hash
     equal the stored outputs.  Their VRF inputs are the example's dummy seeds, not
