@@ -49,7 +49,7 @@ from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  #
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03d_traffic.json")   # tools/profile.sh r03d
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03e_traffic.json")   # tools/profile.sh r03e
 FEMUL_FILE = os.path.join(ROOT, "profiles", "r02", "femul_microbench.txt")  # tools/microbench/femul.hip
 
 
