@@ -915,6 +915,8 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
     }
     if (hipEventRecord(c->v_ev, c->vstream) != hipSuccess || hipStreamWaitEvent(c->stream, c->v_ev, 0) != hipSuccess)
       (void)hipStreamSynchronize(c->vstream);
+    if (hipEventRecord(c->v2_ev, c->vstream2) != hipSuccess || hipStreamWaitEvent(c->stream, c->v2_ev, 0) != hipSuccess)
+      (void)hipStreamSynchronize(c->vstream2);
   }
   return r;
 }
