@@ -293,6 +293,7 @@ struct praos_batch {
   bool v_done = false;             // stage V already queued on ctx->vstream (stored-bytes pipeline)
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   uint8_t* vrf_mid2 = nullptr;  // TPraos: the leader certificate's record (allocated on first use)
+  ge_cached* tab_vrf2 = nullptr; // TPraos: the leader certificate's stage-V lane tables
   size_t vrf_mid2_n = 0;
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
@@ -1100,7 +1101,9 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     // the key tables), then the two joins in order on the VRF stream
     const size_t cap = std::max(n, b->cap_n);
     if (!b->vrf_mid2 || b->vrf_mid2_n < n) {
-      if (dalloc(b, &b->vrf_mid2, VRF_MID_BYTES * cap) != hipSuccess) return PRAOS_E_OOM;
+      if (dalloc(b, &b->vrf_mid2, VRF_MID_BYTES * cap) != hipSuccess ||
+          dalloc(b, (uint8_t**)&b->tab_vrf2, LT_VRF_B * cap) != hipSuccess)
+        return PRAOS_E_OOM;
       b->vrf_mid2_n = cap;
     }
     const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
@@ -1108,16 +1111,21 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     const uint8_t* outv[2] = {b->vrf_out, b->lead_out};
     uint8_t* mid[2] = {b->vrf_mid, b->vrf_mid2};
     uint8_t* beta[2] = {b->beta, b->beta_l};
-    hipStream_t sV = c->concurrent ? c->vstream : c->stream;
+    // the two certificates' stage V side by side (own lane tables): a batch below ~300k
+    // headers leaves most wave slots empty with one V at a time
+    hipStream_t sVk[2] = {c->concurrent ? c->vstream : c->stream, c->concurrent ? c->vstream2 : c->stream};
+    ge_cached* vtab[2] = {b->tab_vrf, b->tab_vrf2};
     const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < 300000);
-    if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
-    HIPCHK(c, hipEventRecord(c->v0_ev, sV));
-    for (int k = 0; k < 2; k++)
-      launch_vrf_v(sV, n, b->vrf_vk, proof[k], b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf, mid[k], 0,
+    for (int k = 0; k < 2; k++) {
+      if (sVk[k] != c->stream) HIPCHK(c, hipStreamWaitEvent(sVk[k], c->ev[0], 0));
+      if (k == 0) HIPCHK(c, hipEventRecord(c->v0_ev, sVk[0]));
+      launch_vrf_v(sVk[k], n, b->vrf_vk, proof[k], b->slot, eta, c->eta0_neutral, b->eta_idx, vtab[k], mid[k], 0,
                    SIZE_MAX, wprio, 1 + k);
-    HIPCHK(c, hipEventRecord(c->v1_ev, sV));
+    }
+    HIPCHK(c, hipEventRecord(c->v1_ev, sVk[0]));
     c->v_timed = true;
-    HIPCHK(c, hipEventRecord(c->v_ev, sV));
+    HIPCHK(c, hipEventRecord(c->v_ev, sVk[0]));
+    HIPCHK(c, hipEventRecord(c->v2_ev, sVk[1]));
     if (kc) {
       praos_batch::KeyCache& k = b->kc[1];
       int r = keycache_lists(k, b->vrf_vk, sv);
@@ -1137,7 +1145,8 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         launch_vrf_u(sv, n, nullptr, nullptr, nullptr, nullptr, nullptr, c->bcomb16, c->btab, b->vrf_vk, proof[q],
                      b->tab_vrfu, mid[q]);
     }
-    if (sv != sV) HIPCHK(c, hipStreamWaitEvent(sv, c->v_ev, 0));
+    if (sv != sVk[0]) HIPCHK(c, hipStreamWaitEvent(sv, c->v_ev, 0));
+    if (sv != sVk[1]) HIPCHK(c, hipStreamWaitEvent(sv, c->v2_ev, 0));
     for (int q = 0; q < 2; q++)
       launch_vrf_join_tp(sv, n, q, b->cold_vk, b->vrf_vk, outv[q], proof[q], c->d_pool_hash, c->d_pool_vrf,
                          c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, beta[q],
