@@ -595,7 +595,7 @@ def main():
     dom_kernel = f"k_{dominant}_ck" if (args.keycache and kst.get(f"{'cold' if dominant == 'ocert' else dominant}_hits")) \
         else f"k_{dominant}"
     if dominant == "vrf" and kser[6] > 0:
-        # the VRF runs in two kernels (k_vrf.hip): stage V (H, Gamma, V = [s]H - [c]Gamma) over
+        # the VRF runs in stages (k_vrf_stage.hip): stage V (H, Gamma, V = [s]H - [c]Gamma) over
         # every header is the largest single kernel of the step; price it alone, on the
         # HIP events around its own launch (serial run, no other kernel on the GPU)
         dom_kernel, dom_ms, dom_work, wk = "k_vrf_v", float(kser[6]), n * W_VRF_V, W_VRF_V

@@ -1157,7 +1157,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                   c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta, b->beta_l,
                   b->nonce, b->tab_vrf, dcls, c->d_gen, b->eta_idx);
   } else if (do_vrf) {
-    // two stages (k_vrf.hip): V over every header on its own stream, from ev[0] on (it
+    // two stages (k_vrf_stage.hip): V over every header on its own stream, from ev[0] on (it
     // needs no key); F after it -- the hits on sv once their key tables exist, the misses
     // on their miss stream (per-lane U)
     const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
