@@ -78,9 +78,17 @@ def test_tpraos_staged_equals_one_kernel(ctx):
         o2 = c2.verify_tpraos_headers(H)
     finally:
         c2.close()
-    assert set(o) == set(o2)
-    for k in o:
-        assert np.array_equal(np.asarray(o[k]), np.asarray(o2[k])), k
+    # and the staged form with every kernel on the ctx stream (no side / V streams)
+    from praos_hip import abi
+    ctx.set_option(abi.OPT_CONCURRENT, 0)
+    try:
+        o3 = ctx.verify_tpraos_headers(H)
+    finally:
+        ctx.set_option(abi.OPT_CONCURRENT, 1)
+    for oo in (o2, o3):
+        assert set(o) == set(oo)
+        for k in o:
+            assert np.array_equal(np.asarray(o[k]), np.asarray(oo[k])), k
     assert np.count_nonzero(corrupted) and any(int(x) & (0x0400 | 0x0800) for x in o["bits"])
 
 
