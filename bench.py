@@ -76,7 +76,8 @@ CONFIGS = {
                workload="configs[1]: 1M OCert Ed25519 verifications, distinct cold keys, 1% corrupted"),
     "c3": dict(items=1_000_000, pools=3000, kernels=4, nkes=0, metric="ECVRF-draft03 verifies + leader checks/sec",
                workload="configs[2]: 1M ECVRF-ED25519-SHA512-Elligator2 verifies + leader checks, single eta0, "
-                        "3000 pools, 1% corrupted"),
+                        "3000 pools, the (slot, pool) pairs of the first 1M blocks of a first-leader-wins "
+                        "schedule (every clean item a leader), 1% corrupted"),
     "c4": dict(items=1_000_000, pools=3000, kernels=2, nkes=0, metric="Sum6KES verifications/sec",
                workload="configs[3]: 1M Sum6KES verifies (depth-6 Blake2b-256 Merkle path + Ed25519 leaf), "
                         "397-byte messages, 1% corrupted"),
@@ -291,57 +292,12 @@ def load_traffic(kernel, workload):
 
 
 def make_input(ctx, args, cfg, rank, world=1):
-    """Returns (H, pool_list, corrupted, params, eta0, c_raw, spkp, maxevo).  Strong
-    scaling: rank r signs blocks [r*n/world, (r+1)*n/world) of the chain."""
-    from praos_hip import abi, chains, fixed
-    import hashlib
-    if args.config in ("c1", "c5"):
-        ccfg = chains.CONFIGS[args.config]
-        if args.config == "c5":
-            sched = chains.load_schedule("c5")
-        else:
-            sched = chains.search_schedule(ctx, ccfg, ccfg["blocks"])
-        n = args.items or cfg["items"]
-        assert n <= len(sched[0]), "the shipped schedule has fewer blocks"
-        if args.scaling == "strong":
-            a, b = n * rank // world, n * (rank + 1) // world
-            sched, n = (sched[0][a:b], sched[1][a:b]), b - a
-        H, pool_list, corrupted, p = chains.make_chain(ctx, ccfg, sched, n=n,
-                                                       corrupt_per_10000=args.corrupt_per_10000)
-        return (H, pool_list, corrupted, p, ccfg["eta0"], fixed.active_slot_log(ccfg["f"]),
-                ccfg["slots_per_kes_period"], ccfg["max_kes_evo"])
-    if args.config == "tp":
-        # TPraos headers (two VRF certificates, the 2^512 leader bound): f = 1 and the pools in
-        # turn, so every header is leader-valid without a schedule search (checkLeaderNatValue's
-        # f = 1 case); stored as BHeader bytes and decoded on the device in every run
-        from fractions import Fraction
-        n = args.items or cfg["items"]
-        ccfg = dict(npools=cfg["pools"], stake_offset=10, f=Fraction(1), slots_per_kes_period=129600,
-                    max_kes_evo=62, eta0=hashlib.blake2b(b"bench-tpraos-nonce", digest_size=32).digest())
-        p = chains.params(ccfg)
-        sl = np.arange(rank * n, (rank + 1) * n, dtype=np.uint64)
-        pl = (sl % cfg["pools"]).astype(np.uint32)
-        H, keys, corrupted = ctx.synthesize(n, cfg["pools"], p, ccfg["eta0"], b"TP" + b"\x5c" * 26 + rank.to_bytes(4, "little"),
-                                            body_len=0, schedule=(sl, pl), tpraos=True,
-                                            corrupt_per_10000=args.corrupt_per_10000)
-        pool_list = [(h, v, s_) for (h, v), s_ in zip(keys, chains.stake(cfg["pools"], 10))]
-        return H, pool_list, corrupted, p, ccfg["eta0"], 0, 129600, 62
-    # single-primitive configs: evenly spaced slots, pools by hash (not a leader-valid chain)
-    n = args.items or cfg["items"]
-    npools = cfg["pools"] or n
-    from fractions import Fraction
-    c_raw = fixed.active_slot_log(Fraction(1, 20))
-    p = abi.params(slots_per_kes_period=129600, max_kes_evo=62, c_raw=c_raw, vrf_check_output=True)
-    eta0 = hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest()
-    # corruptions only in the fields the config's check reads (SURVEY 8(d): 1 % means 1 %)
-    fields = {"c2": abi.CORRUPT_OCERT, "c3": abi.CORRUPT_VRF_PROOF | abi.CORRUPT_VRF_OUT,
-              "c4": abi.CORRUPT_KES_SIG | abi.CORRUPT_BODY}[args.config]
-    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, (b"\x5a" * 27) + bytes([int(args.config[1])]) +
-                                         rank.to_bytes(4, "little"), first_slot=rank * n * 20, slot_stride=20,
-                                         body_len=397, corrupt_per_10000=args.corrupt_per_10000, nkes=cfg["nkes"],
-                                         corrupt_fields=fields)
-    pool_list = [] if cfg["pools"] is None else [(h, v, s) for (h, v), s in zip(pools, chains.stake(npools, 10))]
-    return H, pool_list, corrupted, p, eta0, c_raw, 129600, 62
+    """Returns (H, pool_list, corrupted, params, eta0, c_raw, spkp, maxevo) of the config
+    (praos_hip/configs.py, shared with the full-size -m gpu tests).  Strong scaling: rank r
+    signs blocks [r*n/world, (r+1)*n/world) of the chain."""
+    from praos_hip import configs
+    return configs.build(ctx, args.config, n=args.items or cfg["items"], corrupt_per_10000=args.corrupt_per_10000,
+                         rank=rank, world=world, scaling=args.scaling)
 
 
 def main():
@@ -391,16 +347,12 @@ def main():
     import praos_hip
     from praos_hip import abi
 
+    from praos_hip import configs
     ctx = praos_hip.Context(local)
-    ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
-    ctx.set_option(abi.OPT_KERNELS, cfg["kernels"])
-    ctx.set_option(abi.OPT_KEYCACHE, args.keycache)
     # the dedup belongs to the header pipeline (c1/c5: a chain repeats each pool's OCert);
     # the single-primitive configs measure every signature on its own
-    if cfg["kernels"] != 7 or args.config == "tp":
-        args.dedup = 0
-    ctx.set_option(abi.OPT_DEDUP, args.dedup)
-    ctx.set_option(abi.OPT_PIPELINE, args.pipeline)
+    args.dedup = configs.options(ctx, args.config, concurrent=args.concurrent, keycache=args.keycache,
+                                 dedup=args.dedup, pipeline=args.pipeline)
     t0 = time.perf_counter()
     H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = make_input(ctx, args, cfg, rank, world)
     n = len(H["slot"])
@@ -563,7 +515,7 @@ def main():
     clean_ok = int((crypto_bits[clean] == 0).sum())
     corrupt_caught = int((crypto_bits[~clean] != 0).sum())
     # corruptions that land in a field the config does not check cannot be caught
-    relevant = {1: (1,), 2: (2, 5), 4: (3, 4), 7: (1, 2, 3, 4, 5)}[cfg["kernels"]]
+    relevant = configs.CHECKED_KINDS[cfg["kernels"]]
     rel = np.isin(corrupted, relevant)
     corrupt_caught_rel = int((crypto_bits[rel] != 0).sum())
 

@@ -96,6 +96,34 @@ static constexpr int PIPE_AUTO = 6;                 // chunks in auto mode (432k
                                                     // 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt)
 struct praos_batch;
 
+// The context's last error.  The replay's worker threads (reader, nonce chain, launcher,
+// fold) can fail at the same time, so every assignment takes a lock; while a replay runs
+// (first_only) only the first message of the call is kept -- the one that stopped it.
+class ErrMsg {
+ public:
+  ErrMsg& operator=(const std::string& m) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!(first_ && held_)) s_ = m;
+    held_ = true;
+    return *this;
+  }
+  ErrMsg& operator=(const char* m) { return *this = std::string(m); }
+  const char* c_str() {
+    std::lock_guard<std::mutex> g(mu_);
+    return s_.c_str();
+  }
+  void first_only(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    first_ = on;
+    held_ = false;
+  }
+
+ private:
+  std::mutex mu_;
+  std::string s_;
+  bool first_ = false, held_ = false;
+};
+
 struct praos_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -132,7 +160,7 @@ struct praos_ctx {
   float kernel_ms[7] = {0, 0, 0, 0, 0, 0, 0};
   bool last_from_bytes = false;
   bool v_timed = false;                                // the last run launched k_vrf_v
-  std::string err;
+  ErrMsg err;
   ge_niels* btab = nullptr;
   ge_niels* bcomb16 = nullptr;                         // radix-2^16 comb of the cached-key chains (48 MB)
   // epoch
@@ -295,6 +323,12 @@ struct praos_batch {
   uint8_t* vrf_mid2 = nullptr;  // TPraos: the leader certificate's record (allocated on first use)
   ge_cached* tab_vrf2 = nullptr; // TPraos: the leader certificate's stage-V lane tables
   size_t vrf_mid2_n = 0;
+  // TPraos overlay classes of the batch's slots (praos_set_overlay): device copy sized once
+  // per capacity, host arrays kept with the batch (the async upload reads them)
+  int32_t* dcls = nullptr;
+  size_t dcls_n = 0;
+  std::vector<uint64_t> slots_h;
+  std::vector<int32_t> cls_h;
   // per-run public-key cache (k_keys.hip): [0] cold keys (OCert), [1] VRF keys, [2] KES leaf keys
   struct KeyCache {
     uint32_t cap = 0, max_entries = 0;
@@ -974,13 +1008,20 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   // praos_set_overlay is on) and the leader test takes the certified L output, 2^512 bound
   int32_t* dcls = nullptr;
   if (b->tp_only && c->ovl_on) {
-    std::vector<uint64_t> slots(n);
+    // the slots come from the decode on this stream; the sync also retires the previous
+    // run's upload of cls_h before it is rewritten
+    b->slots_h.resize(n);
+    b->cls_h.resize(n);
+    HIPCHK(c, hipMemcpyAsync(b->slots_h.data(), b->slot, 8 * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(slots.data(), b->slot, 8 * n, hipMemcpyDeviceToHost));
-    std::vector<int32_t> cls(n);
-    for (size_t i = 0; i < n; i++) cls[i] = overlay_class(c, slots[i]);
-    if (dalloc(b, &dcls, 4 * n) != hipSuccess) return PRAOS_E_OOM;
-    HIPCHK(c, hipMemcpy(dcls, cls.data(), 4 * n, hipMemcpyHostToDevice));
+    for (size_t i = 0; i < n; i++) b->cls_h[i] = overlay_class(c, b->slots_h[i]);
+    if (!b->dcls || b->dcls_n < n) {
+      const size_t cap = std::max(n, b->cap_n);
+      if (dalloc(b, &b->dcls, 4 * cap) != hipSuccess) return PRAOS_E_OOM;
+      b->dcls_n = cap;
+    }
+    dcls = b->dcls;
+    HIPCHK(c, hipMemcpyAsync(dcls, b->cls_h.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
   }
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
@@ -1523,6 +1564,7 @@ praos_batch* rp_batch_alloc(praos_ctx* c, size_t n_cap, size_t bytes_cap, bool t
   bool ok = dalloc(b, &b->eta_tab, 9 * 4 * 256) == hipSuccess && dalloc(b, &b->eta_idx, b->cap_n) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&b->dec_ev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&b->run_ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventRecord(b->run_ev, c->stream) == hipSuccess;     // recorded once: waits on it are defined
   ok = ok && hipHostMalloc((void**)&b->eta_h, 9 * 4 * 256, hipHostMallocDefault) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&b->eidx_h, b->cap_n, hipHostMallocDefault) == hipSuccess;
   if (!ok) { rp_batch_destroy(c, b); return nullptr; }
@@ -1551,6 +1593,12 @@ praos_batch* rp_batch_take(praos_ctx* c, int k, size_t n, size_t bytes, bool tpr
   if (b && rp_batch_fits(b, n, bytes) && b->tp_only == tpraos) return b;
   rp_batch_destroy(c, b);
   return rp_batch_alloc(c, n + n / 8 + 64, bytes + bytes / 8 + 4096, tpraos);
+}
+
+void rp_batch_quiesce(praos_batch* b) {
+  if (!b) return;
+  if (b->dec_ev) (void)hipEventSynchronize(b->dec_ev);
+  if (b->run_ev) (void)hipEventSynchronize(b->run_ev);
 }
 
 void rp_batch_keep(praos_ctx* c, int k, praos_batch* b) {
@@ -1597,6 +1645,8 @@ int rp_upload_decode(praos_ctx* c, praos_batch* b, size_t n, const praos_span* s
   for (size_t j = 0; j < nspans; j++) bytes += spans[j].len;
   if (!c || !b || !rp_batch_fits(b, n, bytes) || (n && (!hoff || !hlen))) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
+  // the batch's previous crypto run (ctx stream) reads the buffers rewritten below
+  HIPCHK(c, hipStreamWaitEvent(c->cstream, b->run_ev, 0));
   b->n = n;
   b->arena_len = bytes;
   b->body_bytes_len = (size_t)b->signed_stride * n;
@@ -2044,6 +2094,7 @@ using praos_host::nonce_eq;
 
 // error text for the other host modules of the library (praos_replay.hip)
 void praos_set_error_(praos_ctx* c, const std::string& m) { if (c) c->err = m; }
+void praos_error_first_only_(praos_ctx* c, bool on) { if (c) c->err.first_only(on); }
 
 extern "C" {
 

@@ -54,6 +54,7 @@
 #include <vector>
 
 void praos_set_error_(praos_ctx* c, const std::string& m);   // praos_api.hip
+void praos_error_first_only_(praos_ctx* c, bool on);         // (the replay keeps its first error)
 
 namespace {
 
@@ -501,6 +502,10 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
   folder.join();
   for (int k = 0; k < SLOTS; k++) {
     Slot& C = S[k];
+    // a replay that stopped early may have queued the crypto of up to two later batches:
+    // they finish before the batch goes back to the context (the next call's upload
+    // overwrites its buffers; rp_upload_decode also orders itself after run_ev)
+    if (C.b) rp_batch_quiesce(C.b);
     if (C.b) rp_batch_keep(ctx, k, C.b);
     if (C.bits) (void)hipHostFree(C.bits);
     if (C.pidx) (void)hipHostFree(C.pidx);
@@ -529,8 +534,11 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
                                       const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                                       praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
                                       size_t verdicts_cap, praos_replay_stats* stats) {
-  return replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap, stats,
-                     false, nullptr);
+  praos_error_first_only_(ctx, true);
+  const int r = replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap,
+                            stats, false, nullptr);
+  praos_error_first_only_(ctx, false);
+  return r;
 }
 
 extern "C" int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, const praos_pool* pools,
@@ -538,6 +546,9 @@ extern "C" int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, co
                                              const praos_nonce* extra_entropy, praos_envelope* env,
                                              praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
                                              uint16_t* failures, size_t verdicts_cap, praos_replay_stats* stats) {
-  return replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap, stats,
-                     true, extra_entropy);
+  praos_error_first_only_(ctx, true);
+  const int r = replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap,
+                            stats, true, extra_entropy);
+  praos_error_first_only_(ctx, false);
+  return r;
 }

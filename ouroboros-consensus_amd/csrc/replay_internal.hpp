@@ -21,6 +21,8 @@ bool rp_batch_fits(const praos_batch* b, size_t n, size_t bytes);
 constexpr int RP_SLOTS = 3;
 praos_batch* rp_batch_take(praos_ctx* c, int k, size_t n, size_t bytes, bool tpraos);
 void rp_batch_keep(praos_ctx* c, int k, praos_batch* b);
+// Waits for the batch's last decode and crypto run (a stopped replay leaves queued runs).
+void rp_batch_quiesce(praos_batch* b);
 // Copy stream: the spans' concatenation (the arena) and the per-header (offset, length) go
 // H2D through the pinned staging buffers, then decode and the nonce value of each header's
 // certified VRF output (k_vrf_nonce).  Returns once the host side is queued.

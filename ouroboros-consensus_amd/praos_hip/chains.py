@@ -51,14 +51,18 @@ def params(cfg, vrf_check_output=True):
                       vrf_check_output=vrf_check_output)
 
 
-def search_schedule(ctx, cfg, blocks, first_slot=0, window=200_000, progress=None):
-    """First-leader-wins forgers from first_slot until `blocks` blocks exist.
-    Returns (slots u64[blocks], pools u32[blocks])."""
+def search_schedule(ctx, cfg, blocks, first_slot=0, window=200_000, progress=None, max_seconds=None):
+    """First-leader-wins forgers from first_slot until `blocks` blocks exist (or, with
+    max_seconds, the whole windows searched by then).  Returns (slots u64[], pools u32[])."""
+    import time
+    t0 = time.time()
     sig = stake(cfg["npools"], cfg["stake_offset"])
     p = params(cfg)
     slots, pools = [], []
     s0, found = first_slot, 0
-    while found < blocks:
+    if blocks <= 0:
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint32)
+    while found < blocks and (max_seconds is None or time.time() - t0 < max_seconds):
         lead = ctx.leader_schedule(cfg["seed"], sig, p, cfg["eta0"], s0, window)
         idx = np.nonzero(lead >= 0)[0]
         slots.append((s0 + idx).astype(np.uint64))

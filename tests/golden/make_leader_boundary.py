@@ -23,6 +23,9 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "ouroboros-consensus_amd"))
 
 R = 10 ** 34
+C_RAW_NOTE = ("unpinned: c_raw = activeSlotLog f from praos_hip/fixed.py's restatement of cardano-ledger-core "
+              "ln' (not vendored; constants recalled); the vectors pin the decision GIVEN c_raw, so a later "
+              "correction of ln' changes c_raw and the boundaries without being a regression")
 
 
 def leader_python(l, bound_bits, sigma_fp, c_raw):
@@ -78,8 +81,9 @@ def main():
             assert [v["is_leader"] for v in vec] == [True, True, False, False]
             out.append({"bits": bits, "sigma": f"{sigma.numerator}/{sigma.denominator}",
                         "f": f"{f.numerator}/{f.denominator}", "sigma_fp": str(s_fp), "c_raw": str(c_raw),
+                        "c_raw_parity": "unpinned",
                         "boundary": hex(hi), "vectors": vec})
-    json.dump({"generator": "tests/golden/make_leader_boundary.py", "cases": out},
+    json.dump({"generator": "tests/golden/make_leader_boundary.py", "c_raw_parity": C_RAW_NOTE, "cases": out},
               open(os.path.join(HERE, "leader_boundary.json"), "w"), indent=1)
     print(len(out), "cases;", "max iterations", max(v["iterations"] for c in out for v in c["vectors"]))
 

@@ -1,0 +1,80 @@
+"""BASELINE.json configs[1..3] at their stated size: 1,000,000 items each, built exactly as
+bench.py builds them (praos_hip/configs.py) and run with the bench's context options, through
+the C ABI (praos_batch_upload / praos_batch_run / praos_batch_download).
+
+  c2: OCert Ed25519 (Praos.hs:574-580 -> Ed25519DSIGN verify over hot vk || n || c0), 1M
+      distinct cold keys;
+  c3: ECVRF-draft03 verify + certified output + checkLeaderNatValue (Praos.hs:528-556), the
+      (slot, pool) pairs of a first-leader-wins schedule, so every clean item is a leader;
+  c4: Sum6KES verify (Praos.hs:582, KES.Sum verifyKES: Merkle path + leaf Ed25519) over
+      397-byte messages.
+
+Each asserts: every clean item accepted, every corruption in a field the config checks
+rejected, and a ~200-item sample (evenly spaced + corrupted ones) bit-exact against the
+oracle (bits; for c3 also beta and the leader value)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+OCERT_BAD, KES_MERKLE, KES_LEAF = 0x0004, 0x0008, 0x0010
+VRF_MASK = 0x1F00          # pool unknown, VRF key wrong, proof, output, leader
+
+
+def _hdr(H, i):
+    off, ln = int(H["body_off"][i]), int(H["body_len"][i])
+    return {"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
+            "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
+            "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
+            "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
+            "body": bytes(H["body_bytes"][off:off + ln])}
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c4"])
+def test_config_full_size(ctx, oracle, name):
+    from praos_hip import configs
+    n = configs.ITEMS[name]
+    H, pool_list, corrupted, p, eta0, c_raw, spkp, maxevo = configs.build(ctx, name)
+    assert len(H["slot"]) == n == 1_000_000
+    try:
+        configs.options(ctx, name)
+        ctx.set_epoch(eta0, pool_list, p)
+        b = ctx.upload(H)
+        try:
+            ctx.run(b)
+            ctx.sync()
+            out = ctx.download(b, n)
+        finally:
+            ctx.free(b)
+    finally:
+        configs.options(ctx, "c5")                 # the session context's defaults
+    bits = out["bits"]
+    kernels = configs.KERNELS[name]
+    clean = corrupted == 0
+    # the leader test runs only with the VRF (c3); c2 / c4 carry no leader verdict
+    crypto = bits if name == "c3" else bits & ~np.uint16(0x1000)
+    assert int((crypto[clean] != 0).sum()) == 0, np.nonzero(crypto[clean])[0][:8]
+    rel = np.isin(corrupted, configs.CHECKED_KINDS[kernels])
+    assert rel.sum() == (~clean).sum() > 8_000            # corruptions only in checked fields
+    assert int((crypto[rel] == 0).sum()) == 0, np.nonzero(rel & (crypto == 0))[0][:8]
+    if name == "c3":
+        assert int(((bits & 0x1000) == 0)[clean].sum()) == int(clean.sum())   # every clean item a leader
+    # the oracle on ~200 items
+    sample = sorted(set(np.linspace(0, n - 1, 150).astype(int).tolist() +
+                        np.nonzero(~clean)[0][::max(1, int((~clean).sum()) // 50)][:50].tolist()))
+    if name == "c3":
+        ep = oracle.make_epoch(eta0, spkp, maxevo, c_raw, pool_list)
+    for i in sample:
+        h = _hdr(H, i)
+        if name == "c2":
+            m = h["hot_vk"] + h["n"].to_bytes(8, "big") + h["c0"].to_bytes(8, "big")
+            want = 0 if oracle.ed25519_verify(h["cold_vk"], m, h["ocert_sig"]) else OCERT_BAD
+            assert int(bits[i]) & OCERT_BAD == want, (i, corrupted[i])
+        elif name == "c4":
+            r = oracle.kes_verify(h["hot_vk"], max(h["slot"] // spkp - h["c0"], 0), h["body"], h["kes_sig"])
+            want = {0: 0, 1: KES_MERKLE, 2: KES_LEAF}[r]
+            assert int(bits[i]) & (KES_MERKLE | KES_LEAF) == want, (i, corrupted[i])
+        else:
+            r = oracle.praos_header(ep, h)
+            assert int(bits[i]) & VRF_MASK == r["bits"] & VRF_MASK, (i, hex(int(bits[i])), hex(r["bits"]))
+            assert bytes(out["beta"][i]) == r["beta"] and bytes(out["leader"][i]) == r["leader"], i

@@ -163,6 +163,28 @@ def test_replay_stops_at_corruption(ctx, chain, tmp_path, where):
     assert n > k
 
 
+def test_replay_early_stop_twice_then_clean(ctx, chain, tmp_path):
+    """A header damaged early in a replay of small batches: the fold stops while later batches'
+    crypto is already queued.  Those batches go back to the context (rp_batch_keep) only after
+    their runs end, and the next call's uploads are ordered after them: the same damaged
+    database replayed again gives the same stop, and the clean database then replays whole."""
+    from praos_hip import abi
+    n = len(chain["off"])
+    k = 40
+    db = _copy_db(chain, tmp_path, "early")
+    fname, pos = _locate(chain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + int(chain["len"][k]) - 100] ^= 0x40
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    for _ in range(2):
+        stats, v, st, env = _replay(ctx, chain, path=db, batch_max=61)
+        assert (stats["stop_index"], stats["stop_verdict"], stats["validated"]) == (k, abi.V_KES_SIG, k)
+        assert int((v[:k] != 0).sum()) == 0
+    stats, v, st, env = _replay(ctx, chain, batch_max=61)
+    assert (stats["headers"], stats["validated"], stats["stop_index"]) == (n, n, n)
+    assert st == chain["state"]
+
+
 def test_replay_bad_secondary(ctx, chain, tmp_path):
     """A secondary index whose size is not a whole number of entries, and one whose entry
     points past its chunk, are reported as errors (no silent partial replay)."""

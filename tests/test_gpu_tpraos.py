@@ -243,7 +243,9 @@ def test_tpraos_header_bytes_vs_soa_and_oracle(ctx, oracle):
     assert same.sum() > n - 60
     for k in o1:
         assert np.array_equal(o1[k][same], o2[k][same]), (k, np.nonzero((o1[k] != o2[k]).reshape(n, -1).any(1))[0][:8])
-    assert (o2["bits"][~same] != 0).all()
+    # (round 3's r03d failure: the first version of this test compared those headers bit for bit
+    # too; both paths reject every one of them, with the bits of whichever field the byte hit)
+    assert (o2["bits"][~same] != 0).all() and (o1["bits"][~same] != 0).all()
     assert (D["status"][same] == 0).all()
     for k in ("slot", "cold_vk", "vrf_vk", "vrf_out", "vrf_proof", "hot_vk", "ocert_n", "ocert_c0", "ocert_sig",
               "kes_sig", "leader_out", "leader_proof"):
