@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 11
+#define PRAOS_ABI_VERSION 12
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -647,6 +647,12 @@ int praos_group_set_epoch(praos_group* g, const uint8_t eta0[32], const praos_po
 int praos_group_verify_headers(praos_group* g, const praos_headers* h, praos_out* out);
 int praos_group_verify_header_bytes(praos_group* g, const praos_header_bytes* in, praos_out* out,
                                     praos_decoded* dec);
+/* TPraos batches over the group (ABI 12): praos_verify_tpraos_headers /
+ * praos_verify_tpraos_header_bytes per shard (TPraos.hs:378-387), outputs in place; dec's
+ * signed_body has the PRAOS_TP_SIGNED_STRIDE stride, leader_out / leader_proof may be NULL. */
+int praos_group_verify_tpraos_headers(praos_group* g, const praos_tpraos_headers* h, praos_tpraos_out* out);
+int praos_group_verify_tpraos_header_bytes(praos_group* g, const praos_header_bytes* in, praos_tpraos_out* out,
+                                           praos_decoded* dec, uint8_t* leader_out, uint8_t* leader_proof);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

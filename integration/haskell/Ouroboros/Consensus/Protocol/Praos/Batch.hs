@@ -102,7 +102,7 @@ foreign import ccall safe "praos_replay_immutable_tpraos" c_replay_immutable_tpr
   -> CSize -> Ptr Word8 -> Ptr Word16 -> CSize -> Ptr () -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 11
+abiVersion = 12
 
 -- ---------------------------------------------------------------- context
 

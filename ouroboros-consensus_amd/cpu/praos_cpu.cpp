@@ -980,6 +980,80 @@ int praos_verify_headers(praos_ctx* c, const praos_headers* h, praos_out* out) {
   return PRAOS_OK;
 }
 
+// TPraos (Shelley..Alonzo, d = 0): SL.updateChainDepState's header crypto (TPraos.hs:378-387,
+// cardano-protocol-tpraos OCERT + OVERLAY praosVrfChecks).  The OCERT predicates are the
+// Praos ones; the two VRF certificates are checked against mkSeed seedEta / seedL
+// (Blake2b-256(BE64 slot || eta0) xor Blake2b-256(BE64 k), k = 0 / 1), the leader test takes
+// the 64-byte leader certificate output against the 2^512 bound, and the nonce is
+// mkNonceFromOutputVRF (Blake2b-256 of the eta output).  No overlay schedule here (d = 0).
+int praos_verify_tpraos_headers(praos_ctx* c, const praos_tpraos_headers* th, praos_tpraos_out* out) {
+  if (!c || !th || !out || !out->bits || (th->h.n && (!th->leader_out || !th->leader_proof))) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  const praos_headers* h = &th->h;
+  const praos_params P = c->params;
+  parallel_for(h->n, c->nthreads(), [&](size_t i) {
+    uint16_t b = 0;
+    const uint64_t slot = h->slot[i], c0 = h->ocert_c0[i];
+    const uint64_t kp = slot / P.slots_per_kes_period;
+    if (!(c0 <= kp)) b |= PRAOS_BIT_KES_BEFORE_START;
+    if (!(kp < c0 + P.max_kes_evo)) b |= PRAOS_BIT_KES_AFTER_END;
+    uint8_t msg[48];
+    std::memcpy(msg, h->hot_vk + 32 * i, 32);
+    be64(msg + 32, h->ocert_n[i]);
+    be64(msg + 40, c0);
+    if (!ed25519_verify(h->ocert_sig + 64 * i, msg, 48, h->cold_vk + 32 * i)) b |= PRAOS_BIT_OCERT_SIG;
+    const uint64_t off = h->body_off[i], len = h->body_len[i];
+    if (off > h->body_bytes_len || len > h->body_bytes_len - off) {
+      b |= PRAOS_BIT_INPUT;
+    } else {
+      const int k = kes_verify(h->hot_vk + 32 * i, kp >= c0 ? kp - c0 : 0, h->body_bytes + off, len,
+                               h->kes_sig + 448 * i);
+      if (k == 1) b |= PRAOS_BIT_KES_MERKLE;
+      if (k == 2) b |= PRAOS_BIT_KES_LEAF;
+    }
+    // praosVrfChecks: the issuer's pool, its registered VRF key
+    uint8_t hk[28];
+    blake2b(hk, 28, h->cold_vk + 32 * i, 32);
+    int lo = 0, hi = (int)c->pools.size() - 1, idx = -1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) / 2;
+      const int r = std::memcmp(c->pools[mid].hash28, hk, 28);
+      if (r == 0) { idx = mid; break; }
+      if (r < 0) lo = mid + 1; else hi = mid - 1;
+    }
+    if (idx < 0) {
+      b |= PRAOS_BIT_VRF_KEY_UNKNOWN;
+    } else {
+      uint8_t vh[32];
+      blake2b(vh, 32, h->vrf_vk + 32 * i, 32);
+      if (std::memcmp(vh, c->pools[idx].vrf_hash32, 32) != 0) b |= PRAOS_BIT_VRF_KEY_WRONG;
+    }
+    // the two certificates: mkSeed seedEta (k = 0), seedL (k = 1)
+    uint8_t sb[8], hs[32];
+    be64(sb, slot);
+    blake2b(hs, 32, sb, 8, c->eta0, c->eta0_neutral ? 0 : 32);
+    const uint8_t* certs_out[2] = {h->vrf_out + 64 * i, th->leader_out + 64 * i};
+    const uint8_t* certs_proof[2] = {h->vrf_proof + 80 * i, th->leader_proof + 80 * i};
+    uint8_t* betas[2] = {out->beta_eta ? out->beta_eta + 64 * i : nullptr,
+                         out->beta_leader ? out->beta_leader + 64 * i : nullptr};
+    for (int k = 0; k < 2; k++) {
+      uint8_t kb[8], uc[32], alpha[32], beta[64];
+      be64(kb, (uint64_t)k);
+      blake2b(uc, 32, kb, 8);                                         // mkNonceFromNumber k
+      for (int j = 0; j < 32; j++) alpha[j] = hs[j] ^ uc[j];          // Hash.xor
+      const bool ok = vrf_verify(beta, h->vrf_vk + 32 * i, certs_proof[k], alpha);
+      if (!ok || (P.vrf_check_output && std::memcmp(beta, certs_out[k], 64) != 0))
+        b |= k == 0 ? PRAOS_BIT_TP_VRF_NONCE : PRAOS_BIT_TP_VRF_LEADER;
+      if (betas[k]) std::memcpy(betas[k], beta, 64);
+    }
+    if (idx >= 0 && !P.f_is_one && !leader_check(certs_out[1], 64, c->x[idx].data())) b |= PRAOS_BIT_LEADER;
+    out->bits[i] = b;
+    if (out->pool_idx) out->pool_idx[i] = idx < 0 ? -1 : c->order[idx];
+    if (out->nonce) blake2b(out->nonce + 32 * i, 32, certs_out[0], 64);   // mkNonceFromOutputVRF
+  });
+  return PRAOS_OK;
+}
+
 int praos_verify_ocert(praos_ctx* c, size_t n, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
                        const uint64_t* ocert_c0, const uint8_t* sig, uint8_t* ok) {
   if (!c || (n && (!cold_vk || !hot_vk || !ocert_n || !ocert_c0 || !sig || !ok))) return PRAOS_E_ARG;

@@ -36,7 +36,46 @@ praos_out out_at(const praos_out* o, size_t i) {
   return {at(o->bits, i, 1), at(o->pool_idx, i, 1), at(o->beta, i, 64), at(o->leader, i, 32), at(o->nonce, i, 32)};
 }
 
-praos_decoded dec_at(const praos_decoded* d, size_t i) {
+praos_tpraos_out tp_out_at(const praos_tpraos_out* o, size_t i) {
+  return {at(o->bits, i, 1), at(o->pool_idx, i, 1), at(o->beta_eta, i, 64), at(o->beta_leader, i, 64),
+          at(o->nonce, i, 32)};
+}
+
+// the shard [i0, i1) of a SoA header batch (body_off stays absolute into the shared body_bytes)
+praos_headers headers_at(const praos_headers* h, size_t i0, size_t i1) {
+  praos_headers s = *h;
+  s.n = i1 - i0;
+  s.slot = at(h->slot, i0, 1);
+  s.cold_vk = at(h->cold_vk, i0, 32);
+  s.vrf_vk = at(h->vrf_vk, i0, 32);
+  s.vrf_out = at(h->vrf_out, i0, 64);
+  s.vrf_proof = at(h->vrf_proof, i0, 80);
+  s.hot_vk = at(h->hot_vk, i0, 32);
+  s.ocert_n = at(h->ocert_n, i0, 1);
+  s.ocert_c0 = at(h->ocert_c0, i0, 1);
+  s.ocert_sig = at(h->ocert_sig, i0, 64);
+  s.kes_sig = at(h->kes_sig, i0, 448);
+  s.body_off = at(h->body_off, i0, 1);
+  s.body_len = at(h->body_len, i0, 1);
+  return s;
+}
+
+// only the shard's window of the arena travels to the member's device: offsets rebased
+// into `off`, the window returned
+praos_header_bytes bytes_at(const praos_header_bytes* in, size_t i0, size_t i1, std::vector<uint64_t>& off) {
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (size_t i = i0; i < i1; i++) {
+    lo = std::min<uint64_t>(lo, in->off[i]);
+    hi = std::max<uint64_t>(hi, in->off[i] + in->len[i]);
+  }
+  if (hi > in->bytes_len) { lo = 0; hi = in->bytes_len; }   // out-of-range entries: the decoder flags them
+  lo = std::min<uint64_t>(lo, hi);
+  off.assign(in->off + i0, in->off + i1);
+  for (auto& o : off) o -= std::min<uint64_t>(o, lo);
+  return {i1 - i0, in->bytes + lo, (size_t)(hi - lo), off.data(), in->len + i0};
+}
+
+praos_decoded dec_at(const praos_decoded* d, size_t i, size_t signed_stride = PRAOS_SIGNED_STRIDE) {
   praos_decoded r;
   r.status = at(d->status, i, 1);
   r.block_no = at(d->block_no, i, 1);
@@ -57,7 +96,7 @@ praos_decoded dec_at(const praos_decoded* d, size_t i) {
   r.prot_minor = at(d->prot_minor, i, 1);
   r.kes_sig = at(d->kes_sig, i, 448);
   r.signed_len = at(d->signed_len, i, 1);
-  r.signed_body = at(d->signed_body, i, PRAOS_SIGNED_STRIDE);
+  r.signed_body = at(d->signed_body, i, signed_stride);
   r.header_hash = at(d->header_hash, i, 32);
   return r;
 }
@@ -135,20 +174,7 @@ int praos_group_verify_headers(praos_group* g, const praos_headers* h, praos_out
     size_t i0, i1;
     shard(h->n, m, k, &i0, &i1);
     if (i1 == i0) return (int)PRAOS_OK;
-    praos_headers s = *h;   // body_off stays absolute into the shared body_bytes
-    s.n = i1 - i0;
-    s.slot = at(h->slot, i0, 1);
-    s.cold_vk = at(h->cold_vk, i0, 32);
-    s.vrf_vk = at(h->vrf_vk, i0, 32);
-    s.vrf_out = at(h->vrf_out, i0, 64);
-    s.vrf_proof = at(h->vrf_proof, i0, 80);
-    s.hot_vk = at(h->hot_vk, i0, 32);
-    s.ocert_n = at(h->ocert_n, i0, 1);
-    s.ocert_c0 = at(h->ocert_c0, i0, 1);
-    s.ocert_sig = at(h->ocert_sig, i0, 64);
-    s.kes_sig = at(h->kes_sig, i0, 448);
-    s.body_off = at(h->body_off, i0, 1);
-    s.body_len = at(h->body_len, i0, 1);
+    praos_headers s = headers_at(h, i0, i1);
     praos_out o = out_at(out, i0);
     return praos_verify_headers(g->ctx[k], &s, &o);
   });
@@ -162,21 +188,46 @@ int praos_group_verify_header_bytes(praos_group* g, const praos_header_bytes* in
     size_t i0, i1;
     shard(in->n, m, k, &i0, &i1);
     if (i1 == i0) return (int)PRAOS_OK;
-    // only the shard's window of the arena travels to this member's device
-    uint64_t lo = UINT64_MAX, hi = 0;
-    for (size_t i = i0; i < i1; i++) {
-      lo = std::min<uint64_t>(lo, in->off[i]);
-      hi = std::max<uint64_t>(hi, in->off[i] + in->len[i]);
-    }
-    if (hi > in->bytes_len) { lo = 0; hi = in->bytes_len; }   // out-of-range entries: the decoder flags them
-    lo = std::min<uint64_t>(lo, hi);
-    std::vector<uint64_t> off(in->off + i0, in->off + i1);
-    for (auto& o : off) o -= std::min<uint64_t>(o, lo);
-    praos_header_bytes s{i1 - i0, in->bytes + lo, (size_t)(hi - lo), off.data(), in->len + i0};
+    std::vector<uint64_t> off;
+    praos_header_bytes s = bytes_at(in, i0, i1, off);
     praos_out o = out_at(out, i0);
     if (!dec) return praos_verify_header_bytes(g->ctx[k], &s, &o, nullptr);
     praos_decoded d = dec_at(dec, i0);
     return praos_verify_header_bytes(g->ctx[k], &s, &o, &d);
+  });
+}
+
+// TPraos (Shelley..Alonzo) batches over the group: the same contiguous shards of
+// praos_verify_tpraos_headers / praos_verify_tpraos_header_bytes (TPraos.hs:378-387; one
+// header is checked against the epoch's ledger view only, so the shards need no exchange).
+int praos_group_verify_tpraos_headers(praos_group* g, const praos_tpraos_headers* h, praos_tpraos_out* out) {
+  if (!g || !h || !out || !out->bits || (h->h.n && (!h->leader_out || !h->leader_proof))) return PRAOS_E_ARG;
+  const size_t m = g->ctx.size();
+  return fan_out(g, [&](size_t k) {
+    size_t i0, i1;
+    shard(h->h.n, m, k, &i0, &i1);
+    if (i1 == i0) return (int)PRAOS_OK;
+    praos_tpraos_headers s{headers_at(&h->h, i0, i1), at(h->leader_out, i0, 64), at(h->leader_proof, i0, 80)};
+    praos_tpraos_out o = tp_out_at(out, i0);
+    return praos_verify_tpraos_headers(g->ctx[k], &s, &o);
+  });
+}
+
+int praos_group_verify_tpraos_header_bytes(praos_group* g, const praos_header_bytes* in, praos_tpraos_out* out,
+                                           praos_decoded* dec, uint8_t* leader_out, uint8_t* leader_proof) {
+  if (!g || !in || !out || !out->bits || (in->n && (!in->off || !in->len))) return PRAOS_E_ARG;
+  const size_t m = g->ctx.size();
+  return fan_out(g, [&](size_t k) {
+    size_t i0, i1;
+    shard(in->n, m, k, &i0, &i1);
+    if (i1 == i0) return (int)PRAOS_OK;
+    std::vector<uint64_t> off;
+    praos_header_bytes s = bytes_at(in, i0, i1, off);
+    praos_tpraos_out o = tp_out_at(out, i0);
+    praos_decoded d;
+    if (dec) d = dec_at(dec, i0, PRAOS_TP_SIGNED_STRIDE);
+    return praos_verify_tpraos_header_bytes(g->ctx[k], &s, &o, dec ? &d : nullptr, at(leader_out, i0, 64),
+                                            at(leader_proof, i0, 80));
   });
 }
 

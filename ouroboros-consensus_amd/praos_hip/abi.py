@@ -242,6 +242,11 @@ SIGNATURES = {
     "praos_group_verify_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Headers), ctypes.POINTER(Out)]),
     "praos_group_verify_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
                                                        ctypes.POINTER(Out), ctypes.POINTER(Decoded)]),
+    "praos_group_verify_tpraos_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders),
+                                                         ctypes.POINTER(TPOut)]),
+    "praos_group_verify_tpraos_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
+                                                              ctypes.POINTER(TPOut), ctypes.POINTER(Decoded), u8p,
+                                                              u8p]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -417,22 +422,29 @@ class Context:
         self.check(self.L.praos_verify_headers(self.h, ctypes.byref(hs), ctypes.byref(os_)))
         return o
 
-    def verify_tpraos_headers(self, H):
-        """H as for verify_headers plus leader_out [n,64] / leader_proof [n,80] (the bheaderL cert)."""
-        n = len(H["slot"])
+    @staticmethod
+    def tp_headers_struct(H):
         th = TPHeaders()
-        th.h = self.headers_struct(H)
+        th.h = Context.headers_struct(H)
         th.leader_out = ptr(H["leader_out"])
         th.leader_proof = ptr(H["leader_proof"])
+        return th
+
+    @staticmethod
+    def tp_out(n):
+        """TPraos output arrays and their praos_tpraos_out struct."""
         o = {"bits": np.zeros(n, np.uint16), "pool_idx": np.zeros(n, np.int32),
              "beta_eta": np.zeros((n, 64), np.uint8), "beta_leader": np.zeros((n, 64), np.uint8),
              "nonce": np.zeros((n, 32), np.uint8)}
         to = TPOut()
-        to.bits = ptr(o["bits"], u16p)
-        to.pool_idx = ptr(o["pool_idx"], i32p)
-        to.beta_eta = ptr(o["beta_eta"])
-        to.beta_leader = ptr(o["beta_leader"])
-        to.nonce = ptr(o["nonce"])
+        to.bits, to.pool_idx = ptr(o["bits"], u16p), ptr(o["pool_idx"], i32p)
+        to.beta_eta, to.beta_leader, to.nonce = ptr(o["beta_eta"]), ptr(o["beta_leader"]), ptr(o["nonce"])
+        return o, to
+
+    def verify_tpraos_headers(self, H):
+        """H as for verify_headers plus leader_out [n,64] / leader_proof [n,80] (the bheaderL cert)."""
+        th = self.tp_headers_struct(H)
+        o, to = self.tp_out(len(H["slot"]))
         self.check(self.L.praos_verify_tpraos_headers(self.h, ctypes.byref(th), ctypes.byref(to)))
         return o
 
@@ -589,12 +601,7 @@ class Context:
         arena, off, length = self._chunk(arena, off, length)
         n = len(off)
         hb = self.header_bytes_struct(arena, off, length)
-        o = {"bits": np.zeros(n, np.uint16), "pool_idx": np.zeros(n, np.int32),
-             "beta_eta": np.zeros((n, 64), np.uint8), "beta_leader": np.zeros((n, 64), np.uint8),
-             "nonce": np.zeros((n, 32), np.uint8)}
-        to = TPOut()
-        to.bits, to.pool_idx = ptr(o["bits"], u16p), ptr(o["pool_idx"], i32p)
-        to.beta_eta, to.beta_leader, to.nonce = ptr(o["beta_eta"]), ptr(o["beta_leader"]), ptr(o["nonce"])
+        o, to = self.tp_out(n)
         D, d = self.alloc_decoded(n, TP_SIGNED_STRIDE) if decoded else (None, None)
         lo = np.zeros((n, 64), np.uint8) if decoded else None
         lp = np.zeros((n, 80), np.uint8) if decoded else None
@@ -1084,6 +1091,29 @@ class Group:
         self.check(self.L.praos_group_verify_header_bytes(self.g, ctypes.byref(hb), ctypes.byref(os_),
                                                           ctypes.byref(d) if decoded else None))
         return (o, D) if decoded else o
+
+    def verify_tpraos_headers(self, H):
+        th = Context.tp_headers_struct(H)
+        o, to = Context.tp_out(len(H["slot"]))
+        self.check(self.L.praos_group_verify_tpraos_headers(self.g, ctypes.byref(th), ctypes.byref(to)))
+        return o
+
+    def verify_tpraos_header_bytes(self, arena, off, length, decoded=False):
+        arena, off, length = Context._chunk(arena, off, length)
+        n = len(off)
+        hb = Context.header_bytes_struct(arena, off, length)
+        o, to = Context.tp_out(n)
+        D, d = Context.alloc_decoded(n, TP_SIGNED_STRIDE) if decoded else (None, None)
+        lo = np.zeros((n, 64), np.uint8) if decoded else None
+        lp = np.zeros((n, 80), np.uint8) if decoded else None
+        self.check(self.L.praos_group_verify_tpraos_header_bytes(self.g, ctypes.byref(hb), ctypes.byref(to),
+                                                                 ctypes.byref(d) if decoded else None,
+                                                                 ptr(lo) if decoded else None,
+                                                                 ptr(lp) if decoded else None))
+        if not decoded:
+            return o
+        D["leader_out"], D["leader_proof"] = lo, lp
+        return o, D
 
 
 def _state_struct(state, cap):

@@ -11,7 +11,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 OPT_THREADS = 4
 EXPORTS = ("praos_abi_version", "praos_open", "praos_close", "praos_last_error", "praos_set_option",
            "praos_set_epoch", "praos_verify_headers", "praos_verify_ocert", "praos_verify_kes", "praos_verify_vrf",
-           "praos_check_leader")
+           "praos_check_leader", "praos_verify_tpraos_headers")
 _lib = None
 
 

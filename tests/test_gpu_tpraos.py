@@ -294,3 +294,32 @@ def test_tpraos_header_bytes_golden_and_malformed(ctx):
         assert bytes(o["beta_eta"][i]) == H(k["eta_out"]) and bytes(o["beta_leader"][i]) == H(k["leader_out"])
     for i in (len(KATS), len(KATS) + 1):
         assert D["status"][i] & abi.DEC_FAILED and o["bits"][i] & abi.BIT_INPUT
+
+
+@pytest.mark.parametrize("members", [2, 3])
+def test_tpraos_group_equals_single(ctx, members):
+    """praos_group_verify_tpraos_headers / _header_bytes (ABI 12): a TPraos batch split into
+    contiguous shards over several contexts (one GPU here; devices 0..7 on a node) gives every
+    output -- and with decoded=True every decoded field -- bit for bit as one context."""
+    from praos_hip import abi, fixed
+    from praos_hip.chunk import pack_chunk
+    p, c_raw = _params(Fraction(1, 2))
+    eta0 = b2b(b"tpraos-group")
+    n = 1537
+    H, pools, corrupted = ctx.synthesize(n, 40, p, eta0, b"\x36" * 32, first_slot=7000, slot_stride=3,
+                                         body_len=0, corrupt_per_10000=300, tpraos=True)
+    pool_list = [(h, v, fixed.from_rational(Fraction(1, 40))) for (h, v) in pools]
+    ctx.set_epoch(eta0, pool_list, p)
+    o1 = ctx.verify_tpraos_headers(H)
+    arena, off, ln = pack_chunk(H, era_tag=5)
+    b1, D1 = ctx.verify_tpraos_header_bytes(arena, off, ln, decoded=True)
+    with abi.Group([0] * members) as g:
+        g.set_epoch(eta0, pool_list, p)
+        og = g.verify_tpraos_headers(H)
+        bg, Dg = g.verify_tpraos_header_bytes(arena, off, ln, decoded=True)
+    for k in o1:
+        assert np.array_equal(o1[k], og[k]), k
+        assert np.array_equal(b1[k], bg[k]), k
+    for k in D1:
+        assert np.array_equal(D1[k], Dg[k]), k
+    assert np.count_nonzero(corrupted) and all(int(og["bits"][i]) for i in np.nonzero(corrupted)[0])
