@@ -82,8 +82,9 @@ CONFIGS = {
                workload="configs[3]: 1M Sum6KES verifies (depth-6 Blake2b-256 Merkle path + Ed25519 leaf), "
                         "397-byte messages, 1% corrupted"),
     "tp": dict(items=432_000, pools=3000, kernels=7, metric="TPraos headers validated/sec (2 VRF+KES+OCert+leader)",
-               workload="TPraos (Shelley..Alonzo) headers from stored bytes: 432k BHeaders decoded on the device, "
-                        "3000 pools forging in turn (f = 1), single eta0, 1% corrupted"),
+               workload="TPraos (Shelley..Alonzo) headers from stored bytes: the first 432k blocks of a "
+                        "first-leader-wins TPraos chain (3000 pools, f = 1/20, leader certificate vs 2^512), "
+                        "BHeaders decoded on the device, single eta0, 1% corrupted"),
     "c5": dict(items=432_000, kernels=7, metric="Praos headers validated/sec (VRF+KES+OCert+leader)",
                workload="configs[4]: mainnet-shaped epoch replay, the first 432k blocks of a first-leader-wins "
                         "Praos chain per GPU, 3000-pool stake distribution, single eta0, 1% corrupted"),
@@ -117,7 +118,9 @@ def _hdr_dict(H, i):
             "vrf_out": bytes(H["vrf_out"][i]), "vrf_proof": bytes(H["vrf_proof"][i]),
             "hot_vk": bytes(H["hot_vk"][i]), "n": int(H["ocert_n"][i]), "c0": int(H["ocert_c0"][i]),
             "ocert_sig": bytes(H["ocert_sig"][i]), "kes_sig": bytes(H["kes_sig"][i]),
-            "body": bytes(H["body_bytes"][off:off + ln])}
+            "body": bytes(H["body_bytes"][off:off + ln]),
+            **({"leader_out": bytes(H["leader_out"][i]), "leader_proof": bytes(H["leader_proof"][i])}
+               if "leader_out" in H else {})}
 
 
 def _oracle_worker(payload):
@@ -126,10 +129,11 @@ def _oracle_worker(payload):
     import oracle
     kind, eta0, c_raw, spkp, maxevo, pools, items = payload
     out = []
-    if kind == "header":
+    if kind in ("header", "tpraos"):
         ep = oracle.make_epoch(eta0, spkp, maxevo, c_raw, pools)
         t0 = time.perf_counter()
-        out = [oracle.praos_header(ep, h)["bits"] for h in items]
+        f = oracle.praos_header if kind == "header" else oracle.tpraos_header
+        out = [f(ep, h)["bits"] for h in items]
     elif kind == "ocert":
         t0 = time.perf_counter()
         for h in items:
@@ -202,6 +206,8 @@ def _twin_run(ctx, kind, S, eta0, pool_list, p, spkp):
     n = len(S["slot"])
     if kind == "header":
         return ctx.verify_headers(S)["bits"]
+    if kind == "tpraos":
+        return ctx.verify_tpraos_headers(S)["bits"]
     if kind == "ocert":
         ok = ctx.verify_ocert(S["cold_vk"], S["hot_vk"], S["ocert_n"], S["ocert_c0"], S["ocert_sig"])
         return np.where(ok == 1, 0, 0x0004).astype(np.uint16)
@@ -227,7 +233,7 @@ def _twin_run(ctx, kind, S, eta0, pool_list, p, spkp):
 
 
 def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, seconds, threads, per_item, mask,
-                 whole=False):
+                 whole=False, body_corrupted=None):
     """The CPU twin (libpraos_cpu.so, same ABI, `threads` worker threads) timed over a
     bounded sample of the benchmark input, its single-core rate, and the oracle as
     the checker of both implementations on a sub-sample."""
@@ -242,7 +248,13 @@ def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, sec
     t0 = time.perf_counter()
     bits = _twin_run(twin, kind, S, eta0, pool_list, p, spkp)
     busy = time.perf_counter() - t0
-    agree = int(((gpu_bits[idx] & mask) == (bits & mask)).sum())
+    same = (gpu_bits[idx] & mask) == (bits & mask)
+    if body_corrupted is not None:
+        # stored-bytes GPU path: a corrupted body byte is decoded (it may land in any field),
+        # the twin sees the generator's fields with that body -- compared on accept / reject
+        bc = body_corrupted[idx]
+        same = np.where(bc, (gpu_bits[idx] != 0) == (bits != 0), same)
+    agree = int(same.sum())
     # one core: the first part of the same sample on one thread
     n1 = max(16, min(n_sample, int(3.0 / per_item)))
     twin.set_option(C.OPT_THREADS, 1)
@@ -263,10 +275,12 @@ def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, sec
         for j, v in enumerate(b):
             obits[k + j * workers] = v
     omask = mask if kind != "vrf" else 0x1F00
-    oracle_agree = sum(1 for j, i in enumerate(sub) if (int(gpu_bits[i]) & omask) == (obits[j] & omask))
+    oracle_agree = sum(1 for j, i in enumerate(sub) if (int(gpu_bits[i]) & omask) == (obits[j] & omask) or
+                       (body_corrupted is not None and body_corrupted[i] and
+                        (int(gpu_bits[i]) != 0) == (obits[j] != 0)))
     usable, nproc, model = host_cores()
     single = len(range(n1)) / t1
-    return {"value": round(n_sample / busy, 1), "unit": "items/s" if kind != "header" else "headers/s",
+    return {"value": round(n_sample / busy, 1), "unit": "headers/s" if kind in ("header", "tpraos") else "items/s",
             "cores": threads, "kind": "port",
             "sample": f"{n_sample} items evenly spaced over the benchmark input; CPU twin libpraos_cpu.so "
                       f"(C++, radix-2^51, sliding-window Straus, same ABI) on {threads} threads, {busy:.2f}s",
@@ -621,13 +635,16 @@ def main():
         line["strong_proxy"] = dict(proxy, note="one GPU validating only the first 1/k of the batch (rank 0's "
                                                 "shard of a strong-scaling run at N = k); per_gpu_vs_full = its "
                                                 "rate / this line's value")
-    if world == 1 and not args.no_cpu and args.config != "tp":   # (the CPU twin has no TPraos path)
+    if world == 1 and not args.no_cpu:
         usable, _, _ = host_cores()
         threads = max(1, min(args.cpu_workers, usable))
         kind, per_item, mask = {7: ("header", 2.5e-4, 0x1F1F), 1: ("ocert", 5e-5, 0x0004),
                                 2: ("kes", 6e-5, 0x0018), 4: ("vrf", 1.5e-4, 0x1C00)}[cfg["kernels"]]
+        if args.config == "tp":          # TPraos.updateChainDepState's crypto: two VRF certificates
+            kind, per_item, mask = "tpraos", 4e-4, 0x1F1F
         line["cpu_baseline"] = cpu_baseline(kind, H, out["bits"], eta0, c_raw, p, spkp, maxevo, pool_list,
-                                            args.cpu_seconds, threads, per_item, mask, whole=args.config == "c1")
+                                            args.cpu_seconds, threads, per_item, mask, whole=args.config == "c1",
+                                            body_corrupted=(corrupted == 5) if args.config == "tp" else None)
         line["cpu_baseline"]["openssl_ed25519_verify_per_s_1core"] = openssl_ed25519_rate()
         line["gpu_vs_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
     print(json.dumps(line), flush=True)

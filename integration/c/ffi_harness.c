@@ -23,6 +23,13 @@
  *               cut at epoch boundaries, praos_ticked_epoch_nonce -> praos_set_epoch ->
  *               praos_verify_header_bytes -> praos_validate_headers, stop at the first
  *               invalid header) and the PraosState CBOR (praos_state_encode) it ends in;
+ *   "typed":    the sequence of Batch/Validate.hs validateEpochHeaders (praosValidateHeaderSpans):
+ *               per epoch praos_ticked_epoch_nonce -> praos_set_epoch -> praos_host_register of
+ *               the arena (the binding does it from 64 MiB on; always here, so the path runs) ->
+ *               praos_verify_header_bytes with the decoded fields in one 125-byte-per-header
+ *               allocation -> praos_host_unregister -> praos_validate_headers ->
+ *               praos_state_encode; also prints the stopping header's verdict and bits, what
+ *               Batch.Errors rebuilds the typed HeaderError from (must agree);
  *   "replay":   praos_replay_immutable over the same directory (must agree);
  *   "threads":  the first epoch's headers split over <threads> POSIX threads, each with
  *               its own praos_ctx on device 0, and the same through praos_group_open
@@ -182,12 +189,15 @@ static void genesis_state(state_buf* s) {
   s->st.last_epoch_block.neutral = 1;
 }
 
+/* stop_bits < 0: not reported */
 static void print_state(const char* phase, const state_buf* s, const praos_envelope* env, uint64_t validated,
-                        uint64_t stop, int stop_verdict, uint64_t epochs) {
+                        uint64_t stop, int stop_verdict, uint64_t epochs, long stop_bits) {
   size_t len = 0;
   static uint8_t buf[64 + 48 * CAP];
   if (praos_state_encode(&s->st, buf, sizeof buf, &len) != PRAOS_OK) DIE("state_encode");
-  printf("{\"phase\": \"%s\", \"validated\": %llu, \"stop_index\": %llu, \"stop_verdict\": %d, \"epochs\": %llu, "
+  if (stop_bits >= 0) printf("{\"stop_bits\": %ld, ", stop_bits);
+  else printf("{");
+  printf("\"phase\": \"%s\", \"validated\": %llu, \"stop_index\": %llu, \"stop_verdict\": %d, \"epochs\": %llu, "
          "\"tip_slot\": %llu, \"tip_block_no\": %llu, \"tip_hash\": \"", phase, (unsigned long long)validated,
          (unsigned long long)stop, stop_verdict, (unsigned long long)epochs, (unsigned long long)env->tip_slot,
          (unsigned long long)env->tip_block_no);
@@ -262,7 +272,73 @@ static void phase_binding(const chain_t* ch) {
     if (stopped) break;
     i = j;
   }
-  print_state("binding", &S, &env, validated, stop_index, stop_verdict, epochs);
+  print_state("binding", &S, &env, validated, stop_index, stop_verdict, epochs, -1);
+  praos_close(ctx);
+}
+
+/* ---- phase 1b: Batch/Validate.hs validateEpochHeaders (Storable vectors, registered arena) ---- */
+static void phase_typed(const chain_t* ch) {
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) DIE("praos_open(0)");
+  static state_buf S;
+  genesis_state(&S);
+  praos_envelope env = g_env0;
+  uint64_t validated = 0, stop_index = ch->n, epochs = 0;
+  int stop_verdict = 0;
+  unsigned stop_bits = 0;
+  size_t i = 0;
+  while (i < ch->n) {
+    const uint64_t e = (ch->slot[i] - g_ei.epoch_base_slot) / g_ei.epoch_length;
+    size_t j = i;
+    while (j < ch->n && (ch->slot[j] - g_ei.epoch_base_slot) / g_ei.epoch_length == e) j++;
+    const size_t n = j - i;
+    praos_nonce eta;
+    CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
+    CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
+    epochs++;
+    /* the epoch's arena: its header spans back to back (what the binding concatenates) */
+    size_t alen = 0;
+    for (size_t k = 0; k < n; k++) alen += ch->hlen[i + k];
+    uint8_t* arena = malloc(alen ? alen : 1);
+    uint64_t* off = malloc(8 * n);
+    for (size_t k = 0, o = 0; k < n; o += ch->hlen[i + k], k++) {
+      memcpy(arena + o, ch->bytes + ch->off[i + k], ch->hlen[i + k]);
+      off[k] = o;
+    }
+    uint8_t* verdict = calloc(n, 1);
+    uint16_t* bits = calloc(n, 2);
+    int32_t* pidx = calloc(n, 4);
+    uint8_t* decbuf = calloc(n, 125);      /* slot, block no, ocert n | prev, cold, hash | body size | gen */
+    uint64_t *slot = (uint64_t*)decbuf, *bno = (uint64_t*)(decbuf + 8 * n), *ocn = (uint64_t*)(decbuf + 16 * n);
+    uint8_t *prev = decbuf + 24 * n, *cold = decbuf + 56 * n, *hh = decbuf + 88 * n, *gen = decbuf + 124 * n;
+    uint32_t* bsz = (uint32_t*)(decbuf + 120 * n);
+    praos_header_bytes hb = {n, arena, alen, off, ch->hlen + i};
+    praos_out out = {bits, pidx, NULL, NULL, NULL};
+    praos_decoded dec;
+    memset(&dec, 0, sizeof dec);
+    dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;
+    dec.cold_vk = cold; dec.header_hash = hh; dec.body_size = bsz;
+    CK(ctx, praos_host_register(ctx, arena, alen ? alen : 1));
+    CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
+    CK(ctx, praos_host_unregister(ctx, arena));
+    praos_headers h;
+    memset(&h, 0, sizeof h);
+    h.n = n; h.slot = slot; h.cold_vk = cold; h.ocert_n = ocn;
+    env.block_no = bno; env.header_hash = hh; env.header_size = ch->hlen + i; env.body_size = bsz;
+    size_t stop = 0, done = 0;
+    CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
+    if (done != n) DIE("an epoch batch did not fold through (%zu of %zu)", done, n);
+    const int stopped = stop < n;
+    if (stopped) {
+      stop_index = i + stop; stop_verdict = verdict[stop]; stop_bits = bits[stop]; validated += stop;
+    } else {
+      validated += n;
+    }
+    free(arena); free(off); free(verdict); free(bits); free(pidx); free(decbuf);
+    if (stopped) break;
+    i = j;
+  }
+  print_state("typed", &S, &env, validated, stop_index, stop_verdict, epochs, (long)stop_bits);
   praos_close(ctx);
 }
 
@@ -280,7 +356,7 @@ static void phase_replay(const char* dir) {
   else
     CK(ctx, praos_replay_immutable(ctx, dir, g_pools, g_npools, &g_params, &g_ei, &env, &S.st, 1 << 16, NULL, 0,
                                    &rs));
-  print_state("replay", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs);
+  print_state("replay", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs, -1);
   praos_close(ctx);
 }
 
@@ -362,6 +438,7 @@ int main(int argc, char** argv) {
   chain_t ch;
   read_chain(argv[1], &ch);
   phase_binding(&ch);
+  if (!g_tpraos) phase_typed(&ch);
   phase_replay(argv[1]);
   if (!g_tpraos) phase_threads(&ch, atoi(argv[3]));
   return 0;

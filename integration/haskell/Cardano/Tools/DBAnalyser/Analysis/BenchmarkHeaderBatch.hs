@@ -5,8 +5,8 @@
 
 -- | A db-analyser analysis beside 'BenchmarkLedgerOps' (Analysis.hs:75-88, :479-607):
 -- header revalidation of a Praos (Babbage/Conway) ImmutableDB in per-epoch batches on the
--- GPU through 'Ouroboros.Consensus.Protocol.Praos.Batch', timed per epoch the way
--- BenchmarkLedgerOps times per block (mutator ns), one line per epoch:
+-- GPU through 'Ouroboros.Consensus.Protocol.Praos.Batch' (Storable vectors in and out), timed
+-- per epoch on the monotonic wall clock, one line per epoch:
 --
 --   epoch  headers  validated  stop_verdict  ms  headers/s
 --
@@ -26,8 +26,10 @@ import           Control.Monad (unless, when)
 import qualified Data.ByteString as BS
 import qualified Data.ByteString.Lazy as BSL
 import           Data.IORef
-import           Data.Word (Word64)
-import qualified GHC.Stats as GC
+import qualified Data.Vector.Storable as VS
+import qualified Data.Vector.Storable.Mutable as VSM
+import           Data.Word (Word16, Word32, Word64, Word8)
+import           GHC.Clock (getMonotonicTimeNSec)
 import qualified System.IO as IO
 import           Text.Printf (hPrintf)
 
@@ -68,19 +70,27 @@ benchmarkHeaderBatch mOut EpochBatchEnv {ebEpochInfo, ebEnvLimits, ebPools, ebPa
           tip <- readIORef tipRef
           let hdrs = reverse hdrsRev
               firstSlot = fst (head hdrs)
+              raws = map snd hdrs
+              n = length hdrs
+              arena = BS.concat raws
+              lens = VS.fromListN n (map (fromIntegral . BS.length) raws) :: VS.Vector Word32
+              offs = VS.prescanl' (+) 0 (VS.map fromIntegral lens)
           eta <- praosTickedEpochNonce st ebEpochInfo firstSlot
           praosSetEpoch ctx eta (ebPools e) ebParams
-          t0 <- GC.mutator_elapsed_ns <$> GC.getRTSStats
-          !r <- praosValidateHeaderBytes ctx ebEpochInfo ebEnvLimits tip st (map snd hdrs)
-          t1 <- GC.mutator_elapsed_ns <$> GC.getRTSStats
-          let n = length hdrs
-              ms = fromIntegral (t1 - t0) / 1e6 :: Double
-              stopped = brChainStop r < n
-              verdict = if stopped then brVerdicts r !! brChainStop r else 0
-          hPrintf h "%d\t%d\t%d\t%d\t%.3f\t%.0f\n" e n (brChainStop r) verdict ms
+          verdicts <- VSM.new n :: IO (VSM.IOVector Word8)
+          bits <- VSM.new n :: IO (VSM.IOVector Word16)
+          -- wall clock around the batch (the foreign call is safe: mutator time would not
+          -- count the time the GPU spends)
+          t0 <- getMonotonicTimeNSec
+          !r <- praosValidateHeaderSpans ctx ebEpochInfo ebEnvLimits tip st arena offs lens verdicts bits
+          t1 <- getMonotonicTimeNSec
+          let ms = fromIntegral (t1 - t0) / 1e6 :: Double
+              stopped = srChainStop r < n
+          verdict <- if stopped then VSM.read verdicts (srChainStop r) else pure 0
+          hPrintf h "%d\t%d\t%d\t%d\t%.3f\t%.0f\n" e n (srChainStop r) verdict ms
                   (fromIntegral n / max 1e-9 (ms / 1e3))
-          writeIORef stRef (brState r)
-          writeIORef tipRef (brTip r)
+          writeIORef stRef (srState r)
+          writeIORef tipRef (srTip r)
           pure (not stopped)          -- the reference stops at the first invalid header
     (e, acc, ok) <- stream (0, [], True) $ \(e, acc, ok) (slot, raw) -> do
       let e' = epochOf slot

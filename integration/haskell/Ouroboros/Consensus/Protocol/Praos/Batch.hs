@@ -30,6 +30,9 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
     -- * Headers from stored bytes
   , BatchResult (..)
   , praosValidateHeaderBytes
+    -- * Headers from stored bytes, Storable vectors (Batch.Validate)
+  , SpanResult (..)
+  , praosValidateHeaderSpans
     -- * TPraos (Shelley..Alonzo) headers from stored bytes
   , TPraosBatchResult (..)
   , praosTickedEpochNonceTPraos
@@ -46,6 +49,8 @@ import           Control.Exception (Exception, bracket, throwIO)
 import           Control.Monad (forM_, when)
 import qualified Data.ByteString as BS
 import qualified Data.ByteString.Unsafe as BSU
+import qualified Data.Vector.Storable as VS
+import qualified Data.Vector.Storable.Mutable as VSM
 import           Data.Word (Word16, Word32, Word64, Word8)
 import           Foreign
 import           Foreign.C.String (CString, peekCString, withCString)
@@ -82,6 +87,10 @@ foreign import ccall safe "praos_verify_header_bytes" c_verify_header_bytes
 foreign import ccall safe "praos_validate_headers" c_validate_headers
   :: Ptr PraosCtx -> Ptr () -> Ptr Word8 -> Ptr Word8 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
   -> Ptr Word8 -> Ptr CSize -> Ptr CSize -> IO CInt
+foreign import ccall safe "praos_host_register" c_host_register
+  :: Ptr PraosCtx -> Ptr Word8 -> CSize -> IO CInt
+foreign import ccall safe "praos_host_unregister" c_host_unregister
+  :: Ptr PraosCtx -> Ptr Word8 -> IO CInt
 foreign import ccall safe "praos_state_encode" c_state_encode
   :: Ptr () -> Ptr Word8 -> CSize -> Ptr CSize -> IO CInt
 foreign import ccall safe "praos_state_decode" c_state_decode
@@ -311,6 +320,78 @@ praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
         h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
         pure (Just (s, b, h))
       pure (BatchResult vs bs (fromIntegral stop) st' tip')
+
+-- | 'praosValidateHeaderSpans'' result: the chain stop, the PraosState CBOR and the tip
+-- after the last valid header.
+data SpanResult = SpanResult
+  { srChainStop :: !Int
+  , srState     :: !BS.ByteString
+  , srTip       :: !(Maybe (Word64, Word64, BS.ByteString))
+  }
+
+-- | 'praosValidateHeaderBytes' over Storable vectors: the stored header spans in one arena
+-- with their offsets and lengths, the verdicts (PRAOS_V_*) and check bits (PRAOS_BIT_*)
+-- written into the caller's mutable vectors (length n each).  An arena of 64 MiB or more is
+-- page-locked for the call (praos_host_register: the upload goes by direct DMA, no staging
+-- copy).  The decoded fields the fold reads stay in one allocation of 125 bytes per header.
+praosValidateHeaderSpans :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
+                         -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> BS.ByteString
+                         -> VS.Vector Word64 -> VS.Vector Word32 -> VSM.IOVector Word8 -> VSM.IOVector Word16
+                         -> IO SpanResult
+praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor arena offs lens
+                         verdicts bits = do
+  let n = VS.length offs
+  when (VS.length lens /= n || VSM.length verdicts /= n || VSM.length bits /= n) $
+    throwIO (PraosBatchError (-1) "praosValidateHeaderSpans: vector lengths differ")
+  BSU.unsafeUseAsCStringLen arena $ \(ap, alen) ->
+    VS.unsafeWith offs $ \offp -> VS.unsafeWith lens $ \lenp ->
+    VSM.unsafeWith verdicts $ \verdict -> VSM.unsafeWith bits $ \bitp ->
+    allocaBytes 40 $ \hb -> allocaArray n $ \(pidx :: Ptr Int32) ->
+    -- decoded fields: slot, block no, ocert n (8 B each), prev hash, cold vk, header hash (32 B
+    -- each), body size (4 B), prev-is-genesis (1 B) = 125 B per header, one allocation
+    allocaBytes (125 * n) $ \decbuf ->
+    allocaBytes 168 $ \dec -> allocaBytes 40 $ \out -> allocaBytes 120 $ \hv -> allocaBytes 120 $ \env ->
+    alloca $ \stopp -> alloca $ \donep ->
+    withChainState stateCbor (n + 65536) $ \st -> withEpochInfo ei $ \eip -> do
+      let slot = decbuf :: Ptr Word64
+          bno = decbuf `plusPtr` (8 * n) :: Ptr Word64
+          ocn = decbuf `plusPtr` (16 * n) :: Ptr Word64
+          prev = decbuf `plusPtr` (24 * n) :: Ptr Word8
+          cold = decbuf `plusPtr` (56 * n) :: Ptr Word8
+          hh = decbuf `plusPtr` (88 * n) :: Ptr Word8
+          bsz = decbuf `plusPtr` (120 * n) :: Ptr Word32
+          gen = decbuf `plusPtr` (124 * n) :: Ptr Word8
+          big = alen >= 64 * 1024 * 1024
+      pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
+      pokeByteOff hb 16 (fromIntegral alen :: CSize)
+      pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
+      fillBytes out 0 40 >> pokeByteOff out 0 bitp >> pokeByteOff out 8 pidx
+      fillBytes dec 0 168
+      pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
+      pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
+      when big $ check ctx (c_host_register p (castPtr ap) (fromIntegral alen))
+      check ctx (c_verify_header_bytes p (castPtr hb) (castPtr out) (castPtr dec))
+      when big $ check ctx (c_host_unregister p (castPtr ap))
+      fillBytes hv 0 120
+      pokeByteOff hv 0 (fromIntegral n :: CSize) >> pokeByteOff hv 8 slot >> pokeByteOff hv 16 cold
+      pokeByteOff hv 56 ocn
+      fillBytes env 0 120
+      pokeByteOff env 0 bno >> pokeByteOff env 8 hh >> pokeByteOff env 16 lenp >> pokeByteOff env 24 bsz
+      case tip of
+        Nothing -> pokeByteOff env 32 (1 :: Int32)
+        Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+      pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
+      pokeByteOff env 112 maxBS
+      check ctx (c_validate_headers p (castPtr hv) prev gen (castPtr out) (castPtr env) eip st verdict stopp donep)
+      stop <- peek stopp
+      st' <- encodeChainState st
+      origin :: Int32 <- peekByteOff env 32
+      tip' <- if origin /= 0 then pure Nothing else do
+        s <- peekByteOff env 40
+        b <- peekByteOff env 48
+        h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+        pure (Just (s, b, h))
+      pure (SpanResult (fromIntegral stop) st' tip')
 
 -- ---------------------------------------------------------------- TPraos headers from stored bytes
 

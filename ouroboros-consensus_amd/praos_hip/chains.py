@@ -35,6 +35,11 @@ CONFIGS = {
     "c5": dict(npools=3000, stake_offset=10, f=Fraction(1, 20), slots_per_kes_period=129600, max_kes_evo=62,
                blocks=432_000, eta0=hashlib.blake2b(b"bench-epoch-nonce", digest_size=32).digest(),
                seed=b"C5" + b"\xc5" * 30, epoch_length=8_640_000),
+    # TPraos (Shelley..Alonzo) analogue of C5: the same stake distribution and f, the TPraos
+    # leader certificate (mkSeed seedL, 64-byte output, bound 2^512) decides the forger
+    "tp": dict(npools=3000, stake_offset=10, f=Fraction(1, 20), slots_per_kes_period=129600, max_kes_evo=62,
+               blocks=432_000, eta0=hashlib.blake2b(b"bench-tpraos-nonce", digest_size=32).digest(),
+               seed=b"TP" + b"\x7c" * 30, epoch_length=8_640_000, tpraos=True),
 }
 
 
@@ -63,7 +68,7 @@ def search_schedule(ctx, cfg, blocks, first_slot=0, window=200_000, progress=Non
     if blocks <= 0:
         return np.zeros(0, np.uint64), np.zeros(0, np.uint32)
     while found < blocks and (max_seconds is None or time.time() - t0 < max_seconds):
-        lead = ctx.leader_schedule(cfg["seed"], sig, p, cfg["eta0"], s0, window)
+        lead = ctx.leader_schedule(cfg["seed"], sig, p, cfg["eta0"], s0, window, tpraos=cfg.get("tpraos", False))
         idx = np.nonzero(lead >= 0)[0]
         slots.append((s0 + idx).astype(np.uint64))
         pools.append(lead[idx].astype(np.uint32))
@@ -92,14 +97,17 @@ def make_chain(ctx, cfg, schedule, n=None, corrupt_per_10000=0, cbor_bodies=True
     """Sign the first n blocks of a schedule.  Returns (H, pool_list, corrupted, params)
     with pool_list = [(hash28, vrf_hash32, sigma_fp)] in forger order.  link=True: a real
     chain, hbPrev = headerHash of the previous block (block 0: prev0, None = GenesisHash),
-    H["header_hash"] holds the header hashes (sequential re-signing, ~0.1 ms per block)."""
+    H["header_hash"] holds the header hashes (sequential re-signing, ~0.1 ms per block).
+    TPraos configs (cfg["tpraos"]) sign BHeaders: both certificates, the 15-field BHBody as
+    the KES message."""
     slots, pools = schedule
     n = len(slots) if n is None else n
     p = params(cfg)
     H, keys, corrupted = ctx.synthesize(n, cfg["npools"], p, cfg["eta0"], cfg["seed"],
                                         body_len=0 if cbor_bodies else body_len,
                                         corrupt_per_10000=corrupt_per_10000, nkes=nkes,
-                                        schedule=(slots[:n], pools[:n]), link=link, prev0=prev0)
+                                        schedule=(slots[:n], pools[:n]), link=link, prev0=prev0,
+                                        tpraos=cfg.get("tpraos", False))
     sig = stake(cfg["npools"], cfg["stake_offset"])
     pool_list = [(h, v, s) for (h, v), s in zip(keys, sig)]
     return H, pool_list, corrupted, p

@@ -10,7 +10,8 @@ the -m gpu tests that run them at their stated sizes (host-side plumbing).
   c4  configs[3]: 1M Sum6KES signatures over 397-byte messages, 3000 pools x 64 KES periods,
       1 % corrupted in the KES signature / message
   c5  configs[4]: the first 432,000 blocks of the C5 chain (chains.py, data/c5_schedule.npz)
-  tp  TPraos headers from stored bytes, 3000 pools forging in turn (f = 1)
+  tp  TPraos headers from stored bytes: the first 432,000 blocks of a first-leader-wins TPraos
+      chain (3000 pools, f = 1/20, data/tp_schedule.npz)
 
 Each returns (H, pool_list, corrupted, params, eta0, c_raw, slots_per_kes_period, max_kes_evo);
 `corrupted[i]` is the synthesizer's corruption kind (0 clean, 1 OCert, 2 KES signature,
@@ -43,19 +44,15 @@ def build(ctx, name, n=None, corrupt_per_10000=100, rank=0, world=1, scaling="we
         return (H, pool_list, corrupted, p, ccfg["eta0"], fixed.active_slot_log(ccfg["f"]),
                 ccfg["slots_per_kes_period"], ccfg["max_kes_evo"])
     if name == "tp":
-        # two VRF certificates per header, the 2^512 leader bound; f = 1 and the pools in turn
-        # (checkLeaderNatValue's f = 1 case), stored as BHeader bytes by the caller
-        npools = 3000
-        ccfg = dict(npools=npools, stake_offset=10, f=Fraction(1), slots_per_kes_period=129600,
-                    max_kes_evo=62, eta0=hashlib.blake2b(b"bench-tpraos-nonce", digest_size=32).digest())
-        p = chains.params(ccfg)
-        sl = np.arange(rank * n, (rank + 1) * n, dtype=np.uint64)
-        pl = (sl % npools).astype(np.uint32)
-        H, keys, corrupted = ctx.synthesize(n, npools, p, ccfg["eta0"], b"TP" + b"\x5c" * 26 + rank.to_bytes(4, "little"),
-                                            body_len=0, schedule=(sl, pl), tpraos=True,
-                                            corrupt_per_10000=corrupt_per_10000)
-        pool_list = [(h, v, s_) for (h, v), s_ in zip(keys, chains.stake(npools, 10))]
-        return H, pool_list, corrupted, p, ccfg["eta0"], 0, 129600, 62
+        # TPraos: the first 432,000 blocks of a first-leader-wins TPraos chain (chains.py "tp":
+        # 3000 pools, f = 1/20, the leader certificate against 2^512; data/tp_schedule.npz),
+        # two VRF certificates per header, BHeader bytes stored and decoded by the caller
+        ccfg = chains.CONFIGS["tp"]
+        sched = chains.load_schedule("tp")
+        assert n <= len(sched[0]), "the shipped TPraos schedule has fewer blocks"
+        H, pool_list, corrupted, p = chains.make_chain(ctx, ccfg, sched, n=n, corrupt_per_10000=corrupt_per_10000)
+        return (H, pool_list, corrupted, p, ccfg["eta0"], fixed.active_slot_log(ccfg["f"]),
+                ccfg["slots_per_kes_period"], ccfg["max_kes_evo"])
     if name == "c3":
         # the C5 chain's keys, stake, f and eta0; the (slot, pool) pairs of its schedule's first
         # 1M blocks (a rank > 0 of a weak-scaling run takes the next 1M-block window when the
