@@ -26,7 +26,7 @@
  *   "typed":    the sequence of Batch/Validate.hs validateEpochHeaders (praosValidateHeaderSpans):
  *               per epoch praos_ticked_epoch_nonce -> praos_set_epoch -> praos_host_register of
  *               the arena (the binding does it from 64 MiB on; always here, so the path runs) ->
- *               praos_verify_header_bytes with the decoded fields in one 125-byte-per-header
+ *               praos_verify_header_bytes with the decoded fields in one 157-byte-per-header
  *               allocation -> praos_host_unregister -> praos_validate_headers ->
  *               praos_state_encode; also prints the stopping header's verdict and bits, what
  *               Batch.Errors rebuilds the typed HeaderError from (must agree);
@@ -308,12 +308,13 @@ static void phase_typed(const chain_t* ch) {
     uint8_t* verdict = calloc(n, 1);
     uint16_t* bits = calloc(n, 2);
     int32_t* pidx = calloc(n, 4);
-    uint8_t* decbuf = calloc(n, 125);      /* slot, block no, ocert n | prev, cold, hash | body size | gen */
+    uint8_t* decbuf = calloc(n, 157);      /* slot, block no, ocert n | prev, cold, hash | body size | gen | nonce */
     uint64_t *slot = (uint64_t*)decbuf, *bno = (uint64_t*)(decbuf + 8 * n), *ocn = (uint64_t*)(decbuf + 16 * n);
     uint8_t *prev = decbuf + 24 * n, *cold = decbuf + 56 * n, *hh = decbuf + 88 * n, *gen = decbuf + 124 * n;
     uint32_t* bsz = (uint32_t*)(decbuf + 120 * n);
+    uint8_t* nonce = decbuf + 125 * n;     /* the certified VRF outputs' nonce values (the fold evolves them) */
     praos_header_bytes hb = {n, arena, alen, off, ch->hlen + i};
-    praos_out out = {bits, pidx, NULL, NULL, NULL};
+    praos_out out = {bits, pidx, NULL, NULL, nonce};
     praos_decoded dec;
     memset(&dec, 0, sizeof dec);
     dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;

@@ -333,7 +333,8 @@ data SpanResult = SpanResult
 -- with their offsets and lengths, the verdicts (PRAOS_V_*) and check bits (PRAOS_BIT_*)
 -- written into the caller's mutable vectors (length n each).  An arena of 64 MiB or more is
 -- page-locked for the call (praos_host_register: the upload goes by direct DMA, no staging
--- copy).  The decoded fields the fold reads stay in one allocation of 125 bytes per header.
+-- copy).  The decoded fields and nonce values the fold reads stay in one allocation of 157
+-- bytes per header.
 praosValidateHeaderSpans :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
                          -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> BS.ByteString
                          -> VS.Vector Word64 -> VS.Vector Word32 -> VSM.IOVector Word8 -> VSM.IOVector Word16
@@ -348,8 +349,9 @@ praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
     VSM.unsafeWith verdicts $ \verdict -> VSM.unsafeWith bits $ \bitp ->
     allocaBytes 40 $ \hb -> allocaArray n $ \(pidx :: Ptr Int32) ->
     -- decoded fields: slot, block no, ocert n (8 B each), prev hash, cold vk, header hash (32 B
-    -- each), body size (4 B), prev-is-genesis (1 B) = 125 B per header, one allocation
-    allocaBytes (125 * n) $ \decbuf ->
+    -- each), body size (4 B), prev-is-genesis (1 B), the nonce value of the certified VRF
+    -- output (32 B, the fold evolves the nonce with it) = 157 B per header, one allocation
+    allocaBytes (157 * n) $ \decbuf ->
     allocaBytes 168 $ \dec -> allocaBytes 40 $ \out -> allocaBytes 120 $ \hv -> allocaBytes 120 $ \env ->
     alloca $ \stopp -> alloca $ \donep ->
     withChainState stateCbor (n + 65536) $ \st -> withEpochInfo ei $ \eip -> do
@@ -361,11 +363,12 @@ praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
           hh = decbuf `plusPtr` (88 * n) :: Ptr Word8
           bsz = decbuf `plusPtr` (120 * n) :: Ptr Word32
           gen = decbuf `plusPtr` (124 * n) :: Ptr Word8
+          nonce = decbuf `plusPtr` (125 * n) :: Ptr Word8
           big = alen >= 64 * 1024 * 1024
       pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
       pokeByteOff hb 16 (fromIntegral alen :: CSize)
       pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
-      fillBytes out 0 40 >> pokeByteOff out 0 bitp >> pokeByteOff out 8 pidx
+      fillBytes out 0 40 >> pokeByteOff out 0 bitp >> pokeByteOff out 8 pidx >> pokeByteOff out 32 nonce
       fillBytes dec 0 168
       pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
       pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh

@@ -2180,13 +2180,21 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
                      const praos_nonce* etas = nullptr, uint32_t netas = 0, const uint8_t* eta_idx = nullptr,
                      bool tpraos = false, const praos_nonce* extra_entropy = nullptr, uint16_t* failures = nullptr,
                      const praos_nonce* evol_after = nullptr) {
-  if (!c || !h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash ||
-      ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter)))
+  if (!c) return PRAOS_E_ARG;
+  if (!h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash) {
+    c->err = "fold: a required pointer is NULL (headers, crypto bits / nonce, verdict, epoch info, state, prev_hash)";
     return PRAOS_E_ARG;
-  if (env && h->n && (!env->block_no || !env->header_hash || !env->header_size || !env->body_size))
+  }
+  if (ei->epoch_length == 0 || st->m > st->cap || (st->cap && (!st->counter_hash28 || !st->counter))) {
+    c->err = "fold: epoch_length 0 or a counter map without room";
     return PRAOS_E_ARG;
-  if (!c->have_epoch) return PRAOS_E_STATE;
-  if (eta_idx && (!etas || netas == 0)) return PRAOS_E_ARG;
+  }
+  if (env && h->n && (!env->block_no || !env->header_hash || !env->header_size || !env->body_size)) {
+    c->err = "fold: the envelope needs block_no, header_hash, header_size and body_size";
+    return PRAOS_E_ARG;
+  }
+  if (!c->have_epoch) { c->err = "fold: no epoch installed (praos_set_epoch)"; return PRAOS_E_STATE; }
+  if (eta_idx && (!etas || netas == 0)) { c->err = "fold: eta_idx without etas"; return PRAOS_E_ARG; }
   praos_nonce eta0{};
   eta0.neutral = c->eta0_neutral;
   if (!c->eta0_neutral) std::memcpy(eta0.hash, c->eta0, 32);
