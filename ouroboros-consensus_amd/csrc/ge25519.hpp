@@ -21,14 +21,30 @@ FE_INLINE void ge_p2_identity(ge_p2& p) { fe_set(p.X, 0); fe_set(p.Y, 1); fe_set
 FE_INLINE void ge_cached_identity(ge_cached& c) { fe_set(c.YpX, 1); fe_set(c.YmX, 1); fe_set(c.Z, 1); fe_set(c.T2d, 0); }
 FE_INLINE void ge_niels_identity(ge_niels& c) { fe_set(c.ypx, 1); fe_set(c.ymx, 1); fe_set(c.xy2d, 0); }
 
+// PRAOS_ILP4 (a module built for latency-bound small batches, fewer waves per SIMD): the
+// independent products of each formula -- 3 or 4 of them -- interleaved in one pass
+// (fe_mul3 / fe_mul4 / fe_sq4); otherwise in pairs (fe_mul2 / fe_sq2), which keeps the
+// register footprint of the 3-waves-per-SIMD kernels.  Same operations, same results.
+#ifndef PRAOS_ILP4
+#define PRAOS_ILP4 0
+#endif
+
 // (r and p are distinct objects at every call site; the paired products read p only)
 FE_INLINE void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+#if PRAOS_ILP4
+  fe_mul3(r.X, p.X, p.T, r.Y, p.Y, p.Z, r.Z, p.Z, p.T);
+#else
   fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.Z, p.T);
+#endif
 }
 FE_INLINE void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+#if PRAOS_ILP4
+  fe_mul4(r.X, p.X, p.T, r.Y, p.Y, p.Z, r.Z, p.Z, p.T, r.T, p.X, p.Y);
+#else
   fe_mul2(r.X, p.X, p.T, r.Y, p.Y, p.Z);
   fe_mul2(r.Z, p.Z, p.T, r.T, p.X, p.Y);
+#endif
 }
 FE_INLINE void ge_p3_to_p2(ge_p2& r, const ge_p3& p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
 
@@ -45,8 +61,12 @@ FE_INLINE void ge_p3_to_cached(ge_cached& c, const ge_p3& p) {
 FE_INLINE void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe t0;
   fe_add(r.Y, p.X, p.Y);
+#if PRAOS_ILP4
+  fe_sq4(r.X, p.X, r.Z, p.Y, r.T, p.Z, t0, r.Y);
+#else
   fe_sq2(r.X, p.X, r.Z, p.Y);
   fe_sq2(r.T, p.Z, t0, r.Y);
+#endif
   fe_add(r.T, r.T, r.T);
   fe_add(r.Y, r.Z, r.X);
   fe_sub(r.Z, r.Z, r.X);
@@ -59,8 +79,12 @@ FE_INLINE void ge_add(ge_p1p1& r, const ge_p3& p, const ge_cached& q) {
   fe t0;
   fe_add(r.X, p.Y, p.X);
   fe_sub(r.Y, p.Y, p.X);
+#if PRAOS_ILP4
+  fe_mul4(r.Z, r.X, q.YpX, r.Y, r.Y, q.YmX, r.T, q.T2d, p.T, r.X, p.Z, q.Z);
+#else
   fe_mul2(r.Z, r.X, q.YpX, r.Y, r.Y, q.YmX);
   fe_mul2(r.T, q.T2d, p.T, r.X, p.Z, q.Z);
+#endif
   fe_add(t0, r.X, r.X);
   fe_sub(r.X, r.Z, r.Y);
   fe_add(r.Y, r.Z, r.Y);
@@ -73,8 +97,12 @@ FE_INLINE void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe t0;
   fe_add(r.X, p.Y, p.X);
   fe_sub(r.Y, p.Y, p.X);
+#if PRAOS_ILP4
+  fe_mul3(r.Z, r.X, q.ypx, r.Y, r.Y, q.ymx, r.T, q.xy2d, p.T);
+#else
   fe_mul2(r.Z, r.X, q.ypx, r.Y, r.Y, q.ymx);
   fe_mul(r.T, q.xy2d, p.T);
+#endif
   fe_add(t0, p.Z, p.Z);
   fe_sub(r.X, r.Z, r.Y);
   fe_add(r.Y, r.Z, r.Y);

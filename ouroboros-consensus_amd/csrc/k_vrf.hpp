@@ -53,6 +53,17 @@ __device__ __forceinline__ int32_t pool_search(const uint32_t hk[8], const uint3
   return -1;
 }
 
+// alpha = mkInputVRF(slot, eta) of header i (Praos/VRF.hs:55-69), or for a TPraos
+// certificate mkSeed(ucNonce, slot, eta) (TPraos.hs:378-387 -> BHeader.mkSeed)
+__device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, size_t i) {
+  uint32_t e0[8];
+  const uint32_t* ep = a.eta_idx ? a.eta0 + 9 * (uint32_t)a.eta_idx[i] : a.eta0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) e0[k] = ep[k];
+  const bool neutral = a.eta_idx ? ep[8] != 0 : a.eta0_neutral != 0;
+  if (a.tp_seed) tpraos_seed(alpha, a.slot[i], e0, neutral, (uint64_t)(a.tp_seed - 1));
+  else mk_input_vrf(alpha, a.slot[i], e0, neutral);
+}
 
 static inline VrfIn vrf_in(const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out, const uint8_t* vrf_proof,
                     const uint64_t* slot, const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx,

@@ -13,18 +13,6 @@
 #endif
 
 // ---- two-stage form of the header mode (praos_core.hpp vrf_v_core / vrf_fin_core)
-// alpha = mkInputVRF(slot, eta) of header i (Praos/VRF.hs:55-69), or for a TPraos
-// certificate mkSeed(ucNonce, slot, eta) (TPraos.hs:378-387 -> BHeader.mkSeed)
-__device__ __forceinline__ void header_alpha(uint32_t alpha[8], const VrfIn& a, size_t i) {
-  uint32_t e0[8];
-  const uint32_t* ep = a.eta_idx ? a.eta0 + 9 * (uint32_t)a.eta_idx[i] : a.eta0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) e0[k] = ep[k];
-  const bool neutral = a.eta_idx ? ep[8] != 0 : a.eta0_neutral != 0;
-  if (a.tp_seed) tpraos_seed(alpha, a.slot[i], e0, neutral, (uint64_t)(a.tp_seed - 1));
-  else mk_input_vrf(alpha, a.slot[i], e0, neutral);
-}
-
 // stage V over every header of the batch: no dependence on the key cache
 __global__ void __launch_bounds__(NT, LB_VRF_V) k_vrf_v(size_t n, size_t i0, size_t i1, VrfIn a, uint4* __restrict__ mid) {
   const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // headers [i0, i1), record stride n
@@ -297,7 +285,12 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join_tp(size_t n, int cert
 // ---- host launchers (kernels are only launchable from their own module)
 void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uint8_t* vrf_proof, const uint64_t* slot,
                   const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
-                  size_t i0, size_t i1, int wave_prio, int tp_seed) {
+                  size_t i0, size_t i1, int wave_prio, int tp_seed, int ilp4) {
+  if (ilp4) {
+    launch_vrf_v4(stream, n, i0, i1, vrf_vk, vrf_proof, slot, eta0, eta0_neutral, eta_idx, tabs, mid, wave_prio,
+                  tp_seed);
+    return;
+  }
   VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
                    nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
   a.wave_prio = wave_prio;

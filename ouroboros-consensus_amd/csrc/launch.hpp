@@ -98,7 +98,12 @@ void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uin
                   const uint32_t* eta0, int eta0_neutral, const uint8_t* eta_idx, ge_cached* tabs, void* mid,
                   size_t i0 = 0, size_t i1 = SIZE_MAX,    // headers [i0, min(i1, n)); mid stride n
                   int wave_prio = 0,                       // waves at s_setprio 3
-                  int tp_seed = 0);                        // 1 + k: TPraos mkSeed alpha, ucNonce k
+                  int tp_seed = 0,                         // 1 + k: TPraos mkSeed alpha, ucNonce k
+                  int ilp4 = 0);                           // the ILP-4 build (k_vrf_v4.hip)
+// stage V built with the ILP-4 group formulas at 2 waves per SIMD (k_vrf_v4.hip; small batches)
+void launch_vrf_v4(hipStream_t stream, size_t n, size_t i0, size_t i1, const uint8_t* vrf_vk,
+                   const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
+                   const uint8_t* eta_idx, ge_cached* tabs, void* mid, int wave_prio, int tp_seed);
 void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
                     const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,

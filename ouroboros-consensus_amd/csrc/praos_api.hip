@@ -138,6 +138,9 @@ struct praos_ctx {
   int tp_staged = 1;                                  // TPraos VRF through the staged kernels + VRF key cache
                                                        // (PRAOS_TP_STAGED=0: the one-kernel k_vrf_tp)
   int vrf_prio = 0;                                   // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO; -1: small batches)
+  int vrf_ilp4 = 0;                                   // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
+                                                       // 1 always, 0 never, N > 1: batches below N headers
+  bool v_ilp4(size_t n) const { return vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4); }
   int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
                                                        // the three-kernel form below 300k headers (latency)
   // chunked stored-bytes pipeline (praos_verify_header_bytes): a copy stream, per-chunk
@@ -463,6 +466,7 @@ static bool open_streams(praos_ctx* c) {
   (void)hipEventCreateWithFlags(&c->u_ev, hipEventDisableTiming);
   if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_VRF_PRIO")) c->vrf_prio = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_VRF_ILP4")) c->vrf_ilp4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -1161,7 +1165,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (sVk[k] != c->stream) HIPCHK(c, hipStreamWaitEvent(sVk[k], c->ev[0], 0));
       if (k == 0) HIPCHK(c, hipEventRecord(c->v0_ev, sVk[0]));
       launch_vrf_v(sVk[k], n, b->vrf_vk, proof[k], b->slot, eta, c->eta0_neutral, b->eta_idx, vtab[k], mid[k], 0,
-                   SIZE_MAX, wprio, 1 + k);
+                   SIZE_MAX, wprio, 1 + k, c->v_ilp4(n));
     }
     HIPCHK(c, hipEventRecord(c->v1_ev, sVk[0]));
     c->v_timed = true;
@@ -1210,7 +1214,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
       HIPCHK(c, hipEventRecord(c->v0_ev, sV));
       launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
-                   b->vrf_mid, 0, SIZE_MAX, wprio);
+                   b->vrf_mid, 0, SIZE_MAX, wprio, 0, c->v_ilp4(n));
       HIPCHK(c, hipEventRecord(c->v1_ev, sV));
       c->v_timed = true;
     }
@@ -1810,7 +1814,7 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
       hipStream_t sv = (k & 1) ? c->vstream2 : c->vstream;
       HIPCHK(c, hipStreamWaitEvent(sv, c->done_ev[k], 0));
       launch_vrf_v(sv, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
-                   b->vrf_mid, lo[k], lo[k + 1]);
+                   b->vrf_mid, lo[k], lo[k + 1], 0, 0, c->v_ilp4(n));
       HIPCHK(c, hipGetLastError());
     }
   }
