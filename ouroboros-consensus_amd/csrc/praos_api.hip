@@ -155,6 +155,8 @@ struct praos_ctx {
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
+  int kc_min[3] = {0, 0, 0};                           // per cache (cold, VRF, KES leaf) min uses overriding
+                                                       // keycache when > 0 (PRAOS_KC_MIN="c,v,k")
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
   int key_wave_prio = 0;                               // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO=1; A/B: no gain)
   hipEvent_t ev[6] = {};
@@ -467,6 +469,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_VRF_PRIO")) c->vrf_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_VRF_ILP4")) c->vrf_ilp4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -962,13 +965,14 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
 
 // key cache prepass over items [0, n) (or list[0 .. *count)): hash set, entries, hit/miss lists
 static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint8_t* keys, hipStream_t st,
-                    const uint32_t* list = nullptr, const uint32_t* count = nullptr) {
+                    const uint32_t* list, const uint32_t* count, int which) {
+  const int min_uses = c->kc_min[which] > 0 ? c->kc_min[which] : c->keycache;
   const dim3 g(nblocks(n, NT)), blk(NT);
   HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
   HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
   HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
   launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
-  launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)c->keycache,
+  launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)min_uses,
                     k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
   launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit, k.miss,
                        k.counters);
@@ -1047,7 +1051,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   };
   auto keycache_lists = [&](praos_batch::KeyCache& k, const uint8_t* keys, hipStream_t st,
                             const uint32_t* list = nullptr, const uint32_t* count = nullptr) -> int {
-    return kc_lists(c, k, n, keys, st, list, count);
+    return kc_lists(c, k, n, keys, st, list, count, (int)(&k - b->kc));
   };
   auto keycache_precompute = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
     kc_precompute(c, k, keys, kind, st);
