@@ -138,8 +138,10 @@ struct praos_ctx {
   int tp_staged = 1;                                  // TPraos VRF through the staged kernels + VRF key cache
                                                        // (PRAOS_TP_STAGED=0: the one-kernel k_vrf_tp)
   int vrf_prio = 0;                                   // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO; -1: small batches)
-  int vrf_ilp4 = 0;                                   // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
+  int vrf_ilp4 = 80000;                               // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
                                                        // 1 always, 0 never, N > 1: batches below N headers
+                                                       // (profiles/r04/b: V alone 1.71 -> 1.51 ms at 54k, slower
+                                                       // from 108k: 2.33 -> 2.27 ms alone but the step 4.25 -> 4.37)
   bool v_ilp4(size_t n) const { return vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4); }
   int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
                                                        // the three-kernel form below 300k headers (latency)
