@@ -50,23 +50,28 @@ from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  #
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03e_traffic.json")   # tools/profile.sh r03e
-FEMUL_FILE = os.path.join(ROOT, "profiles", "r02", "femul_microbench.txt")  # tools/microbench/femul.hip
+PMC_FILE = os.path.join(ROOT, "profiles", "r03e_pmc.json")            # tools/profile.sh r03e
 
 
-def issue_weighted_peak():
-    """The integer ceiling the field multiply itself reaches (measured, femul microbench):
-    a multiply is 154 counted ops (tools/workmodel.py M) and takes C SIMD cycles per wave
-    when the SIMD is kept full, so mul-bound work peaks at 154 x 64 / C lane-ops per
-    SIMD-cycle -- below the 128 lane-ops/clk/CU issue peak because v_mad_u64_u32 issues
-    at ~5.2 cycles per wave instruction instead of 2."""
+def load_pmc(kernel):
+    """VALU issue of `kernel` from the committed rocprofv3 PMC summary of the same workload
+    (tools/profile.sh + tools/prof_summary.py): wave-level VALU instructions per launch and
+    VALUBusy = SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs),
+    the fraction of SIMD cycles the vector ALU was issuing while the kernel ran."""
     try:
-        for line in open(FEMUL_FILE):
-            if line.startswith("radix 2^32, asm MAC"):
-                cyc = float(line.split("SIMD cycles")[0].split()[-1])
-                return 154 * 64 / cyc * 4 * 256 * 2.4e9, cyc
-    except (OSError, ValueError, IndexError):
-        pass
-    return None, None
+        d = json.load(open(PMC_FILE)).get(kernel)
+        valu = d["SQ_ACTIVE_INST_VALU"]["per_dispatch"]
+        gui = d["GRBM_GUI_ACTIVE"]["per_dispatch"] / 8
+        insts = d["SQ_INSTS_VALU"]["per_dispatch"]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    return {"valu_busy": round(valu * 4 / (256 * 4) / gui, 4), "valu_wave_insts_per_launch": insts,
+            "simd_cycles_per_valu_inst": round(gui * 256 * 4 / insts, 2),
+            "source": os.path.relpath(PMC_FILE, ROOT),
+            "basis": "VALUBusy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) (rocprof's "
+                     "derived metric); simd_cycles_per_valu_inst = kernel cycles x 1024 SIMDs / SQ_INSTS_VALU, "
+                     "against 2 for the guide's nominal issue rate and ~4 measured for one wave's stream"}
+
 
 CONFIGS = {
     "c1": dict(items=10_000, kernels=7, metric="Praos headers validated/sec (CPU config C1)",
@@ -584,7 +589,7 @@ def main():
     traffic = tk.get("bytes_per_launch") if tk else None
     # the same kernel's average duration in the committed rocprofv3 kernel trace (isolated launches)
     rp_ms = tk.get("rocprof_isolated_avg_ms") if tk else None
-    iw_peak, iw_cyc = issue_weighted_peak()
+    pmc = load_pmc(dom_kernel) if args.config == "c5" else None
     line = {
         "metric": cfg["metric"],
         "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
@@ -614,11 +619,7 @@ def main():
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},
                      "pipeline_ms": round(kms[4], 3), "concurrent_streams": bool(args.concurrent),
                      "peak_basis": "128 int32 lane-ops/clk/CU x 256 CU x 2.4 GHz (VALU issue, MI355X_MICROARCH.md)",
-                     "issue_weighted_peak": round(iw_peak / 1e12, 2) if iw_peak else None,
-                     "frac_of_issue_weighted": round(dom_achieved / iw_peak, 4) if iw_peak else None,
-                     "issue_weighted_basis": (f"field multiply = 154 counted ops in {iw_cyc} SIMD cycles per wave "
-                                              f"(femul microbench, {os.path.relpath(FEMUL_FILE, ROOT)})")
-                                             if iw_peak else None},
+                     "valu_issue_pmc": pmc},
         "keycache": dict(kst, min_uses=args.keycache),
         "ocert_dedup": {"on": bool(args.dedup), "distinct_ocerts_verified": dds["ocert_unique"], "headers": n,
                         "value_without_dedup": round(nodedup, 1) if nodedup else None,
