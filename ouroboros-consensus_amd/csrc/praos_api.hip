@@ -92,6 +92,11 @@ class CopyPool {
 static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2 x 16 MB per context
 static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
 static constexpr size_t PIPE_MIN_CHUNK = 65536;     // headers per chunk at least (auto mode)
+// Batches below this many headers (a strong-scaling shard of an epoch over 8 GPUs is 54k) leave
+// most wave slots empty and run latency-bound: stage V from the ILP-4 build, stage V / join and
+// the key precomputes at raised wave priority (profiles/r04/c: 54k step 3.52 -> 3.34 ms together;
+// each alone within noise, profiles/r03/prio_ab)
+static constexpr size_t SMALL_BATCH = 80000;
 static constexpr int PIPE_AUTO = 6;                 // chunks in auto mode (432k headers: 4 -> 21.9M, 6 -> 23.0M,
                                                     // 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt)
 struct praos_batch;
@@ -137,8 +142,9 @@ struct praos_ctx {
   hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
   int tp_staged = 1;                                  // TPraos VRF through the staged kernels + VRF key cache
                                                        // (PRAOS_TP_STAGED=0: the one-kernel k_vrf_tp)
-  int vrf_prio = 0;                                   // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO; -1: small batches)
-  int vrf_ilp4 = 80000;                               // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
+  int vrf_prio = -1;                                  // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO 1 / 0;
+                                                       // -1: batches below SMALL_BATCH headers)
+  int vrf_ilp4 = (int)SMALL_BATCH;                    // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
                                                        // 1 always, 0 never, N > 1: batches below N headers
                                                        // (profiles/r04/b: V alone 1.71 -> 1.51 ms at 54k, slower
                                                        // from 108k: 2.33 -> 2.27 ms alone but the step 4.25 -> 4.37)
@@ -160,7 +166,8 @@ struct praos_ctx {
   int kc_min[3] = {0, 0, 0};                           // per cache (cold, VRF, KES leaf) min uses overriding
                                                        // keycache when > 0 (PRAOS_KC_MIN="c,v,k")
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
-  int key_wave_prio = 0;                               // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO=1; A/B: no gain)
+  int key_wave_prio = -1;                              // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO 1 / 0;
+                                                       // -1: batches below SMALL_BATCH headers)
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
@@ -455,7 +462,7 @@ const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 
 // streams and events of a context (praos_open, and the pipeline's second engine)
 static bool open_streams(praos_ctx* c) {
-  if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp) != 0;
+  if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp);
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->stream = nullptr;
     return false;
@@ -980,9 +987,10 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
                        k.counters);
   return PRAOS_OK;
 }
-static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
+static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st, size_t n) {
   launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries, k.entry_rep,
-                        keys, k.ktab, k.kinfo, c->key_wave_prio);
+                        keys, k.ktab, k.kinfo,
+                        c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < SMALL_BATCH));
 }
 
 static int batch_run_impl(praos_ctx* c, praos_batch* b) {
@@ -1056,7 +1064,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     return kc_lists(c, k, n, keys, st, list, count, (int)(&k - b->kc));
   };
   auto keycache_precompute = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
-    kc_precompute(c, k, keys, kind, st);
+    kc_precompute(c, k, keys, kind, st, n);
   };
   b->dd_used = false;
   std::function<void()> ocert_miss;
@@ -1166,7 +1174,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     // headers leaves most wave slots empty with one V at a time
     hipStream_t sVk[2] = {c->concurrent ? c->vstream : c->stream, c->concurrent ? c->vstream2 : c->stream};
     ge_cached* vtab[2] = {b->tab_vrf, b->tab_vrf2};
-    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < 300000);
+    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
     for (int k = 0; k < 2; k++) {
       if (sVk[k] != c->stream) HIPCHK(c, hipStreamWaitEvent(sVk[k], c->ev[0], 0));
       if (k == 0) HIPCHK(c, hipEventRecord(c->v0_ev, sVk[0]));
@@ -1215,7 +1223,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     // (stored-bytes pipeline: stage V was queued chunk by chunk on vstream while the later
     // chunks were still uploading; b->v_done)
     hipStream_t sV = (c->concurrent || b->v_done) ? c->vstream : c->stream;
-    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < 300000);
+    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
     if (!b->v_done) {
       if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
       HIPCHK(c, hipEventRecord(c->v0_ev, sV));
