@@ -49,17 +49,30 @@ from workmodel import (W_OCERT, W_KES, W_VRF, W_LEADER, W_OCERT_CK, W_VRF_CK,  #
 # cycles, i.e. 32 lane-ops/clk/SIMD = 128 lane-ops/clk/CU) x 256 CUs x 2.4 GHz
 PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03e_traffic.json")   # tools/profile.sh r03e
-PMC_FILE = os.path.join(ROOT, "profiles", "r03e_pmc.json")            # tools/profile.sh r03e
+# committed rocprofv3 summaries (tools/profile.sh <tag>): <tag>_traffic.json names its workload;
+# the first tag whose workload is the bench's supplies traffic and PMC for the roofline kernel
+PROFILE_TAGS = ("r04c4", "r03e")
 
 
-def load_pmc(kernel):
+def profile_tag(workload):
+    for tag in PROFILE_TAGS:
+        try:
+            if json.load(open(os.path.join(ROOT, "profiles", f"{tag}_traffic.json"))).get("workload") == workload:
+                return tag
+        except (OSError, ValueError):
+            continue
+    return None
+
+
+def load_pmc(kernel, workload):
     """VALU issue of `kernel` from the committed rocprofv3 PMC summary of the same workload
     (tools/profile.sh + tools/prof_summary.py): wave-level VALU instructions per launch and
     VALUBusy = SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs),
     the fraction of SIMD cycles the vector ALU was issuing while the kernel ran."""
+    tag = profile_tag(workload)
+    pmc_file = os.path.join(ROOT, "profiles", f"{tag}_pmc.json")
     try:
-        d = json.load(open(PMC_FILE)).get(kernel)
+        d = json.load(open(pmc_file)).get(kernel)
         valu = d["SQ_ACTIVE_INST_VALU"]["per_dispatch"]
         gui = d["GRBM_GUI_ACTIVE"]["per_dispatch"] / 8
         insts = d["SQ_INSTS_VALU"]["per_dispatch"]
@@ -67,10 +80,12 @@ def load_pmc(kernel):
         return None
     return {"valu_busy": round(valu * 4 / (256 * 4) / gui, 4), "valu_wave_insts_per_launch": insts,
             "simd_cycles_per_valu_inst": round(gui * 256 * 4 / insts, 2),
-            "source": os.path.relpath(PMC_FILE, ROOT),
+            "source": os.path.relpath(pmc_file, ROOT),
             "basis": "VALUBusy = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) (rocprof's "
                      "derived metric); simd_cycles_per_valu_inst = kernel cycles x 1024 SIMDs / SQ_INSTS_VALU, "
-                     "against 2 for the guide's nominal issue rate and ~4 measured for one wave's stream"}
+                     "against 2 for the guide's nominal issue rate and ~4 measured for one wave's stream; "
+                     "GRBM_GUI_ACTIVE spans the dispatch, so values of ~1.0 (within a few %) mean the SIMDs "
+                     "issued VALU instructions every cycle the kernel ran"}
 
 
 CONFIGS = {
@@ -298,16 +313,15 @@ def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, sec
 
 
 def load_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (FETCH_SIZE
-    x2 gfx950 read correction + WRITE_SIZE, separate --pmc passes, tools/pmc_traffic.py)."""
-    try:
-        t = json.load(open(TRAFFIC_FILE))
-    except (OSError, ValueError):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same
+    workload (FETCH_SIZE x2 gfx950 read correction + WRITE_SIZE, separate --pmc passes,
+    tools/prof_summary.py)."""
+    tag = profile_tag(workload)
+    if tag is None:
         return None, None
-    k = t.get("kernels", {}).get(kernel)
-    if not k or t.get("workload") != workload:
-        return None, None
-    return k, os.path.relpath(TRAFFIC_FILE, ROOT)
+    f = os.path.join(ROOT, "profiles", f"{tag}_traffic.json")
+    k = json.load(open(f)).get("kernels", {}).get(kernel)
+    return (k, os.path.relpath(f, ROOT)) if k else (None, None)
 
 
 def make_input(ctx, args, cfg, rank, world=1):
@@ -390,12 +404,12 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kms = np.zeros(7)
+    kms = np.zeros(8)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         ctx.run(b)
         ctx.sync()                                     # per-step HIP-event kernel times
-        kms += [ctx.kernel_ms(k) for k in range(7)]
+        kms += [ctx.kernel_ms(k) for k in range(8)]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -407,11 +421,11 @@ def main():
     # per-kernel durations for the roofline: serial launches (HIP events on the
     # launch stream), untimed, after the timed region
     ctx.set_option(abi.OPT_CONCURRENT, 0)
-    kser = np.zeros(7)
+    kser = np.zeros(8)
     for _ in range(3):
         ctx.run(b)
         ctx.sync()
-        kser += [ctx.kernel_ms(k) for k in range(7)]
+        kser += [ctx.kernel_ms(k) for k in range(8)]
     kser /= 3
     ctx.set_option(abi.OPT_CONCURRENT, args.concurrent)
     kst = ctx.batch_stats(b)
@@ -570,6 +584,13 @@ def main():
         # every header is the largest single kernel of the step; price it alone, on the
         # HIP events around its own launch (serial run, no other kernel on the GPU)
         dom_kernel, dom_ms, dom_work, wk = "k_vrf_v", float(kser[6]), n * W_VRF_V, W_VRF_V
+    stream_frac = None
+    if dominant == "kes" and kser[7] > 0 and kst["kes_hits"]:
+        # the cached Sum6KES kernel alone (HIP events around its launch, serial pass), as stage V
+        # is priced for configs[4]; the KES stream (key lists, precompute, tables, misses) beside it
+        stream_frac = round(dom_work / (dom_ms * 1e-3) / PEAK_INT32, 4)
+        dom_kernel, dom_ms, dom_work = "k_kes_ck", float(kser[7]), kst["kes_hits"] * W_KES_CK
+        wk = W_KES_CK
     if args.config == "tp":
         # the TPraos batch runs decode, the OCert / KES passes of the Praos step (dedup, key
         # caches) and both VRF certificates through the staged kernels against the VRF key
@@ -589,7 +610,7 @@ def main():
     traffic = tk.get("bytes_per_launch") if tk else None
     # the same kernel's average duration in the committed rocprofv3 kernel trace (isolated launches)
     rp_ms = tk.get("rocprof_isolated_avg_ms") if tk else None
-    pmc = load_pmc(dom_kernel) if args.config == "c5" else None
+    pmc = load_pmc(dom_kernel, cfg["workload"])
     line = {
         "metric": cfg["metric"],
         "value": round(value, 1), "unit": "headers/s" if cfg["kernels"] == 7 else "items/s",
@@ -613,7 +634,9 @@ def main():
                      "rocprof_isolated_avg_ms": rp_ms,
                      "frac_rocprof": round(dom_work / (rp_ms * 1e-3) / PEAK_INT32, 4) if rp_ms else None,
                      "work_per_unit": round(wk), "kernel_ms": round(dom_ms, 3),
-                     "kernel_ms_concurrent": round(float(kms[6]), 3) if dom_kernel == "k_vrf_v" else None,
+                     "kernel_ms_concurrent": round(float(kms[6]), 3) if dom_kernel == "k_vrf_v" else
+                     (round(float(kms[7]), 3) if dom_kernel == "k_kes_ck" else None),
+                     "kes_stream_frac": stream_frac,
                      "pipeline_achieved": round(pipe_achieved / 1e12, 3),
                      "pipeline_frac": round(pipe_achieved / PEAK_INT32, 4), "pipeline_work_per_unit": round(w_pipe),
                      "kernel_ms_serial": {k: round(v, 3) for k, v in per_kernel.items()},

@@ -219,7 +219,8 @@ int praos_batch_dedup_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[2]);
 /* Per-kernel time of the last praos_batch_run (ms, HIP events on the ctx stream).
  * which: 0 = ocert, 1 = kes, 2 = vrf, 3 = leader, 4 = whole run, 5 = header
  * decode (batches from praos_batch_upload_bytes; 0 otherwise), 6 = the VRF stage-V
- * kernel k_vrf_v alone (events around its launch on its own stream).  With concurrent
+ * kernel k_vrf_v alone (events around its launch on its own stream), 7 = the cached
+ * Sum6KES kernel k_kes_ck alone (events around its launch on the KES stream).  With concurrent
  * streams, 0-2 are measured from the common start to each kernel's end. */
 float praos_batch_kernel_ms(praos_ctx* ctx, int which);
 

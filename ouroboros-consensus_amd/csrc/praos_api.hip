@@ -139,6 +139,7 @@ struct praos_ctx {
   hipStream_t vstream2 = nullptr;                      // the odd chunks' stage V of the stored-bytes pipeline
   hipEvent_t v_ev = nullptr, v2_ev = nullptr;
   hipEvent_t v0_ev = nullptr, v1_ev = nullptr;         // timing of k_vrf_v on its stream (kernel_ms[6])
+  hipEvent_t kc0_ev = nullptr, kc1_ev = nullptr;       // timing of k_kes_ck on its stream (kernel_ms[7])
   hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
   int tp_staged = 1;                                  // TPraos VRF through the staged kernels + VRF key cache
                                                        // (PRAOS_TP_STAGED=0: the one-kernel k_vrf_tp)
@@ -171,9 +172,10 @@ struct praos_ctx {
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
-  float kernel_ms[7] = {0, 0, 0, 0, 0, 0, 0};
+  float kernel_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   bool last_from_bytes = false;
   bool v_timed = false;                                // the last run launched k_vrf_v
+  bool kes_ck_timed = false;                           // ... and k_kes_ck
   ErrMsg err;
   ge_niels* btab = nullptr;
   ge_niels* bcomb16 = nullptr;                         // radix-2^16 comb of the cached-key chains (48 MB)
@@ -481,6 +483,8 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
+  (void)hipEventCreate(&c->kc0_ev);
+  (void)hipEventCreate(&c->kc1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
@@ -600,6 +604,8 @@ void praos_close(praos_ctx* c) {
   if (c->v0_ev) (void)hipEventDestroy(c->v0_ev);
   if (c->u_ev) (void)hipEventDestroy(c->u_ev);
   if (c->v1_ev) (void)hipEventDestroy(c->v1_ev);
+  if (c->kc0_ev) (void)hipEventDestroy(c->kc0_ev);
+  if (c->kc1_ev) (void)hipEventDestroy(c->kc1_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (int k = 0; k < RP_SLOTS; k++) rp_batch_destroy(c, c->rp_keep[k]);
   for (int k = 0; k < PIPE_MAX; k++) {
@@ -1009,6 +1015,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   hipStream_t sv = c->concurrent ? c->side[2] : c->stream;
   c->last_from_bytes = b->from_bytes;
   c->v_timed = false;
+  c->kes_ck_timed = false;
   if (b->from_bytes) {
     // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
@@ -1142,9 +1149,12 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                  b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
                  bk, (uint8_t*)nullptr, b->tab_kes);
       keycache_precompute(k, b->kes_leaf, 0, sk);
+      HIPCHK(c, hipEventRecord(c->kc0_ev, sk));
       launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                     P.slots_per_kes_period, bk);
+      HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
+      c->kes_ck_timed = true;
     } else {
       launch_kes(g, blk, sk, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->hot_vk, b->kes_sig,
                  b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
@@ -1458,11 +1468,13 @@ int praos_batch_sync(praos_ctx* c) {
   c->kernel_ms[5] = dec;
   c->kernel_ms[6] = 0;
   if (c->v_timed) (void)hipEventElapsedTime(&c->kernel_ms[6], c->v0_ev, c->v1_ev);
+  c->kernel_ms[7] = 0;
+  if (c->kes_ck_timed) (void)hipEventElapsedTime(&c->kernel_ms[7], c->kc0_ev, c->kc1_ev);
   return PRAOS_OK;
 }
 
 float praos_batch_kernel_ms(praos_ctx* c, int which) {
-  if (!c || which < 0 || which > 6) return -1.f;
+  if (!c || which < 0 || which > 7) return -1.f;
   return c->kernel_ms[which];
 }
 
