@@ -323,3 +323,29 @@ def test_tpraos_group_equals_single(ctx, members):
     for k in D1:
         assert np.array_equal(D1[k], Dg[k]), k
     assert np.count_nonzero(corrupted) and all(int(og["bits"][i]) for i in np.nonzero(corrupted)[0])
+
+
+def test_tpraos_gpu_equals_cpu_twin(ctx):
+    """The GPU TPraos path (staged VRF, key caches, 2^512 leader test) against the CPU twin's
+    independent implementation (libpraos_cpu.so praos_verify_tpraos_headers: radix 2^51,
+    sliding-window Straus) on a corrupted synthetic TPraos batch (pools by hash, ~4 headers per
+    key: VRF / cold / KES-leaf cache hits and misses): every output bit for bit."""
+    from praos_hip import cpu as C
+    from praos_hip import fixed
+    p, c_raw = _params(Fraction(1, 2))
+    eta0 = b2b(b"tpraos-twin")
+    n, npools = 3000, 700
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, b"\x37" * 32, first_slot=20000, slot_stride=3,
+                                         corrupt_per_10000=700, tpraos=True)
+    pool_list = [(h, v, fixed.from_rational(Fraction(1, npools))) for (h, v) in pools]
+    ctx.set_epoch(eta0, pool_list, p)
+    o = ctx.verify_tpraos_headers(H)
+    twin = C.CpuContext(16)
+    try:
+        twin.set_epoch(eta0, pool_list, p)
+        t = twin.verify_tpraos_headers(H)
+    finally:
+        twin.close()
+    for k in o:
+        assert np.array_equal(np.asarray(o[k]), np.asarray(t[k])), k
+    assert np.count_nonzero(corrupted) > 100 and int((o["bits"][corrupted != 0] == 0).sum()) == 0
