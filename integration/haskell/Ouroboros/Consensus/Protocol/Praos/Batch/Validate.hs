@@ -49,13 +49,14 @@ import           Data.Word (Word16, Word32, Word64, Word8)
 import           Numeric.Natural (Natural)
 
 import           Cardano.Crypto.Hash (hashToBytes)
-import           Cardano.Ledger.BaseTypes (ActiveSlotCoeff, ProtVer (..), activeSlotLog, activeSlotVal)
+import           Cardano.Ledger.BaseTypes (ActiveSlotCoeff, ProtVer (..), activeSlotLog, activeSlotVal,
+                     unboundRational)
 import           Cardano.Ledger.Binary (Version, getVersion64)
 import           Cardano.Ledger.Keys (KeyHash (..))
 import           Cardano.Ledger.PoolDistr (IndividualPoolStake (..), PoolDistr (..))
 import           Cardano.Slotting.Slot (WithOrigin (..))
-import           Ouroboros.Consensus.Block (BlockProtocol, GetPrevHash (..), Header, HeaderHash, blockNo,
-                     blockSlot)
+import           Ouroboros.Consensus.Block (BlockProtocol, GetPrevHash (..), HasHeader, Header, HeaderHash,
+                     blockNo, blockSlot)
 import           Ouroboros.Consensus.HeaderValidation (AnnTip (..), BasicEnvelopeValidation (..),
                      HasAnnTip (..), HeaderError (..), HeaderState (..), OtherHeaderEnvelopeError)
 import           Ouroboros.Consensus.Protocol.Abstract (ChainDepState, ValidationErr)
@@ -119,7 +120,7 @@ praosParamsC :: PraosParams -> ActiveSlotCoeff -> PraosParamsC
 praosParamsC PraosParams {praosSlotsPerKESPeriod, praosMaxKESEvo} f =
   PraosParamsC { ppSlotsPerKESPeriod = praosSlotsPerKESPeriod
                , ppMaxKESEvo = praosMaxKESEvo
-               , ppFIsOne = activeSlotVal f == maxBound
+               , ppFIsOne = unboundRational (activeSlotVal f) == 1
                , ppActiveSlotLogRaw = let MkFixed raw = activeSlotLog f in raw
                , ppVrfCheckOutput = True }
 
@@ -136,7 +137,7 @@ poolDistrEntries (PoolDistr m) =
 -- at each header, as in the reference.
 validateEpochHeaders
   :: forall blk c.
-     ( BasicEnvelopeValidation blk, HasAnnTip blk, GetPrevHash blk
+     ( BasicEnvelopeValidation blk, HasAnnTip blk, GetPrevHash blk, HasHeader (Header blk)
      , Serialise (PraosState c) )
   => PraosBatchCtx
   -> PraosBlockOps blk c
@@ -190,7 +191,7 @@ validateEpochHeaders ctx ops pp f ei maxPV lv st0 EpochHeaders {ehArena, ehOffse
 -- expected values (HeaderValidation.hs:303-345), protocol verdicts (1..11) as
 -- 'HeaderProtocolError' rebuilt against the state the fold reached (Batch.Errors).
 stopError
-  :: forall blk c. (BasicEnvelopeValidation blk, HasAnnTip blk, GetPrevHash blk)
+  :: forall blk c. (BasicEnvelopeValidation blk, HasAnnTip blk, GetPrevHash blk, HasHeader (Header blk))
   => PraosBlockOps blk c -> PraosParams -> ActiveSlotCoeff -> Version -> Views.LedgerView c
   -> HeaderState blk -> Header blk -> Word8 -> Word16 -> HeaderError blk
 stopError ops pp f maxPV lv before hdr v bits
