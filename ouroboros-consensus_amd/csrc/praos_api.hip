@@ -1051,6 +1051,58 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
   if (c->concurrent)
     for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->side[k], c->ev[0], 0));
+  // Stage V of the VRF needs nothing but the decoded header (no key table, no list), and it is
+  // the longest chain of the step: with concurrent streams it is queued first, so its waves
+  // are dispatched before the key-cache passes' (queued after it, it started ~0.3 ms into a
+  // 54k-header step, behind a dozen list kernels on the other streams)
+  const bool do_vrf = (c->kernels & 4) != 0;
+  const bool tp_staged = do_vrf && b->tp_only && c->tp_staged;
+  const int wprio_v = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
+  bool v_queued = false;
+  if (tp_staged) {
+    const size_t cap = std::max(n, b->cap_n);
+    if (!b->vrf_mid2 || b->vrf_mid2_n < n) {
+      if (dalloc(b, &b->vrf_mid2, VRF_MID_BYTES * cap) != hipSuccess ||
+          dalloc(b, (uint8_t**)&b->tab_vrf2, LT_VRF_B * cap) != hipSuccess)
+        return PRAOS_E_OOM;
+      b->vrf_mid2_n = cap;
+    }
+  }
+  auto queue_stage_v = [&]() -> int {
+    const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
+    if (tp_staged) {
+      // the two certificates' stage V side by side (own lane tables, mkSeed alphas): a batch
+      // below ~300k headers leaves most wave slots empty with one V at a time
+      hipStream_t sVk[2] = {c->concurrent ? c->vstream : c->stream, c->concurrent ? c->vstream2 : c->stream};
+      const uint8_t* proof[2] = {b->vrf_proof, b->lead_proof};
+      uint8_t* mid[2] = {b->vrf_mid, b->vrf_mid2};
+      ge_cached* vtab[2] = {b->tab_vrf, b->tab_vrf2};
+      for (int k = 0; k < 2; k++) {
+        if (sVk[k] != c->stream) HIPCHK(c, hipStreamWaitEvent(sVk[k], c->ev[0], 0));
+        if (k == 0) HIPCHK(c, hipEventRecord(c->v0_ev, sVk[0]));
+        launch_vrf_v(sVk[k], n, b->vrf_vk, proof[k], b->slot, eta, c->eta0_neutral, b->eta_idx, vtab[k], mid[k], 0,
+                     SIZE_MAX, wprio_v, 1 + k, c->v_ilp4(n));
+      }
+      HIPCHK(c, hipEventRecord(c->v1_ev, sVk[0]));
+      HIPCHK(c, hipEventRecord(c->v_ev, sVk[0]));
+      HIPCHK(c, hipEventRecord(c->v2_ev, sVk[1]));
+    } else {
+      hipStream_t sV = c->concurrent ? c->vstream : c->stream;
+      if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
+      HIPCHK(c, hipEventRecord(c->v0_ev, sV));
+      launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
+                   b->vrf_mid, 0, SIZE_MAX, wprio_v, 0, c->v_ilp4(n));
+      HIPCHK(c, hipEventRecord(c->v1_ev, sV));
+    }
+    c->v_timed = true;
+    v_queued = true;
+    return PRAOS_OK;
+  };
+  // (serial runs keep the OCert | KES | VRF order: their per-stream spans are measured in turn)
+  if (c->concurrent && do_vrf && (tp_staged || (!b->tp_only && !b->v_done))) {
+    const int r = queue_stage_v();
+    if (r != PRAOS_OK) return r;
+  }
   const bool kc = c->keycache > 0 && n >= 2;
   b->kc_used = kc;
   // key cache prepass on the kernel's own stream: hash set, entries, hit/miss lists, tables
@@ -1163,38 +1215,19 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   } else
     HIPCHK(c, hipMemsetAsync(bk, 0, 2 * n, sk));
   HIPCHK(c, hipEventRecord(c->side_ev[1], sk));
-  const bool do_vrf = (c->kernels & 4) != 0;
-  if (do_vrf && b->tp_only && c->tp_staged) {
-    // TPraos, staged: stage V of both certificates (mkSeed alphas) on the V stream from ev[0]
-    // on, U of both against the VRF key cache (misses on the miss stream at once, hits after
-    // the key tables), then the two joins in order on the VRF stream
-    const size_t cap = std::max(n, b->cap_n);
-    if (!b->vrf_mid2 || b->vrf_mid2_n < n) {
-      if (dalloc(b, &b->vrf_mid2, VRF_MID_BYTES * cap) != hipSuccess ||
-          dalloc(b, (uint8_t**)&b->tab_vrf2, LT_VRF_B * cap) != hipSuccess)
-        return PRAOS_E_OOM;
-      b->vrf_mid2_n = cap;
+  if (tp_staged) {
+    // TPraos, staged: stage V of both certificates (mkSeed alphas) on the V streams from ev[0]
+    // on (queue_stage_v), U of both against the VRF key cache (misses on the miss stream at
+    // once, hits after the key tables), then the two joins in order on the VRF stream
+    if (!v_queued) {
+      const int r = queue_stage_v();
+      if (r != PRAOS_OK) return r;
     }
-    const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
     const uint8_t* proof[2] = {b->vrf_proof, b->lead_proof};
     const uint8_t* outv[2] = {b->vrf_out, b->lead_out};
     uint8_t* mid[2] = {b->vrf_mid, b->vrf_mid2};
     uint8_t* beta[2] = {b->beta, b->beta_l};
-    // the two certificates' stage V side by side (own lane tables): a batch below ~300k
-    // headers leaves most wave slots empty with one V at a time
     hipStream_t sVk[2] = {c->concurrent ? c->vstream : c->stream, c->concurrent ? c->vstream2 : c->stream};
-    ge_cached* vtab[2] = {b->tab_vrf, b->tab_vrf2};
-    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
-    for (int k = 0; k < 2; k++) {
-      if (sVk[k] != c->stream) HIPCHK(c, hipStreamWaitEvent(sVk[k], c->ev[0], 0));
-      if (k == 0) HIPCHK(c, hipEventRecord(c->v0_ev, sVk[0]));
-      launch_vrf_v(sVk[k], n, b->vrf_vk, proof[k], b->slot, eta, c->eta0_neutral, b->eta_idx, vtab[k], mid[k], 0,
-                   SIZE_MAX, wprio, 1 + k, c->v_ilp4(n));
-    }
-    HIPCHK(c, hipEventRecord(c->v1_ev, sVk[0]));
-    c->v_timed = true;
-    HIPCHK(c, hipEventRecord(c->v_ev, sVk[0]));
-    HIPCHK(c, hipEventRecord(c->v2_ev, sVk[1]));
     if (kc) {
       praos_batch::KeyCache& k = b->kc[1];
       int r = keycache_lists(k, b->vrf_vk, sv);
@@ -1233,14 +1266,10 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     // (stored-bytes pipeline: stage V was queued chunk by chunk on vstream while the later
     // chunks were still uploading; b->v_done)
     hipStream_t sV = (c->concurrent || b->v_done) ? c->vstream : c->stream;
-    const int wprio = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
-    if (!b->v_done) {
-      if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
-      HIPCHK(c, hipEventRecord(c->v0_ev, sV));
-      launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
-                   b->vrf_mid, 0, SIZE_MAX, wprio, 0, c->v_ilp4(n));
-      HIPCHK(c, hipEventRecord(c->v1_ev, sV));
-      c->v_timed = true;
+    const int wprio = wprio_v;
+    if (!b->v_done && !v_queued) {
+      const int r = queue_stage_v();
+      if (r != PRAOS_OK) return r;
     }
     HIPCHK(c, hipEventRecord(c->v_ev, sV));
     if (b->v_done) HIPCHK(c, hipEventRecord(c->v2_ev, c->vstream2));
