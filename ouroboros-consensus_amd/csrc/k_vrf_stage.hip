@@ -288,7 +288,7 @@ void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uin
                   size_t i0, size_t i1, int wave_prio, int tp_seed, int ilp4) {
   if (ilp4) {
     launch_vrf_v4(stream, n, i0, i1, vrf_vk, vrf_proof, slot, eta0, eta0_neutral, eta_idx, tabs, mid, wave_prio,
-                  tp_seed);
+                  tp_seed, ilp4 > 1);
     return;
   }
   VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,

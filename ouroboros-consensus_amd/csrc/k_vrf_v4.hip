@@ -19,15 +19,35 @@ __global__ void __launch_bounds__(NT, 2) k_vrf_v4(size_t n, size_t i0, size_t i1
   vrf_v_core(mid, n, i, pk, pr, pr + 8, pr + 12, alpha, lane_tab(a.tabs, i, LT_VRF));
 }
 
+// The same kernel holding its SIMD alone: touching a255 makes every wave allocate its 202
+// VGPRs plus the 256 accumulation registers (460 of the SIMD's 512), so no other wave of
+// the step's kernels (all above 52 VGPRs) is placed beside it.  A 54k-header step's 844 V
+// waves then take 211 CUs whole and the short first-level chains (uncached verifies, key
+// precomputes) run on the remaining CUs instead of sharing SIMDs with V.
+__global__ void __launch_bounds__(NT, 1) k_vrf_v4x(size_t n, size_t i0, size_t i1, VrfIn a, uint4* __restrict__ mid) {
+  asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+  const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= i1) return;
+  if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
+  uint32_t pk[8], pr[20], alpha[8];
+  load_words(pk, a.vrf_vk + 32 * i, 8);
+  load_words(pr, a.vrf_proof + 80 * i, 20);
+  header_alpha(alpha, a, i);
+  vrf_v_core(mid, n, i, pk, pr, pr + 8, pr + 12, alpha, lane_tab(a.tabs, i, LT_VRF));
+}
+
 void launch_vrf_v4(hipStream_t stream, size_t n, size_t i0, size_t i1, const uint8_t* vrf_vk,
                    const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
-                   const uint8_t* eta_idx, ge_cached* tabs, void* mid, int wave_prio, int tp_seed) {
+                   const uint8_t* eta_idx, ge_cached* tabs, void* mid, int wave_prio, int tp_seed, int excl) {
   VrfIn a = vrf_in(nullptr, vrf_vk, nullptr, vrf_proof, slot, eta0, eta0_neutral, eta_idx, nullptr, nullptr,
                    nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, tabs);
   a.wave_prio = wave_prio;
   a.tp_seed = tp_seed;
   i1 = i1 < n ? i1 : n;
   if (i1 <= i0) return;
-  hipLaunchKernelGGL(k_vrf_v4, dim3((unsigned)((i1 - i0 + NT - 1) / NT)), dim3(NT), 0, stream, n, i0, i1, a,
-                     (uint4*)mid);
+  const dim3 grid((unsigned)((i1 - i0 + NT - 1) / NT));
+  if (excl)
+    hipLaunchKernelGGL(k_vrf_v4x, grid, dim3(NT), 0, stream, n, i0, i1, a, (uint4*)mid);
+  else
+    hipLaunchKernelGGL(k_vrf_v4, grid, dim3(NT), 0, stream, n, i0, i1, a, (uint4*)mid);
 }

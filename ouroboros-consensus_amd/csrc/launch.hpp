@@ -53,6 +53,15 @@ void launch_ocert_fanout(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
 void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
                            uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
                            uint32_t* kinfo, int wave_prio);
+// the uncached verifies of a small batch from the ILP-4 build (k_miss4.hip), list mode only
+void launch_ocert4(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                   const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,
+                   const uint64_t* ocert_c0, const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period,
+                   uint64_t max_kes_evo, uint16_t* bits, uint8_t* ok_out, ge_cached* tabs, int prio);
+void launch_kes4(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
+                 const ge_niels* gbtab, const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off,
+                 const uint32_t* body_len, const uint8_t* body, size_t body_bytes_len, const uint64_t* slot,
+                 const uint64_t* ocert_c0, uint64_t slots_per_kes_period, uint16_t* bits, ge_cached* tabs, int prio);
 void launch_kes(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                 const ge_niels* gbtab, const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off,
                 const uint32_t* body_len, const uint8_t* body, size_t body_bytes_len, const uint64_t* slot,
@@ -62,7 +71,8 @@ void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                    const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off, const uint32_t* body_len,
                    const uint8_t* body, size_t body_bytes_len, const uint64_t* slot, const uint64_t* ocert_c0,
-                   uint64_t slots_per_kes_period, uint16_t* bits);
+                   uint64_t slots_per_kes_period, uint16_t* bits,
+                   uint32_t pair_min);                      // two headers per lane from pair_min hits on (0: never)
 void launch_kes_leafkeys(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* kes_sig,
                          const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
                          uint8_t* keys);
@@ -99,11 +109,13 @@ void launch_vrf_v(hipStream_t stream, size_t n, const uint8_t* vrf_vk, const uin
                   size_t i0 = 0, size_t i1 = SIZE_MAX,    // headers [i0, min(i1, n)); mid stride n
                   int wave_prio = 0,                       // waves at s_setprio 3
                   int tp_seed = 0,                         // 1 + k: TPraos mkSeed alpha, ucNonce k
-                  int ilp4 = 0);                           // the ILP-4 build (k_vrf_v4.hip)
+                  int ilp4 = 0);                           // 1: the ILP-4 build (k_vrf_v4.hip),
+                                                           // 2: the same holding its SIMD alone
+
 // stage V built with the ILP-4 group formulas at 2 waves per SIMD (k_vrf_v4.hip; small batches)
 void launch_vrf_v4(hipStream_t stream, size_t n, size_t i0, size_t i1, const uint8_t* vrf_vk,
                    const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
-                   const uint8_t* eta_idx, ge_cached* tabs, void* mid, int wave_prio, int tp_seed);
+                   const uint8_t* eta_idx, ge_cached* tabs, void* mid, int wave_prio, int tp_seed, int excl);
 void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                     const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb,
                     const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,

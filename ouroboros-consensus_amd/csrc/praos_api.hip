@@ -149,7 +149,18 @@ struct praos_ctx {
                                                        // 1 always, 0 never, N > 1: batches below N headers
                                                        // (profiles/r04/b: V alone 1.71 -> 1.51 ms at 54k, slower
                                                        // from 108k: 2.33 -> 2.27 ms alone but the step 4.25 -> 4.37)
-  bool v_ilp4(size_t n) const { return vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4); }
+  int v_excl = 0;                                      // the ILP-4 stage V holding its SIMDs alone (k_vrf_v4x):
+                                                       // PRAOS_V_EXCL
+  int miss4 = 0;                                       // uncached OCert / KES verifies from the ILP-4 build
+                                                       // (k_miss4.hip): PRAOS_MISS4 1 / 0, -1 below SMALL_BATCH
+  int miss_prio = 0;                                   // ... at s_setprio 3: PRAOS_MISS_PRIO
+  uint32_t kes_pair = 196608;                          // k_kes_ck two headers per lane from this many hits on
+                                                       // (PRAOS_KES_PAIR, 0 = never)
+  bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < SMALL_BATCH); }
+  int v_ilp4(size_t n) const {
+    const bool on = vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4);
+    return on ? (v_excl ? 2 : 1) : 0;
+  }
   int vrf3 = -1;                                       // VRF as V | U | join (1), V | U + join (0), -1 auto:
                                                        // the three-kernel form below 300k headers (latency)
   // chunked stored-bytes pipeline (praos_verify_header_bytes): a copy stream, per-chunk
@@ -480,6 +491,10 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_VRF3")) c->vrf3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_VRF_PRIO")) c->vrf_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_VRF_ILP4")) c->vrf_ilp4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
@@ -1140,8 +1155,14 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
       ocert_miss = [&, k]() {
-        launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                     b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok, b->tab_ocert);
+        if (c->use_miss4(n))
+          launch_ocert4(g, blk, sm_[0], k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
+                        b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
+                        b->tab_ocert, c->miss_prio);
+        else
+          launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
+                       b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
+                       b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
       launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
@@ -1170,9 +1191,14 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (r == PRAOS_OK) r = to_main(0, so);
       if (r != PRAOS_OK) return r;
       ocert_miss = [&, k]() {
-        launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n, b->ocert_c0,
-                     b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, (uint8_t*)nullptr,
-                     b->tab_ocert);
+        if (c->use_miss4(n))
+          launch_ocert4(g, blk, sm_[0], k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
+                        b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
+                        (uint8_t*)nullptr, b->tab_ocert, c->miss_prio);
+        else
+          launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
+                       b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
+                       (uint8_t*)nullptr, b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
       launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
@@ -1197,14 +1223,19 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       int r = keycache_lists(k, b->kes_leaf, sk);
       if (r == PRAOS_OK) r = to_main(1, sk);
       if (r != PRAOS_OK) return r;
-      launch_kes(g, blk, sm_[1], n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
-                 b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
-                 bk, (uint8_t*)nullptr, b->tab_kes);
+      if (c->use_miss4(n))
+        launch_kes4(g, blk, sm_[1], k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
+                    b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, bk, b->tab_kes,
+                    c->miss_prio);
+      else
+        launch_kes(g, blk, sm_[1], n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off,
+                   b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
+                   (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
       keycache_precompute(k, b->kes_leaf, 0, sk);
       HIPCHK(c, hipEventRecord(c->kc0_ev, sk));
       launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
-                    P.slots_per_kes_period, bk);
+                    P.slots_per_kes_period, bk, c->kes_pair);
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
       c->kes_ck_timed = true;
     } else {

@@ -115,11 +115,13 @@ FE_INLINE bool ed25519_verify_core(const uint32_t pk[8], const uint32_t R[8], co
 }
 
 // Same verification with the public key cached (k_keys.hip): kflag bit 0 =
-// ge_is_canonical(pk) && !ge_has_small_order(pk) && decode ok; ktab = tables of
-// -A at 2^0, 2^64, 2^128, 2^192; btab = the four fixed-base tables in LDS.
-FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], const uint32_t hram[16],
-                                     uint32_t kflag, const ge_cached* __restrict__ ktab,
-                                     const ge_niels* __restrict__ btab) {
+// ge_is_canonical(pk) && !ge_has_small_order(pk) && decode ok; ktab = the key's
+// multi-power tables (-A at 2^(16k)); btab = the global radix-2^16 comb of B.
+// ed25519_cached_point: [s]B - [h]A in projective form, and the checks that need no
+// encoding (S canonical, R not of small order, the key flag).
+FE_INLINE bool ed25519_cached_point(ge_p2& Rp, const uint32_t R[8], const uint32_t S[8], const uint32_t hram[16],
+                                    uint32_t kflag, const ge_cached* __restrict__ ktab,
+                                    const ge_niels* __restrict__ btab) {
   bool ok = sc_is_canonical(S) && !ge_has_small_order(R) && (kflag & 1u) != 0;
   uint32_t h[8], s[8];
   sc_reduce512(h, hram);
@@ -130,8 +132,15 @@ FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], c
   sc_recode65536(sw, s);
   ge_p1p1 x;
   straus_comb<16, false>(x, ktab, hw, btab, sw);     // [s]B - [h]A: 4-window chain + comb (btab = global comb)
-  ge_p2 Rp;
   ge_p1p1_to_p2(Rp, x);
+  return ok;
+}
+
+FE_INLINE bool ed25519_verify_cached(const uint32_t R[8], const uint32_t S[8], const uint32_t hram[16],
+                                     uint32_t kflag, const ge_cached* __restrict__ ktab,
+                                     const ge_niels* __restrict__ btab) {
+  ge_p2 Rp;
+  const bool ok = ed25519_cached_point(Rp, R, S, hram, kflag, ktab, btab);
   uint32_t enc[8];
   ge_tobytes(enc, Rp.X, Rp.Y, Rp.Z);
   bool eq = true;
