@@ -505,7 +505,7 @@ static bool open_streams(praos_ctx* c) {
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
-  // 14.3 ms per 432k-header step, tools/gpu_prio_ab.sh).  PRAOS_SIDE_PRIO = three
+  // 14.3 ms per 432k-header step, round-2 A/B).  PRAOS_SIDE_PRIO = three
   // digits overriding that (1 = greatest, 0 = default priority), an A/B knob.
   {
     int least = 0, greatest = 0;
