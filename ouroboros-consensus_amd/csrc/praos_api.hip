@@ -154,8 +154,15 @@ struct praos_ctx {
   int miss4 = 0;                                       // uncached OCert / KES verifies from the ILP-4 build
                                                        // (k_miss4.hip): PRAOS_MISS4 1 / 0, -1 below SMALL_BATCH
   int miss_prio = 0;                                   // ... at s_setprio 3: PRAOS_MISS_PRIO
-  uint32_t kes_pair = 196608;                          // k_kes_ck two headers per lane from this many hits on
-                                                       // (PRAOS_KES_PAIR, 0 = never)
+  long kes_pair = -1;                                  // k_kes_ck two headers per lane from this many hits on
+                                                       // (PRAOS_KES_PAIR, 0 = never; -1: from 196,608 when the
+                                                       // KES pass runs alone -- beside the OCert / VRF passes
+                                                       // the longer paired waves cost the C5 step 2 %,
+                                                       // profiles/r04/i: 12.15 -> 12.40 ms, C4 6.43 -> 6.10 ms)
+  uint32_t kes_pair_min() const {
+    return kes_pair >= 0 ? (uint32_t)kes_pair : ((kernels & 5) ? 0u : 196608u);
+  }
+  int vrf_keys_first = 1;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl)
   bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < SMALL_BATCH); }
   int v_ilp4(size_t n) const {
     const bool on = vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4);
@@ -493,8 +500,9 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_VRF_ILP4")) c->vrf_ilp4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
-  if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   (void)hipEventCreate(&c->v1_ev);
@@ -1140,6 +1148,32 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   auto keycache_precompute = [&](praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st) {
     kc_precompute(c, k, keys, kind, st, n);
   };
+  // Praos VRF in three kernels (below 300k headers): the VRF key lists, the uncached U and the
+  // key precompute + cached U are queued ahead of the OCert and KES passes when the streams
+  // run concurrently (PRAOS_VRF_KEYS_FIRST): after stage V, the VRF key chain -- lists,
+  // precompute, tables, U, join -- is a small batch's longest (profiles/r04/i: its lists
+  // started 0.33 ms into a 54k-header step, behind the OCert and KES lists)
+  const bool vrf3 = do_vrf && !b->tp_only && (c->vrf3 > 0 || (c->vrf3 < 0 && n < 300000));
+  bool vrf_keys_queued = false;
+  auto vrf_keys = [&]() -> int {
+    praos_batch::KeyCache& k = b->kc[1];
+    int r = keycache_lists(k, b->vrf_vk, sv);
+    if (r == PRAOS_OK) r = to_main(2, sv);
+    if (r != PRAOS_OK) return r;
+    launch_vrf_u(sm_[2], n, k.miss, k.counters + 2, nullptr, nullptr, nullptr, c->bcomb16, c->btab, b->vrf_vk,
+                 b->vrf_proof, b->tab_vrfu, b->vrf_mid);
+    if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
+    keycache_precompute(k, b->vrf_vk, 1, sv);
+    launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, c->btab, b->vrf_vk,
+                 b->vrf_proof, b->tab_vrfu, b->vrf_mid);
+    if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
+    vrf_keys_queued = true;
+    return PRAOS_OK;
+  };
+  if (vrf3 && kc && c->concurrent && c->vrf_keys_first) {
+    const int r = vrf_keys();
+    if (r != PRAOS_OK) return r;
+  }
   b->dd_used = false;
   std::function<void()> ocert_miss;
   if ((c->kernels & 1) && c->dedup && n >= 2) {
@@ -1235,7 +1269,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       HIPCHK(c, hipEventRecord(c->kc0_ev, sk));
       launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
-                    P.slots_per_kes_period, bk, c->kes_pair);
+                    P.slots_per_kes_period, bk, c->kes_pair_min());
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
       c->kes_ck_timed = true;
     } else {
@@ -1324,22 +1358,12 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                       c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta,
                       b->leader, b->nonce, b->vrf_mid, wprio);
     };
-    if (c->vrf3 > 0 || (c->vrf3 < 0 && n < 300000)) {
+    if (vrf3) {
       // three kernels: U runs beside V (uncached keys at once on the miss stream, cached keys
       // once their tables exist), the join after both
       int r;
       if (kc) {
-        praos_batch::KeyCache& k = b->kc[1];
-        r = keycache_lists(k, b->vrf_vk, sv);
-        if (r == PRAOS_OK) r = to_main(2, sv);
-        if (r != PRAOS_OK) return r;
-        stage_u(sm_[2], k.miss, k.counters + 2, nullptr);
-        if (sm_[2] != sv) {
-          HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
-        }
-        keycache_precompute(k, b->vrf_vk, 1, sv);
-        stage_u(sv, k.hit, k.counters + 1, &k);
-        if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
+        if (!vrf_keys_queued && (r = vrf_keys()) != PRAOS_OK) return r;
       } else {
         stage_u(sv, nullptr, nullptr, nullptr);
       }
