@@ -143,17 +143,20 @@ struct praos_ctx {
   hipEvent_t u_ev = nullptr;                           // stage U of the uncached VRF keys done
   int tp_staged = 1;                                  // TPraos VRF through the staged kernels + VRF key cache
                                                        // (PRAOS_TP_STAGED=0: the one-kernel k_vrf_tp)
-  int vrf_prio = -1;                                  // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO 1 / 0;
-                                                       // -1: batches below SMALL_BATCH headers)
+  int vrf_prio = 0;                                   // stage V and join waves at s_setprio 3 (PRAOS_VRF_PRIO 1 / 0;
+                                                       // -1: batches below SMALL_BATCH headers).  Off: with the
+                                                       // uncached verifies raised instead a 54k-header step takes
+                                                       // 2.83 ms against 3.16 (profiles/r04/i, r04/j)
   int vrf_ilp4 = (int)SMALL_BATCH;                    // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
                                                        // 1 always, 0 never, N > 1: batches below N headers
                                                        // (profiles/r04/b: V alone 1.71 -> 1.51 ms at 54k, slower
                                                        // from 108k: 2.33 -> 2.27 ms alone but the step 4.25 -> 4.37)
   int v_excl = 0;                                      // the ILP-4 stage V holding its SIMDs alone (k_vrf_v4x):
-                                                       // PRAOS_V_EXCL
-  int miss4 = 0;                                       // uncached OCert / KES verifies from the ILP-4 build
+                                                       // PRAOS_V_EXCL (54k: 3.30 -> 3.46 ms, off)
+  int miss4 = -1;                                      // uncached OCert / KES verifies from the ILP-4 build
                                                        // (k_miss4.hip): PRAOS_MISS4 1 / 0, -1 below SMALL_BATCH
-  int miss_prio = 0;                                   // ... at s_setprio 3: PRAOS_MISS_PRIO
+                                                       // (54k: 3.33 -> 3.09 ms; 108k: 4.26 -> 4.66, so not there)
+  int miss_prio = -1;                                  // ... at s_setprio 3: PRAOS_MISS_PRIO 1 / 0, -1 with miss4
   long kes_pair = -1;                                  // k_kes_ck two headers per lane from this many hits on
                                                        // (PRAOS_KES_PAIR, 0 = never; -1: from 196,608 when the
                                                        // KES pass runs alone -- beside the OCert / VRF passes
@@ -162,7 +165,8 @@ struct praos_ctx {
   uint32_t kes_pair_min() const {
     return kes_pair >= 0 ? (uint32_t)kes_pair : ((kernels & 5) ? 0u : 196608u);
   }
-  int vrf_keys_first = 1;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl)
+  int vrf_keys_first = 0;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl; 54k: 2.80 ->
+                                                       // 2.85 ms, 108k 4.24 -> 4.27: off, profiles/r04/k)
   bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < SMALL_BATCH); }
   int v_ilp4(size_t n) const {
     const bool on = vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4);
@@ -1192,7 +1196,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         if (c->use_miss4(n))
           launch_ocert4(g, blk, sm_[0], k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                         b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
-                        b->tab_ocert, c->miss_prio);
+                        b->tab_ocert, c->miss_prio >= 0 ? c->miss_prio : 1);
         else
           launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                        b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
@@ -1228,7 +1232,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         if (c->use_miss4(n))
           launch_ocert4(g, blk, sm_[0], k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                         b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
-                        (uint8_t*)nullptr, b->tab_ocert, c->miss_prio);
+                        (uint8_t*)nullptr, b->tab_ocert, c->miss_prio >= 0 ? c->miss_prio : 1);
         else
           launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                        b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
@@ -1260,7 +1264,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (c->use_miss4(n))
         launch_kes4(g, blk, sm_[1], k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
                     b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, bk, b->tab_kes,
-                    c->miss_prio);
+                    c->miss_prio >= 0 ? c->miss_prio : 1);
       else
         launch_kes(g, blk, sm_[1], n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off,
                    b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
