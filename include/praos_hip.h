@@ -207,6 +207,12 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * the batch runs once after the last chunk, and the VRF outputs move back while the KES
  * checks finish; auto = up to 6 chunks of at least 65,536 headers. */
 #define PRAOS_OPT_PIPELINE 5
+/* PRAOS_OPT_KES_PAIR (default -1 = automatic): the cached Sum6KES leaf verifies take two
+ * headers per lane from this many cache hits on, encoding both R' with one field inversion
+ * (0 = never).  Automatic: from 196,608 hits when the KES pass runs alone (PRAOS_OPT_KERNELS
+ * == 2); beside the OCert / VRF passes the longer waves cost more than they save.  Verdicts
+ * are identical either way. */
+#define PRAOS_OPT_KES_PAIR 6
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items

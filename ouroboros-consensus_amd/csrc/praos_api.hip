@@ -1530,6 +1530,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_KEYCACHE) { c->keycache = value < 0 ? 0 : value; return PRAOS_OK; }
   if (opt == PRAOS_OPT_DEDUP) { c->dedup = value != 0; return PRAOS_OK; }
   if (opt == PRAOS_OPT_PIPELINE) { c->pipeline = value < 0 ? 0 : std::min(value, PIPE_MAX); return PRAOS_OK; }
+  if (opt == PRAOS_OPT_KES_PAIR) { c->kes_pair = value < 0 ? -1 : value; return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 

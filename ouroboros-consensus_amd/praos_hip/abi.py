@@ -324,7 +324,7 @@ def ptr(a, t=u8p):
     return a.ctypes.data_as(t)
 
 
-OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP, OPT_PIPELINE = 1, 2, 3, 4, 5   # praos_set_option (praos_hip.h)
+OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP, OPT_PIPELINE, OPT_KES_PAIR = 1, 2, 3, 4, 5, 6   # praos_set_option
 
 
 class PraosError(RuntimeError):

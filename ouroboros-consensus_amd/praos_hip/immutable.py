@@ -83,13 +83,15 @@ def _combine(a, b):
 
 
 def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpraos=False, extra_entropy=None,
-                           progress=None):
+                           progress=None, schedules=None):
     """A linked chain over `epochs` epochs of `epoch_length` slots from slot 0 (Origin,
     GenesisHash, epoch 0 nonce = cfg["eta0"]).  Returns dict(arena, off, len, slots,
     header_hash, pools, params, nonces (per epoch), state (after the last
     block, as Context.update_chain_dep_state keeps it)).  tpraos=True: a Shelley..Alonzo
     chain (TPraos leader schedule and BHeaders, stored as Alonzo blocks, era tag 5; the
-    TPraos nonce rules with TICKN's extra_entropy)."""
+    TPraos nonce rules with TICKN's extra_entropy).  schedules: {epoch: (slots, pools)} used
+    instead of the leader-schedule search for those epochs (e.g. epoch 0 of the C5 / tp chain
+    from its shipped schedule, which was searched under the same seed, stake and nonce)."""
     sig = chains.stake(cfg["npools"], cfg["stake_offset"])
     p = chains.params(cfg)
     st = {"last_slot": None, "counters": {}, "evolving": cfg["eta0"], "candidate": cfg["eta0"],
@@ -104,7 +106,11 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
             if tpraos:
                 eta = _combine(eta, extra_entropy)          # TICKN
         nonces.append(eta)
-        if cfg.get("round_robin"):
+        if schedules and e in schedules:
+            sl, pl = schedules[e]
+            keep = (sl >= e * epoch_length) & (sl < (e + 1) * epoch_length)
+            sl, pl = sl[keep].astype(np.uint64), pl[keep].astype(np.uint32)
+        elif cfg.get("round_robin"):
             # f = 1 (every pool a leader in every slot, checkLeaderNatValue's f == 1 case):
             # a block in every slot, forged by the pools in turn -- a dense chain of the C5
             # shape (432k headers per 432k-slot epoch) without the 26e9-evaluation search

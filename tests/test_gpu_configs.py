@@ -78,3 +78,48 @@ def test_config_full_size(ctx, oracle, name):
             r = oracle.praos_header(ep, h)
             assert int(bits[i]) & VRF_MASK == r["bits"] & VRF_MASK, (i, hex(int(bits[i])), hex(r["bits"]))
             assert bytes(out["beta"][i]) == r["beta"] and bytes(out["leader"][i]) == r["leader"], i
+
+
+def _first(H, m):
+    n = len(H["slot"])
+    return {k: (v[:m] if k != "body_bytes" and hasattr(v, "shape") and v.ndim and v.shape[0] == n else v)
+            for k, v in H.items()}
+
+
+def test_kes_pair_equals_single(ctx):
+    """k_kes_ck with two headers per lane (PRAOS_OPT_KES_PAIR, one inversion for both R'
+    encodings) gives the per-header verdicts of the one-header-per-lane form: C4-shaped
+    batches with 1 % corrupted KES signatures / messages, paired from 2 hits on against never
+    paired, down to a prefix with an odd number of cache hits (the last lane then has no
+    second header)."""
+    from praos_hip import abi, configs
+    H0, pool_list, corrupted0, p, eta0, c_raw, spkp, maxevo = configs.build(ctx, "c4", n=40_016)
+    odd = False
+    try:
+        configs.options(ctx, "c4")
+        ctx.set_epoch(eta0, pool_list, p)
+        for m in range(40_016, 40_000, -1):
+            H, corrupted = _first(H0, m), corrupted0[:m]
+            outs, hits = [], []
+            for pair in (0, 2):
+                ctx.set_option(abi.OPT_KES_PAIR, pair)
+                b = ctx.upload(H)
+                try:
+                    ctx.run(b)
+                    ctx.sync()
+                    hits.append(ctx.batch_stats(b)["kes_hits"])
+                    outs.append(ctx.download(b, m)["bits"].copy())
+                finally:
+                    ctx.free(b)
+            assert hits[0] == hits[1] and hits[0] > 1000
+            np.testing.assert_array_equal(outs[0], outs[1])
+            bad = np.isin(corrupted, (2, 5))
+            assert bad.sum() > 100 and int((outs[1][bad] == 0).sum()) == 0
+            assert int((outs[1][corrupted == 0] & np.uint16(0x0018)).sum()) == 0
+            if hits[0] % 2:
+                odd = True
+                break
+    finally:
+        ctx.set_option(abi.OPT_KES_PAIR, -1)
+        configs.options(ctx, "c5")
+    assert odd, "no prefix with an odd hit count"

@@ -34,6 +34,9 @@ def main():
                     help="f = 1 and a block in every slot, pools in turn (the C5 shape: 432k headers per "
                          "432k-slot epoch, 3000 pools, without the leader-schedule search)")
     ap.add_argument("--window", type=int, default=None, help="stability window in slots (default 4k/f, k = 2160)")
+    ap.add_argument("--chain", choices=("c5", "tp"), default=None,
+                    help="the bench chain's configuration (praos_hip.chains.CONFIGS: 3000 pools, f = 1/20, 8.64M-slot "
+                         "epochs); epoch 0 takes the shipped first-leader-wins schedule, later epochs are searched")
     ap.add_argument("--tpraos", action="store_true",
                     help="a Shelley..Alonzo (TPraos) chain replayed by praos_replay_immutable_tpraos (TICKN with extra entropy)")
     args = ap.parse_args()
@@ -45,6 +48,14 @@ def main():
     cfg = dict(npools=args.pools, stake_offset=10, f=f, slots_per_kes_period=129600, max_kes_evo=62,
                eta0=hashlib.blake2b(b"replay-bench", digest_size=32).digest(), seed=b"RB" + b"\x5b" * 30,
                round_robin=args.round_robin)
+    schedules = None
+    if args.chain:
+        from praos_hip import chains
+        assert args.tpraos == (args.chain == "tp") and not args.round_robin
+        cfg = dict(chains.CONFIGS[args.chain])
+        assert args.epoch_length == cfg["epoch_length"] and args.pools == cfg["npools"]
+        f = cfg["f"]
+        schedules = {0: chains.load_schedule(args.chain)}
     window = args.window or int(4 * 2160 / f)   # 4k/f with k = 2160: the Babbage stability window
     t0 = time.perf_counter()
     # heartbeat while the chain is generated (the linked re-signing is sequential: minutes
@@ -60,7 +71,8 @@ def main():
     data = immutable.make_multi_epoch_chain(
         ctx, cfg, args.epochs, args.epoch_length, window, tpraos=args.tpraos, extra_entropy=xe,
         progress=lambda e, n: print(f"epoch {e}: {n} blocks signed and linked ({time.perf_counter() - t0:.0f}s)",
-                                    file=sys.stderr, flush=True))
+                                    file=sys.stderr, flush=True),
+        schedules=schedules)
     gen_done.set()
     t_gen = time.perf_counter() - t0
     n = len(data["off"])
@@ -89,6 +101,7 @@ def main():
                     "epochs": args.epochs, "blocks_per_epoch": round(n / args.epochs), "chunks": nch,
                     "pools": args.pools, "wall_ms": round(best["wall_ms"], 2),
                     "schedule": "round-robin, f = 1" if args.round_robin else "first-leader-wins, f = 1/20",
+                    "chain": args.chain or "replay-bench",
                     "stages_ms": {k: round(best[k], 2) for k in ("ms_io", "ms_device", "ms_nonce", "ms_fold")},
                     "batch_max": batch_max, "batches": best["batches"], "epoch_nonces": best["epochs"],
                     "generate_s": round(t_gen, 1), "reps": args.reps,
