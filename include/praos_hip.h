@@ -213,6 +213,14 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * == 2); beside the OCert / VRF passes the longer waves cost more than they save.  Verdicts
  * are identical either way. */
 #define PRAOS_OPT_KES_PAIR 6
+/* PRAOS_OPT_POOL_KEYS (default -1 = on inside praos_replay_immutable*, off otherwise): the
+ * cold-key and VRF-key cache entries (decoded key, validity flags, multi-power tables) are
+ * kept across runs of the context in a store of 16,384 entries per kind, so a key seen by an
+ * earlier batch is a cache hit without being decoded and expanded again; new keys are cached
+ * from their first use (they recur in the batches that follow).  Keys are matched byte for
+ * byte; verdicts are identical either way.  1 = on, 0 = off, 2 = on and emptied before the
+ * next run.  A store more than 3/4 full is emptied before a run. */
+#define PRAOS_OPT_POOL_KEYS 7
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items

@@ -17,6 +17,12 @@
 //                    one key's tables (L1/L2-resident) instead of 64 different ones;
 //                    misses to the miss list in item order (wave-aggregated)
 //   k_key_precompute per entry: checks, decode, tables (and Y's encoding)
+//
+// Pool-key store (PRAOS_OPT_POOL_KEYS, cold and VRF keys): the entries and tables persist
+// across runs of a context.  k_key_insert first probes the store (keys compared byte for
+// byte) and a key found there is a hit on its stored entry without entering the batch's
+// set; new keys get entry ids after the store's, their tables are built once, and
+// k_pkey_publish adds them to the store for the runs that follow (on the same stream).
 #include "kcommon.hpp"
 
 __device__ __forceinline__ uint32_t key_hash(const uint32_t k[8]) {
@@ -27,14 +33,32 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t k[8]) {
 }
 
 // Items: i in [0, n), or list[0 .. *count) (e.g. the distinct OCerts of k_ocert_dedup).
+// pentry != null: the pool-key store (pkey: 8 words per slot, pentry: entry or -1); an item
+// whose key is stored gets item_slot = -2 - entry.
 __global__ void k_key_insert(size_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                              const uint8_t* __restrict__ keys, uint32_t mask, uint32_t* slot_rep,
-                             uint32_t* slot_cnt, int32_t* __restrict__ item_slot) {
+                             uint32_t* slot_cnt, int32_t* __restrict__ item_slot, const int32_t* __restrict__ pentry,
+                             const uint32_t* __restrict__ pkey, uint32_t pmask) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (list ? (size_t)*count : n)) return;
   const size_t i = list ? list[t] : t;
   uint32_t k[8];
   load_words(k, keys + 32 * i, 8);
+  if (pentry) {
+    uint32_t g = key_hash(k) & pmask;
+    for (uint32_t probe = 0; probe <= pmask; probe++) {
+      const int32_t e = pentry[g];
+      if (e < 0) break;                                // not stored
+      bool same = true;
+#pragma unroll
+      for (int q = 0; q < 8; q++) same &= pkey[8 * (size_t)g + q] == k[q];
+      if (same) {
+        item_slot[i] = -2 - e;
+        return;
+      }
+      g = (g + 1u) & pmask;
+    }
+  }
   uint32_t h = key_hash(k) & mask;
   for (uint32_t probe = 0; probe <= mask; probe++) {
     const uint32_t cur = atomicCAS(&slot_rep[h], 0u, (uint32_t)i + 1u);
@@ -70,29 +94,29 @@ __global__ void k_key_assign(uint32_t cap, const uint32_t* __restrict__ slot_rep
     return;
   }
   const uint32_t lane = __lane_id();
-  // exclusive prefix sum of the taken keys' use counts over the wave
-  uint32_t incl = take ? cnt : 0u;
+  uint32_t e_base = 0;
+  if (lane == 0) e_base = atomicAdd(&counters[0], (uint32_t)__popcll(m));
+  e_base = __shfl(e_base, 0);
+  // entry ids past max_entries (a full pool-key store, or the per-batch cap) stay uncached:
+  // only the keys that get an entry claim a range of the hit list, so it has no holes
+  const uint32_t k = e_base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  const bool got = take && k < max_entries;
+  // exclusive prefix sum of the cached keys' use counts over the wave
+  uint32_t incl = got ? cnt : 0u;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t v = __shfl_up(incl, d);
     if (lane >= (uint32_t)d) incl += v;
   }
   const uint32_t total = __shfl(incl, 63);
-  uint32_t e_base = 0, p_base = 0;
-  if (lane == 0) {
-    e_base = atomicAdd(&counters[0], (uint32_t)__popcll(m));
-    p_base = atomicAdd(&counters[3], total);
-  }
-  e_base = __shfl(e_base, 0);
+  uint32_t p_base = 0;
+  if (lane == 0 && total) p_base = atomicAdd(&counters[3], total);
   p_base = __shfl(p_base, 0);
   int32_t e = -1;
-  if (take) {
-    const uint32_t k = e_base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (k < max_entries) {
-      e = (int32_t)k;
-      entry_rep[k] = rep - 1u;
-      entry_pos[k] = p_base + incl - cnt;            // this key's range of the hit list
-    }
+  if (got) {
+    e = (int32_t)k;
+    entry_rep[k] = rep - 1u;
+    entry_pos[k] = p_base + incl - cnt;              // this key's range of the hit list
   }
   if (in) slot_entry[h] = e;
 }
@@ -112,6 +136,8 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t*
   }
 }
 
+// Stored keys' items (item_slot <= -2) are hits too; they go after the new keys' ranges
+// (counters[3] is the end of those once k_key_assign is done).
 __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                 const int32_t* __restrict__ item_slot, const int32_t* __restrict__ slot_entry,
                                 int32_t* __restrict__ item_entry, uint32_t* __restrict__ entry_pos,
@@ -120,9 +146,12 @@ __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, con
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = t < (list ? (size_t)*count : n);   // every lane stays for the ballots
   const size_t i = in ? (list ? list[t] : t) : 0;
-  const int32_t e = in ? slot_entry[item_slot[i]] : -1;
+  const int32_t sl = in ? item_slot[i] : -1;
+  const bool stored = sl <= -2;
+  const int32_t e = !in ? -1 : (stored ? -2 - sl : slot_entry[sl]);
   if (in) item_entry[i] = e;
-  if (in && e >= 0) hit_list[atomicAdd(&entry_pos[e], 1u)] = (uint32_t)i;
+  if (in && e >= 0 && !stored) hit_list[atomicAdd(&entry_pos[e], 1u)] = (uint32_t)i;
+  wave_append(in && stored, (uint32_t)i, &counters[3], hit_list);
   const uint64_t hits = __ballot(in && e >= 0);
   if (hits && __lane_id() == (uint32_t)(__ffsll((unsigned long long)hits) - 1))
     atomicAdd(&counters[1], (uint32_t)__popcll(hits));
@@ -140,12 +169,13 @@ __device__ __forceinline__ int key_chunks(int kind) { return kind == 0 ? KT_CHUN
 __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t* __restrict__ counters,
                                                         uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
                                                         const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
-                                                        uint32_t* __restrict__ kinfo, int wave_prio) {
+                                                        uint32_t* __restrict__ kinfo, int wave_prio,
+                                                        const uint32_t* __restrict__ base) {
   // latency-bound (a short list of long chains) and on the critical path of the cached
   // chains: raised wave priority wins the SIMD's issue arbitration against the
   // throughput kernels resident beside it
   if (wave_prio) __builtin_amdgcn_s_setprio(3);
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t e = (base ? *base : 0u) + blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ne = min(counters[0], max_entries);
   if (e >= ne) return;
   uint32_t pk[8];
@@ -175,12 +205,36 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
 // pass 2: lane (entry, chunk) expands the chunk base into its 8-entry table
 __global__ void __launch_bounds__(256) k_key_tables(int kind, const uint32_t* __restrict__ counters,
                                                     uint32_t max_entries, ge_cached* __restrict__ ktab,
-                                                    int wave_prio) {
+                                                    int wave_prio, const uint32_t* __restrict__ base) {
   if (wave_prio) __builtin_amdgcn_s_setprio(3);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t e = t / KT_CHUNKS, k = t % KT_CHUNKS;
+  const uint32_t e = (base ? *base : 0u) + t / KT_CHUNKS, k = t % KT_CHUNKS;
   if (e >= min(counters[0], max_entries) || k >= (uint32_t)key_chunks(kind)) return;
   key_chunk_table(ktab + (size_t)e * KT_STRIDE + 8 * k);
+}
+
+// The run's new entries [*base, min(counters[0], max_entries)) into the pool-key store
+// (distinct keys, so a claimed slot needs no comparison); *count = the store's entries after.
+__global__ void k_pkey_publish(const uint32_t* __restrict__ counters, const uint32_t* __restrict__ base,
+                               uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
+                               const uint8_t* __restrict__ keys, int32_t* pentry, uint32_t* __restrict__ pkey,
+                               uint32_t pmask, uint32_t* __restrict__ count) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ne = min(counters[0], max_entries);
+  if (t == 0) *count = ne;
+  const uint32_t e = *base + t;
+  if (e >= ne) return;
+  uint32_t k[8];
+  load_words(k, keys + 32 * (size_t)entry_rep[e], 8);
+  uint32_t g = key_hash(k) & pmask;
+  for (uint32_t probe = 0; probe <= pmask; probe++) {
+    if (atomicCAS(&pentry[g], -1, (int32_t)e) == -1) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) pkey[8 * (size_t)g + q] = k[q];
+      return;
+    }
+    g = (g + 1u) & pmask;
+  }
 }
 
 // ---- OCert signature dedup (PRAOS_OPT_DEDUP)
@@ -253,8 +307,10 @@ __global__ void k_ocert_fanout(size_t n, const uint32_t* __restrict__ item_rep, 
 
 // ---- host launchers
 void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
-                       const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot) {
-  hipLaunchKernelGGL(k_key_insert, grid, block, 0, stream, n, list, count, keys, mask, slot_rep, slot_cnt, item_slot);
+                       const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot,
+                       const int32_t* pentry, const uint32_t* pkey, uint32_t pmask) {
+  hipLaunchKernelGGL(k_key_insert, grid, block, 0, stream, n, list, count, keys, mask, slot_rep, slot_cnt, item_slot,
+                     pentry, pkey, pmask);
 }
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
@@ -269,14 +325,20 @@ void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
   hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, list, count, item_slot, slot_entry, item_entry,
                      entry_pos, hit_list, miss_list, counters);
 }
-void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
-                           uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
-                           uint32_t* kinfo, int wave_prio) {
-  hipLaunchKernelGGL(k_key_precompute, grid, block, 0, stream, kind, counters, max_entries, entry_rep, keys, ktab,
-                     kinfo, wave_prio);
-  const size_t lanes = (size_t)max_entries * KT_CHUNKS;
+void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
+                           const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
+                           int wave_prio, const uint32_t* base, uint32_t span) {
+  hipLaunchKernelGGL(k_key_precompute, dim3((span + 63) / 64), dim3(64), 0, stream, kind, counters, max_entries,
+                     entry_rep, keys, ktab, kinfo, wave_prio, base);
+  const size_t lanes = (size_t)span * KT_CHUNKS;
   hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, kind, counters,
-                     max_entries, ktab, wave_prio);
+                     max_entries, ktab, wave_prio, base);
+}
+void launch_pkey_publish(hipStream_t stream, const uint32_t* counters, const uint32_t* base, uint32_t max_entries,
+                         const uint32_t* entry_rep, const uint8_t* keys, int32_t* pentry, uint32_t* pkey,
+                         uint32_t pmask, uint32_t* count, uint32_t span) {
+  hipLaunchKernelGGL(k_pkey_publish, dim3((span + 255) / 256), dim3(256), 0, stream, counters, base, max_entries,
+                     entry_rep, keys, pentry, pkey, pmask, count);
 }
 void launch_ocert_dedup(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* cold, const uint8_t* hot,
                         const uint64_t* on, const uint64_t* oc, const uint8_t* sig, uint32_t mask, uint32_t* slot_rep,

@@ -35,8 +35,10 @@ void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    int check_output, const uint8_t* alpha_in, uint16_t* bits, int32_t* pool_idx,
                    int32_t* pool_sorted_idx, uint8_t* beta_out, uint8_t* leader_out, uint8_t* nonce_out,
                    uint8_t* ok_out, ge_cached* tabs);
+// pentry / pkey / pmask: the pool-key store probed first (null: none)
 void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
-                       const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot);
+                       const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot,
+                       const int32_t* pentry, const uint32_t* pkey, uint32_t pmask);
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
                        uint32_t* entry_rep, uint32_t* entry_pos, uint32_t* counters);
@@ -50,9 +52,13 @@ void launch_ocert_dedup(dim3 grid, dim3 block, hipStream_t stream, size_t n, con
 void launch_ocert_fanout(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* item_rep,
                          const uint8_t* ok, const uint64_t* slot, const uint64_t* oc, uint64_t slots_per_kes_period,
                          uint64_t max_kes_evo, uint16_t* bits);
-void launch_key_precompute(dim3 grid, dim3 block, hipStream_t stream, int kind, const uint32_t* counters,
-                           uint32_t max_entries, const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab,
-                           uint32_t* kinfo, int wave_prio);
+// entries [*base (0 when null), min(counters[0], max_entries)), at most span of them
+void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
+                           const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
+                           int wave_prio, const uint32_t* base, uint32_t span);
+void launch_pkey_publish(hipStream_t stream, const uint32_t* counters, const uint32_t* base, uint32_t max_entries,
+                         const uint32_t* entry_rep, const uint8_t* keys, int32_t* pentry, uint32_t* pkey,
+                         uint32_t pmask, uint32_t* count, uint32_t span);
 // the uncached verifies of a small batch from the ILP-4 build (k_miss4.hip), list mode only
 void launch_ocert4(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
                    const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,

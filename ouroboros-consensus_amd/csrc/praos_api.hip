@@ -201,6 +201,21 @@ struct praos_ctx {
   ErrMsg err;
   ge_niels* btab = nullptr;
   ge_niels* bcomb16 = nullptr;                         // radix-2^16 comb of the cached-key chains (48 MB)
+  // pool-key store (PRAOS_OPT_POOL_KEYS, k_keys.hip): cold [0] and VRF [1] key entries and
+  // tables kept across runs; allocated on first use (256 MB of tables each)
+  struct PoolKeyStore {
+    uint32_t slots = 0, cap = 0;
+    uint32_t *pkey = nullptr, *count = nullptr, *base = nullptr, *entry_rep = nullptr, *entry_pos = nullptr;
+    uint32_t* kinfo = nullptr;
+    int32_t* pentry = nullptr;
+    ge_cached* ktab = nullptr;
+    uint32_t* count_h = nullptr;                        // pinned: *count after the last run (reset heuristic)
+  } pks[2];
+  int pool_keys = -1;                                  // 1 on, 0 off, -1 on inside praos_replay_immutable*
+  bool replaying = false;
+  bool pk_on = false;                                  // this run uses the store
+  bool pk_reset = false;                               // empty the store before the next run
+  bool pk_reset_run = false;
   // epoch
   bool have_epoch = false;
   praos_params params{};
@@ -374,6 +389,12 @@ struct praos_batch {
     int32_t *slot_entry = nullptr, *item_slot = nullptr, *item_entry = nullptr;
     uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
     ge_cached* ktab = nullptr;
+    // this run's entry space: the arrays above, or the context's pool-key store
+    ge_cached* kt = nullptr;
+    uint32_t *ki = nullptr, *erep = nullptr, *epos = nullptr;
+    const uint32_t* ebase = nullptr;
+    uint32_t emax = 0;
+    int store = -1;
   } kc[3];                       // [2] KES leaf keys
   uint8_t* kes_leaf = nullptr;   // n*32: the leaf key of each header's KES signature
   bool kc_used = false;
@@ -612,6 +633,12 @@ void praos_close(praos_ctx* c) {
   (void)hipFree(c->d_gen);
   (void)hipFree(c->btab);
   (void)hipFree(c->bcomb16);
+  for (auto& ps : c->pks) {
+    for (void* q : {(void*)ps.pkey, (void*)ps.count, (void*)ps.base, (void*)ps.entry_rep, (void*)ps.entry_pos,
+                    (void*)ps.kinfo, (void*)ps.pentry, (void*)ps.ktab})
+      (void)hipFree(q);
+    if (ps.count_h) (void)hipHostFree(ps.count_h);
+  }
   free_spare(c);
   c->pool.reset();
   for (int k = 0; k < 2; k++) {
@@ -1006,24 +1033,82 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
 }
 
 // key cache prepass over items [0, n) (or list[0 .. *count)): hash set, entries, hit/miss lists
+// the pool-key store t (cold 0, VRF 1): 32,768 slots, 16,384 entries
+static bool ensure_pks(praos_ctx* c, int t) {
+  praos_ctx::PoolKeyStore& s = c->pks[t];
+  if (s.ktab) return true;
+  praos_ctx::PoolKeyStore z;
+  z.slots = 1u << 15;
+  z.cap = 1u << 14;
+  bool ok = hipMalloc(&z.pkey, 32 * (size_t)z.slots) == hipSuccess;
+  ok = ok && hipMalloc(&z.pentry, 4 * (size_t)z.slots) == hipSuccess;
+  ok = ok && hipMalloc(&z.count, 8) == hipSuccess;
+  ok = ok && hipMalloc(&z.base, 8) == hipSuccess;
+  ok = ok && hipMalloc(&z.entry_rep, 4 * (size_t)z.cap) == hipSuccess;
+  ok = ok && hipMalloc(&z.entry_pos, 4 * (size_t)z.cap) == hipSuccess;
+  ok = ok && hipMalloc(&z.kinfo, 36 * (size_t)z.cap) == hipSuccess;
+  ok = ok && hipMalloc(&z.ktab, KT_BYTES * (size_t)z.cap) == hipSuccess;
+  ok = ok && hipHostMalloc(&z.count_h, 8) == hipSuccess;
+  ok = ok && hipMemset(z.pentry, 0xff, 4 * (size_t)z.slots) == hipSuccess;
+  ok = ok && hipMemset(z.count, 0, 8) == hipSuccess;
+  if (!ok) {
+    for (void* q : {(void*)z.pkey, (void*)z.count, (void*)z.base, (void*)z.entry_rep, (void*)z.entry_pos,
+                    (void*)z.kinfo, (void*)z.pentry, (void*)z.ktab})
+      (void)hipFree(q);
+    if (z.count_h) (void)hipHostFree(z.count_h);
+    return false;
+  }
+  *z.count_h = 0;
+  s = z;
+  return true;
+}
+
 static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint8_t* keys, hipStream_t st,
                     const uint32_t* list, const uint32_t* count, int which) {
-  const int min_uses = c->kc_min[which] > 0 ? c->kc_min[which] : c->keycache;
+  int min_uses = c->kc_min[which] > 0 ? c->kc_min[which] : c->keycache;
   const dim3 g(nblocks(n, NT)), blk(NT);
+  k.kt = k.ktab; k.ki = k.kinfo; k.erep = k.entry_rep; k.epos = k.entry_pos; k.emax = k.max_entries;
+  k.ebase = nullptr; k.store = -1;
   HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
   HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
   HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
-  launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot);
+  praos_ctx::PoolKeyStore* ps = nullptr;
+  if (c->pk_on && which < 2 && ensure_pks(c, which)) {
+    // pool keys: entries continue the store's, every new key is cached (it recurs in the runs
+    // that follow); a store more than 3/4 full is emptied first
+    ps = &c->pks[which];
+    if (c->pk_reset_run || *ps->count_h > ps->cap / 4 * 3) {
+      HIPCHK(c, hipMemsetAsync(ps->pentry, 0xff, 4 * (size_t)ps->slots, st));
+      HIPCHK(c, hipMemsetAsync(ps->count, 0, 4, st));
+      *ps->count_h = 0;
+    }
+    HIPCHK(c, hipMemcpyAsync(k.counters, ps->count, 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(ps->base, ps->count, 4, hipMemcpyDeviceToDevice, st));
+    k.kt = ps->ktab; k.ki = ps->kinfo; k.erep = ps->entry_rep; k.epos = ps->entry_pos; k.emax = ps->cap;
+    k.ebase = ps->base; k.store = which;
+    min_uses = 1;
+  }
+  launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot,
+                    ps ? ps->pentry : nullptr, ps ? ps->pkey : nullptr, ps ? ps->slots - 1 : 0u);
   launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)min_uses,
-                    k.max_entries, k.slot_entry, k.entry_rep, k.entry_pos, k.counters);
-  launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.entry_pos, k.hit, k.miss,
+                    k.emax, k.slot_entry, k.erep, k.epos, k.counters);
+  launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.epos, k.hit, k.miss,
                        k.counters);
   return PRAOS_OK;
 }
 static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st, size_t n) {
-  launch_key_precompute(dim3(nblocks(k.max_entries, 64)), dim3(64), st, kind, k.counters, k.max_entries, k.entry_rep,
-                        keys, k.ktab, k.kinfo,
-                        c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < SMALL_BATCH));
+  const int prio = c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < SMALL_BATCH);
+  if (k.store < 0) {
+    launch_key_precompute(kind, st, k.counters, k.max_entries, k.entry_rep, keys, k.ktab, k.kinfo, prio, nullptr,
+                          k.max_entries);
+    return;
+  }
+  praos_ctx::PoolKeyStore& ps = c->pks[k.store];
+  const uint32_t span = (uint32_t)std::min<size_t>(n, ps.cap);   // new entries of this run, at most
+  launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, keys, ps.ktab, ps.kinfo, prio, ps.base, span);
+  launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, keys, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
+                      span);
+  (void)hipMemcpyAsync(ps.count_h, ps.count, 4, hipMemcpyDeviceToHost, st);
 }
 
 static int batch_run_impl(praos_ctx* c, praos_batch* b) {
@@ -1043,6 +1128,9 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   c->last_from_bytes = b->from_bytes;
   c->v_timed = false;
   c->kes_ck_timed = false;
+  c->pk_on = c->keycache > 0 && (c->pool_keys > 0 || (c->pool_keys < 0 && c->replaying));
+  c->pk_reset_run = c->pk_reset;
+  c->pk_reset = false;
   if (b->from_bytes) {
     // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
@@ -1168,7 +1256,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                  b->vrf_proof, b->tab_vrfu, b->vrf_mid);
     if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
     keycache_precompute(k, b->vrf_vk, 1, sv);
-    launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, c->btab, b->vrf_vk,
+    launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
                  b->vrf_proof, b->tab_vrfu, b->vrf_mid);
     if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     vrf_keys_queued = true;
@@ -1203,7 +1291,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                        b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
+      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, b->dd_ok);
     } else {
@@ -1239,7 +1327,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                        (uint8_t*)nullptr, b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->cold_vk,
+      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
                       b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
                       P.max_kes_evo, bo, (uint8_t*)nullptr);
     } else {
@@ -1271,7 +1359,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                    (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
       keycache_precompute(k, b->kes_leaf, 0, sk);
       HIPCHK(c, hipEventRecord(c->kc0_ev, sk));
-      launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, b->hot_vk, b->kes_sig,
+      launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                     P.slots_per_kes_period, bk, c->kes_pair_min());
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
@@ -1308,7 +1396,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
       keycache_precompute(k, b->vrf_vk, 1, sv);
       for (int q = 0; q < 2; q++)
-        launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.ktab, k.kinfo, c->bcomb16, c->btab, b->vrf_vk,
+        launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
                      proof[q], b->tab_vrfu, mid[q]);
       if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     } else {
@@ -1348,13 +1436,13 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       return PRAOS_OK;
     };
     auto fin = [&](hipStream_t st, const uint32_t* list, const uint32_t* count, const praos_batch::KeyCache* k) {
-      launch_vrf_fin(st, n, list, count, k ? k->item_entry : nullptr, k ? k->ktab : nullptr, k ? k->kinfo : nullptr,
+      launch_vrf_fin(st, n, list, count, k ? k->item_entry : nullptr, k ? k->kt : nullptr, k ? k->ki : nullptr,
                      c->bcomb16, c->btab, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, c->d_pool_hash,
                      c->d_pool_vrf, c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx,
                      b->pool_sorted, b->beta, b->leader, b->nonce, b->tab_vrf, b->vrf_mid);
     };
     auto stage_u = [&](hipStream_t st, const uint32_t* list, const uint32_t* count, const praos_batch::KeyCache* k) {
-      launch_vrf_u(st, n, list, count, k ? k->item_entry : nullptr, k ? k->ktab : nullptr, k ? k->kinfo : nullptr,
+      launch_vrf_u(st, n, list, count, k ? k->item_entry : nullptr, k ? k->kt : nullptr, k ? k->ki : nullptr,
                    c->bcomb16, c->btab, b->vrf_vk, b->vrf_proof, b->tab_vrfu, b->vrf_mid);
     };
     auto join = [&](hipStream_t st) {
@@ -1505,7 +1593,7 @@ int praos_batch_stats(praos_ctx* c, praos_batch* b, uint32_t out[9]) {
   for (int t = 0; t < 3; t++) {
     uint32_t cnt[4] = {0, 0, 0, 0};
     HIPCHK(c, hipMemcpy(cnt, b->kc[t].counters, 16, hipMemcpyDeviceToHost));
-    out[3 * t] = std::min(cnt[0], b->kc[t].max_entries);
+    out[3 * t] = std::min(cnt[0], b->kc[t].emax ? b->kc[t].emax : b->kc[t].max_entries);
     out[3 * t + 1] = cnt[1];
     out[3 * t + 2] = cnt[2];
   }
@@ -1531,6 +1619,11 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_DEDUP) { c->dedup = value != 0; return PRAOS_OK; }
   if (opt == PRAOS_OPT_PIPELINE) { c->pipeline = value < 0 ? 0 : std::min(value, PIPE_MAX); return PRAOS_OK; }
   if (opt == PRAOS_OPT_KES_PAIR) { c->kes_pair = value < 0 ? -1 : value; return PRAOS_OK; }
+  if (opt == PRAOS_OPT_POOL_KEYS) {
+    c->pool_keys = value < 0 ? -1 : (value != 0);
+    if (value == 2) c->pk_reset = true;
+    return PRAOS_OK;
+  }
   return PRAOS_E_ARG;
 }
 
@@ -2213,7 +2306,11 @@ using praos_host::nonce_eq;
 
 // error text for the other host modules of the library (praos_replay.hip)
 void praos_set_error_(praos_ctx* c, const std::string& m) { if (c) c->err = m; }
-void praos_error_first_only_(praos_ctx* c, bool on) { if (c) c->err.first_only(on); }
+void praos_error_first_only_(praos_ctx* c, bool on) {
+  if (!c) return;
+  c->err.first_only(on);
+  c->replaying = on;                                   // (set for the length of a replay call)
+}
 
 extern "C" {
 

@@ -324,7 +324,8 @@ def ptr(a, t=u8p):
     return a.ctypes.data_as(t)
 
 
-OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP, OPT_PIPELINE, OPT_KES_PAIR = 1, 2, 3, 4, 5, 6   # praos_set_option
+OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP, OPT_PIPELINE, OPT_KES_PAIR, OPT_POOL_KEYS = 1, 2, 3, 4, 5, 6, 7
+# (praos_set_option, praos_hip.h)
 
 
 class PraosError(RuntimeError):
