@@ -1049,8 +1049,12 @@ static bool ensure_pks(praos_ctx* c, int t) {
   ok = ok && hipMalloc(&z.kinfo, 36 * (size_t)z.cap) == hipSuccess;
   ok = ok && hipMalloc(&z.ktab, KT_BYTES * (size_t)z.cap) == hipSuccess;
   ok = ok && hipHostMalloc(&z.count_h, 8) == hipSuccess;
+  // (initialised and waited for here: the context's streams do not order after the null
+  // stream, and a run reads count and pentry from its first kernel on)
   ok = ok && hipMemset(z.pentry, 0xff, 4 * (size_t)z.slots) == hipSuccess;
   ok = ok && hipMemset(z.count, 0, 8) == hipSuccess;
+  ok = ok && hipMemset(z.base, 0, 8) == hipSuccess;
+  ok = ok && hipDeviceSynchronize() == hipSuccess;
   if (!ok) {
     for (void* q : {(void*)z.pkey, (void*)z.count, (void*)z.base, (void*)z.entry_rep, (void*)z.entry_pos,
                     (void*)z.kinfo, (void*)z.pentry, (void*)z.ktab})
