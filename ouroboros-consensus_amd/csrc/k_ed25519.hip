@@ -54,13 +54,33 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes(size_t n, const uint32_t* __r
 // Hits of the leaf-key cache: the leaf key's multi-power tables were built once per
 // batch (k_keys.hip, kind 0), so [h]A is a 16-window chain.  The cached key is the
 // same 32 bytes kes_merkle selects (k_kes_leafkeys reads them the same way).
-// From pair_min hits on (a count the kernel reads itself; 0 = never) each lane takes two headers,
-// q and q + lanes, and encodes both R' with one inversion of Z_a Z_b: the encoding's
-// inversion is ~265 of a cached verify's ~1,000 multiplications.  Smaller batches keep one
-// header per lane, the shorter chain (their waves do not fill the SIMDs).  The first
-// header's R' waits in LDS while the second is computed (24 words per lane).  Verdicts
-// are those of ed25519_verify_cached header by header.
+// k_kes_ck2, the paired form (launched when pairing is enabled, PRAOS_OPT_KES_PAIR): from
+// pair_min hits on (a count the kernel reads itself) each lane takes two headers, q and
+// q + lanes, and encodes both R' with one inversion of Z_a Z_b: the encoding's inversion is
+// ~265 of a cached verify's ~1,000 multiplications.  Below pair_min it keeps one header per
+// lane.  The first header's R' waits in LDS while the second is computed (24 words per
+// lane).  Verdicts are those of ed25519_verify_cached header by header.
 __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck(const uint32_t* __restrict__ list,
+                                                      const uint32_t* __restrict__ count,
+                                                      const int32_t* __restrict__ item_entry,
+                                                      const ge_cached* __restrict__ ktab,
+                                                      const uint32_t* __restrict__ kinfo,
+                                                      const ge_niels* __restrict__ gbtab, KesIn a) {
+  const size_t items = *count;
+  if ((size_t)blockIdx.x * blockDim.x >= items) return;
+  const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= items) return;
+  const size_t i = list[q];
+  const size_t e = (size_t)item_entry[i];
+  uint32_t sg[16], leaf[8], hram[16];
+  bool merkle_ok, in_range;
+  kes_prepare(a, i, sg, leaf, hram, merkle_ok, in_range);
+  const bool leaf_ok = ed25519_verify_cached(sg, sg + 8, hram, kinfo[9 * e], ktab + e * KT_STRIDE, btab);
+  kes_store(a, i, merkle_ok, leaf_ok, in_range);
+}
+
+__global__ void __launch_bounds__(NT, LB_ED) k_kes_ck2(const uint32_t* __restrict__ list,
                                                       const uint32_t* __restrict__ count,
                                                       const int32_t* __restrict__ item_entry,
                                                       const ge_cached* __restrict__ ktab,
@@ -184,7 +204,10 @@ void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    uint64_t slots_per_kes_period, uint16_t* bits, uint32_t pair_min) {
   KesIn a{hot_vk, kes_sig, body_off, body_len, body, body_bytes_len, slot, ocert_c0, slots_per_kes_period,
           nullptr, bits, nullptr, nullptr};
-  hipLaunchKernelGGL(k_kes_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a, pair_min);
+  if (pair_min)     // (the one-header kernel keeps its registers: the paired one spills 176 bytes)
+    hipLaunchKernelGGL(k_kes_ck2, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a, pair_min);
+  else
+    hipLaunchKernelGGL(k_kes_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }
 void launch_kes_leafkeys(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* kes_sig,
                          const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,

@@ -23,7 +23,7 @@
 // byte) and a key found there is a hit on its stored entry without entering the batch's
 // set; new keys get entry ids after the store's, their tables are built once, and
 // k_pkey_publish adds them to the store for the runs that follow (on the same stream).
-#include "kcommon.hpp"
+#include "k_keys.hpp"
 
 __device__ __forceinline__ uint32_t key_hash(const uint32_t k[8]) {
   uint32_t h = k[0] * 0x9E3779B1u;
@@ -158,14 +158,6 @@ __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, con
   wave_append(in && e < 0, (uint32_t)i, &counters[2], miss_list);
 }
 
-// kind 0 (cold key, Ed25519): flag = ge_is_canonical && !ge_has_small_order &&
-//        decodes; tables of -A (ge25519_frombytes_negate_vartime), 16 chunks.
-// kind 1 (VRF key): flag = !ge_has_small_order && decodes (vrf_validate_key);
-//        kinfo[1..8] = canonical encoding of Y; tables of -Y, 9 chunks.
-// chunk tables per key: Ed25519 scalars are < 2^256 (16 chunks); the VRF challenge c
-// is < 2^128 (8 chunks + the top digit's table)
-__device__ __forceinline__ int key_chunks(int kind) { return kind == 0 ? KT_CHUNKS : 9; }
-
 __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t* __restrict__ counters,
                                                         uint32_t max_entries, const uint32_t* __restrict__ entry_rep,
                                                         const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
@@ -178,28 +170,7 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
   const uint32_t e = (base ? *base : 0u) + blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ne = min(counters[0], max_entries);
   if (e >= ne) return;
-  uint32_t pk[8];
-  load_words(pk, keys + 32 * (size_t)entry_rep[e], 8);
-  ge_p3 P;
-  bool ok;
-  uint32_t* info = kinfo + 9 * (size_t)e;
-  if (kind == 0) {
-    ok = ge_is_canonical(pk) && !ge_has_small_order(pk);
-    ok = ge_frombytes(P, pk, /*negate=*/true) && ok;
-  } else {
-    ok = !ge_has_small_order(pk);
-    ge_p3 Y;
-    ok = ge_frombytes(Y, pk, false) && ok;
-    uint32_t ys[8];
-    ge_enc_affine(ys, Y);
-#pragma unroll
-    for (int q = 0; q < 8; q++) info[1 + q] = ys[q];
-    P = Y;
-    fe_neg(P.X, Y.X);
-    fe_neg(P.T, Y.T);
-  }
-  info[0] = ok ? 1u : 0u;
-  key_chunk_bases(ktab + (size_t)e * KT_STRIDE, P, key_chunks(kind));
+  key_precompute_entry(kind, e, entry_rep, keys, ktab, kinfo);
 }
 
 // pass 2: lane (entry, chunk) expands the chunk base into its 8-entry table
@@ -327,9 +298,12 @@ void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 }
 void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
-                           int wave_prio, const uint32_t* base, uint32_t span) {
-  hipLaunchKernelGGL(k_key_precompute, dim3((span + 63) / 64), dim3(64), 0, stream, kind, counters, max_entries,
-                     entry_rep, keys, ktab, kinfo, wave_prio, base);
+                           int wave_prio, const uint32_t* base, uint32_t span, int ilp4) {
+  if (ilp4)
+    launch_key_precompute4(kind, stream, counters, max_entries, entry_rep, keys, ktab, kinfo, wave_prio, base, span);
+  else
+    hipLaunchKernelGGL(k_key_precompute, dim3((span + 63) / 64), dim3(64), 0, stream, kind, counters, max_entries,
+                       entry_rep, keys, ktab, kinfo, wave_prio, base);
   const size_t lanes = (size_t)span * KT_CHUNKS;
   hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, kind, counters,
                      max_entries, ktab, wave_prio, base);

@@ -55,7 +55,11 @@ void launch_ocert_fanout(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
 // entries [*base (0 when null), min(counters[0], max_entries)), at most span of them
 void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
-                           int wave_prio, const uint32_t* base, uint32_t span);
+                           int wave_prio, const uint32_t* base, uint32_t span,
+                           int ilp4);                      // the chain from the ILP-4 build (k_keys4.hip)
+void launch_key_precompute4(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
+                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
+                            int wave_prio, const uint32_t* base, uint32_t span);
 void launch_pkey_publish(hipStream_t stream, const uint32_t* counters, const uint32_t* base, uint32_t max_entries,
                          const uint32_t* entry_rep, const uint8_t* keys, int32_t* pentry, uint32_t* pkey,
                          uint32_t pmask, uint32_t* count, uint32_t span);

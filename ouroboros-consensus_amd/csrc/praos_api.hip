@@ -167,6 +167,9 @@ struct praos_ctx {
   }
   int vrf_keys_first = 0;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl; 54k: 2.80 ->
                                                        // 2.85 ms, 108k 4.24 -> 4.27: off, profiles/r04/k)
+  int key4 = 0;                                        // key precompute from the ILP-4 build (k_keys4.hip):
+                                                       // PRAOS_KEY4 1 / 0, -1 below SMALL_BATCH
+  bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < SMALL_BATCH); }
   bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < SMALL_BATCH); }
   int v_ilp4(size_t n) const {
     const bool on = vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4);
@@ -525,6 +528,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_VRF_ILP4")) c->vrf_ilp4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
@@ -1104,12 +1108,13 @@ static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t*
   const int prio = c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < SMALL_BATCH);
   if (k.store < 0) {
     launch_key_precompute(kind, st, k.counters, k.max_entries, k.entry_rep, keys, k.ktab, k.kinfo, prio, nullptr,
-                          k.max_entries);
+                          k.max_entries, c->use_key4(n));
     return;
   }
   praos_ctx::PoolKeyStore& ps = c->pks[k.store];
   const uint32_t span = (uint32_t)std::min<size_t>(n, ps.cap);   // new entries of this run, at most
-  launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, keys, ps.ktab, ps.kinfo, prio, ps.base, span);
+  launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, keys, ps.ktab, ps.kinfo, prio, ps.base, span,
+                        c->use_key4(n));
   launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, keys, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
                       span);
   (void)hipMemcpyAsync(ps.count_h, ps.count, 4, hipMemcpyDeviceToHost, st);
