@@ -167,8 +167,9 @@ struct praos_ctx {
   }
   int vrf_keys_first = 0;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl; 54k: 2.80 ->
                                                        // 2.85 ms, 108k 4.24 -> 4.27: off, profiles/r04/k)
-  int key4 = 0;                                        // key precompute from the ILP-4 build (k_keys4.hip):
-                                                       // PRAOS_KEY4 1 / 0, -1 below SMALL_BATCH
+  int key4 = -1;                                       // key precompute from the ILP-4 build (k_keys4.hip):
+                                                       // PRAOS_KEY4 1 / 0, -1 below SMALL_BATCH (54k: 2.78-2.84
+                                                       // -> 2.76-2.77 ms; 108k 4.17 -> 4.21, profiles/r04/n)
   bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < SMALL_BATCH); }
   bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < SMALL_BATCH); }
   int v_ilp4(size_t n) const {
