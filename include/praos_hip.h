@@ -225,7 +225,8 @@ int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items
  * uncached; out[3..5] = the same for VRF keys; out[6..8] for the KES leaf keys
- * (the Ed25519 key each Sum6KES signature ends on).  Returns 0. */
+ * (the Ed25519 key each Sum6KES signature ends on).  With the pool-key store on
+ * (PRAOS_OPT_POOL_KEYS) out[0] / out[3] count the store's entries after the run.  Returns 0. */
 int praos_batch_stats(praos_ctx* ctx, praos_batch* b, uint32_t out[9]);
 /* OCert dedup of the last praos_batch_run: out[0] = distinct OCert tuples verified,
  * out[1] = headers (out[0] = 0 when the dedup did not run).  Returns 0. */
