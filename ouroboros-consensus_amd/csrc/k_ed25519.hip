@@ -65,7 +65,9 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck(const uint32_t* __restrict
                                                       const int32_t* __restrict__ item_entry,
                                                       const ge_cached* __restrict__ ktab,
                                                       const uint32_t* __restrict__ kinfo,
-                                                      const ge_niels* __restrict__ gbtab, KesIn a) {
+                                                      const ge_niels* __restrict__ gbtab, KesIn a,
+                                                      const uint32_t* __restrict__ entry_rep,
+                                                      const uint8_t* __restrict__ rep_ok) {
   const size_t items = *count;
   if ((size_t)blockIdx.x * blockDim.x >= items) return;
   const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
@@ -75,7 +77,8 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck(const uint32_t* __restrict
   const size_t e = (size_t)item_entry[i];
   uint32_t sg[16], leaf[8], hram[16];
   bool merkle_ok, in_range;
-  kes_prepare(a, i, sg, leaf, hram, merkle_ok, in_range);
+  kes_prepare_dd(a, i, rep_ok ? entry_rep[e] : i, rep_ok ? rep_ok + e : nullptr, sg, leaf, hram, merkle_ok,
+                 in_range);
   const bool leaf_ok = ed25519_verify_cached(sg, sg + 8, hram, kinfo[9 * e], ktab + e * KT_STRIDE, btab);
   kes_store(a, i, merkle_ok, leaf_ok, in_range);
 }
@@ -86,7 +89,8 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck2(const uint32_t* __restric
                                                       const ge_cached* __restrict__ ktab,
                                                       const uint32_t* __restrict__ kinfo,
                                                       const ge_niels* __restrict__ gbtab, KesIn a,
-                                                      uint32_t pair_min) {
+                                                      uint32_t pair_min, const uint32_t* __restrict__ entry_rep,
+                                                      const uint8_t* __restrict__ rep_ok) {
   __shared__ uint32_t stash[24 * NT];
   const size_t items = *count;
   const size_t lanes = pair_min && items >= pair_min ? (items + 1) / 2 : items;
@@ -105,8 +109,9 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck2(const uint32_t* __restric
     if (h == 1 && !has_b) break;
     const size_t i = h ? list[q + lanes] : ia;
     bool merkle_ok, in_range;
-    kes_prepare(a, i, sg, leaf, hram, merkle_ok, in_range);
     const size_t e = (size_t)item_entry[i];
+    kes_prepare_dd(a, i, rep_ok ? entry_rep[e] : i, rep_ok ? rep_ok + e : nullptr, sg, leaf, hram, merkle_ok,
+                   in_range);
     const bool ok = ed25519_cached_point(R, sg, sg + 8, hram, kinfo[9 * e], ktab + e * KT_STRIDE, btab);
     fl |= ((merkle_ok ? 1u : 0u) | (in_range ? 2u : 0u) | (ok ? 4u : 0u)) << (3 * h);
     if (h == 0) {
@@ -151,6 +156,19 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck2(const uint32_t* __restric
 #pragma unroll
   for (int k = 0; k < 8; k++) eq &= enc[k] == sg[k];
   kes_store(a, ia, (fl & 1u) != 0, (fl & 4u) != 0 && eq, (fl & 2u) != 0);
+}
+
+// The Merkle walk of each leaf-key cache entry's representative, for the path dedup of
+// k_kes_ck / k_kes_ck2 (rep_ok[e] = the walk's verdict).
+__global__ void __launch_bounds__(NT) k_kes_merkle_reps(const uint32_t* __restrict__ counters, uint32_t max_entries,
+                                                        const uint32_t* __restrict__ entry_rep, KesIn a,
+                                                        uint8_t* __restrict__ rep_ok) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= min(counters[0], max_entries)) return;
+  const size_t i = entry_rep[e];
+  uint32_t vk[8], leaf[8];
+  load_words(vk, a.hot_vk + 32 * i, 8);
+  rep_ok[e] = kes_merkle(leaf, vk, kes_t(a, i), a.kes_sig + 448 * i) ? 1 : 0;
 }
 
 // The leaf Ed25519 key each header's KES signature selects (the depth-1 pair entry
@@ -201,13 +219,25 @@ void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                    const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off, const uint32_t* body_len,
                    const uint8_t* body, size_t body_bytes_len, const uint64_t* slot, const uint64_t* ocert_c0,
-                   uint64_t slots_per_kes_period, uint16_t* bits, uint32_t pair_min) {
+                   uint64_t slots_per_kes_period, uint16_t* bits, uint32_t pair_min, const uint32_t* entry_rep,
+                   const uint8_t* rep_ok) {
   KesIn a{hot_vk, kes_sig, body_off, body_len, body, body_bytes_len, slot, ocert_c0, slots_per_kes_period,
           nullptr, bits, nullptr, nullptr};
   if (pair_min)     // (the one-header kernel keeps its registers: the paired one spills 176 bytes)
-    hipLaunchKernelGGL(k_kes_ck2, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a, pair_min);
+    hipLaunchKernelGGL(k_kes_ck2, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a, pair_min,
+                       entry_rep, rep_ok);
   else
-    hipLaunchKernelGGL(k_kes_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
+    hipLaunchKernelGGL(k_kes_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a, entry_rep,
+                       rep_ok);
+}
+void launch_kes_merkle_reps(hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
+                            const uint32_t* entry_rep, const uint8_t* hot_vk, const uint8_t* kes_sig,
+                            const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
+                            uint8_t* rep_ok) {
+  KesIn a{hot_vk, kes_sig, nullptr, nullptr, nullptr, 0, slot, ocert_c0, slots_per_kes_period, nullptr, nullptr,
+          nullptr, nullptr};
+  hipLaunchKernelGGL(k_kes_merkle_reps, dim3((max_entries + NT - 1) / NT), dim3(NT), 0, stream, counters, max_entries,
+                     entry_rep, a, rep_ok);
 }
 void launch_kes_leafkeys(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* kes_sig,
                          const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,

@@ -89,6 +89,66 @@ __device__ __forceinline__ void kes_prepare(const KesIn& a, size_t i, uint32_t s
   sha512_stream(hram, pre, 64, a.body + off, len);
 }
 
+// Merkle walk shared per leaf-key cache entry (KES path dedup): the walk reads hot_vk, t and
+// the six vk pairs sig[64 .. 448); an item whose bytes equal its entry representative's gets
+// the representative's verdict (k_kes_merkle_reps) and selects its leaf as the walk would.
+__device__ __forceinline__ bool kes_path_same(const KesIn& a, size_t i, size_t r, uint64_t ti) {
+  if (i == r) return true;
+  if (kes_t(a, r) != ti) return false;
+  const uint4* p = (const uint4*)(a.kes_sig + 448 * i + 64);
+  const uint4* q = (const uint4*)(a.kes_sig + 448 * r + 64);
+  bool same = true;
+#pragma unroll
+  for (int k = 0; k < 24; k++) {
+    const uint4 x = p[k], y = q[k];
+    same &= x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
+  }
+  const uint4* hp = (const uint4*)(a.hot_vk + 32 * i);
+  const uint4* hq = (const uint4*)(a.hot_vk + 32 * r);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const uint4 x = hp[k], y = hq[k];
+    same &= x.x == y.x && x.y == y.y && x.z == y.z && x.w == y.w;
+  }
+  return same;
+}
+
+// the depth-1 entry kes_merkle ends on (as k_kes_leafkeys)
+__device__ __forceinline__ void kes_leaf_select(uint32_t leaf[8], uint64_t t, const uint8_t* __restrict__ sig) {
+#pragma unroll
+  for (int d = 6; d >= 2; d--) {
+    const uint64_t T = 1ull << (d - 1);
+    t = t >= T ? t - T : t;
+  }
+  load_words(leaf, sig + 64 + (t >= 1 ? 32 : 0), 8);
+}
+
+// kes_prepare with the path dedup: rep / rep_ok = the item's cache entry's representative and
+// its walk verdict (rep_ok null: every item walks)
+__device__ __forceinline__ void kes_prepare_dd(const KesIn& a, size_t i, size_t rep, const uint8_t* rep_ok,
+                                               uint32_t sg[16], uint32_t leaf[8], uint32_t hram[16],
+                                               bool& merkle_ok, bool& in_range) {
+  const uint8_t* sig = a.kes_sig + 448 * i;
+  const uint64_t t = kes_t(a, i);
+  if (rep_ok && kes_path_same(a, i, rep, t)) {
+    merkle_ok = *rep_ok != 0;
+    kes_leaf_select(leaf, t, sig);
+  } else {
+    uint32_t vk[8];
+    load_words(vk, a.hot_vk + 32 * i, 8);
+    merkle_ok = kes_merkle(leaf, vk, t, sig);
+  }
+  load_words(sg, sig, 16);
+  uint64_t off = a.body_off[i];
+  uint32_t len = a.body_len[i];
+  in_range = (off & 7) == 0 && off <= a.body_bytes_len && len <= a.body_bytes_len - off;
+  if (!in_range) { off = 0; len = 0; }
+  uint32_t pre[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) { pre[k] = sg[k]; pre[8 + k] = leaf[k]; }
+  sha512_stream(hram, pre, 64, a.body + off, len);
+}
+
 __device__ __forceinline__ void kes_store(const KesIn& a, size_t i, bool merkle_ok, bool leaf_ok, bool in_range) {
   if (a.result) {
     a.result[i] = !in_range ? 3 : (!merkle_ok ? 1 : (leaf_ok ? 0 : 2));

@@ -82,7 +82,13 @@ void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off, const uint32_t* body_len,
                    const uint8_t* body, size_t body_bytes_len, const uint64_t* slot, const uint64_t* ocert_c0,
                    uint64_t slots_per_kes_period, uint16_t* bits,
-                   uint32_t pair_min);                      // two headers per lane from pair_min hits on (0: never)
+                   uint32_t pair_min,                       // two headers per lane from pair_min hits on (0: never)
+                   const uint32_t* entry_rep,               // with rep_ok (k_kes_merkle_reps): the Merkle path
+                   const uint8_t* rep_ok);                  // dedup per cache entry (null: every item walks)
+void launch_kes_merkle_reps(hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
+                            const uint32_t* entry_rep, const uint8_t* hot_vk, const uint8_t* kes_sig,
+                            const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
+                            uint8_t* rep_ok);
 void launch_kes_leafkeys(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* kes_sig,
                          const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
                          uint8_t* keys);

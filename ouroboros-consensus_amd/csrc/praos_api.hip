@@ -165,6 +165,10 @@ struct praos_ctx {
   uint32_t kes_pair_min() const {
     return kes_pair >= 0 ? (uint32_t)kes_pair : ((kernels & 5) ? 0u : 196608u);
   }
+  int kes_dedup = 0;                                   // KES Merkle path dedup per leaf-key entry (PRAOS_KES_DEDUP):
+                                                       // off, measured slower (C4 10.7 -> 11.2 ms: the
+                                                       // representatives' walks lengthen the KES chain more than
+                                                       // the skipped walks save; C5 unchanged, profiles/r04/r)
   int vrf_keys_first = 0;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl; 54k: 2.80 ->
                                                        // 2.85 ms, 108k 4.24 -> 4.27: off, profiles/r04/k)
   int key4 = -1;                                       // key precompute from the ILP-4 build (k_keys4.hip):
@@ -393,6 +397,7 @@ struct praos_batch {
     int32_t *slot_entry = nullptr, *item_slot = nullptr, *item_entry = nullptr;
     uint32_t *counters = nullptr, *hit = nullptr, *miss = nullptr;   // counters: entries, hits, misses
     ge_cached* ktab = nullptr;
+    uint8_t* rep_ok = nullptr;   // KES leaf keys: the Merkle walk verdict of each entry's representative
     // this run's entry space: the arrays above, or the context's pool-key store
     ge_cached* kt = nullptr;
     uint32_t *ki = nullptr, *erep = nullptr, *epos = nullptr;
@@ -530,6 +535,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
@@ -784,6 +790,7 @@ static bool alloc_keycache(praos_batch* b, praos_batch::KeyCache& k, size_t n) {
   ok &= dalloc(b, &k.entry_pos, 4 * (size_t)k.max_entries) == hipSuccess;
   ok &= dalloc(b, &k.kinfo, 36 * (size_t)k.max_entries) == hipSuccess;
   ok &= dalloc(b, (uint8_t**)&k.ktab, KT_BYTES * k.max_entries) == hipSuccess;
+  ok &= dalloc(b, &k.rep_ok, (size_t)k.max_entries) == hipSuccess;
   return ok;
 }
 
@@ -1367,11 +1374,17 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         launch_kes(g, blk, sm_[1], n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off,
                    b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
                    (const uint32_t*)nullptr, bk, (uint8_t*)nullptr, b->tab_kes);
+      // Merkle path dedup: a pool's headers of one KES period carry the same hot key, period and
+      // six vk pairs, so each cache entry's representative walks once and equal paths reuse it
+      if (c->kes_dedup)
+        launch_kes_merkle_reps(sk, k.counters, k.max_entries, k.entry_rep, b->hot_vk, b->kes_sig, b->slot,
+                               b->ocert_c0, P.slots_per_kes_period, k.rep_ok);
       keycache_precompute(k, b->kes_leaf, 0, sk);
       HIPCHK(c, hipEventRecord(c->kc0_ev, sk));
       launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
                     b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
-                    P.slots_per_kes_period, bk, c->kes_pair_min());
+                    P.slots_per_kes_period, bk, c->kes_pair_min(), c->kes_dedup ? k.entry_rep : nullptr,
+                    c->kes_dedup ? k.rep_ok : nullptr);
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
       c->kes_ck_timed = true;
     } else {
