@@ -23,6 +23,7 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
     PraosBatchCtx
   , withPraosBatchCtx
   , PraosBatchError (..)
+  , praosSetPoolKeyStore
     -- * Per epoch
   , PraosParamsC (..)
   , praosSetEpoch
@@ -78,6 +79,7 @@ foreign import ccall safe "praos_open"        c_open        :: CInt -> IO (Ptr P
 foreign import ccall safe "praos_close"       c_close       :: Ptr PraosCtx -> IO ()
 foreign import ccall safe "praos_last_error"  c_last_error  :: Ptr PraosCtx -> IO CString
 foreign import ccall safe "praos_abi_version" c_abi_version :: IO CInt
+foreign import ccall safe "praos_set_option"  c_set_option  :: Ptr PraosCtx -> CInt -> CInt -> IO CInt
 foreign import ccall safe "praos_set_epoch"   c_set_epoch
   :: Ptr PraosCtx -> Ptr Word8 -> Ptr () -> Word32 -> Ptr () -> IO CInt
 foreign import ccall safe "praos_ticked_epoch_nonce" c_ticked_epoch_nonce
@@ -130,6 +132,13 @@ withPraosBatchCtx dev k = do
   bracket (c_open (fromIntegral dev)) c_close $ \p -> do
     when (p == nullPtr) $ throwIO (PraosBatchError (-1) ("praos_open " ++ show dev))
     k (PraosBatchCtx p)
+
+-- | PRAOS_OPT_POOL_KEYS (7): keep the cold-key and VRF-key cache entries across calls on
+-- this context (a node validating batch after batch of one epoch sees the same pool keys);
+-- verdicts are identical either way.  On by default inside the replay entry points.
+praosSetPoolKeyStore :: PraosBatchCtx -> Bool -> IO ()
+praosSetPoolKeyStore ctx@(PraosBatchCtx p) on =
+  check ctx (c_set_option p 7 (if on then 1 else 0))
 
 check :: PraosBatchCtx -> IO CInt -> IO ()
 check (PraosBatchCtx p) act = do
