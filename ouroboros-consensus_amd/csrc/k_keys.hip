@@ -167,10 +167,11 @@ __global__ void __launch_bounds__(64) k_key_precompute(int kind, const uint32_t*
   // chains: raised wave priority wins the SIMD's issue arbitration against the
   // throughput kernels resident beside it
   if (wave_prio) __builtin_amdgcn_s_setprio(3);
-  const uint32_t e = (base ? *base : 0u) + blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride: the host sizes the grid from the previous run's entry count (a grid sized
+  // for the worst case is thousands of empty blocks that wait for wave slots on a busy GPU)
   const uint32_t ne = min(counters[0], max_entries);
-  if (e >= ne) return;
-  key_precompute_entry(kind, e, entry_rep, keys, ktab, kinfo);
+  for (uint32_t e = (base ? *base : 0u) + blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x)
+    key_precompute_entry(kind, e, entry_rep, keys, ktab, kinfo);
 }
 
 // pass 2: lane (entry, chunk) expands the chunk base into its 8-entry table
@@ -178,10 +179,12 @@ __global__ void __launch_bounds__(256) k_key_tables(int kind, const uint32_t* __
                                                     uint32_t max_entries, ge_cached* __restrict__ ktab,
                                                     int wave_prio, const uint32_t* __restrict__ base) {
   if (wave_prio) __builtin_amdgcn_s_setprio(3);
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t e = (base ? *base : 0u) + t / KT_CHUNKS, k = t % KT_CHUNKS;
-  if (e >= min(counters[0], max_entries) || k >= (uint32_t)key_chunks(kind)) return;
-  key_chunk_table(ktab + (size_t)e * KT_STRIDE + 8 * k);
+  const uint32_t e0 = base ? *base : 0u, ne = min(counters[0], max_entries);
+  const uint32_t lanes = ne > e0 ? (ne - e0) * KT_CHUNKS : 0u;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < lanes; t += gridDim.x * blockDim.x) {
+    const uint32_t e = e0 + t / KT_CHUNKS, k = t % KT_CHUNKS;
+    if (k < (uint32_t)key_chunks(kind)) key_chunk_table(ktab + (size_t)e * KT_STRIDE + 8 * k);
+  }
 }
 
 // The run's new entries [*base, min(counters[0], max_entries)) into the pool-key store
@@ -193,18 +196,18 @@ __global__ void k_pkey_publish(const uint32_t* __restrict__ counters, const uint
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ne = min(counters[0], max_entries);
   if (t == 0) *count = ne;
-  const uint32_t e = *base + t;
-  if (e >= ne) return;
-  uint32_t k[8];
-  load_words(k, keys + 32 * (size_t)entry_rep[e], 8);
-  uint32_t g = key_hash(k) & pmask;
-  for (uint32_t probe = 0; probe <= pmask; probe++) {
-    if (atomicCAS(&pentry[g], -1, (int32_t)e) == -1) {
+  for (uint32_t e = *base + t; e < ne; e += gridDim.x * blockDim.x) {
+    uint32_t k[8];
+    load_words(k, keys + 32 * (size_t)entry_rep[e], 8);
+    uint32_t g = key_hash(k) & pmask;
+    for (uint32_t probe = 0; probe <= pmask; probe++) {
+      if (atomicCAS(&pentry[g], -1, (int32_t)e) == -1) {
 #pragma unroll
-      for (int q = 0; q < 8; q++) pkey[8 * (size_t)g + q] = k[q];
-      return;
+        for (int q = 0; q < 8; q++) pkey[8 * (size_t)g + q] = k[q];
+        break;
+      }
+      g = (g + 1u) & pmask;
     }
-    g = (g + 1u) & pmask;
   }
 }
 

@@ -12,10 +12,9 @@ __global__ void __launch_bounds__(64) k_key_precompute4(int kind, const uint32_t
                                                          uint32_t* __restrict__ kinfo, int wave_prio,
                                                          const uint32_t* __restrict__ base) {
   if (wave_prio) __builtin_amdgcn_s_setprio(3);
-  const uint32_t e = (base ? *base : 0u) + blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t ne = min(counters[0], max_entries);
-  if (e >= ne) return;
-  key_precompute_entry(kind, e, entry_rep, keys, ktab, kinfo);
+  for (uint32_t e = (base ? *base : 0u) + blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x)
+    key_precompute_entry(kind, e, entry_rep, keys, ktab, kinfo);
 }
 
 void launch_key_precompute4(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
