@@ -2329,7 +2329,7 @@ using praos_host::nonce_eq;
 
 // error text for the other host modules of the library (praos_replay.hip)
 void praos_set_error_(praos_ctx* c, const std::string& m) { if (c) c->err = m; }
-void praos_error_first_only_(praos_ctx* c, bool on) {
+void praos_replay_scope_(praos_ctx* c, bool on) {
   if (!c) return;
   c->err.first_only(on);
   c->replaying = on;                                   // (set for the length of a replay call)

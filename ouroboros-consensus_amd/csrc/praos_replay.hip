@@ -54,7 +54,7 @@
 #include <vector>
 
 void praos_set_error_(praos_ctx* c, const std::string& m);   // praos_api.hip
-void praos_error_first_only_(praos_ctx* c, bool on);         // (the replay keeps its first error)
+void praos_replay_scope_(praos_ctx* c, bool on);   // replay call scope: first error kept, pool-key store on
 
 namespace {
 
@@ -534,10 +534,10 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
                                       const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                                       praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
                                       size_t verdicts_cap, praos_replay_stats* stats) {
-  praos_error_first_only_(ctx, true);
+  praos_replay_scope_(ctx, true);
   const int r = replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap,
                             stats, false, nullptr);
-  praos_error_first_only_(ctx, false);
+  praos_replay_scope_(ctx, false);
   return r;
 }
 
@@ -546,9 +546,9 @@ extern "C" int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, co
                                              const praos_nonce* extra_entropy, praos_envelope* env,
                                              praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
                                              uint16_t* failures, size_t verdicts_cap, praos_replay_stats* stats) {
-  praos_error_first_only_(ctx, true);
+  praos_replay_scope_(ctx, true);
   const int r = replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap,
                             stats, true, extra_entropy);
-  praos_error_first_only_(ctx, false);
+  praos_replay_scope_(ctx, false);
   return r;
 }
