@@ -93,10 +93,14 @@ static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2
 static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
 static constexpr size_t PIPE_MIN_CHUNK = 65536;     // headers per chunk at least (auto mode)
 // Batches below this many headers (a strong-scaling shard of an epoch over 8 GPUs is 54k) leave
-// most wave slots empty and run latency-bound: stage V from the ILP-4 build, stage V / join and
-// the key precomputes at raised wave priority (profiles/r04/c: 54k step 3.52 -> 3.34 ms together;
-// each alone within noise, profiles/r03/prio_ab)
+// most wave slots empty and run latency-bound: the key precomputes at raised wave priority
+// (PRAOS_KEY_PRIO; profiles/r04/c, r03/prio_ab)
 static constexpr size_t SMALL_BATCH = 80000;
+// below this many headers stage V, the uncached verifies and the key precompute come from their
+// ILP-4 builds (k_vrf_v4 / k_miss4 / k_keys4): a step's chains are latency-bound there
+// (profiles/r04/y: 96k 4.06 -> 3.64 ms, 108k 4.25 -> 4.10, 112k 4.39 -> 4.15; equal at 120k,
+// slower at 128k)
+static constexpr size_t ILP4_BATCH = 120000;
 static constexpr int PIPE_AUTO = 6;                 // chunks in auto mode (432k headers: 4 -> 21.9M, 6 -> 23.0M,
                                                     // 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt)
 struct praos_batch;
@@ -147,14 +151,16 @@ struct praos_ctx {
                                                        // -1: batches below SMALL_BATCH headers).  Off: with the
                                                        // uncached verifies raised instead a 54k-header step takes
                                                        // 2.83 ms against 3.16 (profiles/r04/i, r04/j)
-  int vrf_ilp4 = (int)SMALL_BATCH;                    // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
+  int vrf_ilp4 = (int)ILP4_BATCH;                    // stage V from the ILP-4 build (k_vrf_v4.hip): PRAOS_VRF_ILP4
                                                        // 1 always, 0 never, N > 1: batches below N headers
-                                                       // (profiles/r04/b: V alone 1.71 -> 1.51 ms at 54k, slower
-                                                       // from 108k: 2.33 -> 2.27 ms alone but the step 4.25 -> 4.37)
+                                                       // (profiles/r04/b: V alone 1.71 -> 1.51 ms at 54k; alone
+                                                       // at 108k the step was slower, 4.25 -> 4.37, but with the
+                                                       // ILP-4 uncached verifies and precompute beside it faster,
+                                                       // profiles/r04/y)
   int v_excl = 0;                                      // the ILP-4 stage V holding its SIMDs alone (k_vrf_v4x):
                                                        // PRAOS_V_EXCL (54k: 3.30 -> 3.46 ms, off)
   int miss4 = -1;                                      // uncached OCert / KES verifies from the ILP-4 build
-                                                       // (k_miss4.hip): PRAOS_MISS4 1 / 0, -1 below SMALL_BATCH
+                                                       // (k_miss4.hip): PRAOS_MISS4 1 / 0, -1 below ILP4_BATCH
                                                        // (54k: 3.33 -> 3.09 ms; 108k: 4.26 -> 4.66, so not there)
   int miss_prio = -1;                                  // ... at s_setprio 3: PRAOS_MISS_PRIO 1 / 0, -1 with miss4
   long kes_pair = -1;                                  // k_kes_ck two headers per lane from this many hits on
@@ -172,10 +178,10 @@ struct praos_ctx {
   int vrf_keys_first = 0;                              // PRAOS_VRF_KEYS_FIRST (see batch_run_impl; 54k: 2.80 ->
                                                        // 2.85 ms, 108k 4.24 -> 4.27: off, profiles/r04/k)
   int key4 = -1;                                       // key precompute from the ILP-4 build (k_keys4.hip):
-                                                       // PRAOS_KEY4 1 / 0, -1 below SMALL_BATCH (54k: 2.78-2.84
+                                                       // PRAOS_KEY4 1 / 0, -1 below ILP4_BATCH (54k: 2.78-2.84
                                                        // -> 2.76-2.77 ms; 108k 4.17 -> 4.21, profiles/r04/n)
-  bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < SMALL_BATCH); }
-  bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < SMALL_BATCH); }
+  bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < ILP4_BATCH); }
+  bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < ILP4_BATCH); }
   int v_ilp4(size_t n) const {
     const bool on = vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4);
     return on ? (v_excl ? 2 : 1) : 0;
