@@ -542,6 +542,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_POOL_KEYS")) c->pool_keys = std::atoi(e);   // (the option's default)
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
