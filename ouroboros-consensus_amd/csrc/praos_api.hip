@@ -93,9 +93,12 @@ static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2
 static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
 static constexpr size_t PIPE_MIN_CHUNK = 65536;     // headers per chunk at least (auto mode)
 // Batches below this many headers (a strong-scaling shard of an epoch over 8 GPUs is 54k) leave
-// most wave slots empty and run latency-bound: the key precomputes at raised wave priority
-// (PRAOS_KEY_PRIO; profiles/r04/c, r03/prio_ab)
+// most wave slots empty and run latency-bound (PRAOS_VRF_PRIO = -1 raises stage V there)
 static constexpr size_t SMALL_BATCH = 80000;
+// below this many headers the key precomputes run at raised wave priority (PRAOS_KEY_PRIO -1):
+// they head the cached chains (profiles/r04/bb: 96k 3.66 -> 3.57 ms, 108k 4.14 -> 3.83, 160k
+// 5.19 -> 4.88, 300k 8.83 -> 8.67; 432k within noise)
+static constexpr size_t KEY_PRIO_BATCH = 400000;
 // below this many headers stage V, the uncached verifies and the key precompute come from their
 // ILP-4 builds (k_vrf_v4 / k_miss4 / k_keys4): a step's chains are latency-bound there
 // (profiles/r04/y: 96k 4.06 -> 3.64 ms, 108k 4.25 -> 4.10, 112k 4.39 -> 4.15; equal at 120k,
@@ -204,7 +207,7 @@ struct praos_ctx {
                                                        // keycache when > 0 (PRAOS_KC_MIN="c,v,k")
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
   int key_wave_prio = -1;                              // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO 1 / 0;
-                                                       // -1: batches below SMALL_BATCH headers)
+                                                       // -1: batches below KEY_PRIO_BATCH headers)
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
   hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
@@ -1120,7 +1123,7 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
   return PRAOS_OK;
 }
 static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st, size_t n) {
-  const int prio = c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < SMALL_BATCH);
+  const int prio = c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < KEY_PRIO_BATCH);
   if (k.store < 0) {
     launch_key_precompute(kind, st, k.counters, k.max_entries, k.entry_rep, keys, k.ktab, k.kinfo, prio, nullptr,
                           k.max_entries, c->use_key4(n));
