@@ -120,3 +120,17 @@ def test_haskell_imports_declared_symbols():
     hs = open(HASKELL).read()
     imported = set(re.findall(r'foreign import ccall safe "(praos_[a-z0-9_]+)"', hs))
     assert imported and imported <= _declared()
+
+
+def test_option_ids_match_header():
+    """praos_set_option ids: the Python constants and the Haskell binding's literal (pool-key
+    store, 7) are the header's PRAOS_OPT_* values."""
+    from praos_hip import abi
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "praos_hip.h")).read()
+    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define PRAOS_OPT_([A-Z_]+) (\d+)", hdr)}
+    assert ids == {"CONCURRENT": 1, "KERNELS": 2, "KEYCACHE": 3, "DEDUP": 4, "PIPELINE": 5, "KES_PAIR": 6,
+                   "POOL_KEYS": 7}
+    for name, v in ids.items():
+        assert getattr(abi, "OPT_" + name) == v, name
+    assert "c_set_option p 7" in open(HASKELL).read()
