@@ -320,10 +320,12 @@ void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const ui
 }
 void launch_vrf_u(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
                   const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const ge_niels* gbtab,
-                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid) {
+                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid, int ilp4) {
   const dim3 g((unsigned)((n + NT - 1) / NT));
   const unsigned bs = lat_block(n);
-  if (ktab)
+  if (ktab && ilp4)
+    launch_vrf_u4(stream, n, list, count, item_entry, ktab, kinfo, comb, vrf_proof, mid);
+  else if (ktab)
     hipLaunchKernelGGL(k_vrf_u, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, list, count, item_entry,
                        ktab, kinfo, comb, vrf_proof, (uint4*)mid);
   else

@@ -36,6 +36,30 @@ __global__ void __launch_bounds__(NT, 1) k_vrf_v4x(size_t n, size_t i0, size_t i
   vrf_v_core(mid, n, i, pk, pr, pr + 8, pr + 12, alpha, lane_tab(a.tabs, i, LT_VRF));
 }
 
+// Stage U of a cached key (k_vrf_stage.hip k_vrf_u) from the same ILP-4 build: small batches
+__global__ void __launch_bounds__(NT, 2) k_vrf_u4(size_t stride, const uint32_t* __restrict__ list,
+                                                  const uint32_t* __restrict__ count,
+                                                  const int32_t* __restrict__ item_entry,
+                                                  const ge_cached* __restrict__ ktab,
+                                                  const uint32_t* __restrict__ kinfo,
+                                                  const ge_niels* __restrict__ comb,
+                                                  const uint8_t* __restrict__ vrf_proof, uint4* __restrict__ mid) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)*count) return;
+  const size_t i = list[t];
+  const size_t e = (size_t)item_entry[i];
+  uint32_t pr[20];
+  load_words(pr, vrf_proof + 80 * i, 20);
+  vrf_u_core<true>(mid, stride, i, nullptr, pr + 8, pr + 12, comb, nullptr, ktab + e * KT_STRIDE, kinfo + 9 * e);
+}
+
+void launch_vrf_u4(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
+                   const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const uint8_t* vrf_proof,
+                   void* mid) {
+  hipLaunchKernelGGL(k_vrf_u4, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, n, list, count, item_entry,
+                     ktab, kinfo, comb, vrf_proof, (uint4*)mid);
+}
+
 void launch_vrf_v4(hipStream_t stream, size_t n, size_t i0, size_t i1, const uint8_t* vrf_vk,
                    const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
                    const uint8_t* eta_idx, ge_cached* tabs, void* mid, int wave_prio, int tp_seed, int excl) {

@@ -143,7 +143,11 @@ void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const ui
 // over list[0 .. *count) or all n, 8-entry lane tables utabs) and the join over all n
 void launch_vrf_u(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
                   const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const ge_niels* gbtab,
-                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid);
+                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid,
+                  int ilp4 = 0);                           // cached keys: the ILP-4 build (k_vrf_v4.hip k_vrf_u4)
+void launch_vrf_u4(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
+                   const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const uint8_t* vrf_proof,
+                   void* mid);
 void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const uint8_t* vrf_vk,
                      const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,

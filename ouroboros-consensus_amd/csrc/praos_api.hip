@@ -184,6 +184,10 @@ struct praos_ctx {
                                                        // PRAOS_KEY4 1 / 0, -1 below ILP4_BATCH (54k: 2.78-2.84
                                                        // -> 2.76-2.77 ms; 108k 4.17 -> 4.21, profiles/r04/n)
   bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < ILP4_BATCH); }
+  int u4 = -1;                                         // cached stage U from the ILP-4 build (PRAOS_U4 1 / 0,
+                                                       // -1 below ILP4_BATCH; 54k 2.79 -> 2.75 ms, 108k 3.87-3.92
+                                                       // -> 3.81-3.83, profiles/r04/hh)
+  bool use_u4(size_t n) const { return u4 > 0 || (u4 < 0 && n < ILP4_BATCH); }
   bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < ILP4_BATCH); }
   int v_ilp4(size_t n) const {
     const bool on = vrf_ilp4 == 1 || (vrf_ilp4 > 1 && n < (size_t)vrf_ilp4);
@@ -544,6 +548,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_U4")) c->u4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_POOL_KEYS")) c->pool_keys = std::atoi(e);   // (the option's default)
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
@@ -1284,7 +1289,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
     keycache_precompute(k, b->vrf_vk, 1, sv);
     launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
-                 b->vrf_proof, b->tab_vrfu, b->vrf_mid);
+                 b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n));
     if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     vrf_keys_queued = true;
     return PRAOS_OK;
@@ -1430,7 +1435,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       keycache_precompute(k, b->vrf_vk, 1, sv);
       for (int q = 0; q < 2; q++)
         launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
-                     proof[q], b->tab_vrfu, mid[q]);
+                     proof[q], b->tab_vrfu, mid[q], c->use_u4(n));
       if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     } else {
       for (int q = 0; q < 2; q++)
