@@ -63,6 +63,17 @@ void launch_key_precompute4(int kind, hipStream_t stream, const uint32_t* counte
 void launch_pkey_publish(hipStream_t stream, const uint32_t* counters, const uint32_t* base, uint32_t max_entries,
                          const uint32_t* entry_rep, const uint8_t* keys, int32_t* pentry, uint32_t* pkey,
                          uint32_t pmask, uint32_t* count, uint32_t span);
+// the cached verifies of a small batch from the ILP-4 build (k_miss4.hip)
+void launch_ocert_ck4(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                      const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                      const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
+                      const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo,
+                      uint16_t* bits, uint8_t* ok_out);
+void launch_kes_ck4(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
+                    const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
+                    const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off, const uint32_t* body_len,
+                    const uint8_t* body, size_t body_bytes_len, const uint64_t* slot, const uint64_t* ocert_c0,
+                    uint64_t slots_per_kes_period, uint16_t* bits);
 // the uncached verifies of a small batch from the ILP-4 build (k_miss4.hip), list mode only
 void launch_ocert4(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* list, const uint32_t* count,
                    const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n,

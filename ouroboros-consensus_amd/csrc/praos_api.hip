@@ -187,6 +187,9 @@ struct praos_ctx {
   int u4 = -1;                                         // cached stage U from the ILP-4 build (PRAOS_U4 1 / 0,
                                                        // -1 below ILP4_BATCH; 54k 2.79 -> 2.75 ms, 108k 3.87-3.92
                                                        // -> 3.81-3.83, profiles/r04/hh)
+  int ck4 = 0;                                         // cached OCert / KES verifies from the ILP-4 build
+                                                       // (PRAOS_CK4 1 / 0, -1 below ILP4_BATCH)
+  bool use_ck4(size_t n) const { return ck4 > 0 || (ck4 < 0 && n < ILP4_BATCH); }
   bool use_u4(size_t n) const { return u4 > 0 || (u4 < 0 && n < ILP4_BATCH); }
   bool use_miss4(size_t n) const { return miss4 > 0 || (miss4 < 0 && n < ILP4_BATCH); }
   int v_ilp4(size_t n) const {
@@ -549,6 +552,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_U4")) c->u4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_CK4")) c->ck4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_POOL_KEYS")) c->pool_keys = std::atoi(e);   // (the option's default)
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
@@ -1323,9 +1327,14 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                        b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
-                      b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
-                      P.max_kes_evo, bo, b->dd_ok);
+      if (c->use_ck4(n))
+        launch_ocert_ck4(so, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk, b->hot_vk,
+                         b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
+                         b->dd_ok);
+      else
+        launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
+                        b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
+                        P.max_kes_evo, bo, b->dd_ok);
     } else {
       launch_ocert(g, blk, so, n, b->dd_reps, b->dd_counters, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                    b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
@@ -1359,9 +1368,14 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                        (uint8_t*)nullptr, b->tab_ocert);
       };
       keycache_precompute(k, b->cold_vk, 0, so);
-      launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
-                      b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
-                      P.max_kes_evo, bo, (uint8_t*)nullptr);
+      if (c->use_ck4(n))
+        launch_ocert_ck4(so, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk, b->hot_vk,
+                         b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
+                         (uint8_t*)nullptr);
+      else
+        launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
+                        b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
+                        P.max_kes_evo, bo, (uint8_t*)nullptr);
     } else {
       launch_ocert(g, blk, so, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk,
                    b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo,
@@ -1396,10 +1410,15 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
                                b->ocert_c0, P.slots_per_kes_period, k.rep_ok);
       keycache_precompute(k, b->kes_leaf, 0, sk);
       HIPCHK(c, hipEventRecord(c->kc0_ev, sk));
-      launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
-                    b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
-                    P.slots_per_kes_period, bk, c->kes_pair_min(), c->kes_dedup ? k.entry_rep : nullptr,
-                    c->kes_dedup ? k.rep_ok : nullptr);
+      if (c->use_ck4(n) && !c->kes_pair_min() && !c->kes_dedup)
+        launch_kes_ck4(sk, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
+                       b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
+                       P.slots_per_kes_period, bk);
+      else
+        launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
+                      b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
+                      P.slots_per_kes_period, bk, c->kes_pair_min(), c->kes_dedup ? k.entry_rep : nullptr,
+                      c->kes_dedup ? k.rep_ok : nullptr);
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
       c->kes_ck_timed = true;
     } else {
