@@ -686,6 +686,18 @@ def main():
                                             body_corrupted=(corrupted == 5) if args.config == "tp" else None)
         line["cpu_baseline"]["openssl_ed25519_verify_per_s_1core"] = openssl_ed25519_rate()
         line["gpu_vs_cpu"] = round(value / line["cpu_baseline"]["value"], 1)
+        # north_star's ratio is against the reference's ALL-host-core CPU rate: the twin's single-core
+        # rate x the host's cores (a linear, i.e. optimistic-for-the-CPU, estimate), at N = 1 and for
+        # configs[4] as stated -- one epoch split over 8 GPUs -- from the one-GPU proxy of the 1/8 shard
+        allc = line["cpu_baseline"].get("all_cores_linear_estimate")
+        if allc:
+            line["gpu_vs_cpu_all_cores"] = round(value / allc, 1)
+            if proxy and "n8" in proxy:
+                line["projected_8gpu_strong"] = {
+                    "value": round(8 * proxy["n8"]["value"], 1),
+                    "vs_cpu_all_cores": round(8 * proxy["n8"]["value"] / allc, 1),
+                    "note": "8 x strong_proxy.n8.value (each GPU validating its contiguous 1/8 of the epoch, no "
+                            "exchange) / cpu_baseline.all_cores_linear_estimate"}
     print(json.dumps(line), flush=True)
     ctx.close()
     if dist:

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 12
+#define PRAOS_ABI_VERSION 13
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -669,6 +669,24 @@ int praos_group_verify_header_bytes(praos_group* g, const praos_header_bytes* in
 int praos_group_verify_tpraos_headers(praos_group* g, const praos_tpraos_headers* h, praos_tpraos_out* out);
 int praos_group_verify_tpraos_header_bytes(praos_group* g, const praos_header_bytes* in, praos_tpraos_out* out,
                                            praos_decoded* dec, uint8_t* leader_out, uint8_t* leader_proof);
+/* ABI 13.  A caller buffer page-locked once for every member (the Haskell arena of an epoch:
+ * each member's shard uploads by direct DMA), and the ImmutableDB replay over the group
+ * (db-analyser's processAllImmutableDB, DBAnalyser/Analysis.hs:815-847, on several GPUs):
+ * consecutive batches are dealt to the members in turn, the nonce chain and the fold
+ * (envelope + updateChainDepState) run once in chain order on member 0; arguments, outputs,
+ * stop and resume exactly as praos_replay_immutable[_tpraos] on one context. */
+int praos_group_set_overlay(praos_group* g, const praos_overlay* ov);   /* praos_set_overlay on every member */
+int praos_group_host_register(praos_group* g, void* p, size_t len);
+int praos_group_host_unregister(praos_group* g, void* p);
+int praos_group_replay_immutable(praos_group* g, const char* dir, const praos_pool* pools, uint32_t npools,
+                                 const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                                 praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
+                                 praos_replay_stats* stats);
+int praos_group_replay_immutable_tpraos(praos_group* g, const char* dir, const praos_pool* pools, uint32_t npools,
+                                        const praos_params* params, const praos_epoch_info* ei,
+                                        const praos_nonce* extra_entropy, praos_envelope* env, praos_chain_state* st,
+                                        size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
+                                        praos_replay_stats* stats);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

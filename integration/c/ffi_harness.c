@@ -30,7 +30,16 @@
  *               allocation -> praos_host_unregister -> praos_validate_headers ->
  *               praos_state_encode; also prints the stopping header's verdict and bits, what
  *               Batch.Errors rebuilds the typed HeaderError from (must agree);
+ *   "typed_group": the same sequence over a praos_group of <threads> members on device 0, as
+ *               validateEpochHeaders runs it on a group context (Batch.hs withPraosBatchDevices):
+ *               praos_group_set_epoch -> praos_group_host_register -> praos_group_verify_header_bytes
+ *               -> praos_group_host_unregister -> praos_validate_headers on member 0 (must agree);
+ *   "binding_group" (TPraos): the TPraos sequence with praos_group_verify_tpraos_header_bytes;
  *   "replay":   praos_replay_immutable over the same directory (must agree);
+ *   "replay_group": praos_group_replay_immutable[_tpraos] over <threads> members (must agree);
+ *   TPraos phases also print the stopping header's PRTCL failure set and the
+ *   SL.ChainTransitionError constructors Batch/Errors.hs tpraosChainTransitionError builds from
+ *   it (the table below mirrors the Haskell one; tests/test_abi.py checks the two agree);
  *   "threads":  the first epoch's headers split over <threads> POSIX threads, each with
  *               its own praos_ctx on device 0, and the same through praos_group_open
  *               with <threads> members: bits / pool_idx / nonce equal to one context's.
@@ -208,10 +217,56 @@ static void print_state(const char* phase, const state_buf* s, const praos_envel
   fflush(stdout);
 }
 
+/* PRAOS_TPF_* -> the PRTCL predicate failure Batch/Errors.hs tpraosChainTransitionError builds,
+ * in the order ValidateAll collects them: OVERLAY's own (NotActiveSlot, or WrongGenesisColdKey
+ * then the first failure of the VRF checks), then those of the OCERT sub-rule in the order
+ * ocertTransition checks them.  (mirrored by the Haskell table;
+ * tests/test_abi.py::test_tpraos_error_table_matches_haskell) */
+static const struct { unsigned bit; const char* name; } TPF_NAMES[] = {
+  {PRAOS_TPF_NOT_ACTIVE, "NotActiveSlotOVERLAY"},
+  {PRAOS_TPF_GEN_COLD, "WrongGenesisColdKeyOVERLAY"},
+  {PRAOS_TPF_VRF_KEY_UNKNOWN, "VRFKeyUnknown"},
+  {PRAOS_TPF_VRF_KEY_WRONG, "VRFKeyWrongVRFKey"},
+  {PRAOS_TPF_GEN_VRF, "WrongGenesisVRFKeyOVERLAY"},
+  {PRAOS_TPF_BAD_NONCE, "VRFKeyBadNonce"},
+  {PRAOS_TPF_BAD_LEADER, "VRFKeyBadLeaderValue"},
+  {PRAOS_TPF_LEADER_TOO_BIG, "VRFLeaderValueTooBig"},
+  {PRAOS_TPF_KES_BEFORE_START, "OcertFailure KESBeforeStartOCERT"},
+  {PRAOS_TPF_KES_AFTER_END, "OcertFailure KESAfterEndOCERT"},
+  {PRAOS_TPF_OCERT_SIG, "OcertFailure InvalidSignatureOCERT"},
+  {PRAOS_TPF_KES_SIG, "OcertFailure InvalidKesSignatureOCERT"},
+  {PRAOS_TPF_COUNTER_MISSING, "OcertFailure NoCounterForKeyHashOCERT"},
+  {PRAOS_TPF_COUNTER_TOO_SMALL, "OcertFailure CounterTooSmallOCERT"},
+  {PRAOS_TPF_COUNTER_OVER_INC, "OcertFailure CounterOverIncrementedOCERT"},
+};
+
+/* the stopping TPraos header's failure set and the ChainTransitionError it stands for */
+static void print_tpraos_stop(unsigned fails) {
+  printf("{\"phase\": \"tpraos_stop\", \"failures\": %u, \"errors\": [", fails);
+  int first = 1;
+  for (size_t k = 0; k < sizeof TPF_NAMES / sizeof TPF_NAMES[0]; k++)
+    if (fails & TPF_NAMES[k].bit) {
+      printf("%s\"OverlayFailure (%s)\"", first ? "" : ", ", TPF_NAMES[k].name);
+      first = 0;
+    }
+  printf("]}\n");
+  fflush(stdout);
+}
+
 /* ---- phase 1: the Haskell binding's call sequence (Batch.hs praosReplayEpochs) ---- */
-static void phase_binding(const chain_t* ch) {
-  praos_ctx* ctx = praos_open(0);
+static void phase_binding(const chain_t* ch, int members) {
+  praos_group* g = NULL;
+  praos_ctx* ctx;
+  if (members > 0) {
+    int devs[64] = {0};
+    g = praos_group_open(devs, members);
+    if (!g) DIE("praos_group_open");
+    ctx = praos_group_ctx(g, 0);
+  } else {
+    ctx = praos_open(0);
+  }
   if (!ctx) DIE("praos_open(0)");
+  unsigned stop_fails = 0;
   static state_buf S;
   genesis_state(&S);
   praos_envelope env = g_env0;
@@ -227,7 +282,12 @@ static void phase_binding(const chain_t* ch) {
     praos_nonce eta;
     if (g_tpraos) CK(ctx, praos_tpraos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &g_extra, &eta));
     else CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
-    CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
+    if (g) {
+      if (praos_group_set_epoch(g, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params) != PRAOS_OK)
+        DIE("%s", praos_group_last_error(g));
+    } else {
+      CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
+    }
     epochs++;
     uint64_t* off = malloc(8 * n);
     for (size_t k = 0; k < n; k++) off[k] = ch->off[i + k];
@@ -252,13 +312,22 @@ static void phase_binding(const chain_t* ch) {
     if (g_tpraos) {
       uint16_t* fails = calloc(n, 2);
       praos_tpraos_out tout = {bits, pidx, NULL, NULL, nonce};
-      CK(ctx, praos_verify_tpraos_header_bytes(ctx, &hb, &tout, &dec, NULL, NULL));
+      if (g) {
+        if (praos_group_verify_tpraos_header_bytes(g, &hb, &tout, &dec, NULL, NULL) != PRAOS_OK)
+          DIE("%s", praos_group_last_error(g));
+      } else {
+        CK(ctx, praos_verify_tpraos_header_bytes(ctx, &hb, &tout, &dec, NULL, NULL));
+      }
       praos_tpraos_headers th;
       memset(&th, 0, sizeof th);
       th.h = h;
       CK(ctx, praos_tpraos_update_chain_dep_state(ctx, &th, prev, gen, &tout, &env, &g_ei, &g_extra, &S.st, verdict,
                                                   fails, &stop, &done));
+      if (stop < n) stop_fails = fails[stop];
       free(fails);
+    } else if (g) {
+      if (praos_group_verify_header_bytes(g, &hb, &out, &dec) != PRAOS_OK) DIE("%s", praos_group_last_error(g));
+      CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
     } else {
       CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
       CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
@@ -272,13 +341,24 @@ static void phase_binding(const chain_t* ch) {
     if (stopped) break;
     i = j;
   }
-  print_state("binding", &S, &env, validated, stop_index, stop_verdict, epochs, -1);
-  praos_close(ctx);
+  print_state(g ? "binding_group" : "binding", &S, &env, validated, stop_index, stop_verdict, epochs, -1);
+  if (g_tpraos && !g && stop_index < ch->n) print_tpraos_stop(stop_fails);
+  if (g) praos_group_close(g);
+  else praos_close(ctx);
 }
 
 /* ---- phase 1b: Batch/Validate.hs validateEpochHeaders (Storable vectors, registered arena) ---- */
-static void phase_typed(const chain_t* ch) {
-  praos_ctx* ctx = praos_open(0);
+static void phase_typed(const chain_t* ch, int members) {
+  praos_group* g = NULL;
+  praos_ctx* ctx;
+  if (members > 0) {
+    int devs[64] = {0};
+    g = praos_group_open(devs, members);
+    if (!g) DIE("praos_group_open");
+    ctx = praos_group_ctx(g, 0);
+  } else {
+    ctx = praos_open(0);
+  }
   if (!ctx) DIE("praos_open(0)");
   static state_buf S;
   genesis_state(&S);
@@ -294,7 +374,12 @@ static void phase_typed(const chain_t* ch) {
     const size_t n = j - i;
     praos_nonce eta;
     CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
-    CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
+    if (g) {
+      if (praos_group_set_epoch(g, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params) != PRAOS_OK)
+        DIE("%s", praos_group_last_error(g));
+    } else {
+      CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
+    }
     epochs++;
     /* the epoch's arena: its header spans back to back (what the binding concatenates) */
     size_t alen = 0;
@@ -319,9 +404,16 @@ static void phase_typed(const chain_t* ch) {
     memset(&dec, 0, sizeof dec);
     dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;
     dec.cold_vk = cold; dec.header_hash = hh; dec.body_size = bsz;
-    CK(ctx, praos_host_register(ctx, arena, alen ? alen : 1));
-    CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
-    CK(ctx, praos_host_unregister(ctx, arena));
+    if (g) {
+      if (praos_group_host_register(g, arena, alen ? alen : 1) != PRAOS_OK ||
+          praos_group_verify_header_bytes(g, &hb, &out, &dec) != PRAOS_OK ||
+          praos_group_host_unregister(g, arena) != PRAOS_OK)
+        DIE("%s", praos_group_last_error(g));
+    } else {
+      CK(ctx, praos_host_register(ctx, arena, alen ? alen : 1));
+      CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
+      CK(ctx, praos_host_unregister(ctx, arena));
+    }
     praos_headers h;
     memset(&h, 0, sizeof h);
     h.n = n; h.slot = slot; h.cold_vk = cold; h.ocert_n = ocn;
@@ -339,18 +431,32 @@ static void phase_typed(const chain_t* ch) {
     if (stopped) break;
     i = j;
   }
-  print_state("typed", &S, &env, validated, stop_index, stop_verdict, epochs, (long)stop_bits);
-  praos_close(ctx);
+  print_state(g ? "typed_group" : "typed", &S, &env, validated, stop_index, stop_verdict, epochs, (long)stop_bits);
+  if (g) praos_group_close(g);
+  else praos_close(ctx);
 }
 
 /* ---- phase 2: the library's own driver ---- */
-static void phase_replay(const char* dir) {
-  praos_ctx* ctx = praos_open(0);
-  if (!ctx) DIE("praos_open(0)");
+static void phase_replay(const char* dir, int members) {
   static state_buf S;
   genesis_state(&S);
   praos_envelope env = g_env0;
   praos_replay_stats rs;
+  if (members > 0) {
+    int devs[64] = {0};
+    praos_group* g = praos_group_open(devs, members);
+    if (!g) DIE("praos_group_open");
+    const int rc = g_tpraos
+        ? praos_group_replay_immutable_tpraos(g, dir, g_pools, g_npools, &g_params, &g_ei, &g_extra, &env, &S.st, 97,
+                                              NULL, NULL, 0, &rs)
+        : praos_group_replay_immutable(g, dir, g_pools, g_npools, &g_params, &g_ei, &env, &S.st, 97, NULL, 0, &rs);
+    if (rc != PRAOS_OK) DIE("group replay -> %d: %s", rc, praos_group_last_error(g));
+    print_state("replay_group", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs, -1);
+    praos_group_close(g);
+    return;
+  }
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) DIE("praos_open(0)");
   if (g_tpraos)
     CK(ctx, praos_replay_immutable_tpraos(ctx, dir, g_pools, g_npools, &g_params, &g_ei, &g_extra, &env, &S.st,
                                           1 << 16, NULL, NULL, 0, &rs));
@@ -438,9 +544,14 @@ int main(int argc, char** argv) {
   read_epoch_file(argv[2]);
   chain_t ch;
   read_chain(argv[1], &ch);
-  phase_binding(&ch);
-  if (!g_tpraos) phase_typed(&ch);
-  phase_replay(argv[1]);
-  if (!g_tpraos) phase_threads(&ch, atoi(argv[3]));
+  const int T = atoi(argv[3]);
+  if (T < 1 || T > 64) DIE("threads: 1..64");
+  phase_binding(&ch, 0);
+  if (g_tpraos) phase_binding(&ch, T);
+  if (!g_tpraos) phase_typed(&ch, 0);
+  if (!g_tpraos) phase_typed(&ch, T);
+  phase_replay(argv[1], 0);
+  phase_replay(argv[1], T);
+  if (!g_tpraos) phase_threads(&ch, T);
   return 0;
 }

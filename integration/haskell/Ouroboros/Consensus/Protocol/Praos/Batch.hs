@@ -1,5 +1,6 @@
 {-# LANGUAGE DataKinds                #-}
 {-# LANGUAGE ForeignFunctionInterface #-}
+{-# LANGUAGE NamedFieldPuns           #-}
 {-# LANGUAGE ScopedTypeVariables      #-}
 
 -- | Batched Praos header validation on AMD MI355X GPUs (libpraos_hip.so).
@@ -19,9 +20,11 @@
 --
 -- Link: @extra-libraries: praos_hip@ (and @amdhip64@), include-dirs: include/.
 module Ouroboros.Consensus.Protocol.Praos.Batch
-  ( -- * Context
+  ( -- * Context (one GPU, or a group of several)
     PraosBatchCtx
   , withPraosBatchCtx
+  , withPraosBatchDevices
+  , praosBatchMembers
   , PraosBatchError (..)
   , praosSetPoolKeyStore
     -- * Per epoch
@@ -37,7 +40,10 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
     -- * TPraos (Shelley..Alonzo) headers from stored bytes
   , TPraosBatchResult (..)
   , praosTickedEpochNonceTPraos
+  , OverlayC (..)
+  , praosSetOverlay
   , praosValidateTPraosHeaderBytes
+  , praosValidateTPraosHeaderSpans
     -- * Whole ImmutableDB replay (db-analyser)
   , ReplayStats (..)
   , praosReplayImmutable
@@ -46,12 +52,13 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
   , verdictToError
   ) where
 
-import           Control.Exception (Exception, bracket, throwIO)
+import           Control.Exception (Exception, bracket, bracket_, throwIO)
 import           Control.Monad (forM_, when)
 import qualified Data.ByteString as BS
 import qualified Data.ByteString.Unsafe as BSU
 import qualified Data.Vector.Storable as VS
 import qualified Data.Vector.Storable.Mutable as VSM
+import           Data.Ratio (denominator, numerator)
 import           Data.Word (Word16, Word32, Word64, Word8)
 import           Foreign
 import           Foreign.C.String (CString, peekCString, withCString)
@@ -60,6 +67,7 @@ import           Foreign.C.Types (CInt (..), CSize (..))
 -- ---------------------------------------------------------------- C ABI (include/praos_hip.h)
 
 data PraosCtx
+data PraosGroup
 
 -- struct praos_params (40 bytes): slots_per_kes_period@0 max_kes_evo@8 f_is_one@16 vrf_check_output@20 c_raw@24
 -- struct praos_pool (76 bytes): hash28@0 vrf_hash32@28 sigma_fp@60
@@ -108,16 +116,47 @@ foreign import ccall safe "praos_verify_tpraos_header_bytes" c_verify_tpraos_hea
 foreign import ccall safe "praos_tpraos_update_chain_dep_state" c_tpraos_update_chain_dep_state
   :: Ptr PraosCtx -> Ptr () -> Ptr Word8 -> Ptr Word8 -> Ptr () -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
   -> Ptr Word8 -> Ptr Word16 -> Ptr CSize -> Ptr CSize -> IO CInt
+foreign import ccall safe "praos_set_overlay" c_set_overlay :: Ptr PraosCtx -> Ptr () -> IO CInt
+foreign import ccall safe "praos_group_set_overlay" c_group_set_overlay :: Ptr PraosGroup -> Ptr () -> IO CInt
 foreign import ccall safe "praos_replay_immutable_tpraos" c_replay_immutable_tpraos
   :: Ptr PraosCtx -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
   -> CSize -> Ptr Word8 -> Ptr Word16 -> CSize -> Ptr () -> IO CInt
+-- several GPUs (include/praos_hip.h: praos_group_*): shards of one batch, or consecutive
+-- replay batches, on the members; outputs in place; the fold on member 0
+foreign import ccall safe "praos_group_open"  c_group_open  :: Ptr CInt -> CInt -> IO (Ptr PraosGroup)
+foreign import ccall safe "praos_group_close" c_group_close :: Ptr PraosGroup -> IO ()
+foreign import ccall safe "praos_group_size"  c_group_size  :: Ptr PraosGroup -> IO CInt
+foreign import ccall safe "praos_group_ctx"   c_group_ctx   :: Ptr PraosGroup -> CInt -> IO (Ptr PraosCtx)
+foreign import ccall safe "praos_group_last_error" c_group_last_error :: Ptr PraosGroup -> IO CString
+foreign import ccall safe "praos_group_set_option" c_group_set_option :: Ptr PraosGroup -> CInt -> CInt -> IO CInt
+foreign import ccall safe "praos_group_set_epoch" c_group_set_epoch
+  :: Ptr PraosGroup -> Ptr Word8 -> Ptr () -> Word32 -> Ptr () -> IO CInt
+foreign import ccall safe "praos_group_verify_header_bytes" c_group_verify_header_bytes
+  :: Ptr PraosGroup -> Ptr () -> Ptr () -> Ptr () -> IO CInt
+foreign import ccall safe "praos_group_verify_tpraos_header_bytes" c_group_verify_tpraos_header_bytes
+  :: Ptr PraosGroup -> Ptr () -> Ptr () -> Ptr () -> Ptr Word8 -> Ptr Word8 -> IO CInt
+foreign import ccall safe "praos_group_host_register" c_group_host_register
+  :: Ptr PraosGroup -> Ptr Word8 -> CSize -> IO CInt
+foreign import ccall safe "praos_group_host_unregister" c_group_host_unregister
+  :: Ptr PraosGroup -> Ptr Word8 -> IO CInt
+foreign import ccall safe "praos_group_replay_immutable" c_group_replay_immutable
+  :: Ptr PraosGroup -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
+foreign import ccall safe "praos_group_replay_immutable_tpraos" c_group_replay_immutable_tpraos
+  :: Ptr PraosGroup -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> CSize -> Ptr Word8 -> Ptr Word16 -> CSize -> Ptr () -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 12
+abiVersion = 13
 
 -- ---------------------------------------------------------------- context
 
-newtype PraosBatchCtx = PraosBatchCtx (Ptr PraosCtx)
+-- | One GPU (a praos_ctx), or a group of several (a praos_group: one context per device,
+-- batches split into contiguous shards, replay batches dealt to the members in turn) together
+-- with its member 0, on which the sequential fold runs.  Every entry point below takes either.
+data PraosBatchCtx
+  = PraosBatchCtx !(Ptr PraosCtx)
+  | PraosBatchGroup !(Ptr PraosGroup) !(Ptr PraosCtx) !Int
 
 data PraosBatchError = PraosBatchError !Int !String
   deriving Show
@@ -133,19 +172,79 @@ withPraosBatchCtx dev k = do
     when (p == nullPtr) $ throwIO (PraosBatchError (-1) ("praos_open " ++ show dev))
     k (PraosBatchCtx p)
 
+-- | The GPUs of one node as one batch context (SURVEY sec. 8e: an epoch's headers shard by
+-- contiguous slot range, no exchange between devices).  One device is 'withPraosBatchCtx';
+-- several are a praos_group (a device may repeat: several contexts on one GPU).
+withPraosBatchDevices :: [Int] -> (PraosBatchCtx -> IO a) -> IO a
+withPraosBatchDevices [] _ = throwIO (PraosBatchError (-1) "withPraosBatchDevices: no device")
+withPraosBatchDevices [dev] k = withPraosBatchCtx dev k
+withPraosBatchDevices devs k = do
+  v <- c_abi_version
+  when (v /= abiVersion) $ throwIO (PraosBatchError (-2) ("libpraos_hip ABI " ++ show v))
+  let m = length devs
+  bracket (withArray (map fromIntegral devs) $ \dp -> c_group_open dp (fromIntegral m)) c_group_close $ \g -> do
+    when (g == nullPtr) $ throwIO (PraosBatchError (-1) ("praos_group_open " ++ show devs))
+    c0 <- c_group_ctx g 0
+    k (PraosBatchGroup g c0 m)
+
+-- | Devices (contexts) a batch context spreads over.
+praosBatchMembers :: PraosBatchCtx -> Int
+praosBatchMembers (PraosBatchCtx _) = 1
+praosBatchMembers (PraosBatchGroup _ _ m) = m
+
+-- | The context the fold and the codecs run on (member 0 of a group).
+ctxPtr :: PraosBatchCtx -> Ptr PraosCtx
+ctxPtr (PraosBatchCtx p) = p
+ctxPtr (PraosBatchGroup _ p _) = p
+
 -- | PRAOS_OPT_POOL_KEYS (7): keep the cold-key and VRF-key cache entries across calls on
 -- this context (a node validating batch after batch of one epoch sees the same pool keys);
 -- verdicts are identical either way.  On by default inside the replay entry points.
 praosSetPoolKeyStore :: PraosBatchCtx -> Bool -> IO ()
-praosSetPoolKeyStore ctx@(PraosBatchCtx p) on =
-  check ctx (c_set_option p 7 (if on then 1 else 0))
+praosSetPoolKeyStore ctx on = check ctx $ case ctx of
+  PraosBatchCtx p -> c_set_option p 7 (if on then 1 else 0)
+  PraosBatchGroup g _ _ -> c_group_set_option g 7 (if on then 1 else 0)
 
+-- | A batch call's return code: the group's error text for group calls, the context's otherwise.
 check :: PraosBatchCtx -> IO CInt -> IO ()
-check (PraosBatchCtx p) act = do
+check ctx act = do
   rc <- act
   when (rc /= 0) $ do
-    msg <- c_last_error p >>= peekCString
+    msg <- case ctx of
+      PraosBatchCtx p -> c_last_error p >>= peekCString
+      PraosBatchGroup g _ _ -> c_group_last_error g >>= peekCString
     throwIO (PraosBatchError (fromIntegral rc) msg)
+
+-- | A call on one context (the fold on member 0 of a group).
+checkCtx :: Ptr PraosCtx -> IO CInt -> IO ()
+checkCtx p = check (PraosBatchCtx p)
+
+-- | praos_verify_header_bytes, or its group form (shards on the members, outputs in place).
+verifyHeaderBytes :: PraosBatchCtx -> Ptr () -> Ptr () -> Ptr () -> IO ()
+verifyHeaderBytes ctx hb out dec = check ctx $ case ctx of
+  PraosBatchCtx p -> c_verify_header_bytes p hb out dec
+  PraosBatchGroup g _ _ -> c_group_verify_header_bytes g hb out dec
+
+verifyTPraosHeaderBytes :: PraosBatchCtx -> Ptr () -> Ptr () -> Ptr () -> IO ()
+verifyTPraosHeaderBytes ctx hb out dec = check ctx $ case ctx of
+  PraosBatchCtx p -> c_verify_tpraos_header_bytes p hb out dec nullPtr nullPtr
+  PraosBatchGroup g _ _ -> c_group_verify_tpraos_header_bytes g hb out dec nullPtr nullPtr
+
+-- | The arena page-locked for the duration of the action when it is 64 MiB or more
+-- (praos_host_register: the upload goes by direct DMA, no staging copy; a group pins it
+-- once for every member).  The unregister runs whatever the action throws (a failing
+-- batch call), so a GHC-owned buffer is never freed while still page-locked.
+withRegisteredArena :: PraosBatchCtx -> Ptr Word8 -> Int -> IO a -> IO a
+withRegisteredArena ctx ap alen act
+  | alen < 64 * 1024 * 1024 = act
+  | otherwise = bracket_ reg unreg act
+  where
+    reg = check ctx $ case ctx of
+      PraosBatchCtx p -> c_host_register p ap (fromIntegral alen)
+      PraosBatchGroup g _ _ -> c_group_host_register g ap (fromIntegral alen)
+    unreg = check ctx $ case ctx of
+      PraosBatchCtx p -> c_host_unregister p ap
+      PraosBatchGroup g _ _ -> c_group_host_unregister g ap
 
 -- ---------------------------------------------------------------- marshalling helpers
 
@@ -215,11 +314,15 @@ peekNonce p off = do
 -- the PoolDistr of the ledger view and the protocol parameters.
 praosSetEpoch :: PraosBatchCtx -> Maybe BS.ByteString -> [(BS.ByteString, BS.ByteString, Integer)]
               -> PraosParamsC -> IO ()
-praosSetEpoch ctx@(PraosBatchCtx p) eta0 pools pp =
+praosSetEpoch ctx eta0 pools pp =
   withPools pools $ \pp' np -> withParams pp $ \par ->
     case eta0 of
-      Nothing -> check ctx (c_set_epoch p nullPtr pp' np par)
-      Just e  -> BSU.unsafeUseAsCString e $ \ep -> check ctx (c_set_epoch p (castPtr ep) pp' np par)
+      Nothing -> set nullPtr pp' np par
+      Just e  -> BSU.unsafeUseAsCString e $ \ep -> set (castPtr ep) pp' np par
+  where
+    set ep pp' np par = check ctx $ case ctx of
+      PraosBatchCtx p -> c_set_epoch p ep pp' np par
+      PraosBatchGroup g _ _ -> c_group_set_epoch g ep pp' np par
 
 -- | The serialised PraosState (Praos.hs:274-310) the fold reads and writes; the ABI
 -- takes the same CBOR through praos_state_encode / praos_state_decode, so the Haskell
@@ -280,7 +383,7 @@ type EnvLimits = (Word64, Word64, Word64, Word64)
 praosValidateHeaderBytes :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
                          -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> [BS.ByteString]
                          -> IO BatchResult
-praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor hdrs = do
+praosValidateHeaderBytes ctx ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor hdrs = do
   let n = length hdrs
       arena = BS.concat hdrs
       lens = map BS.length hdrs
@@ -305,7 +408,7 @@ praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
       fillBytes dec 0 168
       pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
       pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
-      check ctx (c_verify_header_bytes p (castPtr hb) (castPtr out) (castPtr dec))
+      verifyHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
       -- praos_headers: n, slot, cold_vk, ocert_n are what the fold reads
       fillBytes hv 0 120
       pokeByteOff hv 0 (fromIntegral n :: CSize) >> pokeByteOff hv 8 slot >> pokeByteOff hv 16 cold
@@ -317,7 +420,8 @@ praosValidateHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
         Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
       pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
       pokeByteOff env 112 maxBS
-      check ctx (c_validate_headers p (castPtr hv) prev gen (castPtr out) (castPtr env) eip st verdict stopp donep)
+      checkCtx (ctxPtr ctx) (c_validate_headers (ctxPtr ctx) (castPtr hv) prev gen (castPtr out) (castPtr env) eip st
+                                                verdict stopp donep)
       stop <- peek stopp
       vs <- peekArray n verdict
       bs <- peekArray n bits
@@ -348,7 +452,7 @@ praosValidateHeaderSpans :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) ->
                          -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> BS.ByteString
                          -> VS.Vector Word64 -> VS.Vector Word32 -> VSM.IOVector Word8 -> VSM.IOVector Word16
                          -> IO SpanResult
-praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor arena offs lens
+praosValidateHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor arena offs lens
                          verdicts bits = do
   let n = VS.length offs
   when (VS.length lens /= n || VSM.length verdicts /= n || VSM.length bits /= n) $
@@ -373,7 +477,6 @@ praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
           bsz = decbuf `plusPtr` (120 * n) :: Ptr Word32
           gen = decbuf `plusPtr` (124 * n) :: Ptr Word8
           nonce = decbuf `plusPtr` (125 * n) :: Ptr Word8
-          big = alen >= 64 * 1024 * 1024
       pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
       pokeByteOff hb 16 (fromIntegral alen :: CSize)
       pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
@@ -381,9 +484,7 @@ praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
       fillBytes dec 0 168
       pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
       pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
-      when big $ check ctx (c_host_register p (castPtr ap) (fromIntegral alen))
-      check ctx (c_verify_header_bytes p (castPtr hb) (castPtr out) (castPtr dec))
-      when big $ check ctx (c_host_unregister p (castPtr ap))
+      withRegisteredArena ctx (castPtr ap) alen $ verifyHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
       fillBytes hv 0 120
       pokeByteOff hv 0 (fromIntegral n :: CSize) >> pokeByteOff hv 8 slot >> pokeByteOff hv 16 cold
       pokeByteOff hv 56 ocn
@@ -394,7 +495,8 @@ praosValidateHeaderSpans ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS)
         Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
       pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
       pokeByteOff env 112 maxBS
-      check ctx (c_validate_headers p (castPtr hv) prev gen (castPtr out) (castPtr env) eip st verdict stopp donep)
+      checkCtx (ctxPtr ctx) (c_validate_headers (ctxPtr ctx) (castPtr hv) prev gen (castPtr out) (castPtr env) eip st
+                                                verdict stopp donep)
       stop <- peek stopp
       st' <- encodeChainState st
       origin :: Int32 <- peekByteOff env 32
@@ -419,6 +521,38 @@ praosTickedEpochNonceTPraos stateCbor ei slot extra =
     when (rc /= 0) $ throwIO (PraosBatchError (fromIntegral rc) "praos_tpraos_ticked_epoch_nonce")
     peekNonce out 0
 
+-- | The decentralisation overlay of a TPraos ledger view (praos_overlay): d = lvD, f =
+-- activeSlotVal, the fixed-size epoch layout, and lvGenDelegs as (genesis key hash, delegate
+-- cold-key hash, delegate VRF key hash) triples.
+data OverlayC = OverlayC
+  { ovD           :: !Rational
+  , ovF           :: !Rational
+  , ovEpochBase   :: !Word64
+  , ovEpochLength :: !Word64
+  , ovGenDelegs   :: ![(BS.ByteString, BS.ByteString, BS.ByteString)]
+  }
+
+-- | praos_set_overlay (every member of a group): Nothing = no overlay (d = 0).
+-- struct praos_gen_deleg (88 bytes): genesis_hash28@0 delegate_hash28@28 vrf_hash32@56
+-- struct praos_overlay (64 bytes): d_num@0 d_den@8 asc_num@16 asc_den@24 epoch_base_slot@32 epoch_length@40 gen_delegs@48 n_gen_delegs@56
+praosSetOverlay :: PraosBatchCtx -> Maybe OverlayC -> IO ()
+praosSetOverlay ctx Nothing = check ctx $ case ctx of
+  PraosBatchCtx p -> c_set_overlay p nullPtr
+  PraosBatchGroup g _ _ -> c_group_set_overlay g nullPtr
+praosSetOverlay ctx (Just OverlayC {ovD, ovF, ovEpochBase, ovEpochLength, ovGenDelegs}) =
+  allocaBytes (88 * max 1 (length ovGenDelegs)) $ \gd -> allocaBytes 64 $ \ov -> do
+    forM_ (zip [0 ..] ovGenDelegs) $ \(i, (gk, dk, vrf)) -> do
+      let q = gd `plusPtr` (88 * i)
+      pokeBS q 0 gk >> pokeBS q 28 dk >> pokeBS q 56 vrf
+    fillBytes ov 0 64
+    pokeByteOff ov 0 (fromIntegral (numerator ovD) :: Word64) >> pokeByteOff ov 8 (fromIntegral (denominator ovD) :: Word64)
+    pokeByteOff ov 16 (fromIntegral (numerator ovF) :: Word64) >> pokeByteOff ov 24 (fromIntegral (denominator ovF) :: Word64)
+    pokeByteOff ov 32 ovEpochBase >> pokeByteOff ov 40 ovEpochLength
+    pokeByteOff ov 48 gd >> pokeByteOff ov 56 (fromIntegral (length ovGenDelegs) :: Word32)
+    check ctx $ case ctx of
+      PraosBatchCtx p -> c_set_overlay p (castPtr ov)
+      PraosBatchGroup g _ _ -> c_group_set_overlay g (castPtr ov)
+
 -- | One epoch's stored TPraos headers validated (TPraos.updateChainDepState over the
 -- batch, TPraos.hs:378-387, with the envelope): verdicts (PRAOS_V_OK / _ENV_* / _INPUT /
 -- PRAOS_V_TPRAOS), the PRTCL predicate-failure set of each header (PRAOS_TPF_*), the chain
@@ -439,7 +573,7 @@ data TPraosBatchResult = TPraosBatchResult
 praosValidateTPraosHeaderBytes :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
                                -> Maybe BS.ByteString -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString
                                -> [BS.ByteString] -> IO TPraosBatchResult
-praosValidateTPraosHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor hdrs = do
+praosValidateTPraosHeaderBytes ctx ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor hdrs = do
   let n = length hdrs
       arena = BS.concat hdrs
       lens = map BS.length hdrs
@@ -466,7 +600,7 @@ praosValidateTPraosHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, 
       fillBytes dec 0 168
       pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
       pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
-      check ctx (c_verify_tpraos_header_bytes p (castPtr hb) (castPtr out) (castPtr dec) nullPtr nullPtr)
+      verifyTPraosHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
       -- praos_tpraos_headers: h = praos_headers (n, slot, cold_vk, ocert_n read by the fold)
       fillBytes th 0 136
       pokeByteOff th 0 (fromIntegral n :: CSize) >> pokeByteOff th 8 slot >> pokeByteOff th 16 cold
@@ -479,8 +613,8 @@ praosValidateTPraosHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, 
       pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
       pokeByteOff env 112 maxBS
       pokeNonce xe 0 extra
-      check ctx (c_tpraos_update_chain_dep_state p (castPtr th) prev gen (castPtr out) (castPtr env) eip
-                                                 (castPtr xe) st verdict fails stopp donep)
+      checkCtx (ctxPtr ctx) (c_tpraos_update_chain_dep_state (ctxPtr ctx) (castPtr th) prev gen (castPtr out)
+                                                             (castPtr env) eip (castPtr xe) st verdict fails stopp donep)
       stop <- peek stopp
       vs <- peekArray n verdict
       fs <- peekArray n fails
@@ -494,6 +628,67 @@ praosValidateTPraosHeaderBytes ctx@(PraosBatchCtx p) ei (maxPV, pvMajor, maxHS, 
         pure (Just (s, b, h))
       pure (TPraosBatchResult vs fs bs (fromIntegral stop) st' tip')
 
+-- | 'praosValidateTPraosHeaderBytes' over Storable vectors (as 'praosValidateHeaderSpans'):
+-- verdicts (PRAOS_V_*), PRTCL failure sets (PRAOS_TPF_*) and check bits written into the
+-- caller's vectors.  The epoch must have been installed with 'praosSetEpoch' under
+-- 'praosTickedEpochNonceTPraos''s nonce.
+praosValidateTPraosHeaderSpans :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits -> Maybe BS.ByteString
+                               -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> BS.ByteString
+                               -> VS.Vector Word64 -> VS.Vector Word32 -> VSM.IOVector Word8 -> VSM.IOVector Word16
+                               -> VSM.IOVector Word16 -> IO SpanResult
+praosValidateTPraosHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor arena offs lens verdicts
+                               failures bits = do
+  let n = VS.length offs
+  when (VS.length lens /= n || VSM.length verdicts /= n || VSM.length failures /= n || VSM.length bits /= n) $
+    throwIO (PraosBatchError (-1) "praosValidateTPraosHeaderSpans: vector lengths differ")
+  BSU.unsafeUseAsCStringLen arena $ \(ap, alen) ->
+    VS.unsafeWith offs $ \offp -> VS.unsafeWith lens $ \lenp ->
+    VSM.unsafeWith verdicts $ \verdict -> VSM.unsafeWith failures $ \fails -> VSM.unsafeWith bits $ \bitp ->
+    allocaBytes 40 $ \hb -> allocaArray n $ \(pidx :: Ptr Int32) ->
+    allocaBytes (157 * n) $ \decbuf ->      -- the decoded fields the fold reads (praosValidateHeaderSpans)
+    allocaBytes 168 $ \dec -> allocaBytes 40 $ \out -> allocaBytes 136 $ \th -> allocaBytes 120 $ \env ->
+    allocaBytes 36 $ \xe -> alloca $ \stopp -> alloca $ \donep ->
+    withChainState stateCbor (n + 65536) $ \st -> withEpochInfo ei $ \eip -> do
+      let slot = decbuf :: Ptr Word64
+          bno = decbuf `plusPtr` (8 * n) :: Ptr Word64
+          ocn = decbuf `plusPtr` (16 * n) :: Ptr Word64
+          prev = decbuf `plusPtr` (24 * n) :: Ptr Word8
+          cold = decbuf `plusPtr` (56 * n) :: Ptr Word8
+          hh = decbuf `plusPtr` (88 * n) :: Ptr Word8
+          bsz = decbuf `plusPtr` (120 * n) :: Ptr Word32
+          gen = decbuf `plusPtr` (124 * n) :: Ptr Word8
+          nonce = decbuf `plusPtr` (125 * n) :: Ptr Word8
+      pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
+      pokeByteOff hb 16 (fromIntegral alen :: CSize)
+      pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
+      fillBytes out 0 40 >> pokeByteOff out 0 bitp >> pokeByteOff out 8 pidx >> pokeByteOff out 32 nonce
+      fillBytes dec 0 168
+      pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
+      pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
+      withRegisteredArena ctx (castPtr ap) alen $ verifyTPraosHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
+      fillBytes th 0 136
+      pokeByteOff th 0 (fromIntegral n :: CSize) >> pokeByteOff th 8 slot >> pokeByteOff th 16 cold
+      pokeByteOff th 56 ocn
+      fillBytes env 0 120
+      pokeByteOff env 0 bno >> pokeByteOff env 8 hh >> pokeByteOff env 16 lenp >> pokeByteOff env 24 bsz
+      case tip of
+        Nothing -> pokeByteOff env 32 (1 :: Int32)
+        Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+      pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
+      pokeByteOff env 112 maxBS
+      pokeNonce xe 0 extra
+      checkCtx (ctxPtr ctx) (c_tpraos_update_chain_dep_state (ctxPtr ctx) (castPtr th) prev gen (castPtr out)
+                                                             (castPtr env) eip (castPtr xe) st verdict fails stopp donep)
+      stop <- peek stopp
+      st' <- encodeChainState st
+      origin :: Int32 <- peekByteOff env 32
+      tip' <- if origin /= 0 then pure Nothing else do
+        s <- peekByteOff env 40
+        b <- peekByteOff env 48
+        h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+        pure (Just (s, b, h))
+      pure (SpanResult (fromIntegral stop) st' tip')
+
 -- ---------------------------------------------------------------- ImmutableDB replay
 
 data ReplayStats = ReplayStats
@@ -505,12 +700,14 @@ data ReplayStats = ReplayStats
 -- | praos_replay_immutable: the header-validation pass of db-analyser over an ImmutableDB
 -- directory (chunk + secondary index files), from the given state and tip (Nothing =
 -- Origin; otherwise a block of the database to resume after).  Returns the statistics,
--- the final PraosState CBOR and tip.
+-- the final PraosState CBOR and tip.  On a group context (praos_group_replay_immutable)
+-- consecutive batches go to the members in turn; the nonce chain and the fold stay single,
+-- in chain order, so the result is the one-GPU replay's.
 praosReplayImmutable :: PraosBatchCtx -> FilePath -> [(BS.ByteString, BS.ByteString, Integer)] -> PraosParamsC
                      -> (Word64, Word64, Word64, Word64) -> EnvLimits -> Maybe (Word64, Word64, BS.ByteString)
                      -> BS.ByteString -> Int
                      -> IO (ReplayStats, BS.ByteString, Maybe (Word64, Word64, BS.ByteString))
-praosReplayImmutable ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor batchMax =
+praosReplayImmutable ctx dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor batchMax =
   withCString dir $ \cdir -> withPools pools $ \pp' np -> withParams pp $ \par ->
   withEpochInfo ei $ \eip -> withChainState stateCbor 65536 $ \st ->
   allocaBytes 120 $ \env -> allocaBytes 80 $ \rs -> do
@@ -520,8 +717,11 @@ praosReplayImmutable ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxH
       Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
     pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
     pokeByteOff env 112 maxBS
-    check ctx (c_replay_immutable p cdir pp' np par eip (castPtr env) st (fromIntegral batchMax) nullPtr 0
-                                  (castPtr rs))
+    check ctx $ case ctx of
+      PraosBatchCtx p -> c_replay_immutable p cdir pp' np par eip (castPtr env) st (fromIntegral batchMax) nullPtr 0
+                                            (castPtr rs)
+      PraosBatchGroup g _ _ -> c_group_replay_immutable g cdir pp' np par eip (castPtr env) st (fromIntegral batchMax)
+                                                        nullPtr 0 (castPtr rs)
     stats <- ReplayStats <$> peekByteOff rs 0 <*> peekByteOff rs 8 <*> peekByteOff rs 16 <*> peekByteOff rs 24
                          <*> peekByteOff rs 32 <*> peekByteOff rs 36 <*> peekByteOff rs 40 <*> peekByteOff rs 44
                          <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64 <*> peekByteOff rs 72
@@ -541,7 +741,7 @@ praosReplayImmutableTPraos :: PraosBatchCtx -> FilePath -> [(BS.ByteString, BS.B
                            -> (Word64, Word64, Word64, Word64) -> EnvLimits -> Maybe BS.ByteString
                            -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> Int -> Int
                            -> IO (ReplayStats, [Word8], [Word16], BS.ByteString, Maybe (Word64, Word64, BS.ByteString))
-praosReplayImmutableTPraos ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor
+praosReplayImmutableTPraos ctx dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor
                            batchMax cap =
   withCString dir $ \cdir -> withPools pools $ \pp' np -> withParams pp $ \par ->
   withEpochInfo ei $ \eip -> withChainState stateCbor 65536 $ \st ->
@@ -554,8 +754,12 @@ praosReplayImmutableTPraos ctx@(PraosBatchCtx p) dir pools pp ei (maxPV, pvMajor
     pokeByteOff env 88 maxPV >> pokeByteOff env 96 pvMajor >> pokeByteOff env 104 maxHS
     pokeByteOff env 112 maxBS
     pokeNonce xe 0 extra
-    check ctx (c_replay_immutable_tpraos p cdir pp' np par eip (castPtr xe) (castPtr env) st (fromIntegral batchMax)
-                                         verdicts fails (fromIntegral cap) (castPtr rs))
+    check ctx $ case ctx of
+      PraosBatchCtx p -> c_replay_immutable_tpraos p cdir pp' np par eip (castPtr xe) (castPtr env) st
+                                                   (fromIntegral batchMax) verdicts fails (fromIntegral cap) (castPtr rs)
+      PraosBatchGroup g _ _ -> c_group_replay_immutable_tpraos g cdir pp' np par eip (castPtr xe) (castPtr env) st
+                                                               (fromIntegral batchMax) verdicts fails
+                                                               (fromIntegral cap) (castPtr rs)
     stats <- ReplayStats <$> peekByteOff rs 0 <*> peekByteOff rs 8 <*> peekByteOff rs 16 <*> peekByteOff rs 24
                          <*> peekByteOff rs 32 <*> peekByteOff rs 36 <*> peekByteOff rs 40 <*> peekByteOff rs 44
                          <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64 <*> peekByteOff rs 72

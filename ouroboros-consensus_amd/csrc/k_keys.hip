@@ -211,6 +211,21 @@ __global__ void k_pkey_publish(const uint32_t* __restrict__ counters, const uint
   }
 }
 
+// Before a run that uses the store: empty it when asked (force) or when the last run left it more
+// than `limit` entries.  The decision is made on the device from the count that run published
+// (count[0]), into count[1], so the host never reads a count whose copy may still be in flight.
+__global__ void k_pkey_decide(uint32_t* count, uint32_t limit, int force) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t r = (force || count[0] > limit) ? 1u : 0u;
+    count[1] = r;
+    if (r) count[0] = 0;
+  }
+}
+__global__ void k_pkey_clear(const uint32_t* __restrict__ count, int32_t* pentry, uint32_t slots) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < slots && count[1]) pentry[i] = -1;
+}
+
 // ---- OCert signature dedup (PRAOS_OPT_DEDUP)
 // The OCert signature check depends only on (cold vk, hot vk, n, c0, sigma)
 // (Praos.hs:580): every header a pool forges under one operational certificate
@@ -310,6 +325,10 @@ void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counter
   const size_t lanes = (size_t)span * KT_CHUNKS;
   hipLaunchKernelGGL(k_key_tables, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream, kind, counters,
                      max_entries, ktab, wave_prio, base);
+}
+void launch_pkey_reset(hipStream_t stream, uint32_t* count, int32_t* pentry, uint32_t slots, uint32_t limit, int force) {
+  hipLaunchKernelGGL(k_pkey_decide, dim3(1), dim3(64), 0, stream, count, limit, force);
+  hipLaunchKernelGGL(k_pkey_clear, dim3((slots + 255) / 256), dim3(256), 0, stream, count, pentry, slots);
 }
 void launch_pkey_publish(hipStream_t stream, const uint32_t* counters, const uint32_t* base, uint32_t max_entries,
                          const uint32_t* entry_rep, const uint8_t* keys, int32_t* pentry, uint32_t* pkey,

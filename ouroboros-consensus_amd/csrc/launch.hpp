@@ -60,6 +60,7 @@ void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counter
 void launch_key_precompute4(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                             const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
                             int wave_prio, const uint32_t* base, uint32_t span);
+void launch_pkey_reset(hipStream_t stream, uint32_t* count, int32_t* pentry, uint32_t slots, uint32_t limit, int force);
 void launch_pkey_publish(hipStream_t stream, const uint32_t* counters, const uint32_t* base, uint32_t max_entries,
                          const uint32_t* entry_rep, const uint8_t* keys, int32_t* pentry, uint32_t* pkey,
                          uint32_t pmask, uint32_t* count, uint32_t span);

@@ -233,13 +233,17 @@ struct praos_ctx {
     uint32_t* kinfo = nullptr;
     int32_t* pentry = nullptr;
     ge_cached* ktab = nullptr;
-    uint32_t* count_h = nullptr;                        // pinned: *count after the last run (reset heuristic)
-  } pks[2];
+  } pks[3];                                            // [2] KES leaf keys: the stored-bytes pipeline's prefill
   int pool_keys = -1;                                  // 1 on, 0 off, -1 on inside praos_replay_immutable*
   bool replaying = false;
   bool pk_on = false;                                  // this run uses the store
-  bool pk_reset = false;                               // empty the store before the next run
-  bool pk_reset_run = false;
+  bool pk_reset[3] = {false, false, false};            // empty store t before the next run that uses it
+  // stored-bytes pipeline (praos_verify_header_bytes): each landed chunk's cold, KES leaf and VRF
+  // keys go into the stores and get their tables at once (PRAOS_E2E_PREFILL 1 / 0); the batch run
+  // after the last chunk finds them stored.  The stores are emptied at the start of every call
+  // unless PRAOS_OPT_POOL_KEYS is on, so each call builds its own tables.
+  int e2e_prefill = 1;
+  bool prefill = false;                                // inside such a call: every cache on its store
   // epoch
   bool have_epoch = false;
   praos_params params{};
@@ -554,12 +558,13 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_U4")) c->u4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_CK4")) c->ck4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
-  if (const char* e = std::getenv("PRAOS_POOL_KEYS")) c->pool_keys = std::atoi(e);   // (the option's default)
+  if (const char* e = std::getenv("PRAOS_POOL_KEYS")) (void)praos_set_option(c, PRAOS_OPT_POOL_KEYS, std::atoi(e));
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
+  if (const char* e = std::getenv("PRAOS_E2E_PREFILL")) c->e2e_prefill = std::atoi(e);
   (void)hipEventCreate(&c->v1_ev);
   (void)hipEventCreate(&c->kc0_ev);
   (void)hipEventCreate(&c->kc1_ev);
@@ -667,7 +672,6 @@ void praos_close(praos_ctx* c) {
     for (void* q : {(void*)ps.pkey, (void*)ps.count, (void*)ps.base, (void*)ps.entry_rep, (void*)ps.entry_pos,
                     (void*)ps.kinfo, (void*)ps.pentry, (void*)ps.ktab})
       (void)hipFree(q);
-    if (ps.count_h) (void)hipHostFree(ps.count_h);
   }
   free_spare(c);
   c->pool.reset();
@@ -1064,13 +1068,17 @@ int praos_batch_run(praos_ctx* c, praos_batch* b) {
 }
 
 // key cache prepass over items [0, n) (or list[0 .. *count)): hash set, entries, hit/miss lists
-// the pool-key store t (cold 0, VRF 1): 32,768 slots, 16,384 entries
-static bool ensure_pks(praos_ctx* c, int t) {
+// the pool-key store t (cold 0, VRF 1): 32,768 slots, 16,384 entries.  Allocated on first use
+// and initialised on st, the stream every later use of store t is ordered after (the cache's
+// own stream; the context's other streams join it at the end of a run): no device-wide sync.
+static bool ensure_pks(praos_ctx* c, int t, hipStream_t st) {
   praos_ctx::PoolKeyStore& s = c->pks[t];
   if (s.ktab) return true;
   praos_ctx::PoolKeyStore z;
-  z.slots = 1u << 15;
-  z.cap = 1u << 14;
+  // KES leaf keys: a 432k-header epoch has ~59k (one per pool and KES period): 131,072 entries
+  // (2 GB of tables), 262,144 slots
+  z.slots = t == 2 ? 1u << 18 : 1u << 15;
+  z.cap = t == 2 ? 1u << 17 : 1u << 14;
   bool ok = hipMalloc(&z.pkey, 32 * (size_t)z.slots) == hipSuccess;
   ok = ok && hipMalloc(&z.pentry, 4 * (size_t)z.slots) == hipSuccess;
   ok = ok && hipMalloc(&z.count, 8) == hipSuccess;
@@ -1079,21 +1087,16 @@ static bool ensure_pks(praos_ctx* c, int t) {
   ok = ok && hipMalloc(&z.entry_pos, 4 * (size_t)z.cap) == hipSuccess;
   ok = ok && hipMalloc(&z.kinfo, 36 * (size_t)z.cap) == hipSuccess;
   ok = ok && hipMalloc(&z.ktab, KT_BYTES * (size_t)z.cap) == hipSuccess;
-  ok = ok && hipHostMalloc(&z.count_h, 8) == hipSuccess;
-  // (initialised and waited for here: the context's streams do not order after the null
-  // stream, and a run reads count and pentry from its first kernel on)
-  ok = ok && hipMemset(z.pentry, 0xff, 4 * (size_t)z.slots) == hipSuccess;
-  ok = ok && hipMemset(z.count, 0, 8) == hipSuccess;
-  ok = ok && hipMemset(z.base, 0, 8) == hipSuccess;
-  ok = ok && hipDeviceSynchronize() == hipSuccess;
+  ok = ok && hipMemsetAsync(z.pentry, 0xff, 4 * (size_t)z.slots, st) == hipSuccess;
+  ok = ok && hipMemsetAsync(z.count, 0, 8, st) == hipSuccess;
+  ok = ok && hipMemsetAsync(z.base, 0, 8, st) == hipSuccess;
   if (!ok) {
+    (void)hipStreamSynchronize(st);              // (the memsets queued so far) before the frees
     for (void* q : {(void*)z.pkey, (void*)z.count, (void*)z.base, (void*)z.entry_rep, (void*)z.entry_pos,
                     (void*)z.kinfo, (void*)z.pentry, (void*)z.ktab})
       (void)hipFree(q);
-    if (z.count_h) (void)hipHostFree(z.count_h);
     return false;
   }
-  *z.count_h = 0;
   s = z;
   return true;
 }
@@ -1108,15 +1111,13 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
   HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
   HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
   praos_ctx::PoolKeyStore* ps = nullptr;
-  if (c->pk_on && which < 2 && ensure_pks(c, which)) {
+  if (c->pk_on && (which < 2 || c->prefill) && ensure_pks(c, which, st)) {
     // pool keys: entries continue the store's, every new key is cached (it recurs in the runs
-    // that follow); a store more than 3/4 full is emptied first
+    // that follow); a store more than 3/4 full (decided on the device, from the count the last
+    // run left: no host read of a count still in flight) or one asked to be emptied is emptied
     ps = &c->pks[which];
-    if (c->pk_reset_run || *ps->count_h > ps->cap / 4 * 3) {
-      HIPCHK(c, hipMemsetAsync(ps->pentry, 0xff, 4 * (size_t)ps->slots, st));
-      HIPCHK(c, hipMemsetAsync(ps->count, 0, 4, st));
-      *ps->count_h = 0;
-    }
+    launch_pkey_reset(st, ps->count, ps->pentry, ps->slots, ps->cap / 4 * 3, c->pk_reset[which] ? 1 : 0);
+    c->pk_reset[which] = false;
     HIPCHK(c, hipMemcpyAsync(k.counters, ps->count, 4, hipMemcpyDeviceToDevice, st));
     HIPCHK(c, hipMemcpyAsync(ps->base, ps->count, 4, hipMemcpyDeviceToDevice, st));
     k.kt = ps->ktab; k.ki = ps->kinfo; k.erep = ps->entry_rep; k.epos = ps->entry_pos; k.emax = ps->cap;
@@ -1144,7 +1145,40 @@ static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t*
                         c->use_key4(n));
   launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, keys, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
                       span);
-  (void)hipMemcpyAsync(ps.count_h, ps.count, 4, hipMemcpyDeviceToHost, st);
+}
+
+// The stored-bytes pipeline's key prefill: the keys of the landed chunk [lo, hi) go into the
+// pool-key store t (the batch's hash set dedupes them within the chunk, keys already stored are
+// skipped), and the new ones are decoded and expanded into their tables at once, on the cache's
+// stream, while later chunks upload; the batch run after the last chunk then finds every key
+// stored (all hits: no key precompute on its critical path).  reset: empty the store first (the
+// call's first chunk).
+static int kc_prefill(praos_ctx* c, praos_batch* b, int t, const uint8_t* keys, int kind, size_t lo, size_t hi,
+                      hipStream_t st, bool reset, int prio) {
+  praos_batch::KeyCache& k = b->kc[t];
+  if (!ensure_pks(c, t, st)) { c->err = "pool-key store allocation"; return PRAOS_E_OOM; }
+  praos_ctx::PoolKeyStore& ps = c->pks[t];
+  const size_t m = hi - lo;
+  if (reset || c->pk_reset[t]) launch_pkey_reset(st, ps.count, ps.pentry, ps.slots, 0, 1);
+  c->pk_reset[t] = false;
+  if (m == 0) return PRAOS_OK;
+  HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
+  HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
+  HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
+  HIPCHK(c, hipMemcpyAsync(k.counters, ps.count, 4, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(ps.base, ps.count, 4, hipMemcpyDeviceToDevice, st));
+  const uint8_t* ck = keys + 32 * lo;                   // the chunk's keys (item ids relative to lo)
+  launch_key_insert(dim3(nblocks(m, NT)), dim3(NT), st, m, nullptr, nullptr, ck, k.cap - 1, k.slot_rep, k.slot_cnt,
+                    k.item_slot + lo, ps.pentry, ps.pkey, ps.slots - 1);
+  launch_key_assign(dim3(nblocks(k.cap, NT)), dim3(NT), st, k.cap, k.slot_rep, k.slot_cnt, 1u, ps.cap, k.slot_entry,
+                    ps.entry_rep, ps.entry_pos, k.counters);
+  const uint32_t span = (uint32_t)std::min<size_t>(m, ps.cap);
+  launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, ck, ps.ktab, ps.kinfo, prio, ps.base, span,
+                        c->use_key4(m));
+  launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, ck, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
+                      span);
+  HIPCHK(c, hipGetLastError());
+  return PRAOS_OK;
 }
 
 static int batch_run_impl(praos_ctx* c, praos_batch* b) {
@@ -1164,9 +1198,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   c->last_from_bytes = b->from_bytes;
   c->v_timed = false;
   c->kes_ck_timed = false;
-  c->pk_on = c->keycache > 0 && (c->pool_keys > 0 || (c->pool_keys < 0 && c->replaying));
-  c->pk_reset_run = c->pk_reset;
-  c->pk_reset = false;
+  c->pk_on = c->keycache > 0 && (c->prefill || c->pool_keys > 0 || (c->pool_keys < 0 && c->replaying));
   if (b->from_bytes) {
     // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
@@ -1678,7 +1710,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_KES_PAIR) { c->kes_pair = value < 0 ? -1 : value; return PRAOS_OK; }
   if (opt == PRAOS_OPT_POOL_KEYS) {
     c->pool_keys = value < 0 ? -1 : (value != 0);
-    if (value == 2) c->pk_reset = true;
+    if (value == 2) c->pk_reset[0] = c->pk_reset[1] = true;
     return PRAOS_OK;
   }
   return PRAOS_E_ARG;
@@ -2056,6 +2088,9 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
   const bool vrf = (c->kernels & 4) != 0;
+  // key prefill per landed chunk (see praos_ctx::e2e_prefill): Praos header batches with the key
+  // caches and all three crypto passes on their concurrent streams
+  const bool prefill = c->e2e_prefill > 0 && c->keycache > 0 && c->concurrent && c->kernels == 7 && n >= 2;
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
@@ -2073,6 +2108,23 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
                         b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
+    if (prefill) {
+      // cache t on the stream its run uses: cold keys side[0], KES leaf keys side[1], VRF keys side[2]
+      const int sidx[3] = {0, 2, 1};
+      for (int t : {1, 0, 2}) {
+        hipStream_t st = c->side[sidx[t]];
+        HIPCHK(c, hipStreamWaitEvent(st, c->done_ev[k], 0));
+        const uint8_t* keys = t == 0 ? b->cold_vk : (t == 1 ? b->vrf_vk : b->kes_leaf);
+        if (t == 2)
+          launch_kes_leafkeys(dim3(nblocks(m, NT)), dim3(NT), st, m, b->kes_sig + 448 * lo[k], b->slot + lo[k],
+                              b->ocert_c0 + lo[k], c->params.slots_per_kes_period, b->kes_leaf + 32 * lo[k]);
+        // (the last chunk's new keys head the cached chains of the run that follows: raised wave
+        // priority for them; the earlier chunks' fill the SIMDs the chunks' stage V leaves)
+        const int r = kc_prefill(c, b, t, keys, t == 1 ? 1 : 0, lo[k], lo[k + 1], st, k == 0 && c->pool_keys <= 0,
+                                 k == K - 1 ? 1 : 0);
+        if (r != PRAOS_OK) return r;
+      }
+    }
     if (vrf) {
       // the chunks' stage V alternate between two streams: on one they would queue behind
       // each other (a chunk's V alone is latency-bound)
@@ -2085,7 +2137,9 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   b->decoded = true;
   b->v_done = vrf;
+  c->prefill = prefill;
   int r = praos_batch_run(c, b);
+  c->prefill = false;
   b->decoded = false;
   b->v_done = false;
   // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
@@ -2363,6 +2417,21 @@ using praos_host::nonce_eq;
 
 // error text for the other host modules of the library (praos_replay.hip)
 void praos_set_error_(praos_ctx* c, const std::string& m) { if (c) c->err = m; }
+// the group's page-locked ranges (praos_group_host_register: pinned once, known to every member)
+int praos_ctx_note_registered_(praos_ctx* c, void* p, size_t len, bool add) {
+  if (!c) return PRAOS_E_ARG;
+  std::lock_guard<std::mutex> g(c->reg_mu);
+  if (add) {
+    c->registered.emplace_back((uintptr_t)p, len);
+    return PRAOS_OK;
+  }
+  auto it = std::find_if(c->registered.begin(), c->registered.end(),
+                         [&](const std::pair<uintptr_t, size_t>& r) { return r.first == (uintptr_t)p; });
+  if (it == c->registered.end()) return PRAOS_E_ARG;
+  c->registered.erase(it);
+  return PRAOS_OK;
+}
+int praos_ctx_device_(praos_ctx* c) { return c ? c->device : -1; }
 void praos_replay_scope_(praos_ctx* c, bool on) {
   if (!c) return;
   c->err.first_only(on);

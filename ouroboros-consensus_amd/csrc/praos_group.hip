@@ -9,7 +9,10 @@
 //
 // A device may appear several times (several contexts on one GPU: the multi-threaded
 // use the C ABI allows, one context per host thread).
+#include <hip/hip_runtime.h>
+
 #include "praos_hip.h"
+#include "replay_internal.hpp"
 
 #include <algorithm>
 #include <string>
@@ -19,7 +22,12 @@
 struct praos_group {
   std::vector<praos_ctx*> ctx;
   std::string err;
+  std::vector<void*> registered;          // praos_group_host_register ranges
 };
+
+void praos_replay_scope_(praos_ctx* c, bool on);   // praos_api.hip
+int praos_ctx_note_registered_(praos_ctx* c, void* p, size_t len, bool add);   // praos_api.hip
+int praos_ctx_device_(praos_ctx* c);                                            // praos_api.hip
 
 namespace {
 
@@ -167,6 +175,11 @@ int praos_group_set_epoch(praos_group* g, const uint8_t eta0[32], const praos_po
   return fan_out(g, [&](size_t k) { return praos_set_epoch(g->ctx[k], eta0, pools, npools, params); });
 }
 
+int praos_group_set_overlay(praos_group* g, const praos_overlay* ov) {
+  if (!g) return PRAOS_E_ARG;
+  return fan_out(g, [&](size_t k) { return praos_set_overlay(g->ctx[k], ov); });
+}
+
 int praos_group_verify_headers(praos_group* g, const praos_headers* h, praos_out* out) {
   if (!g || !h || !out || !out->bits) return PRAOS_E_ARG;
   const size_t m = g->ctx.size();
@@ -229,6 +242,65 @@ int praos_group_verify_tpraos_header_bytes(praos_group* g, const praos_header_by
     return praos_verify_tpraos_header_bytes(g->ctx[k], &s, &o, dec ? &d : nullptr, at(leader_out, i0, 64),
                                             at(leader_proof, i0, 80));
   });
+}
+
+// Page-locks a caller buffer once for every member (hipHostRegisterPortable: one pinning the
+// member devices all read by DMA), so each member's upload of its shard is a direct copy.
+int praos_group_host_register(praos_group* g, void* p, size_t len) {
+  if (!g || !p || len == 0 || g->ctx.empty()) return PRAOS_E_ARG;
+  if (hipSetDevice(praos_ctx_device_(g->ctx[0])) != hipSuccess ||
+      hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
+    g->err = "hipHostRegister failed";
+    return PRAOS_E_HIP;
+  }
+  for (praos_ctx* c : g->ctx) praos_ctx_note_registered_(c, p, len, true);
+  g->registered.push_back(p);
+  return PRAOS_OK;
+}
+
+int praos_group_host_unregister(praos_group* g, void* p) {
+  if (!g || !p) return PRAOS_E_ARG;
+  auto it = std::find(g->registered.begin(), g->registered.end(), p);
+  if (it == g->registered.end()) { g->err = "range not registered with the group"; return PRAOS_E_ARG; }
+  g->registered.erase(it);
+  for (praos_ctx* c : g->ctx) praos_ctx_note_registered_(c, p, 0, false);
+  (void)hipSetDevice(praos_ctx_device_(g->ctx[0]));
+  if (hipHostUnregister(p) != hipSuccess) { g->err = "hipHostUnregister failed"; return PRAOS_E_HIP; }
+  return PRAOS_OK;
+}
+
+// The ImmutableDB replay over the group (db-analyser's processAllImmutableDB, Analysis.hs:815-847):
+// consecutive batches dealt to the members in turn, one nonce chain and one fold in chain order
+// (rp_replay, praos_replay.hip); outputs as praos_replay_immutable's on one context.
+static int group_replay(praos_group* g, const char* dir, const praos_pool* pools, uint32_t npools,
+                        const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                        praos_chain_state* st, size_t batch_max, uint8_t* verdicts, uint16_t* failures,
+                        size_t verdicts_cap, praos_replay_stats* stats, bool tpraos,
+                        const praos_nonce* extra_entropy) {
+  if (!g || g->ctx.empty()) return PRAOS_E_ARG;
+  for (praos_ctx* c : g->ctx) praos_replay_scope_(c, true);
+  const int r = rp_replay(g->ctx.data(), (int)g->ctx.size(), dir, pools, npools, params, ei, env, st, batch_max,
+                          verdicts, failures, verdicts_cap, stats, tpraos, extra_entropy);
+  for (praos_ctx* c : g->ctx) praos_replay_scope_(c, false);
+  if (r != PRAOS_OK) g->err = praos_last_error(g->ctx[0]);
+  return r;
+}
+
+int praos_group_replay_immutable(praos_group* g, const char* dir, const praos_pool* pools, uint32_t npools,
+                                 const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                                 praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
+                                 praos_replay_stats* stats) {
+  return group_replay(g, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap, stats,
+                      false, nullptr);
+}
+
+int praos_group_replay_immutable_tpraos(praos_group* g, const char* dir, const praos_pool* pools, uint32_t npools,
+                                        const praos_params* params, const praos_epoch_info* ei,
+                                        const praos_nonce* extra_entropy, praos_envelope* env, praos_chain_state* st,
+                                        size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
+                                        praos_replay_stats* stats) {
+  return group_replay(g, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap, stats,
+                      true, extra_entropy);
 }
 
 }  // extern "C"

@@ -14,7 +14,7 @@
 // one the real fold ticks to.  One ledger view (pools, parameters) for the whole replay.
 // Like the reference, the replay ends at the first invalid header.
 //
-// Three host threads, up to three batches in flight:
+// Four host threads, up to three batches in flight per context:
 //   reader (this thread): chunk files are memory-mapped; a batch's header bytes go straight
 //     from the mappings into the pinned staging buffers (coalesced spans, no host copy of
 //     the chunk), H2D on the copy stream, decode + the nonce value of every certified VRF
@@ -163,11 +163,18 @@ constexpr size_t SPAN_GAP = 4096;             // headers this close share one up
 // certificate (Blake2b-256 of the output, no range extension) and TICKN adds the extra
 // entropy (eta0 := eta_c ⭒ eta_h ⭒ extraEntropy) -- and the TPraos fold (PRTCL
 // predicate-failure sets into failures[]).
-static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools, uint32_t npools,
-                       const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
-                       praos_chain_state* st, size_t batch_max, uint8_t* verdicts, uint16_t* failures,
-                       size_t verdicts_cap, praos_replay_stats* stats, bool tpraos,
-                       const praos_nonce* extra_entropy) {
+//
+// Several contexts (a praos_group, praos_group.hip): consecutive batches are dealt to the
+// members in turn (batch k to member k mod m, each member with its own slots and copy /
+// compute streams), the nonce chain and the fold stay single and in chain order (the fold
+// on member 0's context), so the result is the one-context replay's, bit for bit.
+int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* pools, uint32_t npools,
+              const praos_params* params, const praos_epoch_info* ei, praos_envelope* env, praos_chain_state* st,
+              size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
+              praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy) {
+  praos_ctx* const ctx = m > 0 && mem ? mem[0] : nullptr;
+  for (int q = 0; q < m; q++)
+    if (!mem[q]) return PRAOS_E_ARG;
   if (!ctx || !dir || !params || (npools && !pools) || !ei || !env || !st || !stats || batch_max == 0 ||
       ei->epoch_length == 0 || (verdicts_cap && !verdicts))
     return PRAOS_E_ARG;
@@ -208,8 +215,13 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     }
     // (the installed nonce only seeds praos_set_epoch: every batch carries its own nonces)
     if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); return PRAOS_E_ARG; }
-    const int r = praos_set_epoch(ctx, eta0.neutral ? nullptr : eta0.hash, pools, npools, params);
-    if (r != PRAOS_OK) return r;
+    for (int q = 0; q < m; q++) {
+      const int r = praos_set_epoch(mem[q], eta0.neutral ? nullptr : eta0.hash, pools, npools, params);
+      if (r != PRAOS_OK) {
+        if (q) praos_set_error_(ctx, std::string("member ") + std::to_string(q) + ": " + praos_last_error(mem[q]));
+        return r;
+      }
+    }
   }
   struct Slot {
     praos_batch* b = nullptr;
@@ -227,7 +239,11 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     int32_t* pidx = nullptr;                  // pinned
     size_t pin_cap = 0;
   };
-  Slot S[SLOTS];
+  // batch k: slot k mod T (T = m x SLOTS), member k mod m, that member's kept slot (k mod T) / m
+  const int T = m * SLOTS;
+  std::vector<Slot> S(T);
+  auto member = [&](uint64_t k) { return mem[k % (uint64_t)m]; };
+  auto member_slot = [&](uint64_t k) { return (int)((k % (uint64_t)T) / (uint64_t)m); };
   std::mutex mu;
   std::condition_variable cv;
   std::atomic<bool> stop{false};
@@ -255,7 +271,7 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
   uint64_t sp_epoch = sp.origin ? 0 : epoch_of(sp.last);
   std::thread chain([&] {
     for (uint64_t k = 0;; k++) {
-      Slot& C = S[k % SLOTS];
+      Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return stop || k >= nbatches || C.state == 1; });
@@ -329,13 +345,14 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
   // kept off the nonce chain's thread)
   std::thread launcher([&] {
     for (uint64_t k = 0;; k++) {
-      Slot& C = S[k % SLOTS];
+      Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return stop || k >= nbatches || C.state == 2; });
         if (stop || k >= nbatches) return;
       }
-      const int rc = rp_run(ctx, C.b, C.etas.data(), (uint32_t)C.etas.size(), C.eidx.data());
+      const int rc = rp_run(member(k), C.b, C.etas.data(), (uint32_t)C.etas.size(), C.eidx.data());
+      if (rc != PRAOS_OK && member(k) != ctx) praos_set_error_(ctx, praos_last_error(member(k)));
       if (rc != PRAOS_OK) { fail(rc); return; }
       std::lock_guard<std::mutex> g(mu);
       C.state = 3;
@@ -348,15 +365,19 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
   uint8_t stop_verdict = 0;
   std::thread folder([&] {
     for (uint64_t k = 0;; k++) {
-      Slot& C = S[k % SLOTS];
+      Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return stop || k >= nbatches || C.state == 3; });
         if (stop || k >= nbatches) return;
       }
       auto t0 = std::chrono::steady_clock::now();
-      int rc = rp_download_results(ctx, C.b, C.bits, C.pidx);
-      if (rc != PRAOS_OK) { fail(rc); return; }
+      int rc = rp_download_results(member(k), C.b, C.bits, C.pidx);
+      if (rc != PRAOS_OK) {
+        if (member(k) != ctx) praos_set_error_(ctx, praos_last_error(member(k)));
+        fail(rc);
+        return;
+      }
       t_wait += ms_since(t0);
       t0 = std::chrono::steady_clock::now();
       const size_t n = C.n;
@@ -405,10 +426,10 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
       cv.notify_all();
     }
   });
-  // ---- reader (this thread): build, upload and decode batch k into slot k % SLOTS
+  // ---- reader (this thread): build, upload and decode batch k into slot k % T (member k % m)
   uint64_t next_index = 0, built = 0;
   for (uint64_t k = 0;; k++) {
-    Slot& C = S[k % SLOTS];
+    Slot& C = S[k % T];
     {
       std::unique_lock<std::mutex> g(mu);
       cv.wait(g, [&] { return stop || C.state == 0; });
@@ -458,9 +479,10 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     const size_t n = C.n = C.off.size();
     C.index0 = next_index;
     next_index += n;
+    praos_ctx* const mc = member(k);
     if (!rp_batch_fits(C.b, n, arena)) {
-      if (C.b) rp_batch_destroy(ctx, C.b);
-      C.b = rp_batch_take(ctx, (int)(k % SLOTS), n, arena, tpraos);
+      if (C.b) rp_batch_destroy(mc, C.b);
+      C.b = rp_batch_take(mc, member_slot(k), n, arena, tpraos);
       if (!C.b) { fail(PRAOS_E_OOM); break; }
     }
     if (C.pin_cap < n) {
@@ -476,7 +498,7 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
         break;
       }
     }
-    int rc = rp_upload_decode(ctx, C.b, n, C.spans.data(), C.spans.size(), C.off.data(), C.len.data());
+    int rc = rp_upload_decode(mc, C.b, n, C.spans.data(), C.spans.size(), C.off.data(), C.len.data());
     C.chunks.clear();                         // the mappings have been read (except the reader's current one)
     C.dstat.resize(n); C.block_no.resize(n); C.slot.resize(n); C.ocn.resize(n); C.bsize.resize(n);
     C.prev.resize(32 * n); C.gen.resize(n); C.cold.resize(32 * n); C.hh.resize(32 * n); C.nonce.resize(32 * n);
@@ -484,9 +506,13 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
     dec.status = C.dstat.data(); dec.block_no = C.block_no.data(); dec.slot = C.slot.data();
     dec.prev_hash = C.prev.data(); dec.prev_is_genesis = C.gen.data(); dec.cold_vk = C.cold.data();
     dec.body_size = C.bsize.data(); dec.ocert_n = C.ocn.data(); dec.header_hash = C.hh.data();
-    if (rc == PRAOS_OK) rc = rp_download_decoded(ctx, C.b, &dec, C.nonce.data());
+    if (rc == PRAOS_OK) rc = rp_download_decoded(mc, C.b, &dec, C.nonce.data());
     t_dev += ms_since(t0);
-    if (rc != PRAOS_OK) { fail(rc); break; }
+    if (rc != PRAOS_OK) {
+      if (mc != ctx) praos_set_error_(ctx, praos_last_error(mc));
+      fail(rc);
+      break;
+    }
     std::lock_guard<std::mutex> g(mu);
     C.state = 1;
     built = k + 1;
@@ -500,13 +526,13 @@ static int replay_impl(praos_ctx* ctx, const char* dir, const praos_pool* pools,
   chain.join();
   launcher.join();
   folder.join();
-  for (int k = 0; k < SLOTS; k++) {
+  for (int k = 0; k < T; k++) {
     Slot& C = S[k];
     // a replay that stopped early may have queued the crypto of up to two later batches:
     // they finish before the batch goes back to the context (the next call's upload
     // overwrites its buffers; rp_upload_decode also orders itself after run_ev)
     if (C.b) rp_batch_quiesce(C.b);
-    if (C.b) rp_batch_keep(ctx, k, C.b);
+    if (C.b) rp_batch_keep(member(k), member_slot(k), C.b);
     if (C.bits) (void)hipHostFree(C.bits);
     if (C.pidx) (void)hipHostFree(C.pidx);
   }
@@ -535,8 +561,8 @@ extern "C" int praos_replay_immutable(praos_ctx* ctx, const char* dir, const pra
                                       praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
                                       size_t verdicts_cap, praos_replay_stats* stats) {
   praos_replay_scope_(ctx, true);
-  const int r = replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap,
-                            stats, false, nullptr);
+  const int r = rp_replay(&ctx, 1, dir, pools, npools, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap,
+                          stats, false, nullptr);
   praos_replay_scope_(ctx, false);
   return r;
 }
@@ -547,8 +573,8 @@ extern "C" int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, co
                                              praos_chain_state* st, size_t batch_max, uint8_t* verdicts,
                                              uint16_t* failures, size_t verdicts_cap, praos_replay_stats* stats) {
   praos_replay_scope_(ctx, true);
-  const int r = replay_impl(ctx, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap,
-                            stats, true, extra_entropy);
+  const int r = rp_replay(&ctx, 1, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures,
+                          verdicts_cap, stats, true, extra_entropy);
   praos_replay_scope_(ctx, false);
   return r;
 }

@@ -43,3 +43,10 @@ int rp_fold(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, cons
             const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx, const praos_nonce* evolving_after,
             bool tpraos, const praos_nonce* extra_entropy, uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
             size_t* processed);
+// The replay of praos_replay_immutable[_tpraos] over m contexts (praos_replay.hip): batch k is
+// uploaded, decoded and verified on mem[k % m]; the nonce chain and the fold run once, in chain
+// order, the fold and the error text on mem[0].  m = 1 is the single-context replay.
+int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* pools, uint32_t npools,
+              const praos_params* params, const praos_epoch_info* ei, praos_envelope* env, praos_chain_state* st,
+              size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
+              praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy);

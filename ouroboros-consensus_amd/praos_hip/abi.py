@@ -247,6 +247,20 @@ SIGNATURES = {
     "praos_group_verify_tpraos_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
                                                               ctypes.POINTER(TPOut), ctypes.POINTER(Decoded), u8p,
                                                               u8p]),
+    "praos_group_set_overlay": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Overlay)]),
+    "praos_group_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "praos_group_host_unregister": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "praos_group_replay_immutable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(Pool),
+                                                    ctypes.c_uint32, ctypes.POINTER(Params), ctypes.POINTER(EpochInfo),
+                                                    ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
+                                                    ctypes.c_size_t, u8p, ctypes.c_size_t,
+                                                    ctypes.POINTER(ReplayStats)]),
+    "praos_group_replay_immutable_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(Pool),
+                                                           ctypes.c_uint32, ctypes.POINTER(Params),
+                                                           ctypes.POINTER(EpochInfo), ctypes.POINTER(Nonce),
+                                                           ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
+                                                           ctypes.c_size_t, u8p, u16p, ctypes.c_size_t,
+                                                           ctypes.POINTER(ReplayStats)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -803,40 +817,9 @@ class Context:
         update_chain_dep_state) and envelope (limits + "tip") are updated in place.
         Returns (stats dict, verdict u8[verdicts_cap]); tpraos=True (praos_replay_immutable_tpraos,
         extra_entropy None = NeutralNonce) returns (stats, verdict, failures u16[verdicts_cap])."""
-        arr = self.pool_array(pools)
-        st, hk, cv = _state_struct(state, counter_cap)
-        E = Envelope()
-        tip = envelope.get("tip")
-        E.tip_is_origin = int(tip is None)
-        if tip is not None:
-            E.tip_slot, E.tip_block_no = tip[0], tip[1]
-            ctypes.memmove(E.tip_hash, bytes(tip[2]), 32)
-        for k in ("max_major_pv", "lv_prot_major", "max_header_size", "max_body_size"):
-            setattr(E, k, envelope[k])
-        ei = EpochInfo(*epoch_info)
-        verdict = np.zeros(max(verdicts_cap, 1), np.uint8)
-        fails = np.zeros(max(verdicts_cap, 1), np.uint16)
-        S = ReplayStats()
-        if tpraos:
-            xe = None
-            if extra_entropy is not None:
-                xe = Nonce()
-                ctypes.memmove(xe.hash, bytes(extra_entropy), 32)
-            self.check(self.L.praos_replay_immutable_tpraos(
-                self.h, os.fsencode(str(path)), arr, len(pools), ctypes.byref(params), ctypes.byref(ei),
-                ctypes.byref(xe) if xe is not None else None, ctypes.byref(E), ctypes.byref(st), batch_max,
-                ptr(verdict), ptr(fails, u16p), verdicts_cap, ctypes.byref(S)))
-        else:
-            self.check(self.L.praos_replay_immutable(self.h, os.fsencode(str(path)), arr, len(pools),
-                                                     ctypes.byref(params), ctypes.byref(ei), ctypes.byref(E),
-                                                     ctypes.byref(st), batch_max, ptr(verdict), verdicts_cap,
-                                                     ctypes.byref(S)))
-        envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no), bytes(E.tip_hash))
-        state.update(_state_from_struct(st, hk, cv))
-        stats = {name: getattr(S, name) for name, _ in ReplayStats._fields_}
-        if tpraos:
-            return stats, verdict[:verdicts_cap], fails[:verdicts_cap]
-        return stats, verdict[:verdicts_cap]
+        fn = self.L.praos_replay_immutable_tpraos if tpraos else self.L.praos_replay_immutable
+        return _replay(fn, self.h, self.check, path, pools, params, epoch_info, state, envelope, batch_max,
+                       verdicts_cap, counter_cap, tpraos, extra_entropy)
 
     def apply_batch(self, H, crypto, counters=None):
         """counters: dict hash28 -> int.  Returns (verdict u8[n], chain_stop, counters_out)."""
@@ -1099,6 +1082,35 @@ class Group:
         self.check(self.L.praos_group_verify_tpraos_headers(self.g, ctypes.byref(th), ctypes.byref(to)))
         return o
 
+    def set_overlay(self, d, f, epoch_base_slot, epoch_length, gen_delegs):
+        """praos_group_set_overlay (Context.set_overlay on every member)."""
+        if d is None:
+            self.check(self.L.praos_group_set_overlay(self.g, None))
+            return
+        arr = (GenDeleg * max(1, len(gen_delegs)))()
+        for k, (g, dl, v) in enumerate(gen_delegs):
+            ctypes.memmove(arr[k].genesis_hash28, bytes(g), 28)
+            ctypes.memmove(arr[k].delegate_hash28, bytes(dl), 28)
+            ctypes.memmove(arr[k].vrf_hash32, bytes(v), 32)
+        ov = Overlay(d.numerator, d.denominator, f.numerator, f.denominator, epoch_base_slot, epoch_length,
+                     ctypes.cast(arr, ctypes.POINTER(GenDeleg)), len(gen_delegs))
+        self.check(self.L.praos_group_set_overlay(self.g, ctypes.byref(ov)))
+
+    def host_register(self, a):
+        """praos_group_host_register: page-lock a numpy array once for every member."""
+        assert a.flags["C_CONTIGUOUS"] and a.nbytes > 0
+        self.check(self.L.praos_group_host_register(self.g, a.ctypes.data, a.nbytes))
+
+    def host_unregister(self, a):
+        self.check(self.L.praos_group_host_unregister(self.g, a.ctypes.data))
+
+    def replay_immutable(self, path, pools, params: Params, epoch_info, state: dict, envelope: dict,
+                         batch_max=1 << 16, verdicts_cap=0, counter_cap=1 << 16, tpraos=False, extra_entropy=None):
+        """praos_group_replay_immutable[_tpraos]: Context.replay_immutable over the group's members."""
+        fn = self.L.praos_group_replay_immutable_tpraos if tpraos else self.L.praos_group_replay_immutable
+        return _replay(fn, self.g, self.check, path, pools, params, epoch_info, state, envelope, batch_max,
+                       verdicts_cap, counter_cap, tpraos, extra_entropy)
+
     def verify_tpraos_header_bytes(self, arena, off, length, decoded=False):
         arena, off, length = Context._chunk(arena, off, length)
         n = len(off)
@@ -1115,6 +1127,42 @@ class Group:
             return o
         D["leader_out"], D["leader_proof"] = lo, lp
         return o, D
+
+
+def _replay(fn, handle, check, path, pools, params, epoch_info, state, envelope, batch_max, verdicts_cap, counter_cap,
+            tpraos, extra_entropy):
+    """praos_[group_]replay_immutable[_tpraos] (the same arguments after the context / group)."""
+    arr = Context.pool_array(pools)
+    st, hk, cv = _state_struct(state, counter_cap)
+    E = Envelope()
+    tip = envelope.get("tip")
+    E.tip_is_origin = int(tip is None)
+    if tip is not None:
+        E.tip_slot, E.tip_block_no = tip[0], tip[1]
+        ctypes.memmove(E.tip_hash, bytes(tip[2]), 32)
+    for k in ("max_major_pv", "lv_prot_major", "max_header_size", "max_body_size"):
+        setattr(E, k, envelope[k])
+    ei = EpochInfo(*epoch_info)
+    verdict = np.zeros(max(verdicts_cap, 1), np.uint8)
+    fails = np.zeros(max(verdicts_cap, 1), np.uint16)
+    S = ReplayStats()
+    if tpraos:
+        xe = None
+        if extra_entropy is not None:
+            xe = Nonce()
+            ctypes.memmove(xe.hash, bytes(extra_entropy), 32)
+        check(fn(handle, os.fsencode(str(path)), arr, len(pools), ctypes.byref(params), ctypes.byref(ei),
+                 ctypes.byref(xe) if xe is not None else None, ctypes.byref(E), ctypes.byref(st), batch_max,
+                 ptr(verdict), ptr(fails, u16p), verdicts_cap, ctypes.byref(S)))
+    else:
+        check(fn(handle, os.fsencode(str(path)), arr, len(pools), ctypes.byref(params), ctypes.byref(ei),
+                 ctypes.byref(E), ctypes.byref(st), batch_max, ptr(verdict), verdicts_cap, ctypes.byref(S)))
+    envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no), bytes(E.tip_hash))
+    state.update(_state_from_struct(st, hk, cv))
+    stats = {name: getattr(S, name) for name, _ in ReplayStats._fields_}
+    if tpraos:
+        return stats, verdict[:verdicts_cap], fails[:verdicts_cap]
+    return stats, verdict[:verdicts_cap]
 
 
 def _state_struct(state, cap):

@@ -47,7 +47,7 @@ def test_struct_sizes_match_c_layout():
 
 def test_abi_version():
     from praos_hip import abi
-    assert abi.load().praos_abi_version() == 12
+    assert abi.load().praos_abi_version() == 13
 
 
 def test_no_silent_fallback_without_gpu():
@@ -65,7 +65,7 @@ _STRUCTS = {"praos_params": "Params", "praos_pool": "Pool", "praos_headers": "He
             "praos_chain_state": "ChainState", "praos_epoch_info": "EpochInfo", "praos_envelope": "Envelope",
             "praos_replay_stats": "ReplayStats", "praos_decoded": "Decoded", "praos_counters": "Counters",
             "praos_synth_params": "SynthParams", "praos_tpraos_headers": "TPHeaders",
-            "praos_tpraos_out": "TPOut"}
+            "praos_tpraos_out": "TPOut", "praos_gen_deleg": "GenDeleg", "praos_overlay": "Overlay"}
 HASKELL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "haskell",
                        "Ouroboros", "Consensus", "Protocol", "Praos", "Batch.hs")
 
@@ -134,3 +134,45 @@ def test_option_ids_match_header():
     for name, v in ids.items():
         assert getattr(abi, "OPT_" + name) == v, name
     assert "c_set_option p 7" in open(HASKELL).read()
+
+
+def test_haskell_abi_version_matches_header():
+    """Batch.hs checks praos_abi_version against its own constant: it must be the header's."""
+    from praos_hip import abi
+    hdr = open(abi.HEADER_PATH).read()
+    v = int(re.search(r"#define PRAOS_ABI_VERSION (\d+)", hdr).group(1))
+    assert re.search(r"^abiVersion = (\d+)$", open(HASKELL).read(), flags=re.M).group(1) == str(v)
+
+
+def test_haskell_binds_group_entry_points():
+    """The Haskell binding reaches several GPUs: the group entry points validateEpochHeaders[TPraos]
+    and the replay use (withPraosBatchDevices) are imported."""
+    hs = open(HASKELL).read()
+    imported = set(re.findall(r'foreign import ccall safe "(praos_[a-z0-9_]+)"', hs))
+    for name in ("praos_group_open", "praos_group_close", "praos_group_set_epoch", "praos_group_set_overlay",
+                 "praos_group_verify_header_bytes", "praos_group_verify_tpraos_header_bytes",
+                 "praos_group_host_register", "praos_group_host_unregister", "praos_group_replay_immutable",
+                 "praos_group_replay_immutable_tpraos"):
+        assert name in imported, name
+
+
+def test_tpraos_error_table_matches_haskell():
+    """The PRAOS_TPF_* -> ChainTransitionError table of Batch/Errors.hs (tpraosFailureTable, the
+    order ValidateAll collects the failures in) and the one ffi_harness.c prints the stopping
+    header's errors with are the same list, over the header's PRAOS_TPF_* values, and cover
+    every bit."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "praos_hip.h")).read()
+    tpf = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define PRAOS_TPF_([A-Z_]+)\s+0x([0-9a-f]+)u", hdr)}
+    errs = open(os.path.join(os.path.dirname(HASKELL), "Batch", "Errors.hs")).read()
+    block = errs[errs.index("tpraosFailureTable =") :]
+    block = block[: block.index("]")]
+    hs = [(int(a, 16), b) for a, b in re.findall(r"\(0x([0-9A-Fa-f]{4}), TP(\w+)\)", block)]
+    harness = open(os.path.join(root, "integration", "c", "ffi_harness.c")).read()
+    cblock = harness[harness.index("TPF_NAMES[] = {") :]
+    cblock = cblock[: cblock.index("};")]
+    c = [(tpf[a], b.split()[-1]) for a, b in re.findall(r'\{PRAOS_TPF_([A-Z_]+), "([^"]+)"\}', cblock)]
+    assert hs == c
+    assert sorted(b for b, _ in hs) == sorted(tpf.values()) and len(hs) == 15
+    # the Haskell names carry the ledger constructors' names (TP prefix dropped)
+    assert {n for _, n in hs} >= {"KESBeforeStartOCERT", "VRFKeyBadNonce", "WrongGenesisVRFKeyOVERLAY"}

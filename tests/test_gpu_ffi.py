@@ -53,8 +53,8 @@ def _python_replay(ctx, chain, db):
 
 
 def _agree(out, stats, cbor, tip):
-    for phase in ("binding", "typed", "replay"):
-        if phase not in out:                 # (no typed phase for TPraos databases)
+    for phase in ("binding", "binding_group", "typed", "typed_group", "replay", "replay_group"):
+        if phase not in out:                 # (no typed phases for TPraos databases, no binding_group for Praos)
             continue
         o = out[phase]
         assert (o["validated"], o["stop_index"], o["stop_verdict"]) == \
@@ -71,6 +71,9 @@ def test_ffi_sequence_matches_replay(ctx, chain, tmp_path):  # noqa: F811
     n = len(chain["off"])
     assert stats["validated"] == n and out["binding"]["epochs"] == stats["epochs"] == 4
     assert out["typed"]["epochs"] == 4 and out["typed"]["stop_bits"] == 0
+    # the group sequences (validateEpochHeaders on withPraosBatchDevices [0,0,0,0]; the replay dealt
+    # over 4 members in 97-header batches) end in the same state
+    assert {"typed_group", "replay_group"} <= set(out) and out["typed_group"]["stop_bits"] == 0
     _agree(out, stats, cbor, tip)
     t = out["threads"]
     assert t["threads_equal"] and t["group_equal"] and t["group_size"] == 4
@@ -95,6 +98,7 @@ def test_ffi_sequence_stops_with_replay(ctx, chain, tmp_path):  # noqa: F811
     # the typed path (Batch/Validate.hs) gets the stopping header's bits: a KES failure in
     # the leaf signature, which Batch.Errors turns into InvalidKesSignatureOCERT
     assert out["typed"]["stop_bits"] & (abi.BIT_KES_MERKLE | abi.BIT_KES_LEAF)
+    assert out["typed_group"]["stop_bits"] == out["typed"]["stop_bits"]
 
 
 def test_ffi_tpraos_sequence_matches_replay(ctx, tchain, tmp_path):  # noqa: F811
@@ -129,3 +133,65 @@ def test_ffi_tpraos_sequence_matches_replay(ctx, tchain, tmp_path):  # noqa: F81
     stats, cbor, tip = py(db)
     assert (stats["stop_index"], stats["stop_verdict"]) == (k, abi.V_TPRAOS)
     _agree(out, stats, cbor, tip)
+    assert {"binding_group", "replay_group"} <= set(out)
+    assert out["tpraos_stop"]["failures"] == abi.TPF_KES_SIG
+    assert out["tpraos_stop"]["errors"] == ["OverlayFailure (OcertFailure InvalidKesSignatureOCERT)"]
+
+
+# PRAOS_TPF_* -> the SL.ChainTransitionError constructor, in ValidateAll's order (Batch/Errors.hs
+# tpraosFailureTable; tests/test_abi.py holds it equal to the harness's table)
+_TPF_ORDER = [("TPF_NOT_ACTIVE", "NotActiveSlotOVERLAY"), ("TPF_GEN_COLD", "WrongGenesisColdKeyOVERLAY"),
+              ("TPF_VRF_KEY_UNKNOWN", "VRFKeyUnknown"), ("TPF_VRF_KEY_WRONG", "VRFKeyWrongVRFKey"),
+              ("TPF_GEN_VRF", "WrongGenesisVRFKeyOVERLAY"), ("TPF_BAD_NONCE", "VRFKeyBadNonce"),
+              ("TPF_BAD_LEADER", "VRFKeyBadLeaderValue"), ("TPF_LEADER_TOO_BIG", "VRFLeaderValueTooBig"),
+              ("TPF_KES_BEFORE_START", "OcertFailure KESBeforeStartOCERT"),
+              ("TPF_KES_AFTER_END", "OcertFailure KESAfterEndOCERT"),
+              ("TPF_OCERT_SIG", "OcertFailure InvalidSignatureOCERT"),
+              ("TPF_KES_SIG", "OcertFailure InvalidKesSignatureOCERT"),
+              ("TPF_COUNTER_MISSING", "OcertFailure NoCounterForKeyHashOCERT"),
+              ("TPF_COUNTER_TOO_SMALL", "OcertFailure CounterTooSmallOCERT"),
+              ("TPF_COUNTER_OVER_INC", "OcertFailure CounterOverIncrementedOCERT")]
+
+
+@pytest.mark.parametrize("field", ["eta_proof", "leader_proof", "vrf_vk", "cold_vk", "ocert_sig"])
+def test_ffi_tpraos_stop_errors(ctx, tchain, tmp_path, field):  # noqa: F811
+    """One stopping header per TPraos failure kind: a byte of the stored BHeader's field damaged
+    on disk (every such change also breaks the KES signature over the body).  The harness's
+    TPraos sequence stops where the library's replay and the oracle's fold stop, with the
+    oracle's PRTCL failure set, and names the ChainTransitionError constructors in the order
+    ValidateAll collects them -- the list Batch/Errors.hs tpraosChainTransitionError builds."""
+    from praos_hip import abi
+    from test_gpu_replay import TP_EXTRA, _tp_oracle_fold
+    k = int(np.nonzero(tchain["slots"] >= EPOCH_LEN)[0][5])
+    o, D = ctx.verify_tpraos_header_bytes(tchain["arena"], tchain["off"][k:k + 1], tchain["len"][k:k + 1],
+                                          decoded=True)
+    hdr = bytes(tchain["arena"][int(tchain["off"][k]):int(tchain["off"][k]) + int(tchain["len"][k])])
+    value = {"eta_proof": D["vrf_proof"][0], "leader_proof": D["leader_proof"][0], "vrf_vk": D["vrf_vk"][0],
+             "cold_vk": D["cold_vk"][0], "ocert_sig": D["ocert_sig"][0]}[field]
+    at = hdr.index(bytes(value)) + 9
+    db = str(tmp_path / f"tp_{field}")
+    shutil.copytree(tchain["path"], db)
+    fname, pos = _locate(tchain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + at] ^= 0x04
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    ef = str(tmp_path / "epoch_tp.txt")
+    _epoch_file(ef, tchain, tpraos_extra=TP_EXTRA)
+    out = _run_harness(db, ef, threads=2)
+    st, env = _genesis_state(tchain["cfg"]["eta0"]), dict(ENV, tip=None, lv_prot_major=6)
+    stats, v, f = ctx.replay_immutable(db, tchain["pools"], tchain["params"], tchain["epoch_info"], st, env,
+                                       verdicts_cap=len(tchain["off"]), tpraos=True, extra_entropy=TP_EXTRA)
+    assert (stats["stop_index"], stats["stop_verdict"]) == (k, abi.V_TPRAOS)
+    assert out["binding"]["stop_index"] == out["binding_group"]["stop_index"] == k
+    fails = int(out["tpraos_stop"]["failures"])
+    assert fails == int(f[k])
+    # the oracle's fold (oracle/tpraos.py, crypto from the GPU) over the damaged headers: same set
+    data = dict(tchain, path=db)
+    raw_arena = bytearray(tchain["arena"])
+    raw_arena[int(tchain["off"][k]) + at] ^= 0x04
+    data["arena"] = np.frombuffer(bytes(raw_arena), np.uint8)
+    _, ofails, _, _, ostop = _tp_oracle_fold(ctx, data, k + 1)
+    assert ostop == k and ofails[k] == fails
+    want = [f"OverlayFailure ({name})" for bit, name in _TPF_ORDER if fails & getattr(abi, bit)]
+    assert out["tpraos_stop"]["errors"] == want and len(want) >= 2
+    assert fails & abi.TPF_KES_SIG

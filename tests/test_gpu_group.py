@@ -173,6 +173,15 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
                 assert np.array_equal(o1[k], o2[k]), k
             for k in D1:
                 assert np.array_equal(D1[k], D2[k]), k
+        # the key prefill (each landed chunk's keys into the pool-key stores, PRAOS_E2E_PREFILL on by
+        # default) with the stores kept across calls (PRAOS_OPT_POOL_KEYS): the second call finds
+        # every key already stored -- the same outputs
+        ctx.set_option(abi.OPT_POOL_KEYS, 2)
+        for _ in range(2):
+            o3 = ctx.verify_header_bytes(arena, off, ln)
+            for k in o1:
+                assert np.array_equal(o1[k], o3[k]), k
     finally:
         ctx.set_option(abi.OPT_PIPELINE, 0)
+        ctx.set_option(abi.OPT_POOL_KEYS, -1)
     assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT

@@ -367,3 +367,103 @@ def test_tpraos_replay_stops_at_corruption(ctx, tchain, tmp_path):
     assert int((v[:k] != 0).sum()) == 0 and f[k] == abi.TPF_KES_SIG
     _, _, ost, _, ostop = _tp_oracle_fold(ctx, tchain, k)
     assert ostop == k and st == ost
+
+
+# ---------------------------------------------------------------- the replay over a group (several GPUs)
+_TIMES = ("ms_io", "ms_device", "ms_fold", "ms_nonce")
+
+
+def _same_replay(a, b):
+    """Two replays' (stats, verdicts, state, envelope) agree except for the timings (and, for a
+    replay that stopped early, the count of batches whose crypto was already queued: it
+    depends on how many batches the pipeline keeps in flight -- 3 per context)."""
+    (sa, va, sta, ea), (sb, vb, stb, eb) = a, b
+    skip = _TIMES + (("batches",) if sa["stop_index"] < sa["headers"] + sa["skipped"] or sa["stop_verdict"] else ())
+    assert {k: v for k, v in sa.items() if k not in skip} == {k: v for k, v in sb.items() if k not in skip}
+    assert np.array_equal(va, vb) and sta == stb and ea["tip"] == eb["tip"]
+
+
+def _group_replay(g, data, path=None, state=None, tip=None, batch_max=1 << 16):
+    st = state if state is not None else _genesis_state(data["cfg"]["eta0"])
+    env = dict(ENV, tip=tip)
+    stats, v = g.replay_immutable(path or data["path"], data["pools"], data["params"], data["epoch_info"], st, env,
+                                  batch_max=batch_max, verdicts_cap=len(data["off"]))
+    return stats, v, st, env
+
+
+@pytest.mark.parametrize("members,batch_max", [(2, 97), (3, 61), (4, 1 << 16)])
+def test_group_replay_equals_single(ctx, chain, members, batch_max):
+    """praos_group_replay_immutable (batches dealt to the members in turn, one nonce chain and one
+    fold in chain order) over members contexts on device 0: stats, verdicts, PraosState and tip
+    equal to the one-context replay's; with 97-header batches every member runs several."""
+    from praos_hip import abi
+    single = _replay(ctx, chain, batch_max=batch_max)
+    with abi.Group([0] * members) as g:
+        grp = _group_replay(g, chain, batch_max=batch_max)
+        again = _group_replay(g, chain, batch_max=batch_max)          # the members keep their batches
+    _same_replay(single, grp)
+    _same_replay(single, again)
+    assert grp[0]["batches"] >= (members if batch_max < 1000 else 1)
+    assert grp[2] == chain["state"]
+
+
+def test_group_replay_early_stop_then_resume(ctx, chain, tmp_path):
+    """A header damaged at index 40 of a replay in 29-header batches over a 3-member group: the
+    group stops where one context stops (later batches' crypto already queued on other
+    members), twice; a database holding the blocks before it, replayed by the group, then
+    checkpointed (CBOR) and resumed by the group over the clean database, ends in the
+    generator's state."""
+    from praos_hip import abi, immutable
+    n = len(chain["off"])
+    k = 40
+    db = _copy_db(chain, tmp_path, "gearly")
+    fname, pos = _locate(chain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + int(chain["len"][k]) - 100] ^= 0x40
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    single = _replay(ctx, chain, path=db, batch_max=29)
+    assert (single[0]["stop_index"], single[0]["stop_verdict"]) == (k, abi.V_KES_SIG)
+    part = str(tmp_path / "gpart")
+    m = int(np.nonzero(chain["slots"] >= EPOCH_LEN + 350)[0][0])
+    immutable.write_immutable(part, chain["arena"], chain["off"][:m], chain["len"][:m], chain["slots"][:m],
+                              chain["header_hash"][:m], CHUNK_SLOTS)
+    with abi.Group([0, 0, 0]) as g:
+        for _ in range(2):
+            _same_replay(single, _group_replay(g, chain, path=db, batch_max=29))
+        stats, _, st, env = _group_replay(g, chain, path=part, batch_max=29)
+        assert stats["validated"] == m
+        st2 = abi.state_decode(abi.state_encode(st))
+        stats2, v2, st2, env2 = _group_replay(g, chain, state=st2, tip=env["tip"], batch_max=29)
+    assert stats2["skipped"] == m and stats2["validated"] == n - m and int((v2[:n - m] != 0).sum()) == 0
+    assert st2 == chain["state"] and env2["tip"][2] == bytes(chain["header_hash"][-1])
+
+
+def test_group_replay_tpraos_equals_single(ctx, tchain):
+    """praos_group_replay_immutable_tpraos over 2 members = the one-context TPraos replay
+    (verdicts, PRTCL failure sets, state)."""
+    from praos_hip import abi
+    n = len(tchain["off"])
+    s1, v1, f1, st1, e1 = _tp_replay(ctx, tchain, batch_max=61)
+    with abi.Group([0, 0]) as g:
+        st2 = _genesis_state(tchain["cfg"]["eta0"])
+        e2 = dict(ENV, tip=None, lv_prot_major=6)
+        s2, v2, f2 = g.replay_immutable(tchain["path"], tchain["pools"], tchain["params"], tchain["epoch_info"], st2,
+                                        e2, batch_max=61, verdicts_cap=n, tpraos=True, extra_entropy=TP_EXTRA)
+    assert {k: v for k, v in s1.items() if k not in _TIMES} == {k: v for k, v in s2.items() if k not in _TIMES}
+    assert np.array_equal(v1, v2) and np.array_equal(f1, f2) and st1 == st2 == tchain["state"]
+    assert e1["tip"] == e2["tip"]
+
+
+def test_fresh_context_store_on_first_call_replay(chain):
+    """Pool-key store regression (round 4's first box fault): a fresh context whose first call is
+    a replay (the store on by default there, allocated and initialised on the cache's stream
+    inside that call) gives the generator's state; a second replay on it, with the store full
+    of the first one's keys, too."""
+    import praos_hip
+    c = praos_hip.Context(0)
+    try:
+        for _ in range(2):
+            stats, v, st, env = _replay(c, chain)
+            assert stats["validated"] == len(chain["off"]) and st == chain["state"]
+    finally:
+        c.close()
