@@ -205,7 +205,8 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * this many chunks (1 = no pipeline, up to 8): the stored bytes of chunk k+1 move host ->
  * device on a copy stream while chunk k is decoded and its VRF stage V runs; the rest of
  * the batch runs once after the last chunk, and the VRF outputs move back while the KES
- * checks finish; auto = up to 6 chunks of at least 65,536 headers. */
+ * checks finish; auto = up to 8 chunks of at least 49,152 headers, the first a quarter of the
+ * others' size (nothing runs until it has landed). */
 #define PRAOS_OPT_PIPELINE 5
 /* PRAOS_OPT_KES_PAIR (default -1 = automatic): the cached Sum6KES leaf verifies take two
  * headers per lane from this many cache hits on, encoding both R' with one field inversion
@@ -221,6 +222,12 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * byte; verdicts are identical either way.  1 = on, 0 = off, 2 = on and emptied before the
  * next run.  A store more than 3/4 full is emptied before a run. */
 #define PRAOS_OPT_POOL_KEYS 7
+/* PRAOS_OPT_GRAPH (default 0): a resident batch's praos_batch_run is captured once as a HIP
+ * graph (its second run; every stream's launches, copies and event dependencies) and replayed
+ * with one launch while the options and epoch tables stay the same (1 = batches below 300,000
+ * headers, 2 = every size, 0 = direct launches).  Off by default: measured slower than the
+ * direct launches on every size.  Outputs are identical either way. */
+#define PRAOS_OPT_GRAPH 8
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items

@@ -11,12 +11,11 @@
 // is < 2^128 (8 chunks + the top digit's table)
 __device__ __forceinline__ int key_chunks(int kind) { return kind == 0 ? KT_CHUNKS : 9; }
 
-FE_INLINE void key_precompute_entry(int kind, uint32_t e, const uint32_t* __restrict__ entry_rep,
-                                    const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
-                                    uint32_t* __restrict__ kinfo) {
+// decode + checks of entry e's key: P (the point the tables expand), kinfo[9e ..] (when write)
+FE_INLINE void key_decode_entry(int kind, uint32_t e, const uint32_t* __restrict__ entry_rep,
+                                const uint8_t* __restrict__ keys, uint32_t* __restrict__ kinfo, ge_p3& P, bool write) {
   uint32_t pk[8];
   load_words(pk, keys + 32 * (size_t)entry_rep[e], 8);
-  ge_p3 P;
   bool ok;
   uint32_t* info = kinfo + 9 * (size_t)e;
   if (kind == 0) {
@@ -28,12 +27,21 @@ FE_INLINE void key_precompute_entry(int kind, uint32_t e, const uint32_t* __rest
     ok = ge_frombytes(Y, pk, false) && ok;
     uint32_t ys[8];
     ge_enc_affine(ys, Y);
+    if (write) {
 #pragma unroll
-    for (int q = 0; q < 8; q++) info[1 + q] = ys[q];
+      for (int q = 0; q < 8; q++) info[1 + q] = ys[q];
+    }
     P = Y;
     fe_neg(P.X, Y.X);
     fe_neg(P.T, Y.T);
   }
-  info[0] = ok ? 1u : 0u;
+  if (write) info[0] = ok ? 1u : 0u;
+}
+
+FE_INLINE void key_precompute_entry(int kind, uint32_t e, const uint32_t* __restrict__ entry_rep,
+                                    const uint8_t* __restrict__ keys, ge_cached* __restrict__ ktab,
+                                    uint32_t* __restrict__ kinfo) {
+  ge_p3 P;
+  key_decode_entry(kind, e, entry_rep, keys, kinfo, P, true);
   key_chunk_bases(ktab + (size_t)e * KT_STRIDE, P, key_chunks(kind));
 }

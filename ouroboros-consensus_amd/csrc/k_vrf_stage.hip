@@ -11,6 +11,11 @@
 #ifndef LB_VRF_F
 #define LB_VRF_F LB_VRF
 #endif
+// the join / U + join kernels (one batched inversion, the SHA-512 challenge and beta, the
+// Blake2b range extensions): at 3 waves per SIMD they spill ~370 bytes per lane
+#ifndef LB_VRF_J
+#define LB_VRF_J LB_VRF_F
+#endif
 
 // ---- two-stage form of the header mode (praos_core.hpp vrf_v_core / vrf_fin_core)
 // stage V over every header of the batch: no dependence on the key cache
@@ -80,7 +85,7 @@ __device__ __forceinline__ void vrf_fin_item(const VrfIn& a, size_t i, size_t st
 }
 
 // cached keys (the hit list): U from the key's tables and the radix-2^16 comb
-__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_fin(size_t stride, const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_fin(size_t stride, const uint32_t* __restrict__ list,
                                                         const uint32_t* __restrict__ count,
                                                         const int32_t* __restrict__ item_entry,
                                                         const ge_cached* __restrict__ ktab,
@@ -96,7 +101,7 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_fin(size_t stride, const u
 }
 
 // uncached keys (the miss list, or every header): U on a per-lane chain
-__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_fin_nc(size_t n, const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_fin_nc(size_t n, const uint32_t* __restrict__ list,
                                                            const uint32_t* __restrict__ count,
                                                            const ge_niels* __restrict__ gbtab, VrfIn a,
                                                            const uint4* __restrict__ mid) {
@@ -150,7 +155,7 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_u_nc(size_t n, const uint3
 
 // join over every header: pool lookup and key hash (Praos.hs:533-541), the batched
 // inversion, the challenge, beta, the output check and the range extension
-__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
+__global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
@@ -210,7 +215,7 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join(size_t n, VrfIn a, co
 // key hash, Praos.hs:533-541 as TPraos.hs:304-387 uses them) and writes beta_eta + the nonce
 // (mkNonceFromOutputVRF of the stated output); cert 1 adds its bit to bits[i] and writes beta_l.
 // Runs after cert 0's join on the same stream (bits read-modify-write).
-__global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_join_tp(size_t n, int cert, VrfIn a,
+__global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_join_tp(size_t n, int cert, VrfIn a,
                                                             const uint4* __restrict__ mid,
                                                             const int32_t* __restrict__ ovl_class,
                                                             const uint32_t* __restrict__ gen) {

@@ -21,6 +21,9 @@ static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBo
 #include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -91,7 +94,7 @@ class CopyPool {
 
 static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2 x 16 MB per context
 static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
-static constexpr size_t PIPE_MIN_CHUNK = 65536;     // headers per chunk at least (auto mode)
+static constexpr size_t PIPE_MIN_CHUNK = 49152;     // headers per chunk at least (auto mode)
 // Batches below this many headers (a strong-scaling shard of an epoch over 8 GPUs is 54k) leave
 // most wave slots empty and run latency-bound (PRAOS_VRF_PRIO = -1 raises stage V there)
 static constexpr size_t SMALL_BATCH = 80000;
@@ -104,8 +107,11 @@ static constexpr size_t KEY_PRIO_BATCH = 400000;
 // (profiles/r04/y: 96k 4.06 -> 3.64 ms, 108k 4.25 -> 4.10, 112k 4.39 -> 4.15; equal at 120k,
 // slower at 128k)
 static constexpr size_t ILP4_BATCH = 120000;
-static constexpr int PIPE_AUTO = 6;                 // chunks in auto mode (432k headers: 4 -> 21.9M, 6 -> 23.0M,
-                                                    // 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt)
+static constexpr size_t GRAPH_BATCH = 300000;        // PRAOS_GRAPH = 1: graphs below this many headers
+static constexpr int PIPE_AUTO = 8;                 // chunks in auto mode (round 3, equal chunks: 4 -> 21.9M,
+                                                    // 6 -> 23.0M, 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt;
+                                                    // round 5 with the first chunk at 1/4 of the others: 6 ->
+                                                    // 25.3-25.6M, 8 -> 26.4-26.6M, profiles/r05/c8_pipe_head)
 struct praos_batch;
 
 // The context's last error.  The replay's worker threads (reader, nonce chain, launcher,
@@ -184,6 +190,16 @@ struct praos_ctx {
                                                        // PRAOS_KEY4 1 / 0, -1 below ILP4_BATCH (54k: 2.78-2.84
                                                        // -> 2.76-2.77 ms; 108k 4.17 -> 4.21, profiles/r04/n)
   bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < ILP4_BATCH); }
+  int keyq = 0;                                        // key precompute with four lanes per key (k_keysq.hip):
+                                                       // PRAOS_KEYQ 1 / 0, -1 below ILP4_BATCH.  Off: no shorter
+                                                       // than the ILP-4 chain inside a step (54k 0.85-0.95 ms ->
+                                                       // 0.89-1.29) and more issue slots taken: 54k 2.72-2.74 ->
+                                                       // 2.83-2.88 ms, 108k 3.83 -> 4.08-4.12, 432k 12.03 -> 12.88
+                                                       // (profiles/r05/c9_keyq, c10_timeline54k)
+  int key_mode(size_t n) const {
+    if (keyq > 0 || (keyq < 0 && n < ILP4_BATCH)) return 2;
+    return use_key4(n) ? 1 : 0;
+  }
   int u4 = -1;                                         // cached stage U from the ILP-4 build (PRAOS_U4 1 / 0,
                                                        // -1 below ILP4_BATCH; 54k 2.79 -> 2.75 ms, 108k 3.87-3.92
                                                        // -> 3.81-3.83, profiles/r04/hh)
@@ -238,12 +254,31 @@ struct praos_ctx {
   bool replaying = false;
   bool pk_on = false;                                  // this run uses the store
   bool pk_reset[3] = {false, false, false};            // empty store t before the next run that uses it
-  // stored-bytes pipeline (praos_verify_header_bytes): each landed chunk's cold, KES leaf and VRF
-  // keys go into the stores and get their tables at once (PRAOS_E2E_PREFILL 1 / 0); the batch run
-  // after the last chunk finds them stored.  The stores are emptied at the start of every call
-  // unless PRAOS_OPT_POOL_KEYS is on, so each call builds its own tables.
-  int e2e_prefill = 1;
-  bool prefill = false;                                // inside such a call: every cache on its store
+  // stored-bytes pipeline (praos_verify_header_bytes): the cold, KES leaf and VRF keys of the
+  // landed chunks go into the stores and get their tables while later chunks upload -- in two
+  // rounds, after chunk (K-2)/2 and after chunk K-2 (PRAOS_E2E_PREFILL 1 / 0); the batch run after
+  // the last chunk finds them stored and verifies the last chunk's new keys uncached (no key
+  // precompute chain after the upload).  The stores are emptied at the start of every call unless
+  // PRAOS_OPT_POOL_KEYS is on, so each call builds its own tables.  Measured off by default: the
+  // GPU is already busy with the chunks' stage V while they upload, so the prefill only moves work
+  // (and adds the single-use leaf keys' tables and the last chunk's uncached verifies): 432k
+  // headers 16.9 ms without, 19.2 ms with (profiles/r05/c7_e2e_timeline_pf{0,1}.txt).
+  // resident header batches: a batch's run is captured once as a HIP graph (every stream's
+  // launches, memsets and event dependencies) and replayed with one launch (PRAOS_GRAPH 1 / 0).
+  // A step issues ~60 launches on 7 streams; enqueued one by one, the host call sequence put the
+  // VRF key chain's first kernel ~0.35 ms into a 54k-header step.  Measured off by default: the
+  // replayed graph runs its branches with less overlap than the streams do (54k headers 2.97 ms
+  // direct, 5.1-5.2 ms replayed; 432k 13.7 -> 16.7 ms; outputs equal at every size,
+  // profiles/r05/c6_graph_probe.txt).
+  int graphs = 0;
+  bool graph_last = false;                             // the last run was a graph launch (kernel_ms: whole run only)
+  int e2e_prefill = 0;
+  // stored-bytes pipeline: the first chunk's size in percent of the others' (PRAOS_PIPE_HEAD):
+  // nothing runs on the GPU until it has landed and been decoded
+  int pipe_head = 25;                                  // (432k headers, 8 chunks: 100 -> 16.9-17.0 ms,
+                                                       // 50 -> 16.5, 25 -> 16.3-16.4, 12 -> 16.2-16.4)
+  bool prefill = false;                                // inside such a call: every cache on its store,
+                                                       // keys not stored are misses
   // epoch
   bool have_epoch = false;
   praos_params params{};
@@ -387,6 +422,11 @@ static hipError_t d2h(praos_ctx* c, void* dst, const void* src, size_t bytes) {
 
 struct praos_batch {
   size_t n = 0;
+  // the run captured as a HIP graph (PRAOS_GRAPH): its executable and the context state it was
+  // captured under (options, epoch tables); runs counts the direct runs before it
+  hipGraphExec_t gexec = nullptr;
+  std::vector<uintptr_t> gkey;
+  int runs = 0;
   size_t body_bytes_len = 0;
   uint64_t *slot = nullptr, *ocert_n = nullptr, *ocert_c0 = nullptr, *body_off = nullptr;
   uint32_t* body_len = nullptr;
@@ -534,6 +574,18 @@ int praos_host_unregister(praos_ctx* c, void* p) {
 
 const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
+// PRAOS_SEGV_TRACE=1: a host-side crash prints the native backtrace (diagnostics on the box,
+// where no debugger is attached to a GPU process)
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  static const char msg[] = "libpraos_hip: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 // streams and events of a context (praos_open, and the pipeline's second engine)
 static bool open_streams(praos_ctx* c) {
   if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp);
@@ -555,6 +607,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_KEYQ")) c->keyq = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_U4")) c->u4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_CK4")) c->ck4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
@@ -565,6 +618,19 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_E2E_PREFILL")) c->e2e_prefill = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_GRAPH")) c->graphs = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_PIPE_HEAD")) c->pipe_head = std::max(5, std::min(100, std::atoi(e)));
+  if (std::getenv("PRAOS_SEGV_TRACE")) {
+    static char alt[1 << 16];                          // (a stack overflow needs its own stack)
+    stack_t ss{};
+    ss.ss_sp = alt;
+    ss.ss_size = sizeof alt;
+    (void)sigaltstack(&ss, nullptr);
+    struct sigaction sa{};
+    sa.sa_handler = segv_trace;
+    sa.sa_flags = SA_ONSTACK;
+    (void)sigaction(SIGSEGV, &sa, nullptr);
+  }
   (void)hipEventCreate(&c->v1_ev);
   (void)hipEventCreate(&c->kc0_ev);
   (void)hipEventCreate(&c->kc1_ev);
@@ -780,6 +846,11 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
 
 void praos_batch_free(praos_ctx* c, praos_batch* b) {
   if (!b) return;
+  if (b->gexec) {
+    if (c) (void)hipStreamSynchronize(c->stream);
+    (void)hipGraphExecDestroy(b->gexec);
+    b->gexec = nullptr;
+  }
   if (c && c->device >= 0 && b->owner == c) {
     // keep the buffers for the next batch (its kernels are ordered after this one's on
     // the ctx stream, so no wait is needed); drop the older spares it did not take
@@ -1042,11 +1113,81 @@ static int32_t overlay_class(const praos_ctx* c, uint64_t slot);
 static int batch_run_impl(praos_ctx* c, praos_batch* b);
 static int tpraos_download(praos_ctx* c, praos_batch* b, const uint8_t* dbeta_l, praos_tpraos_out* out);
 
+// The context state a captured run depends on: every option batch_run_impl reads and the
+// device tables it passes by pointer (praos_set_epoch reallocates them).
+static std::vector<uintptr_t> graph_key(const praos_ctx* c, const praos_batch* b) {
+  return {(uintptr_t)c->concurrent, (uintptr_t)c->kernels, (uintptr_t)c->keycache, (uintptr_t)c->kc_min[0],
+          (uintptr_t)c->kc_min[1], (uintptr_t)c->kc_min[2], (uintptr_t)c->dedup, (uintptr_t)c->vrf3,
+          (uintptr_t)c->vrf_prio, (uintptr_t)c->vrf_ilp4, (uintptr_t)c->v_excl, (uintptr_t)c->miss4,
+          (uintptr_t)c->miss_prio, (uintptr_t)c->kes_pair, (uintptr_t)c->kes_dedup, (uintptr_t)c->vrf_keys_first,
+          (uintptr_t)c->key4, (uintptr_t)c->keyq, (uintptr_t)c->u4, (uintptr_t)c->ck4, (uintptr_t)c->key_wave_prio,
+          (uintptr_t)c->eta0_neutral, (uintptr_t)c->npools, (uintptr_t)c->d_eta0, (uintptr_t)c->d_pool_hash,
+          (uintptr_t)c->d_pool_vrf, (uintptr_t)c->d_pool_map, (uintptr_t)c->d_pool_x, (uintptr_t)c->btab,
+          (uintptr_t)c->bcomb16, (uintptr_t)c->params.f_is_one, (uintptr_t)c->params.vrf_check_output,
+          (uintptr_t)c->params.slots_per_kes_period, (uintptr_t)c->params.max_kes_evo, (uintptr_t)b->n};
+}
+
+// A resident Praos batch run as one graph launch: the first run of a batch goes direct (it may
+// allocate: the comb, the pool-key store), the second is captured (stream capture of c->stream,
+// the side, miss and V streams joining through the run's own event dependencies) and replayed
+// from then on while graph_key matches.  The same kernels, arguments and order as the direct
+// run: only the host's per-call enqueue cost goes.
+static bool graph_eligible(const praos_ctx* c, const praos_batch* b) {
+  // (PRAOS_GRAPH 1: batches below GRAPH_BATCH headers, where the step is latency-bound and the
+  // host's enqueue cost shows; 2: every size)
+  return c->graphs > 0 && c->concurrent && b->runs >= 1 && !b->tp_only && !b->from_bytes && !b->is_block &&
+         !b->eta_tab && !c->prefill && !c->replaying && c->pool_keys <= 0 && (c->graphs > 1 || b->n < GRAPH_BATCH);
+}
+
+static int batch_run_graph(praos_ctx* c, praos_batch* b) {
+  std::vector<uintptr_t> key = graph_key(c, b);
+  if (!b->gexec || b->gkey != key) {
+    if (b->gexec) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      (void)hipGraphExecDestroy(b->gexec);
+      b->gexec = nullptr;
+    }
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+    const int r = batch_run_impl(c, b);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (r != PRAOS_OK || e != hipSuccess || !g) {
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      std::fprintf(stderr, "libpraos_hip: stream capture of the batch run failed (%s): direct runs\n",
+                   hipGetErrorString(e));
+      c->graphs = 0;                                   // (capture refused: direct runs from now on)
+      return r != PRAOS_OK ? r : batch_run_impl(c, b);
+    }
+    const hipError_t ei = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) {
+      b->gexec = nullptr;
+      (void)hipGetLastError();
+      std::fprintf(stderr, "libpraos_hip: graph instantiation failed (%s): direct runs\n", hipGetErrorString(ei));
+      c->graphs = 0;
+      return batch_run_impl(c, b);
+    }
+    b->gkey.swap(key);
+  }
+  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+  HIPCHK(c, hipGraphLaunch(b->gexec, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+  c->graph_last = true;
+  return PRAOS_OK;
+}
+
 int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (!c || !b) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
   HIPCHK(c, hipSetDevice(c->device));
   if (b->n == 0) return PRAOS_OK;
+  c->graph_last = false;
+  if (graph_eligible(c, b)) {
+    b->runs++;
+    return batch_run_graph(c, b);
+  }
+  b->runs++;
   const int r = batch_run_impl(c, b);
   if (r != PRAOS_OK && c->concurrent) {
     // work already queued on the side streams must be ordered before anything the ctx
@@ -1122,7 +1263,9 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
     HIPCHK(c, hipMemcpyAsync(ps->base, ps->count, 4, hipMemcpyDeviceToDevice, st));
     k.kt = ps->ktab; k.ki = ps->kinfo; k.erep = ps->entry_rep; k.epos = ps->entry_pos; k.emax = ps->cap;
     k.ebase = ps->base; k.store = which;
-    min_uses = 1;
+    // (after a stored-bytes prefill the keys that are not stored yet -- the last chunk's new ones --
+    // are verified uncached at once rather than through a precompute chain after the upload)
+    min_uses = c->prefill ? 0x7fffffff : 1;
   }
   launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot,
                     ps ? ps->pentry : nullptr, ps ? ps->pkey : nullptr, ps ? ps->slots - 1 : 0u);
@@ -1136,13 +1279,13 @@ static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t*
   const int prio = c->key_wave_prio > 0 || (c->key_wave_prio < 0 && n < KEY_PRIO_BATCH);
   if (k.store < 0) {
     launch_key_precompute(kind, st, k.counters, k.max_entries, k.entry_rep, keys, k.ktab, k.kinfo, prio, nullptr,
-                          k.max_entries, c->use_key4(n));
+                          k.max_entries, c->key_mode(n));
     return;
   }
   praos_ctx::PoolKeyStore& ps = c->pks[k.store];
   const uint32_t span = (uint32_t)std::min<size_t>(n, ps.cap);   // new entries of this run, at most
   launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, keys, ps.ktab, ps.kinfo, prio, ps.base, span,
-                        c->use_key4(n));
+                        c->key_mode(n));
   launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, keys, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
                       span);
 }
@@ -1174,7 +1317,7 @@ static int kc_prefill(praos_ctx* c, praos_batch* b, int t, const uint8_t* keys, 
                     ps.entry_rep, ps.entry_pos, k.counters);
   const uint32_t span = (uint32_t)std::min<size_t>(m, ps.cap);
   launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, ck, ps.ktab, ps.kinfo, prio, ps.base, span,
-                        c->use_key4(m));
+                        c->key_mode(m));
   launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, ck, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
                       span);
   HIPCHK(c, hipGetLastError());
@@ -1713,6 +1856,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
     if (value == 2) c->pk_reset[0] = c->pk_reset[1] = true;
     return PRAOS_OK;
   }
+  if (opt == PRAOS_OPT_GRAPH) { c->graphs = value < 0 ? 0 : std::min(value, 2); return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 
@@ -1722,6 +1866,14 @@ int praos_batch_sync(praos_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // per-kernel: from the common start event to each kernel's end event (with
   // concurrent streams these overlap; which = 4 is the whole run)
+  if (c->graph_last) {
+    // a graph launch: the whole run is timed (events around the launch), its kernels are not
+    float all = 0;
+    (void)hipEventElapsedTime(&all, c->ev[0], c->ev[4]);
+    for (int k = 0; k < 8; k++) c->kernel_ms[k] = -1.f;
+    c->kernel_ms[4] = all;
+    return PRAOS_OK;
+  }
   float t[3] = {0, 0, 0};
   for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&t[k], c->ev[0], c->side_ev[k]);
   if (c->concurrent) {
@@ -2053,7 +2205,12 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   // need (relative to base); chunk k's upload covers what earlier chunks did not
   std::vector<size_t> lo(K + 1);
   std::vector<uint64_t> need(K);
-  for (int k = 0; k <= K; k++) lo[k] = n * k / K;
+  {
+    // weights: head / 100 for chunk 0, 1 for the others
+    const size_t W = (size_t)c->pipe_head + 100 * (size_t)(K - 1);
+    lo[0] = 0;
+    for (int k = 1; k <= K; k++) lo[k] = n * ((size_t)c->pipe_head + 100 * (size_t)(k - 1)) / W;
+  }
   uint64_t hw = 0;
   for (int k = 0; k < K; k++) {
     for (size_t i = lo[k]; i < lo[k + 1]; i++)
@@ -2090,7 +2247,8 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   const bool vrf = (c->kernels & 4) != 0;
   // key prefill per landed chunk (see praos_ctx::e2e_prefill): Praos header batches with the key
   // caches and all three crypto passes on their concurrent streams
-  const bool prefill = c->e2e_prefill > 0 && c->keycache > 0 && c->concurrent && c->kernels == 7 && n >= 2;
+  const bool prefill = c->e2e_prefill > 0 && c->keycache > 0 && c->concurrent && c->kernels == 7 && n >= 2 && K >= 3;
+  int pf_chunk = 0;                               // first chunk the next prefill round covers
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
@@ -2108,22 +2266,24 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
                         b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
-    if (prefill) {
-      // cache t on the stream its run uses: cold keys side[0], KES leaf keys side[1], VRF keys side[2]
+    if (prefill && (k == (K - 2) / 2 || k == K - 2)) {
+      // the keys of chunks [pf_lo, k] in two rounds: a key precompute is one long chain per key
+      // whatever the number of keys, so one round per chunk would queue K chains back to back
+      // on each cache's stream.  Cache t on the stream its run uses: cold keys side[0], KES leaf
+      // keys side[1], VRF keys side[2]
       const int sidx[3] = {0, 2, 1};
+      const size_t a = lo[pf_chunk], z = lo[k + 1], mz = z - a;
       for (int t : {1, 0, 2}) {
         hipStream_t st = c->side[sidx[t]];
         HIPCHK(c, hipStreamWaitEvent(st, c->done_ev[k], 0));
         const uint8_t* keys = t == 0 ? b->cold_vk : (t == 1 ? b->vrf_vk : b->kes_leaf);
         if (t == 2)
-          launch_kes_leafkeys(dim3(nblocks(m, NT)), dim3(NT), st, m, b->kes_sig + 448 * lo[k], b->slot + lo[k],
-                              b->ocert_c0 + lo[k], c->params.slots_per_kes_period, b->kes_leaf + 32 * lo[k]);
-        // (the last chunk's new keys head the cached chains of the run that follows: raised wave
-        // priority for them; the earlier chunks' fill the SIMDs the chunks' stage V leaves)
-        const int r = kc_prefill(c, b, t, keys, t == 1 ? 1 : 0, lo[k], lo[k + 1], st, k == 0 && c->pool_keys <= 0,
-                                 k == K - 1 ? 1 : 0);
+          launch_kes_leafkeys(dim3(nblocks(mz, NT)), dim3(NT), st, mz, b->kes_sig + 448 * a, b->slot + a,
+                              b->ocert_c0 + a, c->params.slots_per_kes_period, b->kes_leaf + 32 * a);
+        const int r = kc_prefill(c, b, t, keys, t == 1 ? 1 : 0, a, z, st, pf_chunk == 0 && c->pool_keys <= 0, 0);
         if (r != PRAOS_OK) return r;
       }
+      pf_chunk = k + 1;
     }
     if (vrf) {
       // the chunks' stage V alternate between two streams: on one they would queue behind
@@ -2172,7 +2332,7 @@ int praos_verify_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_
   if (in->n == 0) return PRAOS_OK;
   if (in->n && (!in->off || !in->len || (!in->bytes && in->bytes_len))) return PRAOS_E_ARG;
   {
-    // chunked pipeline (PRAOS_OPT_PIPELINE: chunks; 0 = auto: up to 4 chunks of >= 64k headers)
+    // chunked pipeline (PRAOS_OPT_PIPELINE: chunks; 0 = auto: up to PIPE_AUTO chunks of >= PIPE_MIN_CHUNK)
     int K = c->pipeline;
     if (K == 0) K = (int)std::min<size_t>(PIPE_AUTO, in->n / PIPE_MIN_CHUNK);
     K = std::min<int>(K, (int)std::min<size_t>(PIPE_MAX, in->n));
