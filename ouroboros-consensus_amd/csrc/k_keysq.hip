@@ -28,13 +28,23 @@ FE_INLINE void fe_quad(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = quad_lane<L>(a.v[i]);
 }
-FE_INLINE void fe_sel4(fe& r, uint32_t q, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+// lane masks of the quad position (all ones where q == i), made once: a select written as
+// nested conditionals compiled to divergent branches, four exec-masked paths per limb
+struct QMask { uint32_t m[4]; };
+FE_INLINE QMask quad_masks(uint32_t q) {
+  QMask k;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = q == 0 ? a0.v[i] : (q == 1 ? a1.v[i] : (q == 2 ? a2.v[i] : a3.v[i]));
+  for (int i = 0; i < 4; i++) k.m[i] = 0u - (uint32_t)(q == (uint32_t)i);
+  return k;
+}
+FE_INLINE void fe_sel4(fe& r, const QMask& k, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    r.v[i] = (a0.v[i] & k.m[0]) | (a1.v[i] & k.m[1]) | (a2.v[i] & k.m[2]) | (a3.v[i] & k.m[3]);
 }
 
 // (X : Y : Z) <- 2 (X : Y : Z) as p2; with T: the p3 coordinate T of the result too
-FE_INLINE void quad_dbl(fe& X, fe& Y, fe& Z, fe* T, uint32_t q) {
+FE_INLINE void quad_dbl(fe& X, fe& Y, fe& Z, fe* T, const QMask& q) {
   fe s, xy;
   fe_add(xy, X, Y);
   fe_sel4(s, q, X, Y, Z, xy);
@@ -63,18 +73,19 @@ FE_INLINE void quad_dbl(fe& X, fe& Y, fe& Z, fe* T, uint32_t q) {
 // key_chunk_bases over a quad: Q_0 = P, Q_{k+1} = 2^16 Q_k, lane q stores coordinate q of Q_k
 // (a ge_p3 in the 128 bytes of ktab[8k], as pass 2 reads it)
 FE_INLINE void quad_chunk_bases(ge_cached* __restrict__ ktab, const ge_p3& P, int nchunks, uint32_t q, bool write) {
+  const QMask m = quad_masks(q);
   fe X = P.X, Y = P.Y, Z = P.Z, T = P.T;
 #pragma clang loop unroll(disable)
   for (int k = 0; k < nchunks; k++) {
     if (write) {
       fe w;
-      fe_sel4(w, q, X, Y, Z, T);
+      fe_sel4(w, m, X, Y, Z, T);
       store_words((uint8_t*)(ktab + 8 * k) + 32 * q, w.v, 8);
     }
     if (k + 1 < nchunks) {
 #pragma clang loop unroll(disable)
-      for (int d = 0; d < 15; d++) quad_dbl(X, Y, Z, nullptr, q);
-      quad_dbl(X, Y, Z, &T, q);
+      for (int d = 0; d < 15; d++) quad_dbl(X, Y, Z, nullptr, m);
+      quad_dbl(X, Y, Z, &T, m);
     }
   }
 }

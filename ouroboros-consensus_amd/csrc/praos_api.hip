@@ -191,11 +191,13 @@ struct praos_ctx {
                                                        // -> 2.76-2.77 ms; 108k 4.17 -> 4.21, profiles/r04/n)
   bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < ILP4_BATCH); }
   int keyq = 0;                                        // key precompute with four lanes per key (k_keysq.hip):
-                                                       // PRAOS_KEYQ 1 / 0, -1 below ILP4_BATCH.  Off: no shorter
-                                                       // than the ILP-4 chain inside a step (54k 0.85-0.95 ms ->
-                                                       // 0.89-1.29) and more issue slots taken: 54k 2.72-2.74 ->
-                                                       // 2.83-2.88 ms, 108k 3.83 -> 4.08-4.12, 432k 12.03 -> 12.88
-                                                       // (profiles/r05/c9_keyq, c10_timeline54k)
+                                                       // PRAOS_KEYQ 1 / 0, -1 below ILP4_BATCH.  Off: inside a
+                                                       // step its chains are about as long as the ILP-4 build's
+                                                       // (54k: cold 0.90 -> 0.65 ms, KES 0.85 -> 1.09, VRF 0.95 ->
+                                                       // 0.90) and its four lanes per key take issue slots from
+                                                       // the rest: 54k 2.72-2.75 -> 2.84-2.88 ms, 108k 3.79-3.84
+                                                       // -> 4.00 (profiles/r05/c11_keyq_nobranch; c9_keyq: the
+                                                       // first build, whose selects compiled to branches)
   int key_mode(size_t n) const {
     if (keyq > 0 || (keyq < 0 && n < ILP4_BATCH)) return 2;
     return use_key4(n) ? 1 : 0;
