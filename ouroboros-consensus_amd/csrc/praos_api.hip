@@ -258,13 +258,17 @@ struct praos_ctx {
   bool pk_reset[3] = {false, false, false};            // empty store t before the next run that uses it
   // stored-bytes pipeline (praos_verify_header_bytes): the cold, KES leaf and VRF keys of the
   // landed chunks go into the stores and get their tables while later chunks upload -- in two
-  // rounds, after chunk (K-2)/2 and after chunk K-2 (PRAOS_E2E_PREFILL 1 / 0); the batch run after
-  // the last chunk finds them stored and verifies the last chunk's new keys uncached (no key
-  // precompute chain after the upload).  The stores are emptied at the start of every call unless
-  // PRAOS_OPT_POOL_KEYS is on, so each call builds its own tables.  Measured off by default: the
-  // GPU is already busy with the chunks' stage V while they upload, so the prefill only moves work
-  // (and adds the single-use leaf keys' tables and the last chunk's uncached verifies): 432k
-  // headers 16.9 ms without, 19.2 ms with (profiles/r05/c7_e2e_timeline_pf{0,1}.txt).
+  // rounds, after chunk (K-2)/2 and after chunk K-2 (PRAOS_E2E_PREFILL 1 / 0), each caching the
+  // keys used at least the usual count within its range; the batch run after the last chunk
+  // finds them stored and caches the rest by their count over the whole batch (its precompute
+  // chain then covers only the keys the prefill did not).  The stores are emptied at the start of
+  // every call unless PRAOS_OPT_POOL_KEYS is on, so each call builds its own tables.  Off by
+  // default, measured slower in both forms: the GPU is busy with the chunks' stage V while they
+  // upload, so the prefill only moves work there, and any key first seen in the last chunk still
+  // needs one latency-bound chain (a precompute or an uncached verify) after it lands.  432k
+  // headers, 8 chunks: 16.3-16.4 ms without, 18.2-18.5 ms with (profiles/r05/c12_prefill_v3);
+  // the first form (every key of a prefill range cached, the last chunk's new keys verified
+  // uncached): 16.9 -> 19.2 ms (profiles/r05/c7_e2e_timeline_pf{0,1}.txt).
   // resident header batches: a batch's run is captured once as a HIP graph (every stream's
   // launches, memsets and event dependencies) and replayed with one launch (PRAOS_GRAPH 1 / 0).
   // A step issues ~60 launches on 7 streams; enqueued one by one, the host call sequence put the
@@ -1265,9 +1269,10 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
     HIPCHK(c, hipMemcpyAsync(ps->base, ps->count, 4, hipMemcpyDeviceToDevice, st));
     k.kt = ps->ktab; k.ki = ps->kinfo; k.erep = ps->entry_rep; k.epos = ps->entry_pos; k.emax = ps->cap;
     k.ebase = ps->base; k.store = which;
-    // (after a stored-bytes prefill the keys that are not stored yet -- the last chunk's new ones --
-    // are verified uncached at once rather than through a precompute chain after the upload)
-    min_uses = c->prefill ? 0x7fffffff : 1;
+    // (after a stored-bytes prefill, the keys not stored yet -- the last chunk's new ones, and the
+    // ones used once per prefill range -- are cached only from the usual count: a single-use key's
+    // tables cost more than its uncached verify)
+    if (!c->prefill) min_uses = 1;
   }
   launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot,
                     ps ? ps->pentry : nullptr, ps ? ps->pkey : nullptr, ps ? ps->slots - 1 : 0u);
@@ -1315,8 +1320,11 @@ static int kc_prefill(praos_ctx* c, praos_batch* b, int t, const uint8_t* keys, 
   const uint8_t* ck = keys + 32 * lo;                   // the chunk's keys (item ids relative to lo)
   launch_key_insert(dim3(nblocks(m, NT)), dim3(NT), st, m, nullptr, nullptr, ck, k.cap - 1, k.slot_rep, k.slot_cnt,
                     k.item_slot + lo, ps.pentry, ps.pkey, ps.slots - 1);
-  launch_key_assign(dim3(nblocks(k.cap, NT)), dim3(NT), st, k.cap, k.slot_rep, k.slot_cnt, 1u, ps.cap, k.slot_entry,
-                    ps.entry_rep, ps.entry_pos, k.counters);
+  // keys used at least the usual count within the landed range; the others are counted again by
+  // the run after the last chunk
+  const uint32_t min_uses = (uint32_t)std::max(1, c->kc_min[t] > 0 ? c->kc_min[t] : c->keycache);
+  launch_key_assign(dim3(nblocks(k.cap, NT)), dim3(NT), st, k.cap, k.slot_rep, k.slot_cnt, min_uses, ps.cap,
+                    k.slot_entry, ps.entry_rep, ps.entry_pos, k.counters);
   const uint32_t span = (uint32_t)std::min<size_t>(m, ps.cap);
   launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, ck, ps.ktab, ps.kinfo, prio, ps.base, span,
                         c->key_mode(m));
