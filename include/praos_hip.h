@@ -222,12 +222,6 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * byte; verdicts are identical either way.  1 = on, 0 = off, 2 = on and emptied before the
  * next run.  A store more than 3/4 full is emptied before a run. */
 #define PRAOS_OPT_POOL_KEYS 7
-/* PRAOS_OPT_GRAPH (default 0): a resident batch's praos_batch_run is captured once as a HIP
- * graph (its second run; every stream's launches, copies and event dependencies) and replayed
- * with one launch while the options and epoch tables stay the same (1 = batches below 300,000
- * headers, 2 = every size, 0 = direct launches).  Off by default: measured slower than the
- * direct launches on every size.  Outputs are identical either way. */
-#define PRAOS_OPT_GRAPH 8
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items

@@ -21,9 +21,6 @@ static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBo
 #include <condition_variable>
 #include <cstdlib>
 #include <cstdio>
-#include <csignal>
-#include <execinfo.h>
-#include <unistd.h>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -107,7 +104,6 @@ static constexpr size_t KEY_PRIO_BATCH = 400000;
 // (profiles/r04/y: 96k 4.06 -> 3.64 ms, 108k 4.25 -> 4.10, 112k 4.39 -> 4.15; equal at 120k,
 // slower at 128k)
 static constexpr size_t ILP4_BATCH = 120000;
-static constexpr size_t GRAPH_BATCH = 300000;        // PRAOS_GRAPH = 1: graphs below this many headers
 static constexpr int PIPE_AUTO = 8;                 // chunks in auto mode (round 3, equal chunks: 4 -> 21.9M,
                                                     // 6 -> 23.0M, 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt;
                                                     // round 5 with the first chunk at 1/4 of the others: 6 ->
@@ -269,15 +265,6 @@ struct praos_ctx {
   // headers, 8 chunks: 16.3-16.4 ms without, 18.2-18.5 ms with (profiles/r05/c12_prefill_v3);
   // the first form (every key of a prefill range cached, the last chunk's new keys verified
   // uncached): 16.9 -> 19.2 ms (profiles/r05/c7_e2e_timeline_pf{0,1}.txt).
-  // resident header batches: a batch's run is captured once as a HIP graph (every stream's
-  // launches, memsets and event dependencies) and replayed with one launch (PRAOS_GRAPH 1 / 0).
-  // A step issues ~60 launches on 7 streams; enqueued one by one, the host call sequence put the
-  // VRF key chain's first kernel ~0.35 ms into a 54k-header step.  Measured off by default: the
-  // replayed graph runs its branches with less overlap than the streams do (54k headers 2.97 ms
-  // direct, 5.1-5.2 ms replayed; 432k 13.7 -> 16.7 ms; outputs equal at every size,
-  // profiles/r05/c6_graph_probe.txt).
-  int graphs = 0;
-  bool graph_last = false;                             // the last run was a graph launch (kernel_ms: whole run only)
   int e2e_prefill = 0;
   // stored-bytes pipeline: the first chunk's size in percent of the others' (PRAOS_PIPE_HEAD):
   // nothing runs on the GPU until it has landed and been decoded
@@ -428,11 +415,6 @@ static hipError_t d2h(praos_ctx* c, void* dst, const void* src, size_t bytes) {
 
 struct praos_batch {
   size_t n = 0;
-  // the run captured as a HIP graph (PRAOS_GRAPH): its executable and the context state it was
-  // captured under (options, epoch tables); runs counts the direct runs before it
-  hipGraphExec_t gexec = nullptr;
-  std::vector<uintptr_t> gkey;
-  int runs = 0;
   size_t body_bytes_len = 0;
   uint64_t *slot = nullptr, *ocert_n = nullptr, *ocert_c0 = nullptr, *body_off = nullptr;
   uint32_t* body_len = nullptr;
@@ -580,18 +562,6 @@ int praos_host_unregister(praos_ctx* c, void* p) {
 
 const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 
-// PRAOS_SEGV_TRACE=1: a host-side crash prints the native backtrace (diagnostics on the box,
-// where no debugger is attached to a GPU process)
-static void segv_trace(int sig) {
-  void* fr[64];
-  const int n = backtrace(fr, 64);
-  static const char msg[] = "libpraos_hip: fatal signal, native backtrace:\n";
-  (void)!write(2, msg, sizeof msg - 1);
-  backtrace_symbols_fd(fr, n, 2);
-  signal(sig, SIG_DFL);
-  raise(sig);
-}
-
 // streams and events of a context (praos_open, and the pipeline's second engine)
 static bool open_streams(praos_ctx* c) {
   if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp);
@@ -624,19 +594,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_E2E_PREFILL")) c->e2e_prefill = std::atoi(e);
-  if (const char* e = std::getenv("PRAOS_GRAPH")) c->graphs = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PIPE_HEAD")) c->pipe_head = std::max(5, std::min(100, std::atoi(e)));
-  if (std::getenv("PRAOS_SEGV_TRACE")) {
-    static char alt[1 << 16];                          // (a stack overflow needs its own stack)
-    stack_t ss{};
-    ss.ss_sp = alt;
-    ss.ss_size = sizeof alt;
-    (void)sigaltstack(&ss, nullptr);
-    struct sigaction sa{};
-    sa.sa_handler = segv_trace;
-    sa.sa_flags = SA_ONSTACK;
-    (void)sigaction(SIGSEGV, &sa, nullptr);
-  }
   (void)hipEventCreate(&c->v1_ev);
   (void)hipEventCreate(&c->kc0_ev);
   (void)hipEventCreate(&c->kc1_ev);
@@ -852,11 +810,6 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
 
 void praos_batch_free(praos_ctx* c, praos_batch* b) {
   if (!b) return;
-  if (b->gexec) {
-    if (c) (void)hipStreamSynchronize(c->stream);
-    (void)hipGraphExecDestroy(b->gexec);
-    b->gexec = nullptr;
-  }
   if (c && c->device >= 0 && b->owner == c) {
     // keep the buffers for the next batch (its kernels are ordered after this one's on
     // the ctx stream, so no wait is needed); drop the older spares it did not take
@@ -1119,81 +1072,11 @@ static int32_t overlay_class(const praos_ctx* c, uint64_t slot);
 static int batch_run_impl(praos_ctx* c, praos_batch* b);
 static int tpraos_download(praos_ctx* c, praos_batch* b, const uint8_t* dbeta_l, praos_tpraos_out* out);
 
-// The context state a captured run depends on: every option batch_run_impl reads and the
-// device tables it passes by pointer (praos_set_epoch reallocates them).
-static std::vector<uintptr_t> graph_key(const praos_ctx* c, const praos_batch* b) {
-  return {(uintptr_t)c->concurrent, (uintptr_t)c->kernels, (uintptr_t)c->keycache, (uintptr_t)c->kc_min[0],
-          (uintptr_t)c->kc_min[1], (uintptr_t)c->kc_min[2], (uintptr_t)c->dedup, (uintptr_t)c->vrf3,
-          (uintptr_t)c->vrf_prio, (uintptr_t)c->vrf_ilp4, (uintptr_t)c->v_excl, (uintptr_t)c->miss4,
-          (uintptr_t)c->miss_prio, (uintptr_t)c->kes_pair, (uintptr_t)c->kes_dedup, (uintptr_t)c->vrf_keys_first,
-          (uintptr_t)c->key4, (uintptr_t)c->keyq, (uintptr_t)c->u4, (uintptr_t)c->ck4, (uintptr_t)c->key_wave_prio,
-          (uintptr_t)c->eta0_neutral, (uintptr_t)c->npools, (uintptr_t)c->d_eta0, (uintptr_t)c->d_pool_hash,
-          (uintptr_t)c->d_pool_vrf, (uintptr_t)c->d_pool_map, (uintptr_t)c->d_pool_x, (uintptr_t)c->btab,
-          (uintptr_t)c->bcomb16, (uintptr_t)c->params.f_is_one, (uintptr_t)c->params.vrf_check_output,
-          (uintptr_t)c->params.slots_per_kes_period, (uintptr_t)c->params.max_kes_evo, (uintptr_t)b->n};
-}
-
-// A resident Praos batch run as one graph launch: the first run of a batch goes direct (it may
-// allocate: the comb, the pool-key store), the second is captured (stream capture of c->stream,
-// the side, miss and V streams joining through the run's own event dependencies) and replayed
-// from then on while graph_key matches.  The same kernels, arguments and order as the direct
-// run: only the host's per-call enqueue cost goes.
-static bool graph_eligible(const praos_ctx* c, const praos_batch* b) {
-  // (PRAOS_GRAPH 1: batches below GRAPH_BATCH headers, where the step is latency-bound and the
-  // host's enqueue cost shows; 2: every size)
-  return c->graphs > 0 && c->concurrent && b->runs >= 1 && !b->tp_only && !b->from_bytes && !b->is_block &&
-         !b->eta_tab && !c->prefill && !c->replaying && c->pool_keys <= 0 && (c->graphs > 1 || b->n < GRAPH_BATCH);
-}
-
-static int batch_run_graph(praos_ctx* c, praos_batch* b) {
-  std::vector<uintptr_t> key = graph_key(c, b);
-  if (!b->gexec || b->gkey != key) {
-    if (b->gexec) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      (void)hipGraphExecDestroy(b->gexec);
-      b->gexec = nullptr;
-    }
-    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
-    const int r = batch_run_impl(c, b);
-    hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(c->stream, &g);
-    if (r != PRAOS_OK || e != hipSuccess || !g) {
-      if (g) (void)hipGraphDestroy(g);
-      (void)hipGetLastError();
-      std::fprintf(stderr, "libpraos_hip: stream capture of the batch run failed (%s): direct runs\n",
-                   hipGetErrorString(e));
-      c->graphs = 0;                                   // (capture refused: direct runs from now on)
-      return r != PRAOS_OK ? r : batch_run_impl(c, b);
-    }
-    const hipError_t ei = hipGraphInstantiate(&b->gexec, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (ei != hipSuccess) {
-      b->gexec = nullptr;
-      (void)hipGetLastError();
-      std::fprintf(stderr, "libpraos_hip: graph instantiation failed (%s): direct runs\n", hipGetErrorString(ei));
-      c->graphs = 0;
-      return batch_run_impl(c, b);
-    }
-    b->gkey.swap(key);
-  }
-  HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
-  HIPCHK(c, hipGraphLaunch(b->gexec, c->stream));
-  HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
-  c->graph_last = true;
-  return PRAOS_OK;
-}
-
 int praos_batch_run(praos_ctx* c, praos_batch* b) {
   if (!c || !b) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
   HIPCHK(c, hipSetDevice(c->device));
   if (b->n == 0) return PRAOS_OK;
-  c->graph_last = false;
-  if (graph_eligible(c, b)) {
-    b->runs++;
-    return batch_run_graph(c, b);
-  }
-  b->runs++;
   const int r = batch_run_impl(c, b);
   if (r != PRAOS_OK && c->concurrent) {
     // work already queued on the side streams must be ordered before anything the ctx
@@ -1866,7 +1749,6 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
     if (value == 2) c->pk_reset[0] = c->pk_reset[1] = true;
     return PRAOS_OK;
   }
-  if (opt == PRAOS_OPT_GRAPH) { c->graphs = value < 0 ? 0 : std::min(value, 2); return PRAOS_OK; }
   return PRAOS_E_ARG;
 }
 
@@ -1876,14 +1758,6 @@ int praos_batch_sync(praos_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // per-kernel: from the common start event to each kernel's end event (with
   // concurrent streams these overlap; which = 4 is the whole run)
-  if (c->graph_last) {
-    // a graph launch: the whole run is timed (events around the launch), its kernels are not
-    float all = 0;
-    (void)hipEventElapsedTime(&all, c->ev[0], c->ev[4]);
-    for (int k = 0; k < 8; k++) c->kernel_ms[k] = -1.f;
-    c->kernel_ms[4] = all;
-    return PRAOS_OK;
-  }
   float t[3] = {0, 0, 0};
   for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&t[k], c->ev[0], c->side_ev[k]);
   if (c->concurrent) {

@@ -143,44 +143,6 @@ def test_stream_schedule_equivalence(ctx, oracle):
         assert int(outs[1]["bits"][i]) & BITS_FROM_ORACLE == rr["bits"], (i, hex(outs[1]["bits"][i]), hex(rr["bits"]))
 
 
-def test_graph_replay_equivalence(ctx):
-    """A resident batch run again and again with PRAOS_OPT_GRAPH on (the first run direct, the
-    second captured as a HIP graph, the others replayed from it; a changed option or a new epoch
-    re-captures) gives the serial schedule's outputs bit for bit on every run, with cache
-    hits and misses in all three caches and the OCert dedup on."""
-    from praos_hip import abi
-    H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 1500, 23, 1500, seed=b"\x5b" * 32)
-    r = rng(78)
-    for j in range(0, 60, 3):
-        H["cold_vk"][100 + j] = np.frombuffer(rbytes(r, 32), np.uint8)
-        H["vrf_vk"][400 + j] = np.frombuffer(rbytes(r, 32), np.uint8)
-        H["slot"][700 + j] += 129600 * (1 + j % 3)
-    n = len(H["slot"])
-    ctx.set_option(abi.OPT_CONCURRENT, 0)
-    ref = _run_batch(ctx, H, 2, dedup=1)[0]
-    ctx.set_option(abi.OPT_CONCURRENT, 1)
-    ctx.set_option(abi.OPT_GRAPH, 2)
-    b = ctx.upload(H)
-    try:
-        outs = []
-        for k in range(6):
-            if k == 4:
-                ctx.set_option(abi.OPT_DEDUP, 0)          # a new option set: captured again
-            if k == 5:
-                ctx.set_epoch(eta0, pool_list, p)         # new epoch tables (reallocated): captured again
-            ctx.run(b)
-            ctx.sync()
-            outs.append(ctx.download(b, n))
-            assert ctx.kernel_ms(4) > 0
-    finally:
-        ctx.set_option(abi.OPT_GRAPH, 0)
-        ctx.set_option(abi.OPT_DEDUP, 1)
-        ctx.free(b)
-    for k, o in enumerate(outs):
-        for key in ("bits", "beta", "leader", "nonce", "pool_idx"):
-            assert np.array_equal(o[key], ref[key]), (k, key)
-
-
 def test_header_edge_inputs(ctx, oracle):
     """Unknown issuer, wrong VRF key, KES period out of range, neutral nonce."""
     H, pool_list, corrupted, p, c_raw, eta0 = _chain(ctx, 64, 5, 0, seed=b"\x07" * 32)
