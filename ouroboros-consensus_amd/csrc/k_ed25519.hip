@@ -27,6 +27,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_ocert_ck(const uint32_t* __restri
   const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= items) return;
+  wave_setprio(a.wave_prio);
   const size_t i = list[t];
   const size_t e = (size_t)item_entry[i];
   uint32_t pk[8], sg[16], hram[16];
@@ -73,6 +74,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck(const uint32_t* __restrict
   const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
   const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= items) return;
+  wave_setprio(a.wave_prio);
   const size_t i = list[q];
   const size_t e = (size_t)item_entry[i];
   uint32_t sg[16], leaf[8], hram[16];
@@ -98,6 +100,7 @@ __global__ void __launch_bounds__(NT, LB_ED) k_kes_ck2(const uint32_t* __restric
   const ge_niels* btab = gbtab;                                 // the radix-2^16 comb, read in place
   const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= lanes) return;
+  wave_setprio(a.wave_prio);
   const bool has_b = q + lanes < items;                         // a second header (paired batches)
   const size_t ia = list[q];
   uint32_t sg[16], leaf[8], hram[16];
@@ -201,8 +204,9 @@ void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* 
                      const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                      const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
                      const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo,
-                     uint16_t* bits, uint8_t* ok_out) {
-  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out, nullptr};
+                     uint16_t* bits, uint8_t* ok_out, int prio) {
+  OcertIn a{cold_vk, hot_vk, ocert_n, ocert_c0, sig, slot, slots_per_kes_period, max_kes_evo, bits, ok_out, nullptr,
+            prio};
   hipLaunchKernelGGL(k_ocert_ck, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a);
 }
 
@@ -220,9 +224,9 @@ void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    const uint8_t* hot_vk, const uint8_t* kes_sig, const uint64_t* body_off, const uint32_t* body_len,
                    const uint8_t* body, size_t body_bytes_len, const uint64_t* slot, const uint64_t* ocert_c0,
                    uint64_t slots_per_kes_period, uint16_t* bits, uint32_t pair_min, const uint32_t* entry_rep,
-                   const uint8_t* rep_ok) {
+                   const uint8_t* rep_ok, int prio) {
   KesIn a{hot_vk, kes_sig, body_off, body_len, body, body_bytes_len, slot, ocert_c0, slots_per_kes_period,
-          nullptr, bits, nullptr, nullptr};
+          nullptr, bits, nullptr, nullptr, prio};
   if (pair_min)     // (the one-header kernel keeps its registers: the paired one spills 176 bytes)
     hipLaunchKernelGGL(k_kes_ck2, grid, block, 0, stream, list, count, item_entry, ktab, kinfo, gbtab, a, pair_min,
                        entry_rep, rep_ok);

@@ -19,6 +19,7 @@ struct OcertIn {
   uint16_t* __restrict__ bits;
   uint8_t* __restrict__ ok_out;
   ge_cached* __restrict__ tabs;          // per-lane tables (LT_ED entries per item)
+  int wave_prio;                         // cached verifies: waves at s_setprio <wave_prio> (0 = off)
 };
 
 __device__ __forceinline__ void ocert_store(const OcertIn& a, size_t i, bool ok) {
@@ -62,6 +63,7 @@ struct KesIn {
   uint16_t* __restrict__ bits;
   uint8_t* __restrict__ result;
   ge_cached* __restrict__ tabs;
+  int wave_prio;                         // cached verifies: waves at s_setprio <wave_prio> (0 = off)
 };
 
 __device__ __forceinline__ uint64_t kes_t(const KesIn& a, size_t i) {

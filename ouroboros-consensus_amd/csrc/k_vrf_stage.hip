@@ -122,9 +122,11 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_u(size_t stride, const uin
                                                       const ge_cached* __restrict__ ktab,
                                                       const uint32_t* __restrict__ kinfo,
                                                       const ge_niels* __restrict__ comb,
-                                                      const uint8_t* __restrict__ vrf_proof, uint4* __restrict__ mid) {
+                                                      const uint8_t* __restrict__ vrf_proof, uint4* __restrict__ mid,
+                                                      int prio) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (size_t)*count) return;
+  wave_setprio(prio);
   const size_t i = list[t];
   const size_t e = (size_t)item_entry[i];
   uint32_t pr[20];
@@ -325,14 +327,15 @@ void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const ui
 }
 void launch_vrf_u(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
                   const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const ge_niels* gbtab,
-                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid, int ilp4) {
+                  const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid, int ilp4,
+                  int prio) {
   const dim3 g((unsigned)((n + NT - 1) / NT));
   const unsigned bs = lat_block(n);
   if (ktab && ilp4)
-    launch_vrf_u4(stream, n, list, count, item_entry, ktab, kinfo, comb, vrf_proof, mid);
+    launch_vrf_u4(stream, n, list, count, item_entry, ktab, kinfo, comb, vrf_proof, mid, prio);
   else if (ktab)
     hipLaunchKernelGGL(k_vrf_u, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, list, count, item_entry,
-                       ktab, kinfo, comb, vrf_proof, (uint4*)mid);
+                       ktab, kinfo, comb, vrf_proof, (uint4*)mid, prio);
   else
     hipLaunchKernelGGL(k_vrf_u_nc, g, dim3(NT), 0, stream, n, list, count, gbtab, vrf_vk, vrf_proof, utabs,
                        (uint4*)mid);

@@ -43,9 +43,11 @@ __global__ void __launch_bounds__(NT, 2) k_vrf_u4(size_t stride, const uint32_t*
                                                   const ge_cached* __restrict__ ktab,
                                                   const uint32_t* __restrict__ kinfo,
                                                   const ge_niels* __restrict__ comb,
-                                                  const uint8_t* __restrict__ vrf_proof, uint4* __restrict__ mid) {
+                                                  const uint8_t* __restrict__ vrf_proof, uint4* __restrict__ mid,
+                                                  int prio) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (size_t)*count) return;
+  wave_setprio(prio);
   const size_t i = list[t];
   const size_t e = (size_t)item_entry[i];
   uint32_t pr[20];
@@ -55,9 +57,9 @@ __global__ void __launch_bounds__(NT, 2) k_vrf_u4(size_t stride, const uint32_t*
 
 void launch_vrf_u4(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
                    const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const uint8_t* vrf_proof,
-                   void* mid) {
+                   void* mid, int prio) {
   hipLaunchKernelGGL(k_vrf_u4, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, n, list, count, item_entry,
-                     ktab, kinfo, comb, vrf_proof, (uint4*)mid);
+                     ktab, kinfo, comb, vrf_proof, (uint4*)mid, prio);
 }
 
 void launch_vrf_v4(hipStream_t stream, size_t n, size_t i0, size_t i1, const uint8_t* vrf_vk,

@@ -66,3 +66,9 @@ __device__ __forceinline__ const ge_niels* stage_btab(const ge_niels* __restrict
   __syncthreads();
   return s;
 }
+
+// s_setprio takes an immediate: wave priority 2 or 3 from a runtime value (0 and others: unchanged)
+__device__ __forceinline__ void wave_setprio(int p) {
+  if (p == 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+}

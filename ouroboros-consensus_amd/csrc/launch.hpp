@@ -19,7 +19,7 @@ void launch_ocert_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* 
                      const int32_t* item_entry, const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* gbtab,
                      const uint8_t* cold_vk, const uint8_t* hot_vk, const uint64_t* ocert_n, const uint64_t* ocert_c0,
                      const uint8_t* sig, const uint64_t* slot, uint64_t slots_per_kes_period, uint64_t max_kes_evo,
-                     uint16_t* bits, uint8_t* ok_out);
+                     uint16_t* bits, uint8_t* ok_out, int prio = 0);
 void launch_vrf(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                 const ge_niels* gbtab, const uint8_t* cold_vk, const uint8_t* vrf_vk, const uint8_t* vrf_out,
                 const uint8_t* vrf_proof, const uint64_t* slot, const uint32_t* eta0, int eta0_neutral,
@@ -100,7 +100,7 @@ void launch_kes_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
                    uint64_t slots_per_kes_period, uint16_t* bits,
                    uint32_t pair_min,                       // two headers per lane from pair_min hits on (0: never)
                    const uint32_t* entry_rep,               // with rep_ok (k_kes_merkle_reps): the Merkle path
-                   const uint8_t* rep_ok);                  // dedup per cache entry (null: every item walks)
+                   const uint8_t* rep_ok, int prio = 0);                  // dedup per cache entry (null: every item walks)
 void launch_kes_merkle_reps(hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                             const uint32_t* entry_rep, const uint8_t* hot_vk, const uint8_t* kes_sig,
                             const uint64_t* slot, const uint64_t* ocert_c0, uint64_t slots_per_kes_period,
@@ -160,10 +160,11 @@ void launch_vrf_fin(hipStream_t stream, size_t n, const uint32_t* list, const ui
 void launch_vrf_u(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
                   const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const ge_niels* gbtab,
                   const uint8_t* vrf_vk, const uint8_t* vrf_proof, ge_cached* utabs, void* mid,
-                  int ilp4 = 0);                           // cached keys: the ILP-4 build (k_vrf_v4.hip k_vrf_u4)
+                  int ilp4 = 0,                            // cached keys: the ILP-4 build (k_vrf_v4.hip k_vrf_u4)
+                  int prio = 0);                           // cached keys: waves at s_setprio <prio>
 void launch_vrf_u4(hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count, const int32_t* item_entry,
                    const ge_cached* ktab, const uint32_t* kinfo, const ge_niels* comb, const uint8_t* vrf_proof,
-                   void* mid);
+                   void* mid, int prio = 0);
 void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const uint8_t* vrf_vk,
                      const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,

@@ -227,6 +227,12 @@ struct praos_ctx {
   int kc_min[3] = {0, 0, 0};                           // per cache (cold, VRF, KES leaf) min uses overriding
                                                        // keycache when > 0 (PRAOS_KC_MIN="c,v,k")
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
+  // the cached chains' last kernels -- cached U, the join, the cached OCert / KES verifies -- at
+  // s_setprio ck_prio (the join at 3) in batches below ILP4_BATCH (PRAOS_CK_PRIO 0 / 2 / 3).  Off:
+  // U shortens (54k 0.71 -> 0.43 ms) but stage V stretches past it and the step with it (54k
+  // 2.74-2.76 -> 2.89-2.95 ms, 108k 3.83 -> 3.92-4.00, profiles/r05/c14_ckprio)
+  int ck_prio = 0;
+  int ck_prio_at(size_t n) const { return n < ILP4_BATCH ? ck_prio : 0; }
   int key_wave_prio = -1;                              // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO 1 / 0;
                                                        // -1: batches below KEY_PRIO_BATCH headers)
   hipEvent_t ev[6] = {};
@@ -565,6 +571,7 @@ const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 // streams and events of a context (praos_open, and the pipeline's second engine)
 static bool open_streams(praos_ctx* c) {
   if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp);
+  if (const char* e = std::getenv("PRAOS_CK_PRIO")) c->ck_prio = std::atoi(e);
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->stream = nullptr;
     return false;
@@ -1361,7 +1368,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
     keycache_precompute(k, b->vrf_vk, 1, sv);
     launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
-                 b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n));
+                 b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n), c->ck_prio_at(n));
     if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     vrf_keys_queued = true;
     return PRAOS_OK;
@@ -1402,7 +1409,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       else
         launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
                         b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
-                        P.max_kes_evo, bo, b->dd_ok);
+                        P.max_kes_evo, bo, b->dd_ok, c->ck_prio_at(n));
     } else {
       launch_ocert(g, blk, so, n, b->dd_reps, b->dd_counters, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                    b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
@@ -1443,7 +1450,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       else
         launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
                         b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
-                        P.max_kes_evo, bo, (uint8_t*)nullptr);
+                        P.max_kes_evo, bo, (uint8_t*)nullptr, c->ck_prio_at(n));
     } else {
       launch_ocert(g, blk, so, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk,
                    b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo,
@@ -1486,7 +1493,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
                       b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                       P.slots_per_kes_period, bk, c->kes_pair_min(), c->kes_dedup ? k.entry_rep : nullptr,
-                      c->kes_dedup ? k.rep_ok : nullptr);
+                      c->kes_dedup ? k.rep_ok : nullptr, c->ck_prio_at(n));
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
       c->kes_ck_timed = true;
     } else {
@@ -1573,7 +1580,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     auto join = [&](hipStream_t st) {
       launch_vrf_join(st, n, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, c->d_pool_hash, c->d_pool_vrf,
                       c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta,
-                      b->leader, b->nonce, b->vrf_mid, wprio);
+                      b->leader, b->nonce, b->vrf_mid, wprio || c->ck_prio_at(n));
     };
     if (vrf3) {
       // three kernels: U runs beside V (uncached keys at once on the miss stream, cached keys
