@@ -10,8 +10,10 @@ the C ABI (praos_batch_upload / praos_batch_run / praos_batch_download).
       397-byte messages.
 
 Each asserts: every clean item accepted, every corruption in a field the config checks
-rejected, and a ~200-item sample (evenly spaced + corrupted ones) bit-exact against the
-oracle (bits; for c3 also beta and the leader value)."""
+rejected, a ~200-item sample (evenly spaced + corrupted ones) bit-exact against the
+oracle (bits; for c3 also beta and the leader value), and all 1,000,000 items bit-exact
+against the CPU twin (libpraos_cpu.so: an independent restatement, radix 2^51 and
+sliding-window Straus, itself gated bit for bit against the oracle in test_cpu_twin.py)."""
 import numpy as np
 import pytest
 
@@ -78,6 +80,43 @@ def test_config_full_size(ctx, oracle, name):
             r = oracle.praos_header(ep, h)
             assert int(bits[i]) & VRF_MASK == r["bits"] & VRF_MASK, (i, hex(int(bits[i])), hex(r["bits"]))
             assert bytes(out["beta"][i]) == r["beta"] and bytes(out["leader"][i]) == r["leader"], i
+    _twin_equal(name, H, out, pool_list, p, eta0, spkp)
+
+
+def _twin_equal(name, H, out, pool_list, p, eta0, spkp):
+    """Every item's verdict (and for c3 beta and the leader value) against the CPU twin on the
+    box's 16-thread share."""
+    from praos_hip import abi
+    from praos_hip import cpu as C
+    bits = out["bits"]
+    n = len(bits)
+    twin = C.CpuContext(threads=16)
+    try:
+        if name == "c2":
+            ok = twin.verify_ocert(H["cold_vk"], H["hot_vk"], H["ocert_n"], H["ocert_c0"], H["ocert_sig"])
+            want = np.where(ok != 0, 0, OCERT_BAD).astype(np.uint16)
+            got = bits & np.uint16(OCERT_BAD)
+        elif name == "c4":
+            kp = H["slot"] // np.uint64(spkp)
+            period = np.where(kp >= H["ocert_c0"], kp - H["ocert_c0"], 0).astype(np.uint32)
+            res = np.zeros(n, np.uint8)
+            twin.check(twin.L.praos_verify_kes(twin.h, n, abi.ptr(H["hot_vk"]), abi.ptr(period, abi.u32p),
+                                               abi.ptr(H["kes_sig"]), abi.ptr(H["body_off"], abi.u64p),
+                                               abi.ptr(H["body_len"], abi.u32p), abi.ptr(H["body_bytes"]),
+                                               len(H["body_bytes"]), abi.ptr(res)))
+            want = np.array([0, KES_MERKLE, KES_LEAF], np.uint16)[res]
+            got = bits & np.uint16(KES_MERKLE | KES_LEAF)
+        else:
+            twin.set_epoch(eta0, pool_list, p)
+            t = twin.verify_headers(H)
+            want = t["bits"] & np.uint16(VRF_MASK)
+            got = bits & np.uint16(VRF_MASK)
+            assert np.array_equal(out["beta"], t["beta"]) and np.array_equal(out["leader"], t["leader"])
+            assert np.array_equal(out["pool_idx"], t["pool_idx"])
+    finally:
+        twin.close()
+    diff = np.nonzero(got != want)[0]
+    assert diff.size == 0, (name, diff[:8], got[diff[:8]], want[diff[:8]])
 
 
 def _first(H, m):
