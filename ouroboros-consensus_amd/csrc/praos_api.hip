@@ -274,6 +274,11 @@ struct praos_ctx {
   int e2e_prefill = 0;
   // stored-bytes pipeline: the first chunk's size in percent of the others' (PRAOS_PIPE_HEAD):
   // nothing runs on the GPU until it has landed and been decoded
+  int pipe_tail = 100;                                 // ... and the last chunk's (PRAOS_PIPE_TAIL): the run after it
+                                                       // waits for its decode, but a smaller one leaves more of the
+                                                       // batch's stage V after the upload (432k, 8 chunks: 100 ->
+                                                       // 16.4-16.7 ms, 50 -> 17.1-17.3, 25 -> 18.5-18.8;
+                                                       // profiles/r05/c16_pipe_tail)
   int pipe_head = 25;                                  // (432k headers, 8 chunks: 100 -> 16.9-17.0 ms,
                                                        // 50 -> 16.5, 25 -> 16.3-16.4, 12 -> 16.2-16.4)
   bool prefill = false;                                // inside such a call: every cache on its store,
@@ -602,6 +607,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
   if (const char* e = std::getenv("PRAOS_E2E_PREFILL")) c->e2e_prefill = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PIPE_HEAD")) c->pipe_head = std::max(5, std::min(100, std::atoi(e)));
+  if (const char* e = std::getenv("PRAOS_PIPE_TAIL")) c->pipe_tail = std::max(5, std::min(100, std::atoi(e)));
   (void)hipEventCreate(&c->v1_ev);
   (void)hipEventCreate(&c->kc0_ev);
   (void)hipEventCreate(&c->kc1_ev);
@@ -2097,10 +2103,14 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   std::vector<size_t> lo(K + 1);
   std::vector<uint64_t> need(K);
   {
-    // weights: head / 100 for chunk 0, 1 for the others
-    const size_t W = (size_t)c->pipe_head + 100 * (size_t)(K - 1);
+    // weights: head / 100 for chunk 0, tail / 100 for chunk K-1, 1 for the others
+    std::vector<size_t> w(K, 100);
+    w[0] = (size_t)c->pipe_head;
+    if (K > 2) w[K - 1] = (size_t)c->pipe_tail;
+    size_t W = 0, acc = 0;
+    for (int k = 0; k < K; k++) W += w[k];
     lo[0] = 0;
-    for (int k = 1; k <= K; k++) lo[k] = n * ((size_t)c->pipe_head + 100 * (size_t)(k - 1)) / W;
+    for (int k = 1; k <= K; k++) { acc += w[k - 1]; lo[k] = n * acc / W; }
   }
   uint64_t hw = 0;
   for (int k = 0; k < K; k++) {
