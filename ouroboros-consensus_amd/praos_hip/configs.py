@@ -87,7 +87,7 @@ def options(ctx, name, concurrent=1, keycache=2, dedup=1, pipeline=0):
     """The context options the bench runs a config with: the OCert dedup belongs to the header
     pipeline (a chain repeats each pool's OCert); single-primitive configs verify every item."""
     k = KERNELS[name]
-    if k != 7 or name == "tp":
+    if k != 7:
         dedup = 0
     ctx.set_option(abi.OPT_CONCURRENT, concurrent)
     ctx.set_option(abi.OPT_KERNELS, k)

@@ -92,6 +92,34 @@ def test_tpraos_staged_equals_one_kernel(ctx):
     assert np.count_nonzero(corrupted) and any(int(x) & (0x0400 | 0x0800) for x in o["bits"])
 
 
+def test_tpraos_ocert_dedup_equals_off(ctx):
+    """The OCert dedup (PRAOS_OPT_DEDUP: each distinct (cold vk, hot vk, n, c0, sigma) tuple of
+    the batch verified once, its verdict fanned out with each header's own KES-period checks)
+    on a TPraos batch with corrupted OCert signatures and KES periods out of range: every
+    output equal to verifying each header's OCert on its own, and the dedup did collapse the
+    pools' repeated certificates."""
+    from praos_hip import abi, fixed
+    p, c_raw = _params(Fraction(1, 2))
+    eta0 = b2b(b"tpraos-dedup")
+    n, npools = 4000, 300           # ~13 headers per pool: one OCert tuple repeated per pool
+    H, pools, corrupted = ctx.synthesize(n, npools, p, eta0, b"\x36" * 32, first_slot=9000, slot_stride=2,
+                                         corrupt_per_10000=900, tpraos=True)
+    H["ocert_c0"][::97] += 10 ** 6                   # KESBeforeStart on some headers of a shared tuple
+    pool_list = [(h, v, fixed.from_rational(Fraction(1, npools))) for (h, v) in pools]
+    ctx.set_epoch(eta0, pool_list, p)
+    outs = []
+    for dd in (1, 0):
+        ctx.set_option(abi.OPT_DEDUP, dd)
+        try:
+            outs.append(ctx.verify_tpraos_headers(H))
+        finally:
+            ctx.set_option(abi.OPT_DEDUP, 1)
+    o, o0 = outs
+    for k in o:
+        assert np.array_equal(np.asarray(o[k]), np.asarray(o0[k])), k
+    assert any(int(x) & 0x0004 for x in o["bits"]) and any(int(x) & 0x0001 for x in o["bits"])
+
+
 def test_tpraos_golden_blocks(ctx):
     """The golden TPraos blocks: OCert and KES verify, both certificates' proof_to_hash
     equal the stored outputs.  Their VRF inputs are the example's dummy seeds, not
