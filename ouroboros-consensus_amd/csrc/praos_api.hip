@@ -274,15 +274,15 @@ struct praos_ctx {
   int e2e_prefill = 0;
   // stored-bytes pipeline: the first chunk's size in percent of the others' (PRAOS_PIPE_HEAD):
   // nothing runs on the GPU until it has landed and been decoded
+  int pipe_head = 25;                                  // (432k headers, 8 chunks: 100 -> 16.9-17.0 ms,
+                                                       // 50 -> 16.5, 25 -> 16.3-16.4, 12 -> 16.2-16.4)
   int pipe_tail = 100;                                 // ... and the last chunk's (PRAOS_PIPE_TAIL): the run after it
                                                        // waits for its decode, but a smaller one leaves more of the
                                                        // batch's stage V after the upload (432k, 8 chunks: 100 ->
                                                        // 16.4-16.7 ms, 50 -> 17.1-17.3, 25 -> 18.5-18.8;
                                                        // profiles/r05/c16_pipe_tail)
-  int pipe_head = 25;                                  // (432k headers, 8 chunks: 100 -> 16.9-17.0 ms,
-                                                       // 50 -> 16.5, 25 -> 16.3-16.4, 12 -> 16.2-16.4)
-  bool prefill = false;                                // inside such a call: every cache on its store,
-                                                       // keys not stored are misses
+  bool prefill = false;                                // inside such a call (after a prefill): every cache on
+                                                       // its store, new keys cached by their batch count
   // epoch
   bool have_epoch = false;
   praos_params params{};
@@ -1193,12 +1193,12 @@ static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t*
                       span);
 }
 
-// The stored-bytes pipeline's key prefill: the keys of the landed chunk [lo, hi) go into the
-// pool-key store t (the batch's hash set dedupes them within the chunk, keys already stored are
-// skipped), and the new ones are decoded and expanded into their tables at once, on the cache's
-// stream, while later chunks upload; the batch run after the last chunk then finds every key
-// stored (all hits: no key precompute on its critical path).  reset: empty the store first (the
-// call's first chunk).
+// The stored-bytes pipeline's key prefill (off by default, see praos_ctx::e2e_prefill): the keys
+// of the landed chunks [lo, hi) go into the pool-key store t (the batch's hash set counts them
+// within the range, keys already stored are skipped), and the new ones used at least the usual
+// count are decoded and expanded into their tables at once, on the cache's stream, while later
+// chunks upload; the batch run after the last chunk finds them stored.  reset: empty the store
+// first (the call's first prefill round).
 static int kc_prefill(praos_ctx* c, praos_batch* b, int t, const uint8_t* keys, int kind, size_t lo, size_t hi,
                       hipStream_t st, bool reset, int prio) {
   praos_batch::KeyCache& k = b->kc[t];
