@@ -41,6 +41,9 @@ def main():
                     help="comma list of pool-key store modes (PRAOS_OPT_POOL_KEYS) to time: off (per-batch key "
                          "caches only), cold (the store emptied before each replay call: a fresh replay job), warm "
                          "(the store kept across calls)")
+    ap.add_argument("--members", default="1",
+                    help="comma list: 1 = one context, m > 1 = a praos_group of m contexts on device 0 "
+                         "(praos_group_replay_immutable: batches dealt to the members in turn, one fold)")
     ap.add_argument("--tpraos", action="store_true",
                     help="a Shelley..Alonzo (TPraos) chain replayed by praos_replay_immutable_tpraos (TICKN with extra entropy)")
     args = ap.parse_args()
@@ -86,35 +89,39 @@ def main():
         nch = immutable.write_immutable(path, data["arena"], data["off"], data["len"], data["slots"],
                                         data["header_hash"], args.chunk_slots)
         from praos_hip import abi
-        for mode in args.pool_keys.split(","):
-            for batch_max in [int(x) for x in args.batch_sizes.split(",")]:
-                runs = []
-                for rep in range(args.reps + 1):                              # rep 0 warms caches / allocator
-                    ctx.set_option(abi.OPT_POOL_KEYS, {"off": 0, "cold": 2, "warm": 1}[mode])
-                    st = {"last_slot": None, "counters": {}, "evolving": cfg["eta0"], "candidate": cfg["eta0"],
-                          "epoch_nonce": cfg["eta0"], "lab": None, "leb": None}
-                    env = dict(env_limits, tip=None)
-                    t = time.perf_counter()
-                    stats = ctx.replay_immutable(path, data["pools"], data["params"], data["epoch_info"], st, env,
-                                                 batch_max=batch_max, tpraos=args.tpraos, extra_entropy=xe)[0]
-                    wall = time.perf_counter() - t
-                    assert stats["validated"] == n and st == data["state"], stats
-                    if rep:
-                        runs.append(dict(stats, wall_ms=wall * 1e3))
-                best = min(runs, key=lambda r: r["wall_ms"])
-                line = {"metric": f"replayed {'TPraos' if args.tpraos else 'Praos'} headers/s from an ImmutableDB "
-                                  "(read + GPU decode/crypto + host fold)",
-                        "value": round(n / (best["wall_ms"] * 1e-3), 1), "unit": "headers/s", "headers": n,
-                        "epochs": args.epochs, "blocks_per_epoch": round(n / args.epochs), "chunks": nch,
-                        "pools": args.pools, "wall_ms": round(best["wall_ms"], 2),
-                        "schedule": "round-robin, f = 1" if args.round_robin else "first-leader-wins, f = 1/20",
-                        "chain": args.chain or "replay-bench", "pool_keys": mode,
-                        "stages_ms": {k: round(best[k], 2) for k in ("ms_io", "ms_device", "ms_nonce", "ms_fold")},
-                        "batch_max": batch_max, "batches": best["batches"], "epoch_nonces": best["epochs"],
-                        "generate_s": round(t_gen, 1), "reps": args.reps,
-                        "data": "synthetic linked first-leader-wins chain, GPU-signed; written to a temp dir"}
-                print(json.dumps(line), flush=True)
-        ctx.set_option(abi.OPT_POOL_KEYS, -1)
+        for members in [int(x) for x in args.members.split(",")]:
+          runner = ctx if members == 1 else abi.Group([0] * members)
+          for mode in args.pool_keys.split(","):
+              for batch_max in [int(x) for x in args.batch_sizes.split(",")]:
+                  runs = []
+                  for rep in range(args.reps + 1):                              # rep 0 warms caches / allocator
+                      runner.set_option(abi.OPT_POOL_KEYS, {"off": 0, "cold": 2, "warm": 1}[mode])
+                      st = {"last_slot": None, "counters": {}, "evolving": cfg["eta0"], "candidate": cfg["eta0"],
+                            "epoch_nonce": cfg["eta0"], "lab": None, "leb": None}
+                      env = dict(env_limits, tip=None)
+                      t = time.perf_counter()
+                      stats = runner.replay_immutable(path, data["pools"], data["params"], data["epoch_info"], st, env,
+                                                      batch_max=batch_max, tpraos=args.tpraos, extra_entropy=xe)[0]
+                      wall = time.perf_counter() - t
+                      assert stats["validated"] == n and st == data["state"], stats
+                      if rep:
+                          runs.append(dict(stats, wall_ms=wall * 1e3))
+                  best = min(runs, key=lambda r: r["wall_ms"])
+                  line = {"metric": f"replayed {'TPraos' if args.tpraos else 'Praos'} headers/s from an ImmutableDB "
+                                    "(read + GPU decode/crypto + host fold)",
+                          "value": round(n / (best["wall_ms"] * 1e-3), 1), "unit": "headers/s", "headers": n,
+                          "epochs": args.epochs, "blocks_per_epoch": round(n / args.epochs), "chunks": nch,
+                          "pools": args.pools, "wall_ms": round(best["wall_ms"], 2),
+                          "schedule": "round-robin, f = 1" if args.round_robin else "first-leader-wins, f = 1/20",
+                          "chain": args.chain or "replay-bench", "pool_keys": mode, "members": members,
+                          "stages_ms": {k: round(best[k], 2) for k in ("ms_io", "ms_device", "ms_nonce", "ms_fold")},
+                          "batch_max": batch_max, "batches": best["batches"], "epoch_nonces": best["epochs"],
+                          "generate_s": round(t_gen, 1), "reps": args.reps,
+                          "data": "synthetic linked first-leader-wins chain, GPU-signed; written to a temp dir"}
+                  print(json.dumps(line), flush=True)
+          runner.set_option(abi.OPT_POOL_KEYS, -1)
+          if runner is not ctx:
+              runner.close()
     ctx.close()
 
 
