@@ -10,7 +10,7 @@ the C ABI (praos_batch_upload / praos_batch_run / praos_batch_download).
       397-byte messages.
 
 Each asserts: every clean item accepted, every corruption in a field the config checks
-rejected, a ~200-item sample (evenly spaced + corrupted ones) bit-exact against the
+rejected, a ~1,000-item sample (evenly spaced + corrupted ones) bit-exact against the
 oracle (bits; for c3 also beta and the leader value), and all 1,000,000 items bit-exact
 against the CPU twin (libpraos_cpu.so: an independent restatement, radix 2^51 and
 sliding-window Straus, itself gated bit for bit against the oracle in test_cpu_twin.py)."""
@@ -61,9 +61,9 @@ def test_config_full_size(ctx, oracle, name):
     assert int((crypto[rel] == 0).sum()) == 0, np.nonzero(rel & (crypto == 0))[0][:8]
     if name == "c3":
         assert int(((bits & 0x1000) == 0)[clean].sum()) == int(clean.sum())   # every clean item a leader
-    # the oracle on ~200 items
-    sample = sorted(set(np.linspace(0, n - 1, 150).astype(int).tolist() +
-                        np.nonzero(~clean)[0][::max(1, int((~clean).sum()) // 50)][:50].tolist()))
+    # the oracle on ~1,000 items (750 evenly spaced, 250 corrupted)
+    sample = sorted(set(np.linspace(0, n - 1, 750).astype(int).tolist() +
+                        np.nonzero(~clean)[0][::max(1, int((~clean).sum()) // 250)][:250].tolist()))
     if name == "c3":
         ep = oracle.make_epoch(eta0, spkp, maxevo, c_raw, pool_list)
     for i in sample:
