@@ -46,6 +46,11 @@ FE_INLINE void fe_const(fe& r, const uint32_t c[8]) {
   for (int i = 0; i < 8; i++) r.v[i] = c[i];
 }
 
+// PRAOS_RED_BRANCH=1: the second fold's carry propagation in a rarely taken branch (below)
+#ifndef PRAOS_RED_BRANCH
+#define PRAOS_RED_BRANCH 1
+#endif
+
 // r = t[0..15] mod p, t = 512-bit product
 FE_INLINE void fe_reduce512(fe& r, const uint32_t t[16]) {
   uint64_t s[8];
@@ -56,16 +61,54 @@ FE_INLINE void fe_reduce512(fe& r, const uint32_t t[16]) {
 #pragma unroll
   for (int i = 1; i < 8; i++) r.v[i] = addc((uint32_t)s[i], (uint32_t)(s[i - 1] >> 32), c, &c);
   uint32_t k = (uint32_t)(s[7] >> 32) + c;           // < 40
+#if PRAOS_RED_BRANCH
+  // 38 k < 1520 carries out of limb 0 only when limb 0 >= 2^32 - 1520 (probability < 2^-21
+  // per product): the seven-limb carry propagation runs in a branch the wave almost never
+  // takes, instead of as a serial VCC chain in every product.
+  r.v[0] = addc(r.v[0], k * 38u, 0, &c);
+  if (__builtin_expect(c != 0, 0)) {
+#pragma unroll
+    for (int i = 1; i < 8; i++) r.v[i] = addc(r.v[i], 0, c, &c);
+    r.v[0] += 38u * c;                               // cannot carry: value wrapped to < 2^11
+  }
+#else
   uint64_t s0 = (uint64_t)k * 38u + r.v[0];
   r.v[0] = (uint32_t)s0;
   c = (uint32_t)(s0 >> 32);
 #pragma unroll
   for (int i = 1; i < 8; i++) r.v[i] = addc(r.v[i], 0, c, &c);
   r.v[0] += 38u * c;                                 // cannot carry: value wrapped to < 2^11
+#endif
+}
+
+// PRAOS_MACG=1: the products come from fe_cols.hpp (tools/gen_fe_cols.py), each column one asm
+// block with its MACs software-pipelined so no carry read needs s_nop padding; 0 keeps the
+// FE_MAC / FE_MAC2 forms below (the A/B reference).
+#ifndef PRAOS_MACG
+#define PRAOS_MACG 1
+#endif
+#include "fe_cols.hpp"
+
+// 2 t[0 .. 16) + the diagonal squares a_i^2, reduced: the square from its cross products
+FE_INLINE void fe_sq_finish(fe& r, uint32_t (&t)[16], const fe& a) {
+#pragma unroll
+  for (int i = 15; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
+  t[0] = 0;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)a.v[i] * a.v[i];
+    t[2 * i] = addc(t[2 * i], (uint32_t)d, c, &c);
+    t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(d >> 32), c, &c);
+  }
+  fe_reduce512(r, t);
 }
 
 FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   uint32_t t[16];
+#if PRAOS_MACG
+  fe_prod_g(t, a, b);
+#else
   uint64_t acc = (uint64_t)a.v[0] * b.v[0];
   t[0] = (uint32_t)acc;
   acc >>= 32;
@@ -84,11 +127,15 @@ FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
     acc = (acc >> 32) | ((uint64_t)top << 32);
   }
   t[15] = (uint32_t)acc;
+#endif
   fe_reduce512(r, t);
 }
 
 FE_INLINE void fe_sq(fe& r, const fe& a) {
   uint32_t t[16];
+#if PRAOS_MACG
+  fe_cross_g(t, a);
+#else
   // cross products a_i a_j, i < j
   uint64_t acc = 0;
   t[0] = 0;
@@ -107,19 +154,8 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
     acc = (acc >> 32) | ((uint64_t)top << 32);
   }
   t[15] = (uint32_t)acc;
-  // double (cross sum < 2^511, so no bit is lost)
-#pragma unroll
-  for (int i = 15; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
-  t[0] = 0;
-  // add diagonal squares
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t d = (uint64_t)a.v[i] * a.v[i];
-    t[2 * i] = addc(t[2 * i], (uint32_t)d, c, &c);
-    t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(d >> 32), c, &c);
-  }
-  fe_reduce512(r, t);
+#endif
+  fe_sq_finish(r, t, a);                             // cross sum < 2^511: doubling loses no bit
 }
 
 // ---- two independent products interleaved MAC by MAC (ILP for the group formulas,
@@ -175,7 +211,12 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
 
 // r1 = a1 b1, r2 = a2 b2 (outputs may alias any input: written after both products)
 FE_INLINE void fe_mul2(fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2, const fe& b2) {
-#if PRAOS_ILP2
+#if PRAOS_ILP2 && PRAOS_MACG
+  uint32_t t1[16], t2[16];
+  fe_prod2_g(t1, t2, a1, b1, a2, b2);
+  fe_reduce512(r1, t1);
+  fe_reduce512(r2, t2);
+#elif PRAOS_ILP2
   uint32_t t1[16], t2[16];
   uint64_t acc1 = (uint64_t)a1.v[0] * b1.v[0], acc2 = (uint64_t)a2.v[0] * b2.v[0];
   t1[0] = (uint32_t)acc1;
@@ -213,7 +254,12 @@ FE_INLINE void fe_mul2(fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2,
 
 // r1 = a1^2, r2 = a2^2 (outputs may alias inputs)
 FE_INLINE void fe_sq2(fe& r1, const fe& a1, fe& r2, const fe& a2) {
-#if PRAOS_ILP2
+#if PRAOS_ILP2 && PRAOS_MACG
+  uint32_t t1[16], t2[16];
+  fe_cross2_g(t1, t2, a1, a2);
+  fe_sq_finish(r1, t1, a1);
+  fe_sq_finish(r2, t2, a2);
+#elif PRAOS_ILP2
   uint32_t t1[16], t2[16];
   uint64_t acc1 = 0, acc2 = 0;
   t1[0] = 0;

@@ -176,3 +176,15 @@ def test_tpraos_error_table_matches_haskell():
     assert sorted(b for b, _ in hs) == sorted(tpf.values()) and len(hs) == 15
     # the Haskell names carry the ledger constructors' names (TP prefix dropped)
     assert {n for _, n in hs} >= {"KESBeforeStartOCERT", "VRFKeyBadNonce", "WrongGenesisVRFKeyOVERLAY"}
+
+
+def test_fe_cols_header_is_generated():
+    """csrc/fe_cols.hpp (the software-pipelined field products) is exactly what
+    tools/gen_fe_cols.py prints: the header is generated, never hand-edited."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_fe_cols.py")], check=True,
+                         capture_output=True, text=True).stdout
+    with open(os.path.join(root, "ouroboros-consensus_amd", "csrc", "fe_cols.hpp")) as f:
+        assert f.read() == out
