@@ -474,15 +474,26 @@ FE_INLINE void fe_sq4(fe& r1, const fe& a1, fe& r2, const fe& a2, fe& r3, const 
   fe_reduce512(r4, t[3]);
 }
 
+// The fold of the 2^256 carry (borrow) adds (subtracts) 38 at limb 0; that carries (borrows)
+// further only when limb 0 >= 2^32 - 38 (< 38): with PRAOS_RED_BRANCH the propagation runs in a
+// branch the wave almost never takes, as in fe_reduce512.
 FE_INLINE void fe_add(fe& r, const fe& a, const fe& b) {
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = addc(a.v[i], b.v[i], c, &c);
   uint32_t c2 = 0;
   r.v[0] = addc(r.v[0], 38u * c, 0, &c2);
+#if PRAOS_RED_BRANCH
+  if (__builtin_expect(c2 != 0, 0)) {
+#pragma unroll
+    for (int i = 1; i < 8; i++) r.v[i] = addc(r.v[i], 0, c2, &c2);
+    r.v[0] += 38u * c2;
+  }
+#else
 #pragma unroll
   for (int i = 1; i < 8; i++) r.v[i] = addc(r.v[i], 0, c2, &c2);
   r.v[0] += 38u * c2;
+#endif
 }
 
 FE_INLINE void fe_sub(fe& r, const fe& a, const fe& b) {
@@ -491,9 +502,17 @@ FE_INLINE void fe_sub(fe& r, const fe& a, const fe& b) {
   for (int i = 0; i < 8; i++) r.v[i] = subb(a.v[i], b.v[i], bw, &bw);
   uint32_t b2 = 0;
   r.v[0] = subb(r.v[0], 38u * bw, 0, &b2);
+#if PRAOS_RED_BRANCH
+  if (__builtin_expect(b2 != 0, 0)) {
+#pragma unroll
+    for (int i = 1; i < 8; i++) r.v[i] = subb(r.v[i], 0, b2, &b2);
+    r.v[0] -= 38u * b2;
+  }
+#else
 #pragma unroll
   for (int i = 1; i < 8; i++) r.v[i] = subb(r.v[i], 0, b2, &b2);
   r.v[0] -= 38u * b2;
+#endif
 }
 
 FE_INLINE void fe_neg(fe& r, const fe& a) {

@@ -41,6 +41,31 @@ def test_fe_ring_ops(ctx, op):
         assert z < 2 ** 256 and z % P == want, (op, hex(x), hex(y))
 
 
+def _rare_fold_pairs():
+    """(op, x, y) pairs whose second 2^256 fold carries (add, mul) or borrows (sub) out of limb 0,
+    the branch fe25519.hpp takes with probability < 2^-21 on random operands (PRAOS_RED_BRANCH)."""
+    m = 2 ** 256
+    pairs = [("add", m - 1, 2 ** 32 - 9), ("add", m - 1, m - 9), ("add", m - 1, m - 1),
+             ("add", m - 38, m - 1), ("sub", 3, 2 ** 32), ("sub", 0, m - 5), ("sub", 37, m - 1),
+             ("sub", 0, 1), ("sub", 0, m - 1)]
+    # (2^256 - 1) b folds to 37 b - 38 (b < 2^256 / 37): limb 0 = 2^32 - 1 for b = 2^32 j + 1, and
+    # 37 b - 38 >= 2^256 - 38 (the carry runs through every limb) for b = ceil(2^256 / 37)
+    pairs += [("mul", m - 1, 2 ** 32 * j + 1) for j in (1, 2, 3, 2 ** 64, 2 ** 190)]
+    pairs += [("mul", m - 1, -(-m // 37)), ("mul", -(-m // 37), m - 1)]
+    return pairs
+
+
+def test_fe_rare_fold_carry(ctx):
+    code = {"mul": 0, "add": 2, "sub": 3}
+    for op in code:
+        pr = [(x, y) for o, x, y in _rare_fold_pairs() if o == op]
+        xs, ys = [x for x, _ in pr], [y for _, y in pr]
+        out = _from(ctx.debug_fe(code[op], _to(xs), _to(ys)))
+        for x, y, z in zip(xs, ys, out):
+            want = {"mul": x * y, "add": x + y, "sub": x - y}[op] % P
+            assert z < 2 ** 256 and z % P == want, (op, hex(x), hex(y))
+
+
 def test_fe_invert_pow_canon(ctx):
     xs, _ = _fe_inputs(2, 200)
     inv = _from(ctx.debug_fe(4, _to(xs)))

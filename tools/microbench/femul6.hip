@@ -4,6 +4,7 @@
 //   sq   : x = x^2            (fe_sq)
 //   mul2 : x = x*y, z = z*y   (fe_mul2, two products interleaved)
 //   sq2  : x = x^2, z = z^2   (fe_sq2)
+//   addsub: two fe_add + two fe_sub, dependent (per "product" read: per add / sub)
 // at 1..4 waves per SIMD (blocks of 4 waves, CUs x W blocks).
 // Build: hipcc --offload-arch=gfx950 -O3 -I../../ouroboros-consensus_amd/csrc -DPRAOS_MACG=1 -o femul6_g femul6.hip
 #include <hip/hip_runtime.h>
@@ -30,7 +31,13 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, uint32_t seed) {
     if constexpr (V == 0) fe_mul(x, x, y);
     else if constexpr (V == 1) fe_sq(x, x);
     else if constexpr (V == 2) fe_mul2(x, x, y, z, z, y);
-    else fe_sq2(x, x, z, z);
+    else if constexpr (V == 3) fe_sq2(x, x, z, z);
+    else {
+      fe_add(x, x, y);
+      fe_sub(z, z, x);
+      fe_add(y, y, z);
+      fe_sub(x, x, z);
+    }
   }
   uint32_t h = 0;
 #pragma unroll
@@ -57,7 +64,7 @@ int main() {
   hipDeviceProp_t p;
   CHK(hipGetDeviceProperties(&p, 0));
   const int ncu = p.multiProcessorCount;
-  const char* names[4] = {"fe_mul", "fe_sq", "fe_mul2", "fe_sq2"};
+  const char* names[5] = {"fe_mul", "fe_sq", "fe_mul2", "fe_sq2", "addsub"};
   uint32_t* d;
   CHK(hipMalloc(&d, (size_t)ncu * 4 * 256 * 4));
   uint32_t* h = new uint32_t[(size_t)ncu * 4 * 256];
@@ -65,15 +72,18 @@ int main() {
   for (int W = 1; W <= 4; W++) {
     const int blocks = ncu * W;
     const size_t lanes = (size_t)blocks * 256;
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 5; v++) {
       float ms;
-      int rc = v == 0 ? run<0>(d, blocks, &ms) : v == 1 ? run<1>(d, blocks, &ms) : v == 2 ? run<2>(d, blocks, &ms)
-                                                                                          : run<3>(d, blocks, &ms);
+      int rc = v == 0   ? run<0>(d, blocks, &ms)
+               : v == 1 ? run<1>(d, blocks, &ms)
+               : v == 2 ? run<2>(d, blocks, &ms)
+               : v == 3 ? run<3>(d, blocks, &ms)
+                        : run<4>(d, blocks, &ms);
       if (rc) return rc;
       CHK(hipMemcpy(h, d, lanes * 4, hipMemcpyDeviceToHost));
       uint64_t sum = 0;
       for (size_t i = 0; i < lanes; i++) sum = sum * 1000003u + h[i];
-      const double products = (double)lanes * ITERS * (v >= 2 ? 2 : 1);
+      const double products = (double)lanes * ITERS * (v == 4 ? 4 : v >= 2 ? 2 : 1);
       printf("W=%d %-8s %8.3f ms  %7.1f SIMD cycles per wave-product (2.4 GHz)  checksum %016llx\n", W, names[v], ms,
              ms * 1e-3 * 2.4e9 * ncu * 4 / (products / 64), (unsigned long long)sum);
     }
