@@ -51,29 +51,48 @@ H_INLINE void sha512_init(uint64_t H[8]) {
   H[6] = 0x1f83d9abfb41bd6bULL; H[7] = 0x5be0cd19137e2179ULL;
 }
 
-// W: 16 big-endian message words (already byte-swapped); consumed in place.
+// One SHA-512 round on the working variables v[] named for round j (a = v[-j mod 8], ..., h =
+// v[7 - j mod 8]): no register rotation, the next round reads the same array renamed.
+#define SHA512_ROUND(j, kw)                                                                       \
+  do {                                                                                           \
+    uint64_t& a_ = v[(8 - ((j) & 7)) & 7];                                                       \
+    uint64_t& b_ = v[(9 - ((j) & 7)) & 7];                                                       \
+    uint64_t& c_ = v[(10 - ((j) & 7)) & 7];                                                      \
+    uint64_t& d_ = v[(11 - ((j) & 7)) & 7];                                                      \
+    uint64_t& e_ = v[(12 - ((j) & 7)) & 7];                                                      \
+    uint64_t& f_ = v[(13 - ((j) & 7)) & 7];                                                      \
+    uint64_t& g_ = v[(14 - ((j) & 7)) & 7];                                                      \
+    uint64_t& h_ = v[(15 - ((j) & 7)) & 7];                                                      \
+    const uint64_t t1_ = h_ + (ror64(e_, 14) ^ ror64(e_, 18) ^ ror64(e_, 41)) + ((e_ & f_) ^ (~e_ & g_)) + (kw); \
+    const uint64_t t2_ = (ror64(a_, 28) ^ ror64(a_, 34) ^ ror64(a_, 39)) + ((a_ & b_) ^ (c_ & (a_ ^ b_))); \
+    d_ += t1_;                                                                                   \
+    h_ = t1_ + t2_;                                                                              \
+  } while (0)
+
+// W: 16 big-endian message words (already byte-swapped); consumed in place.  Rounds in
+// blocks of 16 with constant W indices and renamed working variables (an 80-round unroll
+// request is not honoured at this size: the rolled loop then indexed W through
+// s_set_gpr_idx and rotated a..h with eight 64-bit moves per round); the first block
+// unrolled, the message schedule's four blocks one runtime loop.
 H_INLINE void sha512_block(uint64_t H[8], uint64_t W[16]) {
-  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+  uint64_t v[8];
 #pragma unroll
-  for (int i = 0; i < 80; i++) {
-    uint64_t w;
-    if (i < 16) {
-      w = W[i];
-    } else {
-      const uint64_t w15 = W[(i - 15) & 15], w2 = W[(i - 2) & 15];
+  for (int i = 0; i < 8; i++) v[i] = H[i];
+#pragma unroll
+  for (int j = 0; j < 16; j++) SHA512_ROUND(j, SHA512_K[j] + W[j]);
+#pragma clang loop unroll(disable)
+  for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
       const uint64_t s0 = ror64(w15, 1) ^ ror64(w15, 8) ^ (w15 >> 7);
       const uint64_t s1 = ror64(w2, 19) ^ ror64(w2, 61) ^ (w2 >> 6);
-      w = W[i & 15] + s0 + W[(i - 7) & 15] + s1;
-      W[i & 15] = w;
+      W[j] += s0 + W[(j + 9) & 15] + s1;
+      SHA512_ROUND(j, SHA512_K[r + j] + W[j]);
     }
-    const uint64_t S1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = h + S1 + ch + SHA512_K[i] + w;
-    const uint64_t S0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
-    const uint64_t mj = (a & b) ^ (c & (a ^ b));
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
-  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+#pragma unroll
+  for (int i = 0; i < 8; i++) H[i] += v[i];
 }
 
 // digest as 16 little-endian u32 words (byte order of the 64-byte output)
