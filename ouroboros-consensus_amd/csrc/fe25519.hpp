@@ -3,13 +3,15 @@
 // Representation: 8 x 32-bit limbs, radix 2^32, value in [0, 2^256) ("weakly
 // reduced": congruent mod p, canonicalised only for encoding / comparison).
 //
-// Why radix 2^32 (measured on MI355X, tools/microbench/intrate.hip):
-// v_mad_u64_u32 (32x32+64 -> 64 with carry-out) issues at ~5.2 cycles per
-// wave64 instruction vs ~4.3 for other VOP3 ops, so a full 32-bit MAC costs
-// barely more than an add.  The 8x8 schoolbook product is 64 MACs, each paired
-// with one v_addc_co_u32 that counts the column carry; reduction folds the
-// high 256 bits with 2^256 = 38 (mod p).  This beats radix 2^25.5 (100 MACs +
-// 64-bit carry chains) and uses 8 instead of 10 VGPRs per element.
+// Why radix 2^32 (measured on MI355X, tools/microbench/intrate.hip at 3 waves per SIMD):
+// v_mad_u64_u32 (32x32+64 -> 64 with carry-out) issues at ~5.0 SIMD cycles per wave64
+// instruction, a carry add at ~4.6 and other VOP3 ops at ~4.4, so a full 32-bit MAC costs
+// barely more than an add.  The 8x8 schoolbook product is 64 MACs, each paired with one
+// v_addc_co_u32 that counts the column carry; reduction folds the high 256 bits with
+// 2^256 = 38 (mod p).  This beats radix 2^25.5 (100 MACs + 64-bit carry chains) and 9 x 29-bit
+// limbs (81 carry-free MACs, but a 64-bit shift and mask per column: 771 / 661 vs 744 / 574
+// cycles per multiply / squaring, tools/microbench/fe29.hip), and uses 8 VGPRs per element.
+// The shipped products are the generated columns of fe_cols.hpp (PRAOS_MACG, below).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,7 +22,8 @@ struct fe { uint32_t v[8]; };
 
 // acc(64) += a*b with the carry-out counted into top.  gfx950 needs two wait
 // states between a VALU write of VCC and a VALU read of it as carry-in (the
-// compiler inserts the same `s_nop 1` in its own carry chains).
+// compiler inserts the same `s_nop 1` in its own carry chains).  FE_MAC / FE_MAC2 are the
+// PRAOS_MACG=0 forms; FE_MAC3 / FE_MAC4 (the ILP-4 builds) are padding-free already.
 #define FE_MAC(acc, top, a, b)                                                     \
   asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc" \
       : "+v"(acc), "+v"(top) : "v"(a), "v"(b) : "vcc")
