@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 13
+#define PRAOS_ABI_VERSION 14
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -633,6 +633,33 @@ int praos_replay_immutable(praos_ctx* ctx, const char* dir, const praos_pool* po
                            const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                            praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
                            praos_replay_stats* stats);
+/* ABI 14.  The ledger view per epoch, as db-analyser sources it: the reference forecasts each
+ * header's LedgerView from the ledger state it advances block by block (Analysis.hs:564-572,
+ * ledgerViewForecastAt over applyTheBlock; Shelley/Ledger/SupportsProtocol.hs:100-125: lvPoolDistr
+ * = nesPd, lvMaxHeaderSize / lvMaxBodySize / lvProtocolVersion from the epoch's protocol
+ * parameters).  All of them change only at an epoch boundary (the NEWEPOCH rule), so one view
+ * per epoch is the reference's per-header forecast.  views[] is sorted by first_epoch; epoch e
+ * uses the last entry with first_epoch <= e (a view holds until the next entry's epoch). */
+typedef struct {
+  uint64_t first_epoch;
+  const praos_pool* pools;        /* lvPoolDistr: hash28, VRF key hash, sigma (Fixed E34) */
+  uint32_t npools;
+  uint32_t reserved;              /* 0 */
+  uint64_t lv_prot_major;         /* pvMajor (lvProtocolVersion) */
+  uint64_t max_header_size;       /* lvMaxHeaderSize */
+  uint64_t max_body_size;         /* lvMaxBodySize */
+} praos_ledger_view;
+
+/* praos_replay_immutable with a ledger view per epoch instead of one for the whole replay: a
+ * batch never spans two views; each member's device gets a view's pool tables (hash, VRF key
+ * hash, leader threshold x = -(sigma * c)) before the first batch that needs them, and the fold
+ * of a batch uses that batch's view (PoolDistr membership for the OCert counters, the envelope
+ * limits; env's limit fields are ignored).  Everything else -- pipeline, stop, resume, outputs --
+ * as praos_replay_immutable.  PRAOS_E_ARG when no view covers a replayed epoch. */
+int praos_replay_immutable_views(praos_ctx* ctx, const char* dir, const praos_ledger_view* views, uint32_t nviews,
+                                 const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
+                                 praos_chain_state* st, size_t batch_max, uint8_t* verdicts, size_t verdicts_cap,
+                                 praos_replay_stats* stats);
 /* The same replay over a TPraos (Shelley..Alonzo) ImmutableDB: stored BHeaders, the TPraos
  * nonce rules (mkNonceFromOutputVRF of the eta certificate; TICKN with extra_entropy, NULL
  * = NeutralNonce) and the TPraos fold; failures (may be NULL, verdicts_cap entries) gets
@@ -688,6 +715,15 @@ int praos_group_replay_immutable_tpraos(praos_group* g, const char* dir, const p
                                         const praos_nonce* extra_entropy, praos_envelope* env, praos_chain_state* st,
                                         size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
                                         praos_replay_stats* stats);
+/* ABI 14: praos_verify_block_integrity over the group (ImmutableDB chunk validation on several
+ * GPUs: contiguous shards of the blocks, results in place). */
+int praos_group_verify_block_integrity(praos_group* g, const praos_header_bytes* blocks,
+                                       uint64_t slots_per_kes_period, uint8_t* result, uint8_t* body_hash);
+/* ABI 14: praos_replay_immutable_views over the group. */
+int praos_group_replay_immutable_views(praos_group* g, const char* dir, const praos_ledger_view* views,
+                                       uint32_t nviews, const praos_params* params, const praos_epoch_info* ei,
+                                       praos_envelope* env, praos_chain_state* st, size_t batch_max,
+                                       uint8_t* verdicts, size_t verdicts_cap, praos_replay_stats* stats);
 
 /* ---- synthetic chain generator (db-synthesizer analogue, for benches) ----
  * Signs on the GPU: OCert (Ed25519), Sum6KES (Blake2b-256 tree + Ed25519 leaf),

@@ -5,6 +5,16 @@
  * the JSON this prints with its own results.
  *
  *   ffi_harness <immutable dir> <epoch file> <threads>
+ *   ffi_harness --chunk <immutable dir> <chunk no> <slots per KES period> <members>
+ *
+ * --chunk: ImmutableDB chunk validation as Batch.hs verifyChunkIntegrity runs it (the batched
+ *   checkIntegrity of parseChunkFile, ImmutableDB/Impl/Parser.hs:118-141, Validation.hs:379-384):
+ *   the chunk's blocks cut at the secondary index's block offsets, each block's CRC32 against
+ *   the entry's checksum, and the blocks whose CRC does not match through
+ *   praos_verify_block_integrity (phase "chunk") and praos_group_verify_block_integrity over
+ *   <members> contexts on device 0 (phase "chunk_group").  Prints per block -1 (CRC matched, not
+ *   checked) or the PRAOS_BLK_* bits, the first corrupt block and the offset parseChunkFile
+ *   truncates the chunk file at.
  *
  * epoch file (text, one record per line):
  *   eta0 <64 hex>                      genesis epoch nonce
@@ -12,6 +22,12 @@
  *   epoch <base_slot> <base_no> <length> <stability_window>
  *   env <max_major_pv> <lv_prot_major> <max_header_size> <max_body_size>
  *   pool <hash28 56 hex> <vrf_hash32 64 hex> <sigma_fp 32 hex, LE>
+ *   view <first_epoch> <lv_prot_major> <max_header_size> <max_body_size>   (optional, Praos) from
+ *                                      this epoch on, the ledger view is the pool lines that follow
+ *                                      (until the next view line) and these limits: the LedgerView
+ *                                      db-analyser forecasts per epoch (ledgerViewForecastAt,
+ *                                      Analysis.hs:564-572).  Pool lines before the first view line
+ *                                      form view 0 (from epoch 0, the env line's limits).
  *   tpraos <extra entropy 64 hex | neutral>   (optional) a TPraos (Shelley..Alonzo) database:
  *                                      the binding's TPraos sequence (praos_tpraos_ticked_epoch_nonce
  *                                      -> praos_set_epoch -> praos_verify_tpraos_header_bytes ->
@@ -37,6 +53,18 @@
  *   "binding_group" (TPraos): the TPraos sequence with praos_group_verify_tpraos_header_bytes;
  *   "replay":   praos_replay_immutable over the same directory (must agree);
  *   "replay_group": praos_group_replay_immutable[_tpraos] over <threads> members (must agree);
+ *   "analysis": the db-analyser analysis (integration/haskell/.../BenchmarkHeaderBatch.hs): the
+ *               ImmutableDB streamed epoch by epoch into a reused, once-registered arena; at each
+ *               epoch boundary the next epoch's ledger view is "forecast" (looked up here; the
+ *               Haskell side forecasts it from the ledger state it advances) while the previous
+ *               epoch validates on a worker thread -- forecast -> praos_ticked_epoch_nonce ->
+ *               praos_set_epoch (that epoch's PoolDistr) -> praos_verify_header_bytes ->
+ *               praos_validate_headers (that epoch's envelope limits) -> praos_state_encode;
+ *               "analysis_group" the same on a group (must agree);
+ *   "replay_views" / "replay_views_group": praos_[group_]replay_immutable_views with every view of
+ *               the file in one call (must agree with "analysis"); with several views "binding",
+ *               "typed" and "replay" use view 0 throughout (a single ledger view for the whole
+ *               database, which the test expects to diverge once the PoolDistr changes);
  *   TPraos phases also print the stopping header's PRTCL failure set and the
  *   SL.ChainTransitionError constructors Batch/Errors.hs tpraosChainTransitionError builds from
  *   it (the table below mirrors the Haskell one; tests/test_abi.py checks the two agree);
@@ -95,15 +123,40 @@ static praos_pool* g_pools;
 static uint32_t g_npools;
 static int g_tpraos;
 static praos_nonce g_extra;              /* TICKN's extra entropy (TPraos) */
+/* ledger views per epoch ("view" lines); view 0 = the pools before the first view line */
+enum { MAXV = 256 };
+static praos_ledger_view g_views[MAXV];
+static uint32_t g_nviews;
+static praos_pool* g_vpools[MAXV];
+static uint32_t g_vcap[MAXV];
 
 static void read_epoch_file(const char* path) {
   FILE* f = fopen(path, "r");
   if (!f) DIE("open %s", path);
   char line[512], a[128], b[128], c[128];
   uint32_t cap = 0;
+  int cur = 0;                               /* the view pool lines go to (0: g_pools) */
   while (fgets(line, sizeof line, f)) {
     unsigned long long x, y, z, w;
-    if (sscanf(line, "eta0 %127s", a) == 1) {
+    if (sscanf(line, "view %llu %llu %llu %llu", &x, &y, &z, &w) == 4) {
+      if (g_nviews == 0) g_nviews = 1;       /* view 0 = g_pools (filled in below) */
+      if (g_nviews == MAXV) DIE("too many views");
+      cur = (int)g_nviews++;
+      memset(&g_views[cur], 0, sizeof g_views[cur]);
+      g_views[cur].first_epoch = x;
+      g_views[cur].lv_prot_major = y; g_views[cur].max_header_size = z; g_views[cur].max_body_size = w;
+    } else if (cur > 0 && sscanf(line, "pool %127s %127s %127s", a, b, c) == 3) {
+      praos_ledger_view* v = &g_views[cur];
+      if (v->npools == g_vcap[cur]) {
+        g_vcap[cur] = g_vcap[cur] ? 2 * g_vcap[cur] : 64;
+        g_vpools[cur] = realloc(g_vpools[cur], g_vcap[cur] * sizeof *g_vpools[cur]);
+      }
+      praos_pool* pp = &g_vpools[cur][v->npools++];
+      hex_in(a, pp->hash28, 28);
+      hex_in(b, pp->vrf_hash32, 32);
+      hex_in(c, pp->sigma_fp, 16);
+      v->pools = g_vpools[cur];
+    } else if (sscanf(line, "eta0 %127s", a) == 1) {
       hex_in(a, g_eta0, 32);
     } else if (sscanf(line, "params %llu %llu %llu %llu %127s", &x, &y, &z, &w, a) == 5) {
       g_params.slots_per_kes_period = x;
@@ -132,6 +185,23 @@ static void read_epoch_file(const char* path) {
   }
   fclose(f);
   g_env0.tip_is_origin = 1;
+  if (g_nviews == 0) g_nviews = 1;
+  g_views[0].first_epoch = 0;
+  g_views[0].pools = g_pools;
+  g_views[0].npools = g_npools;
+  g_views[0].lv_prot_major = g_env0.lv_prot_major;
+  g_views[0].max_header_size = g_env0.max_header_size;
+  g_views[0].max_body_size = g_env0.max_body_size;
+  for (uint32_t k = 1; k < g_nviews; k++)
+    if (g_views[k].first_epoch <= g_views[k - 1].first_epoch) DIE("view lines: first_epoch must increase");
+}
+
+/* the "forecast": the ledger view of epoch e (the last view line with first_epoch <= e) */
+static const praos_ledger_view* view_for(uint64_t e) {
+  const praos_ledger_view* v = &g_views[0];
+  for (uint32_t k = 1; k < g_nviews; k++)
+    if (g_views[k].first_epoch <= e) v = &g_views[k];
+  return v;
 }
 
 /* the stored headers, in chain order, through the secondary indexes */
@@ -467,6 +537,206 @@ static void phase_replay(const char* dir, int members) {
   praos_close(ctx);
 }
 
+/* ---- phase 2b: the db-analyser analysis (BenchmarkHeaderBatch.hs), epoch e on a worker thread
+ *      while the stream / ledger of epoch e+1 goes on ---- */
+typedef struct {                 /* one epoch's arena as the analysis fills it (reused, registered once) */
+  uint8_t* bytes;
+  size_t cap, len;
+  uint64_t* off;
+  uint32_t* hlen;
+  size_t n, ncap;
+  uint64_t first_slot, epoch;
+  int registered;
+} arena_t;
+
+typedef struct {
+  praos_ctx* ctx;
+  praos_group* g;
+  arena_t* a;
+  const praos_ledger_view* view;
+  state_buf* S;
+  praos_envelope* env;
+  /* out */
+  size_t stop;
+  int verdict;
+  int rc;
+  char err[256];
+} epoch_job;
+
+static void arena_push(arena_t* a, const uint8_t* hdr, uint32_t len, uint64_t slot, uint64_t epoch,
+                       praos_ctx* ctx, praos_group* g) {
+  if (a->n == 0) { a->first_slot = slot; a->epoch = epoch; a->len = 0; }
+  if (a->len + len > a->cap) {              /* grow: unregister, reallocate, register once more */
+    if (a->registered) {
+      if (g) praos_group_host_unregister(g, a->bytes);
+      else praos_host_unregister(ctx, a->bytes);
+    }
+    a->cap = 2 * (a->len + len);
+    a->bytes = realloc(a->bytes, a->cap);
+    const int rc = g ? praos_group_host_register(g, a->bytes, a->cap) : praos_host_register(ctx, a->bytes, a->cap);
+    if (rc != PRAOS_OK) DIE("host_register -> %d", rc);
+    a->registered = 1;
+  }
+  if (a->n == a->ncap) {
+    a->ncap = a->ncap ? 2 * a->ncap : 4096;
+    a->off = realloc(a->off, 8 * a->ncap);
+    a->hlen = realloc(a->hlen, 4 * a->ncap);
+  }
+  memcpy(a->bytes + a->len, hdr, len);
+  a->off[a->n] = a->len;
+  a->hlen[a->n] = len;
+  a->len += len;
+  a->n++;
+}
+
+/* validateEpochHeaders (Batch/Validate.hs) of one epoch under its forecast ledger view */
+static void* epoch_worker(void* arg) {
+  epoch_job* j = arg;
+  arena_t* a = j->a;
+  const size_t n = a->n;
+  j->rc = PRAOS_OK;
+  j->stop = n;
+  praos_nonce eta;
+  int rc = praos_ticked_epoch_nonce(&j->S->st, &g_ei, a->first_slot, &eta);
+  if (rc == PRAOS_OK)
+    rc = j->g ? praos_group_set_epoch(j->g, eta.neutral ? NULL : eta.hash, j->view->pools, j->view->npools, &g_params)
+              : praos_set_epoch(j->ctx, eta.neutral ? NULL : eta.hash, j->view->pools, j->view->npools, &g_params);
+  uint8_t* verdict = calloc(n, 1);
+  uint16_t* bits = calloc(n, 2);
+  int32_t* pidx = calloc(n, 4);
+  uint8_t* decbuf = calloc(n, 157);
+  uint64_t *slot = (uint64_t*)decbuf, *bno = (uint64_t*)(decbuf + 8 * n), *ocn = (uint64_t*)(decbuf + 16 * n);
+  uint8_t *prev = decbuf + 24 * n, *cold = decbuf + 56 * n, *hh = decbuf + 88 * n, *gen = decbuf + 124 * n;
+  uint32_t* bsz = (uint32_t*)(decbuf + 120 * n);
+  uint8_t* nonce = decbuf + 125 * n;
+  praos_header_bytes hb = {n, a->bytes, a->len, a->off, a->hlen};
+  praos_out out = {bits, pidx, NULL, NULL, nonce};
+  praos_decoded dec;
+  memset(&dec, 0, sizeof dec);
+  dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;
+  dec.cold_vk = cold; dec.header_hash = hh; dec.body_size = bsz;
+  if (rc == PRAOS_OK)
+    rc = j->g ? praos_group_verify_header_bytes(j->g, &hb, &out, &dec) : praos_verify_header_bytes(j->ctx, &hb, &out, &dec);
+  if (rc == PRAOS_OK) {
+    praos_headers h;
+    memset(&h, 0, sizeof h);
+    h.n = n; h.slot = slot; h.cold_vk = cold; h.ocert_n = ocn;
+    praos_envelope* env = j->env;
+    env->lv_prot_major = j->view->lv_prot_major;        /* the forecast view's envelope limits */
+    env->max_header_size = j->view->max_header_size;
+    env->max_body_size = j->view->max_body_size;
+    env->block_no = bno; env->header_hash = hh; env->header_size = a->hlen; env->body_size = bsz;
+    size_t stop = 0, done = 0;
+    praos_ctx* c0 = j->g ? praos_group_ctx(j->g, 0) : j->ctx;
+    rc = praos_validate_headers(c0, &h, prev, gen, &out, env, &g_ei, &j->S->st, verdict, &stop, &done);
+    env->block_no = NULL; env->header_hash = NULL; env->header_size = NULL; env->body_size = NULL;
+    if (rc == PRAOS_OK && done != n) { rc = -100; snprintf(j->err, sizeof j->err, "epoch did not fold through"); }
+    j->stop = stop;
+    if (stop < n) j->verdict = verdict[stop];
+  }
+  if (rc != PRAOS_OK && !j->err[0])
+    snprintf(j->err, sizeof j->err, "%s", j->g ? praos_group_last_error(j->g) : praos_last_error(j->ctx));
+  j->rc = rc;
+  free(verdict); free(bits); free(pidx); free(decbuf);
+  return NULL;
+}
+
+static void phase_analysis(const chain_t* ch, int members) {
+  praos_group* g = NULL;
+  praos_ctx* ctx = NULL;
+  if (members > 0) {
+    int devs[64] = {0};
+    if (members > 64) DIE("members: 1..64");
+    g = praos_group_open(devs, members);
+    if (!g) DIE("praos_group_open");
+  } else {
+    ctx = praos_open(0);
+    if (!ctx) DIE("praos_open(0)");
+  }
+  static state_buf S;
+  genesis_state(&S);
+  praos_envelope env = g_env0;
+  arena_t ar[2];
+  memset(ar, 0, sizeof ar);
+  uint64_t validated = 0, stop_index = ch->n, epochs = 0, first_index[2] = {0, 0};
+  int stop_verdict = 0, cur = 0, running = 0, stopped = 0;
+  pthread_t th;
+  epoch_job job;
+  /* waits for the epoch on the worker; 1 if the chain goes on */
+  #define JOIN_WORKER()                                                                   \
+    do {                                                                                  \
+      if (running) {                                                                      \
+        pthread_join(th, NULL);                                                           \
+        running = 0;                                                                      \
+        if (job.rc != PRAOS_OK) DIE("analysis epoch: %d %s", job.rc, job.err);            \
+        const int w = 1 - cur;                                                            \
+        if (job.stop < ar[w].n) {                                                         \
+          stop_index = first_index[w] + job.stop; stop_verdict = job.verdict;             \
+          validated += job.stop; stopped = 1;                                             \
+        } else {                                                                          \
+          validated += ar[w].n;                                                           \
+        }                                                                                 \
+      }                                                                                   \
+    } while (0)
+  for (size_t i = 0; i <= ch->n && !stopped; i++) {
+    const uint64_t e = i < ch->n ? (ch->slot[i] - g_ei.epoch_base_slot) / g_ei.epoch_length : UINT64_MAX;
+    if (ar[cur].n && (i == ch->n || e != ar[cur].epoch)) {
+      /* epoch ar[cur] complete: its view was forecast from the ledger state before its first
+       * block; the previous epoch's validation must finish first (its state is this one's input) */
+      JOIN_WORKER();
+      if (stopped) break;
+      memset(&job, 0, sizeof job);
+      job.ctx = ctx; job.g = g; job.a = &ar[cur]; job.view = view_for(ar[cur].epoch); job.S = &S; job.env = &env;
+      epochs++;
+      if (pthread_create(&th, NULL, epoch_worker, &job) != 0) DIE("pthread_create");
+      running = 1;
+      cur = 1 - cur;                          /* the stream goes on into the other arena */
+      ar[cur].n = 0;
+    }
+    if (i == ch->n) break;
+    if (ar[cur].n == 0) first_index[cur] = i;
+    arena_push(&ar[cur], ch->bytes + ch->off[i], ch->hlen[i], ch->slot[i], e, ctx, g);
+  }
+  JOIN_WORKER();
+  #undef JOIN_WORKER
+  print_state(g ? "analysis_group" : "analysis", &S, &env, validated, stop_index, stop_verdict, epochs, -1);
+  for (int k = 0; k < 2; k++) {
+    if (ar[k].registered) {
+      if (g) praos_group_host_unregister(g, ar[k].bytes);
+      else praos_host_unregister(ctx, ar[k].bytes);
+    }
+    free(ar[k].bytes); free(ar[k].off); free(ar[k].hlen);
+  }
+  if (g) praos_group_close(g);
+  else praos_close(ctx);
+}
+
+/* ---- phase 2c: every ledger view in one replay call ---- */
+static void phase_replay_views(const char* dir, int members) {
+  static state_buf S;
+  genesis_state(&S);
+  praos_envelope env = g_env0;
+  praos_replay_stats rs;
+  if (members > 0) {
+    int devs[64] = {0};
+    if (members > 64) DIE("members: 1..64");
+    praos_group* g = praos_group_open(devs, members);
+    if (!g) DIE("praos_group_open");
+    const int rc = praos_group_replay_immutable_views(g, dir, g_views, g_nviews, &g_params, &g_ei, &env, &S.st, 97,
+                                                      NULL, 0, &rs);
+    if (rc != PRAOS_OK) DIE("group views replay -> %d: %s", rc, praos_group_last_error(g));
+    print_state("replay_views_group", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs, -1);
+    praos_group_close(g);
+    return;
+  }
+  praos_ctx* ctx = praos_open(0);
+  if (!ctx) DIE("praos_open(0)");
+  CK(ctx, praos_replay_immutable_views(ctx, dir, g_views, g_nviews, &g_params, &g_ei, &env, &S.st, 1 << 16, NULL, 0,
+                                       &rs));
+  print_state("replay_views", &S, &env, rs.validated, rs.stop_index, (int)rs.stop_verdict, rs.epochs, -1);
+  praos_close(ctx);
+}
+
 /* ---- phase 3: several threads, one context each; and a group ---- */
 typedef struct {
   const chain_t* ch;
@@ -538,9 +808,91 @@ static void phase_threads(const chain_t* ch, int T) {
   fflush(stdout);
 }
 
+/* ---- chunk validation (Batch.hs verifyChunkIntegrity) ---- */
+static uint32_t crc32_ieee(const uint8_t* p, size_t n) {   /* System.FS.CRC (zlib's CRC-32) */
+  static uint32_t tab[256];
+  static int init;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tab[i] = c;
+    }
+    init = 1;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+static int chunk_main(const char* dir, int chunk, uint64_t spkp, int members) {
+  char p[4096];
+  size_t dl, sl;
+  snprintf(p, sizeof p, "%s/%05d.chunk", dir, chunk);
+  uint8_t* data = slurp(p, &dl);
+  snprintf(p, sizeof p, "%s/%05d.secondary", dir, chunk);
+  uint8_t* sec = slurp(p, &sl);
+  if (!data || !sec || sl % 56) DIE("chunk %d: missing file or malformed secondary index", chunk);
+  const size_t n = sl / 56;
+  /* block i = [blockOffset_i, blockOffset_i+1), the last to the end of the chunk (Secondary.hs) */
+  uint64_t* boff = calloc(n + 1, 8);
+  for (size_t i = 0; i < n; i++) boff[i] = be(sec + 56 * i, 8);
+  boff[n] = dl;
+  size_t nchk = 0;
+  uint64_t* off = calloc(n + 1, 8);
+  uint32_t* len = calloc(n + 1, 4);
+  size_t* which = calloc(n + 1, sizeof *which);
+  for (size_t i = 0; i < n; i++) {
+    if (boff[i] > boff[i + 1] || boff[i + 1] > dl) DIE("entry %zu outside its chunk", i);
+    const uint32_t want = (uint32_t)be(sec + 56 * i + 12, 4);
+    if (crc32_ieee(data + boff[i], boff[i + 1] - boff[i]) == want) continue;   /* checksum matches: trusted */
+    off[nchk] = boff[i];
+    len[nchk] = (uint32_t)(boff[i + 1] - boff[i]);
+    which[nchk++] = i;
+  }
+  praos_header_bytes hb = {nchk, data, dl, off, len};
+  uint8_t* res = calloc(nchk + 1, 1);
+  for (int pass = 0; pass < 2; pass++) {
+    memset(res, 0xEE, nchk + 1);
+    if (pass == 0) {
+      praos_ctx* ctx = praos_open(0);
+      if (!ctx) DIE("praos_open(0)");
+      CK(ctx, praos_verify_block_integrity(ctx, &hb, spkp, res, NULL));
+      praos_close(ctx);
+    } else {
+      int devs[64] = {0};
+      if (members < 1 || members > 64) DIE("members: 1..64");
+      praos_group* g = praos_group_open(devs, members);
+      if (!g) DIE("praos_group_open");
+      if (praos_group_verify_block_integrity(g, &hb, spkp, res, NULL) != PRAOS_OK)
+        DIE("%s", praos_group_last_error(g));
+      praos_group_close(g);
+    }
+    /* parseChunkFile stops at the first corrupt block and truncates the file at its offset */
+    size_t first = n;
+    for (size_t j = 0; j < nchk; j++)
+      if (res[j]) { first = which[j]; break; }
+    printf("{\"phase\": \"%s\", \"blocks\": %zu, \"checked\": %zu, \"first_corrupt\": %zu, "
+           "\"truncate_at\": %llu, \"results\": [", pass ? "chunk_group" : "chunk", n, nchk, first,
+           (unsigned long long)(first < n ? boff[first] : dl));
+    for (size_t i = 0, j = 0; i < n; i++) {
+      int r = -1;
+      if (j < nchk && which[j] == i) r = res[j++];
+      printf("%s%d", i ? ", " : "", r);
+    }
+    printf("]}\n");
+    fflush(stdout);
+  }
+  free(boff); free(off); free(len); free(which); free(res); free(data); free(sec);
+  return 0;
+}
+
 int main(int argc, char** argv) {
-  if (argc != 4) DIE("usage: %s <immutable dir> <epoch file> <threads>", argv[0]);
   if (praos_abi_version() != PRAOS_ABI_VERSION) DIE("ABI version %d, header %d", praos_abi_version(), PRAOS_ABI_VERSION);
+  if (argc == 6 && strcmp(argv[1], "--chunk") == 0)
+    return chunk_main(argv[2], atoi(argv[3]), strtoull(argv[4], NULL, 10), atoi(argv[5]));
+  if (argc != 4) DIE("usage: %s <immutable dir> <epoch file> <threads> | --chunk <dir> <chunk> <spkp> <members>",
+                     argv[0]);
   read_epoch_file(argv[2]);
   chain_t ch;
   read_chain(argv[1], &ch);
@@ -552,6 +904,12 @@ int main(int argc, char** argv) {
   if (!g_tpraos) phase_typed(&ch, T);
   phase_replay(argv[1], 0);
   phase_replay(argv[1], T);
+  if (!g_tpraos) {
+    phase_analysis(&ch, 0);
+    phase_analysis(&ch, T);
+    phase_replay_views(argv[1], 0);
+    phase_replay_views(argv[1], T);
+  }
   if (!g_tpraos) phase_threads(&ch, T);
   return 0;
 }

@@ -36,7 +36,10 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
   , praosValidateHeaderBytes
     -- * Headers from stored bytes, Storable vectors (Batch.Validate)
   , SpanResult (..)
+  , ArenaPin (..)
   , praosValidateHeaderSpans
+  , praosHostRegister
+  , praosHostUnregister
     -- * TPraos (Shelley..Alonzo) headers from stored bytes
   , TPraosBatchResult (..)
   , praosTickedEpochNonceTPraos
@@ -48,6 +51,12 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
   , ReplayStats (..)
   , praosReplayImmutable
   , praosReplayImmutableTPraos
+  , LedgerViewC (..)
+  , praosReplayImmutableViews
+    -- * ImmutableDB chunk validation (verifyBlockIntegrity batched)
+  , ChunkValidation (..)
+  , verifyChunkIntegrity
+  , praosVerifyBlockIntegrity
     -- * Error reconstruction (typed constructors: module Batch.Errors)
   , verdictToError
   ) where
@@ -82,6 +91,7 @@ data PraosGroup
 -- struct praos_decoded (168 bytes): status@0 block_no@8 slot@16 prev_hash@24 prev_is_genesis@32 cold_vk@40 body_size@72 ocert_n@96 header_hash@160
 -- struct praos_tpraos_headers (136 bytes): h@0 leader_out@120 leader_proof@128
 -- struct praos_tpraos_out (40 bytes): bits@0 pool_idx@8 beta_eta@16 beta_leader@24 nonce@32
+-- struct praos_ledger_view (48 bytes): first_epoch@0 pools@8 npools@16 reserved@20 lv_prot_major@24 max_header_size@32 max_body_size@40
 
 foreign import ccall safe "praos_open"        c_open        :: CInt -> IO (Ptr PraosCtx)
 foreign import ccall safe "praos_close"       c_close       :: Ptr PraosCtx -> IO ()
@@ -145,9 +155,20 @@ foreign import ccall safe "praos_group_replay_immutable" c_group_replay_immutabl
 foreign import ccall safe "praos_group_replay_immutable_tpraos" c_group_replay_immutable_tpraos
   :: Ptr PraosGroup -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
   -> CSize -> Ptr Word8 -> Ptr Word16 -> CSize -> Ptr () -> IO CInt
+-- ABI 14: a ledger view per epoch in the replay; block integrity (ImmutableDB chunk validation)
+foreign import ccall safe "praos_replay_immutable_views" c_replay_immutable_views
+  :: Ptr PraosCtx -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
+foreign import ccall safe "praos_group_replay_immutable_views" c_group_replay_immutable_views
+  :: Ptr PraosGroup -> CString -> Ptr () -> Word32 -> Ptr () -> Ptr () -> Ptr () -> Ptr ()
+  -> CSize -> Ptr Word8 -> CSize -> Ptr () -> IO CInt
+foreign import ccall safe "praos_verify_block_integrity" c_verify_block_integrity
+  :: Ptr PraosCtx -> Ptr () -> Word64 -> Ptr Word8 -> Ptr Word8 -> IO CInt
+foreign import ccall safe "praos_group_verify_block_integrity" c_group_verify_block_integrity
+  :: Ptr PraosGroup -> Ptr () -> Word64 -> Ptr Word8 -> Ptr Word8 -> IO CInt
 
 abiVersion :: CInt
-abiVersion = 13
+abiVersion = 14
 
 -- ---------------------------------------------------------------- context
 
@@ -230,21 +251,34 @@ verifyTPraosHeaderBytes ctx hb out dec = check ctx $ case ctx of
   PraosBatchCtx p -> c_verify_tpraos_header_bytes p hb out dec nullPtr nullPtr
   PraosBatchGroup g _ _ -> c_group_verify_tpraos_header_bytes g hb out dec nullPtr nullPtr
 
+-- | Who page-locks a batch's arena: 'PinForCall' -- the call registers it for its own
+-- duration when it is 64 MiB or more -- or 'PinnedByCaller': the caller registered it once
+-- ('praosHostRegister', e.g. an arena reused epoch after epoch and re-registered only when it
+-- grows), so the call's time holds no pinning.
+data ArenaPin = PinForCall | PinnedByCaller
+  deriving (Eq, Show)
+
+-- | praos_host_register (every member of a group): uploads from inside the range go by direct
+-- DMA.  Pair with 'praosHostUnregister' before the buffer is freed or moved.
+praosHostRegister :: PraosBatchCtx -> Ptr Word8 -> Int -> IO ()
+praosHostRegister ctx ap alen = check ctx $ case ctx of
+  PraosBatchCtx p -> c_host_register p ap (fromIntegral alen)
+  PraosBatchGroup g _ _ -> c_group_host_register g ap (fromIntegral alen)
+
+praosHostUnregister :: PraosBatchCtx -> Ptr Word8 -> IO ()
+praosHostUnregister ctx ap = check ctx $ case ctx of
+  PraosBatchCtx p -> c_host_unregister p ap
+  PraosBatchGroup g _ _ -> c_group_host_unregister g ap
+
 -- | The arena page-locked for the duration of the action when it is 64 MiB or more
 -- (praos_host_register: the upload goes by direct DMA, no staging copy; a group pins it
--- once for every member).  The unregister runs whatever the action throws (a failing
--- batch call), so a GHC-owned buffer is never freed while still page-locked.
-withRegisteredArena :: PraosBatchCtx -> Ptr Word8 -> Int -> IO a -> IO a
-withRegisteredArena ctx ap alen act
-  | alen < 64 * 1024 * 1024 = act
-  | otherwise = bracket_ reg unreg act
-  where
-    reg = check ctx $ case ctx of
-      PraosBatchCtx p -> c_host_register p ap (fromIntegral alen)
-      PraosBatchGroup g _ _ -> c_group_host_register g ap (fromIntegral alen)
-    unreg = check ctx $ case ctx of
-      PraosBatchCtx p -> c_host_unregister p ap
-      PraosBatchGroup g _ _ -> c_group_host_unregister g ap
+-- once for every member) and the caller has not pinned it.  The unregister runs whatever the
+-- action throws (a failing batch call), so a GHC-owned buffer is never freed while still
+-- page-locked.
+withRegisteredArena :: PraosBatchCtx -> ArenaPin -> Ptr Word8 -> Int -> IO a -> IO a
+withRegisteredArena ctx pin ap alen act
+  | pin == PinnedByCaller || alen < 64 * 1024 * 1024 = act
+  | otherwise = bracket_ (praosHostRegister ctx ap alen) (praosHostUnregister ctx ap) act
 
 -- ---------------------------------------------------------------- marshalling helpers
 
@@ -449,10 +483,10 @@ data SpanResult = SpanResult
 -- copy).  The decoded fields and nonce values the fold reads stay in one allocation of 157
 -- bytes per header.
 praosValidateHeaderSpans :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits
-                         -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> BS.ByteString
+                         -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> ArenaPin -> BS.ByteString
                          -> VS.Vector Word64 -> VS.Vector Word32 -> VSM.IOVector Word8 -> VSM.IOVector Word16
                          -> IO SpanResult
-praosValidateHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor arena offs lens
+praosValidateHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor pin arena offs lens
                          verdicts bits = do
   let n = VS.length offs
   when (VS.length lens /= n || VSM.length verdicts /= n || VSM.length bits /= n) $
@@ -484,7 +518,7 @@ praosValidateHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) tip stateCbor are
       fillBytes dec 0 168
       pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
       pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
-      withRegisteredArena ctx (castPtr ap) alen $ verifyHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
+      withRegisteredArena ctx pin (castPtr ap) alen $ verifyHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
       fillBytes hv 0 120
       pokeByteOff hv 0 (fromIntegral n :: CSize) >> pokeByteOff hv 8 slot >> pokeByteOff hv 16 cold
       pokeByteOff hv 56 ocn
@@ -633,10 +667,10 @@ praosValidateTPraosHeaderBytes ctx ei (maxPV, pvMajor, maxHS, maxBS) extra tip s
 -- caller's vectors.  The epoch must have been installed with 'praosSetEpoch' under
 -- 'praosTickedEpochNonceTPraos''s nonce.
 praosValidateTPraosHeaderSpans :: PraosBatchCtx -> (Word64, Word64, Word64, Word64) -> EnvLimits -> Maybe BS.ByteString
-                               -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> BS.ByteString
+                               -> Maybe (Word64, Word64, BS.ByteString) -> BS.ByteString -> ArenaPin -> BS.ByteString
                                -> VS.Vector Word64 -> VS.Vector Word32 -> VSM.IOVector Word8 -> VSM.IOVector Word16
                                -> VSM.IOVector Word16 -> IO SpanResult
-praosValidateTPraosHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor arena offs lens verdicts
+praosValidateTPraosHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) extra tip stateCbor pin arena offs lens verdicts
                                failures bits = do
   let n = VS.length offs
   when (VS.length lens /= n || VSM.length verdicts /= n || VSM.length failures /= n || VSM.length bits /= n) $
@@ -665,7 +699,7 @@ praosValidateTPraosHeaderSpans ctx ei (maxPV, pvMajor, maxHS, maxBS) extra tip s
       fillBytes dec 0 168
       pokeByteOff dec 8 bno >> pokeByteOff dec 16 slot >> pokeByteOff dec 24 prev >> pokeByteOff dec 32 gen
       pokeByteOff dec 40 cold >> pokeByteOff dec 72 bsz >> pokeByteOff dec 96 ocn >> pokeByteOff dec 160 hh
-      withRegisteredArena ctx (castPtr ap) alen $ verifyTPraosHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
+      withRegisteredArena ctx pin (castPtr ap) alen $ verifyTPraosHeaderBytes ctx (castPtr hb) (castPtr out) (castPtr dec)
       fillBytes th 0 136
       pokeByteOff th 0 (fromIntegral n :: CSize) >> pokeByteOff th 8 slot >> pokeByteOff th 16 cold
       pokeByteOff th 56 ocn
@@ -774,6 +808,128 @@ praosReplayImmutableTPraos ctx dir pools pp ei (maxPV, pvMajor, maxHS, maxBS) ex
       h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
       pure (Just (s, b, h))
     pure (stats, vs, fs, st', tip')
+
+-- | A LedgerView as the ABI takes it (praos_ledger_view): from which epoch on it holds, the
+-- PoolDistr entries and the envelope limits (pvMajor lvProtocolVersion, lvMaxHeaderSize,
+-- lvMaxBodySize).  db-analyser forecasts one per epoch from the ledger state it advances
+-- (Analysis.hs:564-572; all of them change only at an epoch boundary).
+data LedgerViewC = LedgerViewC
+  { lvcFirstEpoch :: !Word64
+  , lvcPools      :: ![(BS.ByteString, BS.ByteString, Integer)]
+  , lvcProtMajor  :: !Word64
+  , lvcMaxHeader  :: !Word64
+  , lvcMaxBody    :: !Word64
+  }
+
+-- | praos_[group_]replay_immutable_views: 'praosReplayImmutable' with a ledger view per epoch
+-- (the list sorted by first epoch; epoch e uses the last view starting at or before it) instead
+-- of one for the whole database.  A batch never spans two views; the fold of each batch uses
+-- its view's PoolDistr and envelope limits.
+praosReplayImmutableViews :: PraosBatchCtx -> FilePath -> [LedgerViewC] -> PraosParamsC
+                          -> (Word64, Word64, Word64, Word64) -> Word64 -> Maybe (Word64, Word64, BS.ByteString)
+                          -> BS.ByteString -> Int
+                          -> IO (ReplayStats, BS.ByteString, Maybe (Word64, Word64, BS.ByteString))
+praosReplayImmutableViews ctx dir views pp ei maxPV tip stateCbor batchMax =
+  withCString dir $ \cdir -> withViews views $ \vp nv -> withParams pp $ \par ->
+  withEpochInfo ei $ \eip -> withChainState stateCbor 65536 $ \st ->
+  allocaBytes 120 $ \env -> allocaBytes 80 $ \rs -> do
+    fillBytes env 0 120
+    case tip of
+      Nothing -> pokeByteOff env 32 (1 :: Int32)
+      Just (s, b, h) -> pokeByteOff env 40 s >> pokeByteOff env 48 b >> pokeBS env 56 h
+    pokeByteOff env 88 maxPV             -- the limits of each view come from the view
+    check ctx $ case ctx of
+      PraosBatchCtx p -> c_replay_immutable_views p cdir vp nv par eip (castPtr env) st (fromIntegral batchMax)
+                                                  nullPtr 0 (castPtr rs)
+      PraosBatchGroup g _ _ -> c_group_replay_immutable_views g cdir vp nv par eip (castPtr env) st
+                                                              (fromIntegral batchMax) nullPtr 0 (castPtr rs)
+    stats <- ReplayStats <$> peekByteOff rs 0 <*> peekByteOff rs 8 <*> peekByteOff rs 16 <*> peekByteOff rs 24
+                         <*> peekByteOff rs 32 <*> peekByteOff rs 36 <*> peekByteOff rs 40 <*> peekByteOff rs 44
+                         <*> peekByteOff rs 48 <*> peekByteOff rs 56 <*> peekByteOff rs 64 <*> peekByteOff rs 72
+    st' <- encodeChainState st
+    origin :: Int32 <- peekByteOff env 32
+    tip' <- if origin /= 0 then pure Nothing else do
+      s <- peekByteOff env 40
+      b <- peekByteOff env 48
+      h <- BS.packCStringLen (castPtr (env `plusPtr` 56), 32)
+      pure (Just (s, b, h))
+    pure (stats, st', tip')
+
+-- | The praos_ledger_view array (48 bytes each), every view's pool array kept alive around it.
+withViews :: [LedgerViewC] -> (Ptr () -> Word32 -> IO a) -> IO a
+withViews views k = allocaBytes (48 * max 1 (length views)) $ \vp -> go vp (zip [0 ..] views)
+  where
+    go vp [] = k (castPtr vp) (fromIntegral (length views))
+    go vp ((i, LedgerViewC {lvcFirstEpoch, lvcPools, lvcProtMajor, lvcMaxHeader, lvcMaxBody}) : rest) =
+      withPools lvcPools $ \pp np -> do
+        let q = vp `plusPtr` (48 * i)
+        fillBytes q 0 48
+        pokeByteOff q 0 lvcFirstEpoch >> pokeByteOff q 8 pp >> pokeByteOff q 16 np
+        pokeByteOff q 24 lvcProtMajor >> pokeByteOff q 32 lvcMaxHeader >> pokeByteOff q 40 lvcMaxBody
+        go vp rest
+
+-- ---------------------------------------------------------------- ImmutableDB chunk validation
+
+-- | praos_[group_]verify_block_integrity: 'verifyBlockIntegrity' (Shelley/Ledger/Integrity.hs:14-20
+-- = verifyHeaderIntegrity, KES at t = max 0 (kp - c0), and blockMatchesHeader, hashTxSeq of the
+-- stored segments) of the blocks @arena[off_i .. off_i + len_i)@, in one GPU batch (sharded over
+-- a group's members).  Per block 0 (True) or PRAOS_BLK_* bits (1 decode, 2 KES, 4 body hash).
+praosVerifyBlockIntegrity :: PraosBatchCtx -> Word64 -> BS.ByteString -> VS.Vector Word64 -> VS.Vector Word32
+                          -> IO (VS.Vector Word8)
+praosVerifyBlockIntegrity ctx spkp arena offs lens = do
+  let n = VS.length offs
+  when (VS.length lens /= n) $ throwIO (PraosBatchError (-1) "praosVerifyBlockIntegrity: vector lengths differ")
+  res <- VSM.new n
+  BSU.unsafeUseAsCStringLen arena $ \(ap, alen) ->
+    VS.unsafeWith offs $ \offp -> VS.unsafeWith lens $ \lenp -> VSM.unsafeWith res $ \rp ->
+    allocaBytes 40 $ \hb -> do
+      pokeByteOff hb 0 (fromIntegral n :: CSize) >> pokeByteOff hb 8 ap
+      pokeByteOff hb 16 (fromIntegral alen :: CSize)
+      pokeByteOff hb 24 offp >> pokeByteOff hb 32 lenp
+      check ctx $ case ctx of
+        PraosBatchCtx p -> c_verify_block_integrity p (castPtr hb) spkp rp nullPtr
+        PraosBatchGroup g _ _ -> c_group_verify_block_integrity g (castPtr hb) spkp rp nullPtr
+  VS.unsafeFreeze res
+
+-- | One chunk's validation outcome: per block Nothing (its CRC matched the secondary index's
+-- checksum: trusted without the integrity check) or the PRAOS_BLK_* bits (0 = intact), the first
+-- corrupt block and the offset the chunk file is truncated at (its length when none).
+data ChunkValidation = ChunkValidation
+  { cvResults      :: ![Maybe Word8]
+  , cvFirstCorrupt :: !(Maybe Int)
+  , cvTruncateAt   :: !Word64
+  }
+
+-- | The expensive part of ImmutableDB chunk validation batched on the GPUs: parseChunkFile
+-- (ImmutableDB/Impl/Parser.hs:118-141, called from validateChunk, Validation.hs:379-384) runs
+-- @checkIntegrity@ (= verifyBlockIntegrity) on every block whose CRC32 does not match the
+-- secondary index entry's checksum, in file order, and stops at the first corrupt block,
+-- truncating the chunk file at its offset.  Here the blocks are the chunk bytes cut at the
+-- entries' block offsets (block i ends where block i+1 starts, the last at the end of the
+-- chunk, Secondary.hs:93-128); the CRCs are computed on the host ('computeCRC', as parseChunkFile
+-- does for every block anyway) and the mismatching blocks go to 'praosVerifyBlockIntegrity' in
+-- one call.  (The block decode, the CRC and the prev-hash line-up stay the reference's; this
+-- replaces only the @isNotCorrupt@ calls.  Replayed from C by ffi_harness --chunk.)
+verifyChunkIntegrity :: PraosBatchCtx -> Word64 -> (BS.ByteString -> Word32) -> BS.ByteString
+                     -> [(Word64, Word32)] -> IO ChunkValidation
+verifyChunkIntegrity ctx spkp crc32 chunk entries = do
+  let n = length entries
+      bounds = zip (map fst entries) (drop 1 (map fst entries) ++ [fromIntegral (BS.length chunk)])
+      spans = [ (i, o, e - o) | (i, ((o, e), (_, want))) <- zip [0 ..] (zip bounds entries)
+                              , crc32 (BS.take (fromIntegral (e - o)) (BS.drop (fromIntegral o) chunk)) /= want ]
+  when (or [ e < o || e > fromIntegral (BS.length chunk) | (o, e) <- bounds ]) $
+    throwIO (PraosBatchError (-2) "verifyChunkIntegrity: a secondary index entry outside its chunk")
+  res <- praosVerifyBlockIntegrity ctx spkp chunk (VS.fromList [ o | (_, o, _) <- spans ])
+                                   (VS.fromList [ fromIntegral l | (_, _, l) <- spans ])
+  let checked = zip [ i | (i, _, _) <- spans ] (VS.toList res)
+      results = [ lookup i checked | i <- [0 .. n - 1] ]
+      firstBad = case [ i | (i, r) <- checked, r /= 0 ] of
+        (i : _) -> Just i
+        []      -> Nothing
+  pure ChunkValidation
+    { cvResults = results
+    , cvFirstCorrupt = firstBad
+    , cvTruncateAt = maybe (fromIntegral (BS.length chunk)) (\i -> fst (entries !! i)) firstBad }
 
 -- ---------------------------------------------------------------- errors
 

@@ -100,12 +100,15 @@ data PraosBlockOps blk c = PraosBlockOps
 
 -- | One epoch's headers as the ImmutableDB stores them: the header spans back to back in one
 -- arena (what 'GetRawHeader' streams), their offsets and lengths, and a way to decode header
--- i (called for the header that stops the fold and for the last valid header's 'AnnTip').
+-- i (called for the header that stops the fold and for the last valid header's 'AnnTip'), and
+-- whether the caller keeps the arena page-locked itself ('PinnedByCaller': an arena reused epoch
+-- after epoch, registered once per growth, so no pinning happens inside the call).
 data EpochHeaders blk = EpochHeaders
   { ehArena  :: !BS.ByteString
   , ehOffset :: !(VS.Vector Word64)
   , ehLength :: !(VS.Vector Word32)
   , ehDecode :: Int -> Header blk
+  , ehPin    :: !ArenaPin
   }
 
 -- | The outcome of the fold and the batch's per-header verdicts (PRAOS_V_*: 0 valid; the
@@ -165,7 +168,7 @@ validateEpochHeaders
   -> HeaderState blk
   -> EpochHeaders blk
   -> IO (EpochValidation blk)
-validateEpochHeaders ctx ops pp f ei maxPV lv st0 EpochHeaders {ehArena, ehOffset, ehLength, ehDecode} = do
+validateEpochHeaders ctx ops pp f ei maxPV lv st0 EpochHeaders {ehArena, ehOffset, ehLength, ehDecode, ehPin} = do
   let n = VS.length ehOffset
   when (VS.length ehLength /= n) $ throwIO (PraosBatchError (-1) "offsets and lengths differ in length")
   if n == 0 then pure (EpochValidation VS.empty VS.empty 0 (Right st0)) else do
@@ -181,7 +184,7 @@ validateEpochHeaders ctx ops pp f ei maxPV lv st0 EpochHeaders {ehArena, ehOffse
     praosSetEpoch ctx eta (poolDistrEntries lvPoolDistr) (praosParamsC pp f)
     verdicts <- VSM.new n
     bits <- VSM.new n
-    r <- praosValidateHeaderSpans ctx ei limits tip0 stateCbor ehArena ehOffset ehLength verdicts bits
+    r <- praosValidateHeaderSpans ctx ei limits tip0 stateCbor ehPin ehArena ehOffset ehLength verdicts bits
     vs <- VS.unsafeFreeze verdicts
     bs <- VS.unsafeFreeze bits
     let stop = srChainStop r
@@ -317,7 +320,7 @@ validateEpochHeadersTPraos
   -> EpochHeaders blk
   -> IO (EpochValidationTPraos blk)
 validateEpochHeadersTPraos ctx ops (spkp, maxEvo, f) cRaw ei@(baseSlot, _, epochLen, _) maxPV lv st0
-                           EpochHeaders {ehArena, ehOffset, ehLength, ehDecode} = do
+                           EpochHeaders {ehArena, ehOffset, ehLength, ehDecode, ehPin} = do
   let n = VS.length ehOffset
   when (VS.length ehLength /= n) $ throwIO (PraosBatchError (-1) "offsets and lengths differ in length")
   if n == 0 then pure (EpochValidationTPraos (EpochValidation VS.empty VS.empty 0 (Right st0)) VS.empty) else do
@@ -345,7 +348,8 @@ validateEpochHeadersTPraos ctx ops (spkp, maxEvo, f) cRaw ei@(baseSlot, _, epoch
     verdicts <- VSM.new n
     fails <- VSM.new n
     bits <- VSM.new n
-    r <- praosValidateTPraosHeaderSpans ctx ei limits extra tip0 stateCbor ehArena ehOffset ehLength verdicts fails bits
+    r <- praosValidateTPraosHeaderSpans ctx ei limits extra tip0 stateCbor ehPin ehArena ehOffset ehLength verdicts fails
+                                        bits
     vs <- VS.unsafeFreeze verdicts
     fs <- VS.unsafeFreeze fails
     bs <- VS.unsafeFreeze bits

@@ -753,30 +753,115 @@ void praos_close(praos_ctx* c) {
   delete c;
 }
 
-int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
-                    const praos_params* params) {
-  if (!c || !params || (npools && !pools) || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
-  // Validate and build every table into locals first; the context is only
-  // touched once all of it succeeded (a failed call leaves NO epoch: runs
-  // return PRAOS_E_STATE until the next successful praos_set_epoch).
+}  // extern "C"
+
+// The pool part of a ledger view (lvPoolDistr): the caller's pools, the map hash28 -> caller
+// index (OCert counter slots), and on a device the tables the VRF join and the leader test read
+// (hashes sorted, 7 words each | VRF key hashes, 8 | x = -(sigma * c) in Fixed E34, 4 | sorted
+// index -> caller index).  praos_set_epoch installs one in the context; the per-epoch replay
+// (praos_replay_immutable_views) keeps one per view and swaps its device tables in between batches.
+struct rp_view {
+  int device = -1;
+  uint32_t npools = 0;
+  std::vector<praos_pool> pools;
+  std::map<std::string, int32_t> by_hash;
+  uint32_t *d_hash = nullptr, *d_vrf = nullptr, *d_x = nullptr;
+  int32_t* d_map = nullptr;
+};
+
+static void pool_tables_free(rp_view* v) {
+  if (!v || v->device < 0) return;
+  (void)hipFree(v->d_hash); (void)hipFree(v->d_vrf); (void)hipFree(v->d_x); (void)hipFree(v->d_map);
+  v->d_hash = v->d_vrf = v->d_x = nullptr;
+  v->d_map = nullptr;
+}
+
+// Builds v's host map and, for device >= 0, its device tables (on the current device).  On
+// failure nothing is left allocated and err says why.
+static int pool_tables_build(rp_view* v, int device, const praos_pool* pools, uint32_t npools,
+                             const praos_params* params, std::string* err) {
   std::vector<int32_t> order(npools);
   for (uint32_t i = 0; i < npools; i++) order[i] = (int32_t)i;
   std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
     return std::memcmp(pools[a].hash28, pools[b].hash28, 28) < 0;
   });
-  std::vector<uint32_t> h(7 * (size_t)std::max(1u, npools)), v(8 * (size_t)std::max(1u, npools)),
+  std::vector<uint32_t> h(7 * (size_t)std::max(1u, npools)), vr(8 * (size_t)std::max(1u, npools)),
       x(4 * (size_t)std::max(1u, npools));
   std::map<std::string, int32_t> by_hash;
-  bool bad = false;
   for (uint32_t s = 0; s < npools; s++) {
     const praos_pool& p = pools[order[s]];
     std::memcpy(&h[7 * s], p.hash28, 28);
-    std::memcpy(&v[8 * s], p.vrf_hash32, 32);
+    std::memcpy(&vr[8 * s], p.vrf_hash32, 32);
     uint8_t xr[16];
-    if (!praos_host::leader_x_raw(xr, p.sigma_fp, params->c_raw)) bad = true;
+    if (!praos_host::leader_x_raw(xr, p.sigma_fp, params->c_raw)) {
+      *err = "sigma * activeSlotLog out of range (x_raw > 16 * 10^34)";
+      return PRAOS_E_ARG;
+    }
     std::memcpy(&x[4 * s], xr, 16);
     by_hash[std::string((const char*)p.hash28, 28)] = order[s];
   }
+  v->device = device;
+  if (device >= 0) {
+    bool ok = hipMalloc(&v->d_hash, h.size() * 4) == hipSuccess && hipMalloc(&v->d_vrf, vr.size() * 4) == hipSuccess &&
+              hipMalloc(&v->d_x, x.size() * 4) == hipSuccess &&
+              hipMalloc(&v->d_map, std::max<size_t>(1, npools) * 4) == hipSuccess;
+    ok = ok && hipMemcpy(v->d_hash, h.data(), h.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(v->d_vrf, vr.data(), vr.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(v->d_x, x.data(), x.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         (!npools || hipMemcpy(v->d_map, order.data(), npools * 4, hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) {
+      pool_tables_free(v);
+      *err = "pool tables: device allocation / copy failed";
+      return PRAOS_E_OOM;
+    }
+  }
+  v->npools = npools;
+  v->pools.assign(pools, pools + npools);
+  v->by_hash.swap(by_hash);
+  return PRAOS_OK;
+}
+
+rp_view* rp_view_make(praos_ctx* c, const praos_pool* pools, uint32_t npools, const praos_params* params,
+                      bool device) {
+  if (!c || !params || (npools && !pools)) return nullptr;
+  if (device && c->device < 0) return nullptr;
+  if (device) (void)hipSetDevice(c->device);
+  rp_view* v = new rp_view;
+  std::string err;
+  if (pool_tables_build(v, device ? c->device : -1, pools, npools, params, &err) != PRAOS_OK) {
+    c->err = err;
+    delete v;
+    return nullptr;
+  }
+  return v;
+}
+
+void rp_view_free(praos_ctx* c, rp_view* v) {
+  if (!v) return;
+  if (c && v->device >= 0) (void)hipSetDevice(v->device);
+  pool_tables_free(v);
+  delete v;
+}
+
+rp_tables rp_tables_get(const praos_ctx* c) {
+  return {c->npools, c->d_pool_hash, c->d_pool_vrf, c->d_pool_x, c->d_pool_map};
+}
+
+void rp_tables_set(praos_ctx* c, const rp_tables& t) {
+  c->npools = t.npools;
+  c->d_pool_hash = t.hash; c->d_pool_vrf = t.vrf; c->d_pool_x = t.x; c->d_pool_map = t.map;
+}
+
+rp_tables rp_view_tables(const rp_view* v) { return {v->npools, v->d_hash, v->d_vrf, v->d_x, v->d_map}; }
+
+extern "C" {
+
+int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
+                    const praos_params* params) {
+  if (!c || !params || (npools && !pools) || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
+  // Validate and build every table first; the context is only touched once all of it
+  // succeeded (a failed call leaves NO epoch: runs return PRAOS_E_STATE until the next
+  // successful praos_set_epoch).
   if (c->device >= 0) {
     HIPCHK(c, hipSetDevice(c->device));
     (void)hipStreamSynchronize(c->stream);      // no run in flight reads the old tables
@@ -786,37 +871,30 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
   c->npools = 0;
   c->pools.clear();
   c->pool_by_hash.clear();
-  if (bad) {
-    c->err = "sigma * activeSlotLog out of range (x_raw > 16 * 10^34)";
-    return PRAOS_E_ARG;
-  }
+  rp_view v;
+  std::string err;
+  int r = pool_tables_build(&v, c->device, pools, npools, params, &err);
+  if (r != PRAOS_OK) { c->err = err; return r; }
   if (c->device >= 0) {
-    uint32_t *dh = nullptr, *dv = nullptr, *dx = nullptr, *de = nullptr;
-    int32_t* dm = nullptr;
-    bool ok = hipMalloc(&dh, h.size() * 4) == hipSuccess && hipMalloc(&dv, v.size() * 4) == hipSuccess &&
-              hipMalloc(&dx, x.size() * 4) == hipSuccess &&
-              hipMalloc(&dm, std::max<size_t>(1, npools) * 4) == hipSuccess && hipMalloc(&de, 32) == hipSuccess;
     uint32_t e0[8] = {0};
     if (eta0) std::memcpy(e0, eta0, 32);
-    ok = ok && hipMemcpy(dh, h.data(), h.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(dv, v.data(), v.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(dx, x.data(), x.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-         (!npools || hipMemcpy(dm, order.data(), npools * 4, hipMemcpyHostToDevice) == hipSuccess) &&
-         hipMemcpy(de, e0, 32, hipMemcpyHostToDevice) == hipSuccess;
-    if (!ok) {
-      (void)hipFree(dh); (void)hipFree(dv); (void)hipFree(dx); (void)hipFree(dm); (void)hipFree(de);
+    if (hipMalloc(&c->d_eta0, 32) != hipSuccess ||
+        hipMemcpy(c->d_eta0, e0, 32, hipMemcpyHostToDevice) != hipSuccess) {
+      pool_tables_free(&v);
+      (void)hipFree(c->d_eta0);
+      c->d_eta0 = nullptr;
       c->err = "praos_set_epoch: device allocation / copy failed";
       return PRAOS_E_OOM;
     }
-    c->d_pool_hash = dh; c->d_pool_vrf = dv; c->d_pool_x = dx; c->d_pool_map = dm; c->d_eta0 = de;
+    c->d_pool_hash = v.d_hash; c->d_pool_vrf = v.d_vrf; c->d_pool_x = v.d_x; c->d_pool_map = v.d_map;
   }
   c->params = *params;
   c->eta0_neutral = eta0 == nullptr;
   std::memset(c->eta0, 0, 32);
   if (eta0) std::memcpy(c->eta0, eta0, 32);
   c->npools = npools;
-  c->pools.assign(pools, pools + npools);
-  c->pool_by_hash.swap(by_hash);
+  c->pools.swap(v.pools);
+  c->pool_by_hash.swap(v.by_hash);
   c->have_epoch = true;
   return PRAOS_OK;
 }
@@ -1759,7 +1837,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_KES_PAIR) { c->kes_pair = value < 0 ? -1 : value; return PRAOS_OK; }
   if (opt == PRAOS_OPT_POOL_KEYS) {
     c->pool_keys = value < 0 ? -1 : (value != 0);
-    if (value == 2) c->pk_reset[0] = c->pk_reset[1] = true;
+    if (value == 2) c->pk_reset[0] = c->pk_reset[1] = c->pk_reset[2] = true;   // store 2: the KES leaf keys
     return PRAOS_OK;
   }
   return PRAOS_E_ARG;
@@ -2467,7 +2545,7 @@ static uint16_t tpraos_failures(uint16_t b, bool have, uint64_t m, uint64_t n) {
 
 static std::string issuer_hash(const praos_ctx* c, const praos_headers* h, const praos_out* crypto, size_t i) {
   const int32_t pidx = crypto->pool_idx ? crypto->pool_idx[i] : -1;
-  if (pidx >= 0 && (uint32_t)pidx < c->npools) return std::string((const char*)c->pools[pidx].hash28, 28);
+  if (pidx >= 0 && (size_t)pidx < c->pools.size()) return std::string((const char*)c->pools[pidx].hash28, 28);
   uint8_t hh[28];
   praos_host::blake2b(hh, 28, h->cold_vk + 32 * i, 32);
   return std::string((const char*)hh, 28);
@@ -2563,10 +2641,10 @@ struct CounterTab {
   std::map<std::string, uint32_t> extra;
 };
 
-static uint32_t counter_slot(const praos_ctx* c, CounterTab& T, const uint8_t* hash28) {
+static uint32_t counter_slot(const std::map<std::string, int32_t>& by_hash, CounterTab& T, const uint8_t* hash28) {
   const std::string k((const char*)hash28, 28);
-  auto p = c->pool_by_hash.find(k);
-  if (p != c->pool_by_hash.end()) return (uint32_t)p->second;
+  auto p = by_hash.find(k);
+  if (p != by_hash.end()) return (uint32_t)p->second;
   auto e = T.extra.find(k);
   if (e != T.extra.end()) return e->second;
   const uint32_t slot = (uint32_t)T.ctr.size();
@@ -2582,7 +2660,7 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
                      praos_chain_state* st, uint8_t* verdict, size_t* chain_stop, size_t* processed,
                      const praos_nonce* etas = nullptr, uint32_t netas = 0, const uint8_t* eta_idx = nullptr,
                      bool tpraos = false, const praos_nonce* extra_entropy = nullptr, uint16_t* failures = nullptr,
-                     const praos_nonce* evol_after = nullptr) {
+                     const praos_nonce* evol_after = nullptr, const rp_view* view = nullptr) {
   if (!c) return PRAOS_E_ARG;
   if (!h || !crypto || !crypto->bits || !crypto->nonce || !verdict || !ei || !st || !prev_hash) {
     c->err = "fold: a required pointer is NULL (headers, crypto bits / nonce, verdict, epoch info, state, prev_hash)";
@@ -2615,12 +2693,15 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     praos_nonce evolving, candidate, epoch_nonce, lab, leb;
     EnvTip tip;
   };
-  const uint32_t np = c->npools;
+  // the ledger view's pools: the batch's own (per-epoch replay) or the context's praos_set_epoch
+  const uint32_t np = view ? view->npools : (uint32_t)c->pools.size();
+  const praos_pool* vpools = view ? view->pools.data() : c->pools.data();
+  const std::map<std::string, int32_t>& by_hash = view ? view->by_hash : c->pool_by_hash;
   CounterTab T;
   T.ctr.assign(np, 0);
   T.has.assign(np, 0);
   for (size_t k = 0; k < st->m; k++) {
-    const uint32_t slot = counter_slot(c, T, st->counter_hash28 + 28 * k);
+    const uint32_t slot = counter_slot(by_hash, T, st->counter_hash28 + 28 * k);
     T.ctr[slot] = st->counter[k];
     T.has[slot] = 1;
   }
@@ -2665,7 +2746,7 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
     } else {
       uint8_t hh[28];
       praos_host::blake2b(hh, 28, h->cold_vk + 32 * i, 32);
-      k = counter_slot(c, T, hh);
+      k = counter_slot(by_hash, T, hh);
     }
     const uint64_t n = h->ocert_n[i];
     const bool has = T.has[k];
@@ -2733,7 +2814,7 @@ static int fold_impl(praos_ctx* c, const praos_headers* h, const uint8_t* prev_h
   size_t j = 0;
   for (size_t k = 0; k < Rhas.size(); k++) {
     if (!Rhas[k]) continue;
-    const uint8_t* key = k < np ? c->pools[k].hash28 : (const uint8_t*)T.extra_keys[k - np].data();
+    const uint8_t* key = k < np ? vpools[k].hash28 : (const uint8_t*)T.extra_keys[k - np].data();
     std::memcpy(st->counter_hash28 + 28 * j, key, 28);
     st->counter[j++] = Rctr[k];
   }
@@ -2757,10 +2838,10 @@ int rp_fold(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, cons
             const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei, praos_chain_state* st,
             const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx, const praos_nonce* evolving_after,
             bool tpraos, const praos_nonce* extra_entropy, uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
-            size_t* processed) {
+            size_t* processed, const rp_view* view) {
   if (!etas || !eta_idx || k == 0) return PRAOS_E_ARG;
   return fold_impl(c, h, prev_hash, prev_is_genesis, crypto, env, ei, st, verdict, chain_stop, processed, etas, k,
-                   eta_idx, tpraos, extra_entropy, failures, evolving_after);
+                   eta_idx, tpraos, extra_entropy, failures, evolving_after, view);
 }
 
 extern "C" {

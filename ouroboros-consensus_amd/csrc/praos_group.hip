@@ -148,7 +148,15 @@ praos_group* praos_group_open(const int* devices, int ndev) {
 
 void praos_group_close(praos_group* g) {
   if (!g) return;
+  // ranges the caller left registered are unpinned here (after the members' work has drained)
+  std::vector<void*> left;
+  left.swap(g->registered);
+  const int dev0 = g->ctx.empty() ? -1 : praos_ctx_device_(g->ctx[0]);
   for (praos_ctx* c : g->ctx) praos_close(c);
+  if (dev0 >= 0 && !left.empty()) {
+    (void)hipSetDevice(dev0);
+    for (void* p : left) (void)hipHostUnregister(p);
+  }
   delete g;
 }
 
@@ -244,6 +252,22 @@ int praos_group_verify_tpraos_header_bytes(praos_group* g, const praos_header_by
   });
 }
 
+// ImmutableDB chunk validation over the group (ABI 14): verifyBlockIntegrity of each block
+// (Shelley/Ledger/Integrity.hs:14-20), blocks independent, contiguous shards on the members.
+int praos_group_verify_block_integrity(praos_group* g, const praos_header_bytes* blocks, uint64_t slots_per_kes_period,
+                                       uint8_t* result, uint8_t* body_hash) {
+  if (!g || !blocks || !result || (blocks->n && (!blocks->off || !blocks->len))) return PRAOS_E_ARG;
+  const size_t m = g->ctx.size();
+  return fan_out(g, [&](size_t k) {
+    size_t i0, i1;
+    shard(blocks->n, m, k, &i0, &i1);
+    if (i1 == i0) return (int)PRAOS_OK;
+    std::vector<uint64_t> off;
+    praos_header_bytes s = bytes_at(blocks, i0, i1, off);
+    return praos_verify_block_integrity(g->ctx[k], &s, slots_per_kes_period, result + i0, at(body_hash, i0, 32));
+  });
+}
+
 // Page-locks a caller buffer once for every member (hipHostRegisterPortable: one pinning the
 // member devices all read by DMA), so each member's upload of its shard is a direct copy.
 int praos_group_host_register(praos_group* g, void* p, size_t len) {
@@ -276,11 +300,12 @@ static int group_replay(praos_group* g, const char* dir, const praos_pool* pools
                         const praos_params* params, const praos_epoch_info* ei, praos_envelope* env,
                         praos_chain_state* st, size_t batch_max, uint8_t* verdicts, uint16_t* failures,
                         size_t verdicts_cap, praos_replay_stats* stats, bool tpraos,
-                        const praos_nonce* extra_entropy) {
+                        const praos_nonce* extra_entropy, const praos_ledger_view* views = nullptr,
+                        uint32_t nviews = 0) {
   if (!g || g->ctx.empty()) return PRAOS_E_ARG;
   for (praos_ctx* c : g->ctx) praos_replay_scope_(c, true);
   const int r = rp_replay(g->ctx.data(), (int)g->ctx.size(), dir, pools, npools, params, ei, env, st, batch_max,
-                          verdicts, failures, verdicts_cap, stats, tpraos, extra_entropy);
+                          verdicts, failures, verdicts_cap, stats, tpraos, extra_entropy, views, nviews);
   for (praos_ctx* c : g->ctx) praos_replay_scope_(c, false);
   if (r != PRAOS_OK) g->err = praos_last_error(g->ctx[0]);
   return r;
@@ -301,6 +326,15 @@ int praos_group_replay_immutable_tpraos(praos_group* g, const char* dir, const p
                                         praos_replay_stats* stats) {
   return group_replay(g, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures, verdicts_cap, stats,
                       true, extra_entropy);
+}
+
+int praos_group_replay_immutable_views(praos_group* g, const char* dir, const praos_ledger_view* views,
+                                       uint32_t nviews, const praos_params* params, const praos_epoch_info* ei,
+                                       praos_envelope* env, praos_chain_state* st, size_t batch_max,
+                                       uint8_t* verdicts, size_t verdicts_cap, praos_replay_stats* stats) {
+  if (!views || nviews == 0) return PRAOS_E_ARG;
+  return group_replay(g, dir, nullptr, 0, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap, stats,
+                      false, nullptr, views, nviews);
 }
 
 }  // extern "C"

@@ -47,6 +47,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -171,13 +172,51 @@ constexpr size_t SPAN_GAP = 4096;             // headers this close share one up
 int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* pools, uint32_t npools,
               const praos_params* params, const praos_epoch_info* ei, praos_envelope* env, praos_chain_state* st,
               size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
-              praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy) {
+              praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy,
+              const praos_ledger_view* views, uint32_t nviews) {
   praos_ctx* const ctx = m > 0 && mem ? mem[0] : nullptr;
   for (int q = 0; q < m; q++)
     if (!mem[q]) return PRAOS_E_ARG;
   if (!ctx || !dir || !params || (npools && !pools) || !ei || !env || !st || !stats || batch_max == 0 ||
-      ei->epoch_length == 0 || (verdicts_cap && !verdicts))
+      ei->epoch_length == 0 || (verdicts_cap && !verdicts) || (views && (nviews == 0 || tpraos)))
     return PRAOS_E_ARG;
+  // The ledger views: one for the whole replay (pools + env's limits), or one per epoch range
+  // (praos_replay_immutable_views: the LedgerView db-analyser forecasts for each epoch).
+  struct View {
+    uint64_t first_epoch;
+    const praos_pool* pools;
+    uint32_t npools;
+    uint64_t prot, maxh, maxb;
+  };
+  std::vector<View> V;
+  if (views) {
+    for (uint32_t j = 0; j < nviews; j++) {
+      const praos_ledger_view& w = views[j];
+      if ((w.npools && !w.pools) || (j && w.first_epoch <= views[j - 1].first_epoch)) {
+        praos_set_error_(ctx, "replay: ledger views must have pools and strictly increasing first_epoch");
+        return PRAOS_E_ARG;
+      }
+      V.push_back({w.first_epoch, w.pools, w.npools, w.lv_prot_major, w.max_header_size, w.max_body_size});
+    }
+  } else {
+    V.push_back({0, pools, npools, env->lv_prot_major, env->max_header_size, env->max_body_size});
+  }
+  auto view_of = [&](uint64_t e) -> int {     // the last view with first_epoch <= e, or -1
+    int lo = -1;
+    for (int a = 0, b = (int)V.size() - 1; a <= b;) {
+      const int mid = (a + b) / 2;
+      if (V[mid].first_epoch <= e) { lo = mid; a = mid + 1; } else { b = mid - 1; }
+    }
+    return lo;
+  };
+  // the fold's pools per view (host maps; the context's praos_set_epoch tables when one view)
+  std::vector<std::unique_ptr<rp_view, std::function<void(rp_view*)>>> hv;
+  if (views)
+    for (const View& w : V) {
+      rp_view* v = rp_view_make(ctx, w.pools, w.npools, params, false);
+      if (!v) return PRAOS_E_ARG;
+      hv.emplace_back(v, [ctx](rp_view* p) { rp_view_free(ctx, p); });
+    }
   std::memset(stats, 0, sizeof *stats);
   ChunkReader rd;
   rd.dir = dir;
@@ -201,9 +240,10 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       return PRAOS_E_ARG;
     }
   }
-  // The ledger view (pools, parameters) is installed once; the epoch nonces travel
-  // with each batch, so a batch may span many epochs and stay large enough to fill the
-  // device even when epochs are short.
+  // The ledger view (pools, parameters) is installed once (per view with views); the epoch
+  // nonces travel with each batch, so a batch may span many epochs and stay large enough to fill
+  // the device even when epochs are short.
+  int v0 = 0;
   {
     praos_nonce eta0{};
     uint32_t l;
@@ -215,8 +255,13 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     }
     // (the installed nonce only seeds praos_set_epoch: every batch carries its own nonces)
     if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); return PRAOS_E_ARG; }
+    v0 = rd.peek(&p, &l, &s0) ? view_of(epoch_of(s0)) : 0;
+    if (v0 < 0) {
+      praos_set_error_(ctx, "replay: no ledger view for epoch " + std::to_string(epoch_of(s0)));
+      return PRAOS_E_ARG;
+    }
     for (int q = 0; q < m; q++) {
-      const int r = praos_set_epoch(mem[q], eta0.neutral ? nullptr : eta0.hash, pools, npools, params);
+      const int r = praos_set_epoch(mem[q], eta0.neutral ? nullptr : eta0.hash, V[v0].pools, V[v0].npools, params);
       if (r != PRAOS_OK) {
         if (q) praos_set_error_(ctx, std::string("member ") + std::to_string(q) + ": " + praos_last_error(mem[q]));
         return r;
@@ -227,6 +272,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     praos_batch* b = nullptr;
     int state = 0;                            // 0 free, 1 decoded, 2 nonces known, 3 crypto queued
     size_t n = 0;
+    int view = 0;                             // its ledger view (a batch never spans two)
     uint64_t index0 = 0;
     std::vector<praos_span> spans;
     std::vector<std::shared_ptr<Chunk>> chunks;
@@ -341,6 +387,11 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       cv.notify_all();
     }
   });
+  // per member: its own (praos_set_epoch) tables, the view they hold now, the other views' tables
+  std::vector<rp_tables> own(m);
+  std::vector<int> cur_view(m, v0);
+  std::vector<std::vector<rp_view*>> dev_views(m, std::vector<rp_view*>(V.size(), nullptr));
+  for (int q = 0; q < m; q++) own[q] = rp_tables_get(mem[q]);
   // ---- launcher: queues each batch's crypto (~30 launches: 1-2 ms of host time per batch,
   // kept off the nonce chain's thread)
   std::thread launcher([&] {
@@ -350,6 +401,24 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return stop || k >= nbatches || C.state == 2; });
         if (stop || k >= nbatches) return;
+      }
+      if (views && cur_view[k % (uint64_t)m] != C.view) {
+        // the member's launches from here on read this view's pool tables (queued kernels of
+        // earlier batches keep the tables they were launched with; all are freed at the end)
+        const int q = (int)(k % (uint64_t)m);
+        if (C.view == v0) {
+          rp_tables_set(mem[q], own[q]);
+        } else {
+          rp_view*& t = dev_views[q][C.view];
+          if (!t) t = rp_view_make(mem[q], V[C.view].pools, V[C.view].npools, params, true);
+          if (!t) {
+            if (mem[q] != ctx) praos_set_error_(ctx, praos_last_error(mem[q]));
+            fail(PRAOS_E_OOM);
+            return;
+          }
+          rp_tables_set(mem[q], rp_view_tables(t));
+        }
+        cur_view[q] = C.view;
       }
       const int rc = rp_run(member(k), C.b, C.etas.data(), (uint32_t)C.etas.size(), C.eidx.data());
       if (rc != PRAOS_OK && member(k) != ctx) praos_set_error_(ctx, praos_last_error(member(k)));
@@ -394,8 +463,14 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       env->header_size = C.len.data();
       env->body_size = C.bsize.data();
       size_t stp = 0, done = 0;
+      if (views) {                            // the envelope limits of the batch's ledger view
+        env->lv_prot_major = V[C.view].prot;
+        env->max_header_size = V[C.view].maxh;
+        env->max_body_size = V[C.view].maxb;
+      }
       rc = rp_fold(ctx, &h, C.prev.data(), C.gen.data(), &out, env, ei, st, C.etas.data(), (uint32_t)C.etas.size(),
-                   C.eidx.data(), C.evol.data(), tpraos, extra_entropy, C.v.data(), C.fails.data(), &stp, &done);
+                   C.eidx.data(), C.evol.data(), tpraos, extra_entropy, C.v.data(), C.fails.data(), &stp, &done,
+                   views ? hv[C.view].get() : nullptr);
       env->block_no = nullptr;
       env->header_hash = nullptr;
       env->header_size = nullptr;
@@ -449,10 +524,15 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     // the first batch is a quarter of the others: the nonce chain (the replay's sequential
     // part) starts as soon as possible
     const size_t cap = k == 0 ? std::max<size_t>(1, batch_max / 4) : batch_max;
+    bool no_view = false;
     while (C.off.size() < cap && rd.peek(&p, &l, &s)) {
       const uint64_t e = epoch_of(s);
       if (C.off.empty() || e != e_prev) {
         if (nep == 256) break;
+        const int w = view_of(e);
+        if (w < 0) { no_view = true; break; }
+        if (C.off.empty()) C.view = w;
+        else if (w != C.view) break;          // a batch never spans two ledger views
         nep++;
         e_prev = e;
       }
@@ -474,6 +554,11 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     }
     t_io += ms_since(t0);
     if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); fail(PRAOS_E_ARG); break; }
+    if (no_view && C.off.empty()) {
+      praos_set_error_(ctx, "replay: no ledger view for epoch " + std::to_string(epoch_of(s)));
+      fail(PRAOS_E_ARG);
+      break;
+    }
     if (C.off.empty()) break;
     t0 = std::chrono::steady_clock::now();
     const size_t n = C.n = C.off.size();
@@ -536,6 +621,11 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     if (C.bits) (void)hipHostFree(C.bits);
     if (C.pidx) (void)hipHostFree(C.pidx);
   }
+  // every batch has finished: the members get their own tables back, the views' go
+  for (int q = 0; q < m; q++) {
+    rp_tables_set(mem[q], own[q]);
+    for (rp_view* t : dev_views[q]) rp_view_free(mem[q], t);
+  }
   stats->ms_io = t_io;
   stats->ms_device = t_dev + t_wait;
   stats->ms_nonce = t_nonce;
@@ -575,6 +665,18 @@ extern "C" int praos_replay_immutable_tpraos(praos_ctx* ctx, const char* dir, co
   praos_replay_scope_(ctx, true);
   const int r = rp_replay(&ctx, 1, dir, pools, npools, params, ei, env, st, batch_max, verdicts, failures,
                           verdicts_cap, stats, true, extra_entropy);
+  praos_replay_scope_(ctx, false);
+  return r;
+}
+
+extern "C" int praos_replay_immutable_views(praos_ctx* ctx, const char* dir, const praos_ledger_view* views,
+                                            uint32_t nviews, const praos_params* params, const praos_epoch_info* ei,
+                                            praos_envelope* env, praos_chain_state* st, size_t batch_max,
+                                            uint8_t* verdicts, size_t verdicts_cap, praos_replay_stats* stats) {
+  if (!views || nviews == 0) return PRAOS_E_ARG;
+  praos_replay_scope_(ctx, true);
+  const int r = rp_replay(&ctx, 1, dir, nullptr, 0, params, ei, env, st, batch_max, verdicts, nullptr, verdicts_cap,
+                          stats, false, nullptr, views, nviews);
   praos_replay_scope_(ctx, false);
   return r;
 }

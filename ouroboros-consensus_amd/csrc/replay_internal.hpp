@@ -36,17 +36,37 @@ int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t*
 int rp_run(praos_ctx* c, praos_batch* b, const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx);
 // Waits for the run and copies its bits and pool indices out (download stream).
 int rp_download_results(praos_ctx* c, praos_batch* b, uint16_t* bits, int32_t* pool_idx);
+// The pool part of one ledger view (praos_api.hip): host map (hash28 -> caller index) and, when
+// built for a device, the tables the VRF join and the leader test read.
+struct rp_view;
+rp_view* rp_view_make(praos_ctx* c, const praos_pool* pools, uint32_t npools, const praos_params* params,
+                      bool device);
+void rp_view_free(praos_ctx* c, rp_view* v);
+// The device pool tables a context's launches read (praos_set_epoch's, or a view's swapped in by
+// the launcher thread: kernels already queued keep the pointers they were launched with).
+struct rp_tables {
+  uint32_t npools;
+  uint32_t *hash, *vrf, *x;
+  int32_t* map;
+};
+rp_tables rp_tables_get(const praos_ctx* c);
+void rp_tables_set(praos_ctx* c, const rp_tables& t);
+rp_tables rp_view_tables(const rp_view* v);
 // praos_validate_headers_nonces / praos_tpraos_validate_headers_nonces with the evolving nonce
-// after each header precomputed by the caller's nonce chain (used until the first invalid header).
+// after each header precomputed by the caller's nonce chain (used until the first invalid header);
+// view (may be NULL: the context's praos_set_epoch pools) is the ledger view the batch was verified
+// under.
 int rp_fold(praos_ctx* c, const praos_headers* h, const uint8_t* prev_hash, const uint8_t* prev_is_genesis,
             const praos_out* crypto, praos_envelope* env, const praos_epoch_info* ei, praos_chain_state* st,
             const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx, const praos_nonce* evolving_after,
             bool tpraos, const praos_nonce* extra_entropy, uint8_t* verdict, uint16_t* failures, size_t* chain_stop,
-            size_t* processed);
-// The replay of praos_replay_immutable[_tpraos] over m contexts (praos_replay.hip): batch k is
-// uploaded, decoded and verified on mem[k % m]; the nonce chain and the fold run once, in chain
-// order, the fold and the error text on mem[0].  m = 1 is the single-context replay.
+            size_t* processed, const rp_view* view);
+// The replay of praos_replay_immutable[_tpraos|_views] over m contexts (praos_replay.hip): batch k
+// is uploaded, decoded and verified on mem[k % m]; the nonce chain and the fold run once, in chain
+// order, the fold and the error text on mem[0].  m = 1 is the single-context replay.  views
+// (nviews > 0, Praos only): a ledger view per epoch instead of pools / env's limits.
 int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* pools, uint32_t npools,
               const praos_params* params, const praos_epoch_info* ei, praos_envelope* env, praos_chain_state* st,
               size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
-              praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy);
+              praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy,
+              const praos_ledger_view* views = nullptr, uint32_t nviews = 0);

@@ -130,6 +130,12 @@ class ReplayStats(ctypes.Structure):
                 ("ms_fold", ctypes.c_double), ("ms_nonce", ctypes.c_double)]
 
 
+class LedgerView(ctypes.Structure):
+    _fields_ = [("first_epoch", ctypes.c_uint64), ("pools", ctypes.c_void_p), ("npools", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("lv_prot_major", ctypes.c_uint64),
+                ("max_header_size", ctypes.c_uint64), ("max_body_size", ctypes.c_uint64)]
+
+
 class Counters(ctypes.Structure):
     _fields_ = [("hash28", u8p), ("counter", u64p), ("m", ctypes.c_size_t)]
 
@@ -218,6 +224,11 @@ SIGNATURES = {
                                                      ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
                                                      ctypes.c_size_t, u8p, u16p, ctypes.c_size_t,
                                                      ctypes.POINTER(ReplayStats)]),
+    "praos_replay_immutable_views": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(LedgerView),
+                                                    ctypes.c_uint32, ctypes.POINTER(Params), ctypes.POINTER(EpochInfo),
+                                                    ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
+                                                    ctypes.c_size_t, u8p, ctypes.c_size_t,
+                                                    ctypes.POINTER(ReplayStats)]),
     "praos_batch_upload_tpraos_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
     "praos_batch_download_tpraos": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(TPOut)]),
     "praos_tpraos_validate_headers_nonces": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(TPHeaders), u8p, u8p,
@@ -261,6 +272,14 @@ SIGNATURES = {
                                                            ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
                                                            ctypes.c_size_t, u8p, u16p, ctypes.c_size_t,
                                                            ctypes.POINTER(ReplayStats)]),
+    "praos_group_verify_block_integrity": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
+                                                          ctypes.c_uint64, u8p, u8p]),
+    "praos_group_replay_immutable_views": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
+                                                          ctypes.POINTER(LedgerView), ctypes.c_uint32,
+                                                          ctypes.POINTER(Params), ctypes.POINTER(EpochInfo),
+                                                          ctypes.POINTER(Envelope), ctypes.POINTER(ChainState),
+                                                          ctypes.c_size_t, u8p, ctypes.c_size_t,
+                                                          ctypes.POINTER(ReplayStats)]),
     "praos_synthesize": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SynthParams), ctypes.POINTER(Params), u8p,
                                         ctypes.POINTER(Pool), u64p, u8p, u8p, u8p, u8p, u8p, u64p, u64p, u8p, u8p,
                                         u64p, u32p, u8p, u8p]),
@@ -821,6 +840,14 @@ class Context:
         return _replay(fn, self.h, self.check, path, pools, params, epoch_info, state, envelope, batch_max,
                        verdicts_cap, counter_cap, tpraos, extra_entropy)
 
+    def replay_immutable_views(self, path, views, params: Params, epoch_info, state: dict, envelope: dict,
+                               batch_max=1 << 16, verdicts_cap=0, counter_cap=1 << 16):
+        """praos_replay_immutable_views: views = [(first_epoch, pools, {lv_prot_major, max_header_size,
+        max_body_size})] sorted by first_epoch, a ledger view per epoch range; otherwise as
+        replay_immutable (envelope's limits are not read)."""
+        return _replay_views(self.L.praos_replay_immutable_views, self.h, self.check, path, views, params, epoch_info,
+                             state, envelope, batch_max, verdicts_cap, counter_cap)
+
     def apply_batch(self, H, crypto, counters=None):
         """counters: dict hash28 -> int.  Returns (verdict u8[n], chain_stop, counters_out)."""
         n = len(H["slot"])
@@ -1111,6 +1138,23 @@ class Group:
         return _replay(fn, self.g, self.check, path, pools, params, epoch_info, state, envelope, batch_max,
                        verdicts_cap, counter_cap, tpraos, extra_entropy)
 
+    def verify_block_integrity(self, arena, off, length, slots_per_kes_period):
+        """praos_group_verify_block_integrity: Context.verify_block_integrity sharded over the members."""
+        arena, off, length = Context._chunk(arena, off, length)
+        n = len(off)
+        hb = Context.header_bytes_struct(arena, off, length)
+        res = np.zeros(n, np.uint8)
+        bh = np.zeros((n, 32), np.uint8)
+        self.check(self.L.praos_group_verify_block_integrity(self.g, ctypes.byref(hb), slots_per_kes_period,
+                                                             ptr(res), ptr(bh)))
+        return res, bh
+
+    def replay_immutable_views(self, path, views, params: Params, epoch_info, state: dict, envelope: dict,
+                               batch_max=1 << 16, verdicts_cap=0, counter_cap=1 << 16):
+        """praos_group_replay_immutable_views: Context.replay_immutable_views over the group's members."""
+        return _replay_views(self.L.praos_group_replay_immutable_views, self.g, self.check, path, views, params,
+                             epoch_info, state, envelope, batch_max, verdicts_cap, counter_cap)
+
     def verify_tpraos_header_bytes(self, arena, off, length, decoded=False):
         arena, off, length = Context._chunk(arena, off, length)
         n = len(off)
@@ -1162,6 +1206,37 @@ def _replay(fn, handle, check, path, pools, params, epoch_info, state, envelope,
     stats = {name: getattr(S, name) for name, _ in ReplayStats._fields_}
     if tpraos:
         return stats, verdict[:verdicts_cap], fails[:verdicts_cap]
+    return stats, verdict[:verdicts_cap]
+
+
+def _replay_views(fn, handle, check, path, views, params, epoch_info, state, envelope, batch_max, verdicts_cap,
+                  counter_cap):
+    """praos_[group_]replay_immutable_views (the same arguments after the context / group)."""
+    keep = [Context.pool_array(pools) for _, pools, _ in views]
+    V = (LedgerView * max(1, len(views)))()
+    for j, (first, pools, lim) in enumerate(views):
+        V[j].first_epoch = first
+        V[j].pools = ctypes.cast(keep[j], ctypes.c_void_p)
+        V[j].npools = len(pools)
+        V[j].lv_prot_major = lim["lv_prot_major"]
+        V[j].max_header_size = lim["max_header_size"]
+        V[j].max_body_size = lim["max_body_size"]
+    st, hk, cv = _state_struct(state, counter_cap)
+    E = Envelope()
+    tip = envelope.get("tip")
+    E.tip_is_origin = int(tip is None)
+    if tip is not None:
+        E.tip_slot, E.tip_block_no = tip[0], tip[1]
+        ctypes.memmove(E.tip_hash, bytes(tip[2]), 32)
+    E.max_major_pv = envelope["max_major_pv"]
+    ei = EpochInfo(*epoch_info)
+    verdict = np.zeros(max(verdicts_cap, 1), np.uint8)
+    S = ReplayStats()
+    check(fn(handle, os.fsencode(str(path)), V, len(views), ctypes.byref(params), ctypes.byref(ei), ctypes.byref(E),
+             ctypes.byref(st), batch_max, ptr(verdict), verdicts_cap, ctypes.byref(S)))
+    envelope["tip"] = None if E.tip_is_origin else (int(E.tip_slot), int(E.tip_block_no), bytes(E.tip_hash))
+    state.update(_state_from_struct(st, hk, cv))
+    stats = {name: getattr(S, name) for name, _ in ReplayStats._fields_}
     return stats, verdict[:verdicts_cap]
 
 

@@ -83,7 +83,7 @@ def _combine(a, b):
 
 
 def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpraos=False, extra_entropy=None,
-                           progress=None, schedules=None):
+                           progress=None, schedules=None, stakes=None):
     """A linked chain over `epochs` epochs of `epoch_length` slots from slot 0 (Origin,
     GenesisHash, epoch 0 nonce = cfg["eta0"]).  Returns dict(arena, off, len, slots,
     header_hash, pools, params, nonces (per epoch), state (after the last
@@ -91,8 +91,13 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
     chain (TPraos leader schedule and BHeaders, stored as Alonzo blocks, era tag 5; the
     TPraos nonce rules with TICKN's extra_entropy).  schedules: {epoch: (slots, pools)} used
     instead of the leader-schedule search for those epochs (e.g. epoch 0 of the C5 / tp chain
-    from its shipped schedule, which was searched under the same seed, stake and nonce)."""
-    sig = chains.stake(cfg["npools"], cfg["stake_offset"])
+    from its shipped schedule, which was searched under the same seed, stake and nonce).
+    stakes: a function epoch -> per-pool Fixed E34 stake (0 = the pool is not in that epoch's
+    PoolDistr), so the stake distribution changes between epochs as the ledger's NEWEPOCH makes
+    it (the leader schedule of epoch e is searched under epoch e's stake); the result then has
+    "views": [(epoch, pool list)] -- the LedgerView's PoolDistr per epoch."""
+    sig0 = chains.stake(cfg["npools"], cfg["stake_offset"])
+    views = []
     p = chains.params(cfg)
     st = {"last_slot": None, "counters": {}, "evolving": cfg["eta0"], "candidate": cfg["eta0"],
           "epoch_nonce": cfg["eta0"], "lab": None, "leb": None}
@@ -106,6 +111,7 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
             if tpraos:
                 eta = _combine(eta, extra_entropy)          # TICKN
         nonces.append(eta)
+        sig = list(stakes(e)) if stakes else sig0
         if schedules and e in schedules:
             sl, pl = schedules[e]
             keep = (sl >= e * epoch_length) & (sl < (e + 1) * epoch_length)
@@ -125,7 +131,8 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
         n = len(sl)
         H, keys, _ = ctx.synthesize(n, cfg["npools"], p, eta, cfg["seed"], body_len=0, schedule=(sl, pl),
                                     block_no0=block_no, link=True, prev0=prev, tpraos=tpraos)
-        pool_list = [(h, v, s) for (h, v), s in zip(keys, sig)]
+        pool_list = [(h, v, s) for (h, v), s in zip(keys, sig) if s > 0]
+        views.append((e, pool_list))
         # fold the clean chain to learn the next nonce (the generator's own ledger)
         ctx.set_epoch(eta, pool_list, p)
         o = ctx.verify_tpraos_headers(H) if tpraos else ctx.verify_headers(H)
@@ -161,4 +168,4 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
     return {"arena": np.concatenate(arenas), "off": np.concatenate(offs), "len": np.concatenate(lens),
             "slots": np.concatenate(slots_all), "header_hash": np.concatenate(hh_all), "pools": pool_list,
             "params": p, "nonces": nonces, "state": st,
-            "epoch_info": ei}
+            "epoch_info": ei, "views": views}

@@ -47,7 +47,7 @@ def test_struct_sizes_match_c_layout():
 
 def test_abi_version():
     from praos_hip import abi
-    assert abi.load().praos_abi_version() == 13
+    assert abi.load().praos_abi_version() == 14
 
 
 def test_no_silent_fallback_without_gpu():
@@ -65,7 +65,8 @@ _STRUCTS = {"praos_params": "Params", "praos_pool": "Pool", "praos_headers": "He
             "praos_chain_state": "ChainState", "praos_epoch_info": "EpochInfo", "praos_envelope": "Envelope",
             "praos_replay_stats": "ReplayStats", "praos_decoded": "Decoded", "praos_counters": "Counters",
             "praos_synth_params": "SynthParams", "praos_tpraos_headers": "TPHeaders",
-            "praos_tpraos_out": "TPOut", "praos_gen_deleg": "GenDeleg", "praos_overlay": "Overlay"}
+            "praos_tpraos_out": "TPOut", "praos_gen_deleg": "GenDeleg", "praos_overlay": "Overlay",
+            "praos_ledger_view": "LedgerView"}
 HASKELL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "haskell",
                        "Ouroboros", "Consensus", "Protocol", "Praos", "Batch.hs")
 
@@ -188,3 +189,34 @@ def test_fe_cols_header_is_generated():
                          capture_output=True, text=True).stdout
     with open(os.path.join(root, "ouroboros-consensus_amd", "csrc", "fe_cols.hpp")) as f:
         assert f.read() == out
+
+
+def test_haskell_binds_abi14_entry_points():
+    """ABI 14 reaches the reference side: the per-epoch ledger views of the replay and the
+    block-integrity batch (single context and group) are imported by Batch.hs."""
+    hs = open(HASKELL).read()
+    imported = set(re.findall(r'foreign import ccall safe "(praos_[a-z0-9_]+)"', hs))
+    for name in ("praos_replay_immutable_views", "praos_group_replay_immutable_views",
+                 "praos_verify_block_integrity", "praos_group_verify_block_integrity"):
+        assert name in imported, name
+    for fn in ("praosReplayImmutableViews", "verifyChunkIntegrity", "praosHostRegister"):
+        assert re.search(rf"^{fn} ::", hs, flags=re.M), fn
+
+
+def test_db_analyser_patch_wires_the_analysis():
+    """integration/haskell/db-analyser.patch adds the AnalysisName constructor, its runAnalysis
+    equation, the --benchmark-header-batch flag and the cabal modules; the analysis module exists."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    patch = open(os.path.join(root, "integration", "haskell", "db-analyser.patch")).read()
+    added = "\n".join(ln[1:] for ln in patch.splitlines() if ln.startswith("+") and not ln.startswith("+++"))
+    assert "| BenchmarkHeaderBatch HeaderBatchArgs" in added
+    assert "go (BenchmarkHeaderBatch args)" in added
+    assert 'long "benchmark-header-batch"' in added
+    assert "Cardano.Tools.DBAnalyser.Analysis.BenchmarkHeaderBatch" in added
+    assert "processAll db registry ((,) <$> GetBlock <*> GetRawHeader)" in added
+    mod = open(os.path.join(root, "integration", "haskell", "Cardano", "Tools", "DBAnalyser", "Analysis",
+                            "BenchmarkHeaderBatch.hs")).read()
+    for needle in ("ledgerViewForecastAt", "forecastFor", "tickThenReapply", "validateEpochHeaders",
+                   "validateEpochHeadersTPraos", "instance CardanoHardForkConstraints c => HasHeaderBatch (CardanoBlock c)",
+                   "praosHostRegister"):
+        assert needle in mod, needle
