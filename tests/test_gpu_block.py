@@ -136,7 +136,7 @@ def test_ffi_chunk_validation(tmp_path):
     """Batch.hs verifyChunkIntegrity's call sequence from C (ffi_harness --chunk): the ImmutableDB
     chunk validation of parseChunkFile (Parser.hs:118-141) with its expensive checkIntegrity
     (Validation.hs:379-384 -> verifyBlockIntegrity, Integrity.hs:14-20) batched on the GPU, one
-    context and a 3-member group.  (a) every stored checksum zeroed: every block is checked, each
+    context and a 3-member group.  (a) every stored checksum wrong: every block is checked, each
     result equals oracle/block_integrity.py, and the chunk is cut at the first corrupt block;
     (b) correct checksums over a chunk damaged on disk in two blocks, plus one stale checksum of an
     intact block: exactly those three are checked, the intact one passes, the chunk is cut at the
@@ -150,8 +150,8 @@ def test_ffi_chunk_validation(tmp_path):
         blocks += [blk] + [bc.mutate(blk, f, r, kind) for kind in bc.MUTATIONS]
     blocks += [bytes.fromhex(k["block_cbor"]) for k in kats if k["kind"] == "praos"]    # golden Babbage/Conway
     want = [bi.verify_block_integrity(b, 0, len(b), SPKP)[0] for b in blocks]
-    # (a) no usable checksum
-    data = _write_chunk(str(tmp_path / "a"), blocks, [0] * len(blocks))
+    # (a) no usable checksum (every stored one off by a bit)
+    data = _write_chunk(str(tmp_path / "a"), blocks, [zlib.crc32(b) ^ 1 for b in blocks])
     out = _harness_chunk(str(tmp_path / "a"))
     first = next(i for i, w in enumerate(want) if w)
     offs = np.cumsum([0] + [len(b) for b in blocks])
