@@ -317,9 +317,7 @@ void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, c
 void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
                            int wave_prio, const uint32_t* base, uint32_t span, int mode) {
-  if (mode == 2)
-    launch_key_precomputeq(kind, stream, counters, max_entries, entry_rep, keys, ktab, kinfo, wave_prio, base, span);
-  else if (mode == 1)
+  if (mode == 1)
     launch_key_precompute4(kind, stream, counters, max_entries, entry_rep, keys, ktab, kinfo, wave_prio, base, span);
   else
     hipLaunchKernelGGL(k_key_precompute, dim3((span + 63) / 64), dim3(64), 0, stream, kind, counters, max_entries,

@@ -56,11 +56,7 @@ void launch_ocert_fanout(dim3 grid, dim3 block, hipStream_t stream, size_t n, co
 void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
                            int wave_prio, const uint32_t* base, uint32_t span,
-                           int mode);                      // 1: the chain from the ILP-4 build (k_keys4.hip),
-                                                           // 2: four lanes per key (k_keysq.hip)
-void launch_key_precomputeq(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
-                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
-                            int wave_prio, const uint32_t* base, uint32_t span);
+                           int mode);                      // 1: the chain from the ILP-4 build (k_keys4.hip)
 void launch_key_precompute4(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                             const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,
                             int wave_prio, const uint32_t* base, uint32_t span);

@@ -186,18 +186,11 @@ struct praos_ctx {
                                                        // PRAOS_KEY4 1 / 0, -1 below ILP4_BATCH (54k: 2.78-2.84
                                                        // -> 2.76-2.77 ms; 108k 4.17 -> 4.21, profiles/r04/n)
   bool use_key4(size_t n) const { return key4 > 0 || (key4 < 0 && n < ILP4_BATCH); }
-  int keyq = 0;                                        // key precompute with four lanes per key (k_keysq.hip):
-                                                       // PRAOS_KEYQ 1 / 0, -1 below ILP4_BATCH.  Off: inside a
-                                                       // step its chains are about as long as the ILP-4 build's
-                                                       // (54k: cold 0.90 -> 0.65 ms, KES 0.85 -> 1.09, VRF 0.95 ->
-                                                       // 0.90) and its four lanes per key take issue slots from
-                                                       // the rest: 54k 2.72-2.75 -> 2.84-2.88 ms, 108k 3.79-3.84
-                                                       // -> 4.00 (profiles/r05/c11_keyq_nobranch; c9_keyq: the
-                                                       // first build, whose selects compiled to branches)
-  int key_mode(size_t n) const {
-    if (keyq > 0 || (keyq < 0 && n < ILP4_BATCH)) return 2;
-    return use_key4(n) ? 1 : 0;
-  }
+  // (round 5 also measured a key precompute with four lanes per key, DPP quad broadcasts: inside a
+  // step its chains were about as long as the ILP-4 build's and its four lanes per key took issue
+  // slots from the rest, 54k 2.72-2.75 -> 2.84-2.88 ms, 108k 3.79-3.84 -> 4.00,
+  // profiles/r05/c11_keyq_nobranch; removed in round 6)
+  int key_mode(size_t n) const { return use_key4(n) ? 1 : 0; }
   int u4 = -1;                                         // cached stage U from the ILP-4 build (PRAOS_U4 1 / 0,
                                                        // -1 below ILP4_BATCH; 54k 2.79 -> 2.75 ms, 108k 3.87-3.92
                                                        // -> 3.81-3.83, profiles/r04/hh)
@@ -227,12 +220,10 @@ struct praos_ctx {
   int kc_min[3] = {0, 0, 0};                           // per cache (cold, VRF, KES leaf) min uses overriding
                                                        // keycache when > 0 (PRAOS_KC_MIN="c,v,k")
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
-  // the cached chains' last kernels -- cached U, the join, the cached OCert / KES verifies -- at
-  // s_setprio ck_prio (the join at 3) in batches below ILP4_BATCH (PRAOS_CK_PRIO 0 / 2 / 3).  Off:
-  // U shortens (54k 0.71 -> 0.43 ms) but stage V stretches past it and the step with it (54k
-  // 2.74-2.76 -> 2.89-2.95 ms, 108k 3.83 -> 3.92-4.00, profiles/r05/c14_ckprio)
-  int ck_prio = 0;
-  int ck_prio_at(size_t n) const { return n < ILP4_BATCH ? ck_prio : 0; }
+  // (round 5 measured the cached chains' last kernels -- cached U, the join, the cached OCert /
+  // KES verifies -- at s_setprio 2 / 3 below ILP4_BATCH: U shortened (54k 0.71 -> 0.43 ms) but
+  // stage V stretched past it and the step with it, 54k 2.74-2.76 -> 2.89-2.95 ms,
+  // profiles/r05/c14_ckprio; the option was removed in round 6)
   int key_wave_prio = -1;                              // key precompute waves at s_setprio 3 (PRAOS_KEY_PRIO 1 / 0;
                                                        // -1: batches below KEY_PRIO_BATCH headers)
   hipEvent_t ev[6] = {};
@@ -253,25 +244,17 @@ struct praos_ctx {
     uint32_t* kinfo = nullptr;
     int32_t* pentry = nullptr;
     ge_cached* ktab = nullptr;
-  } pks[3];                                            // [2] KES leaf keys: the stored-bytes pipeline's prefill
+  } pks[2];                                            // [0] cold keys, [1] VRF keys
   int pool_keys = -1;                                  // 1 on, 0 off, -1 on inside praos_replay_immutable*
   bool replaying = false;
   bool pk_on = false;                                  // this run uses the store
-  bool pk_reset[3] = {false, false, false};            // empty store t before the next run that uses it
-  // stored-bytes pipeline (praos_verify_header_bytes): the cold, KES leaf and VRF keys of the
-  // landed chunks go into the stores and get their tables while later chunks upload -- in two
-  // rounds, after chunk (K-2)/2 and after chunk K-2 (PRAOS_E2E_PREFILL 1 / 0), each caching the
-  // keys used at least the usual count within its range; the batch run after the last chunk
-  // finds them stored and caches the rest by their count over the whole batch (its precompute
-  // chain then covers only the keys the prefill did not).  The stores are emptied at the start of
-  // every call unless PRAOS_OPT_POOL_KEYS is on, so each call builds its own tables.  Off by
-  // default, measured slower in both forms: the GPU is busy with the chunks' stage V while they
-  // upload, so the prefill only moves work there, and any key first seen in the last chunk still
-  // needs one latency-bound chain (a precompute or an uncached verify) after it lands.  432k
-  // headers, 8 chunks: 16.3-16.4 ms without, 18.2-18.5 ms with (profiles/r05/c12_prefill_v3);
-  // the first form (every key of a prefill range cached, the last chunk's new keys verified
-  // uncached): 16.9 -> 19.2 ms (profiles/r05/c7_e2e_timeline_pf{0,1}.txt).
-  int e2e_prefill = 0;
+  bool pk_reset[2] = {false, false};                   // empty store t before the next run that uses it
+  // (round 5 measured a per-chunk key prefill in the stored-bytes pipeline -- the landed chunks'
+  // cold, KES leaf and VRF keys stored and their tables built while later chunks upload -- in two
+  // forms, both slower: the GPU is busy with the chunks' stage V during the upload, so the
+  // prefill only moves work there, and a key first seen in the last chunk still needs a
+  // latency-bound chain after it lands (432k, 8 chunks: 16.3-16.4 -> 18.2-18.5 ms,
+  // profiles/r05/c12_prefill_v3; 16.9 -> 19.2 ms, c7_e2e_timeline_pf{0,1}.txt).  Removed in round 6.)
   // stored-bytes pipeline: the first chunk's size in percent of the others' (PRAOS_PIPE_HEAD):
   // nothing runs on the GPU until it has landed and been decoded
   int pipe_head = 25;                                  // (432k headers, 8 chunks: 100 -> 16.9-17.0 ms,
@@ -281,8 +264,6 @@ struct praos_ctx {
                                                        // batch's stage V after the upload (432k, 8 chunks: 100 ->
                                                        // 16.4-16.7 ms, 50 -> 17.1-17.3, 25 -> 18.5-18.8;
                                                        // profiles/r05/c16_pipe_tail)
-  bool prefill = false;                                // inside such a call (after a prefill): every cache on
-                                                       // its store, new keys cached by their batch count
   // epoch
   bool have_epoch = false;
   praos_params params{};
@@ -576,7 +557,6 @@ const char* praos_last_error(praos_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 // streams and events of a context (praos_open, and the pipeline's second engine)
 static bool open_streams(praos_ctx* c) {
   if (const char* kp = std::getenv("PRAOS_KEY_PRIO")) c->key_wave_prio = std::atoi(kp);
-  if (const char* e = std::getenv("PRAOS_CK_PRIO")) c->ck_prio = std::atoi(e);
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     c->stream = nullptr;
     return false;
@@ -595,7 +575,6 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_V_EXCL")) c->v_excl = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS4")) c->miss4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KEY4")) c->key4 = std::atoi(e);
-  if (const char* e = std::getenv("PRAOS_KEYQ")) c->keyq = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_U4")) c->u4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_CK4")) c->ck4 = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_DEDUP")) c->kes_dedup = std::atoi(e);
@@ -605,7 +584,6 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
   if (const char* e = std::getenv("PRAOS_TP_STAGED")) c->tp_staged = std::atoi(e) != 0;
-  if (const char* e = std::getenv("PRAOS_E2E_PREFILL")) c->e2e_prefill = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PIPE_HEAD")) c->pipe_head = std::max(5, std::min(100, std::atoi(e)));
   if (const char* e = std::getenv("PRAOS_PIPE_TAIL")) c->pipe_tail = std::max(5, std::min(100, std::atoi(e)));
   (void)hipEventCreate(&c->v1_ev);
@@ -1232,7 +1210,7 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
   HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
   HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
   praos_ctx::PoolKeyStore* ps = nullptr;
-  if (c->pk_on && (which < 2 || c->prefill) && ensure_pks(c, which, st)) {
+  if (c->pk_on && which < 2 && ensure_pks(c, which, st)) {
     // pool keys: entries continue the store's, every new key is cached (it recurs in the runs
     // that follow); a store more than 3/4 full (decided on the device, from the count the last
     // run left: no host read of a count still in flight) or one asked to be emptied is emptied
@@ -1243,10 +1221,7 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
     HIPCHK(c, hipMemcpyAsync(ps->base, ps->count, 4, hipMemcpyDeviceToDevice, st));
     k.kt = ps->ktab; k.ki = ps->kinfo; k.erep = ps->entry_rep; k.epos = ps->entry_pos; k.emax = ps->cap;
     k.ebase = ps->base; k.store = which;
-    // (after a stored-bytes prefill, the keys not stored yet -- the last chunk's new ones, and the
-    // ones used once per prefill range -- are cached only from the usual count: a single-use key's
-    // tables cost more than its uncached verify)
-    if (!c->prefill) min_uses = 1;
+    min_uses = 1;
   }
   launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot,
                     ps ? ps->pentry : nullptr, ps ? ps->pkey : nullptr, ps ? ps->slots - 1 : 0u);
@@ -1271,43 +1246,6 @@ static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t*
                       span);
 }
 
-// The stored-bytes pipeline's key prefill (off by default, see praos_ctx::e2e_prefill): the keys
-// of the landed chunks [lo, hi) go into the pool-key store t (the batch's hash set counts them
-// within the range, keys already stored are skipped), and the new ones used at least the usual
-// count are decoded and expanded into their tables at once, on the cache's stream, while later
-// chunks upload; the batch run after the last chunk finds them stored.  reset: empty the store
-// first (the call's first prefill round).
-static int kc_prefill(praos_ctx* c, praos_batch* b, int t, const uint8_t* keys, int kind, size_t lo, size_t hi,
-                      hipStream_t st, bool reset, int prio) {
-  praos_batch::KeyCache& k = b->kc[t];
-  if (!ensure_pks(c, t, st)) { c->err = "pool-key store allocation"; return PRAOS_E_OOM; }
-  praos_ctx::PoolKeyStore& ps = c->pks[t];
-  const size_t m = hi - lo;
-  if (reset || c->pk_reset[t]) launch_pkey_reset(st, ps.count, ps.pentry, ps.slots, 0, 1);
-  c->pk_reset[t] = false;
-  if (m == 0) return PRAOS_OK;
-  HIPCHK(c, hipMemsetAsync(k.slot_rep, 0, 4 * (size_t)k.cap, st));
-  HIPCHK(c, hipMemsetAsync(k.slot_cnt, 0, 4 * (size_t)k.cap, st));
-  HIPCHK(c, hipMemsetAsync(k.counters, 0, 16, st));
-  HIPCHK(c, hipMemcpyAsync(k.counters, ps.count, 4, hipMemcpyDeviceToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(ps.base, ps.count, 4, hipMemcpyDeviceToDevice, st));
-  const uint8_t* ck = keys + 32 * lo;                   // the chunk's keys (item ids relative to lo)
-  launch_key_insert(dim3(nblocks(m, NT)), dim3(NT), st, m, nullptr, nullptr, ck, k.cap - 1, k.slot_rep, k.slot_cnt,
-                    k.item_slot + lo, ps.pentry, ps.pkey, ps.slots - 1);
-  // keys used at least the usual count within the landed range; the others are counted again by
-  // the run after the last chunk
-  const uint32_t min_uses = (uint32_t)std::max(1, c->kc_min[t] > 0 ? c->kc_min[t] : c->keycache);
-  launch_key_assign(dim3(nblocks(k.cap, NT)), dim3(NT), st, k.cap, k.slot_rep, k.slot_cnt, min_uses, ps.cap,
-                    k.slot_entry, ps.entry_rep, ps.entry_pos, k.counters);
-  const uint32_t span = (uint32_t)std::min<size_t>(m, ps.cap);
-  launch_key_precompute(kind, st, k.counters, ps.cap, ps.entry_rep, ck, ps.ktab, ps.kinfo, prio, ps.base, span,
-                        c->key_mode(m));
-  launch_pkey_publish(st, k.counters, ps.base, ps.cap, ps.entry_rep, ck, ps.pentry, ps.pkey, ps.slots - 1, ps.count,
-                      span);
-  HIPCHK(c, hipGetLastError());
-  return PRAOS_OK;
-}
-
 static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   const size_t n = b->n;
   const praos_params& P = c->params;
@@ -1325,7 +1263,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   c->last_from_bytes = b->from_bytes;
   c->v_timed = false;
   c->kes_ck_timed = false;
-  c->pk_on = c->keycache > 0 && (c->prefill || c->pool_keys > 0 || (c->pool_keys < 0 && c->replaying));
+  c->pk_on = c->keycache > 0 && (c->pool_keys > 0 || (c->pool_keys < 0 && c->replaying));
   if (b->from_bytes) {
     // stored bytes -> SoA (k_decode.hip); the crypto kernels read its output
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
@@ -1452,7 +1390,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     if (sm_[2] != sv) HIPCHK(c, hipEventRecord(c->u_ev, sm_[2]));
     keycache_precompute(k, b->vrf_vk, 1, sv);
     launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
-                 b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n), c->ck_prio_at(n));
+                 b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n), 0);
     if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     vrf_keys_queued = true;
     return PRAOS_OK;
@@ -1493,7 +1431,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       else
         launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
                         b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
-                        P.max_kes_evo, bo, b->dd_ok, c->ck_prio_at(n));
+                        P.max_kes_evo, bo, b->dd_ok, 0);
     } else {
       launch_ocert(g, blk, so, n, b->dd_reps, b->dd_counters, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                    b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
@@ -1534,7 +1472,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       else
         launch_ocert_ck(gl, bl, so, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->cold_vk,
                         b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period,
-                        P.max_kes_evo, bo, (uint8_t*)nullptr, c->ck_prio_at(n));
+                        P.max_kes_evo, bo, (uint8_t*)nullptr, 0);
     } else {
       launch_ocert(g, blk, so, n, (const uint32_t*)nullptr, (const uint32_t*)nullptr, c->btab, b->cold_vk,
                    b->hot_vk, b->ocert_n, b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo,
@@ -1577,7 +1515,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
                       b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0,
                       P.slots_per_kes_period, bk, c->kes_pair_min(), c->kes_dedup ? k.entry_rep : nullptr,
-                      c->kes_dedup ? k.rep_ok : nullptr, c->ck_prio_at(n));
+                      c->kes_dedup ? k.rep_ok : nullptr, 0);
       HIPCHK(c, hipEventRecord(c->kc1_ev, sk));
       c->kes_ck_timed = true;
     } else {
@@ -1664,7 +1602,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     auto join = [&](hipStream_t st) {
       launch_vrf_join(st, n, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, c->d_pool_hash, c->d_pool_vrf,
                       c->d_pool_map, c->npools, (int)P.vrf_check_output, bv, b->pool_idx, b->pool_sorted, b->beta,
-                      b->leader, b->nonce, b->vrf_mid, wprio || c->ck_prio_at(n));
+                      b->leader, b->nonce, b->vrf_mid, wprio);
     };
     if (vrf3) {
       // three kernels: U runs beside V (uncached keys at once on the miss stream, cached keys
@@ -1837,7 +1775,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_KES_PAIR) { c->kes_pair = value < 0 ? -1 : value; return PRAOS_OK; }
   if (opt == PRAOS_OPT_POOL_KEYS) {
     c->pool_keys = value < 0 ? -1 : (value != 0);
-    if (value == 2) c->pk_reset[0] = c->pk_reset[1] = c->pk_reset[2] = true;   // store 2: the KES leaf keys
+    if (value == 2) c->pk_reset[0] = c->pk_reset[1] = true;
     return PRAOS_OK;
   }
   return PRAOS_E_ARG;
@@ -1982,6 +1920,25 @@ int praos_decode_headers(praos_ctx* c, const praos_header_bytes* in, praos_decod
 }  // extern "C"
 
 // ---------------------------------------------------------------- replay pipeline (internal, C++ linkage)
+// A batch the context keeps between calls (the replay's RP_SLOTS batches, the stored-bytes
+// pipeline's batch) goes through here every time it is taken for another run: every per-run field
+// back to the state of a fresh batch, so nothing one call set (its header count, "decoded",
+// "stage V queued", the key-cache / dedup use of its last run, the nonce table's use) can reach
+// the next call, whichever entry point made either.  Buffers, capacities and events stay.
+static void batch_reuse_reset(praos_batch* b) {
+  b->n = 0;
+  b->arena_len = 0;
+  b->body_bytes_len = 0;
+  b->decoded = false;
+  b->v_done = false;
+  b->kc_used = false;
+  b->dd_used = false;
+  for (auto& k : b->kc) {            // this run's entry space (set again by the run's key lists)
+    k.kt = nullptr; k.ki = nullptr; k.erep = nullptr; k.epos = nullptr; k.ebase = nullptr;
+    k.emax = 0; k.store = -1;
+  }
+}
+
 praos_batch* rp_batch_alloc(praos_ctx* c, size_t n_cap, size_t bytes_cap, bool tpraos) {
   if (!c || c->device < 0) return nullptr;
   (void)hipSetDevice(c->device);
@@ -2018,7 +1975,10 @@ praos_batch* rp_batch_take(praos_ctx* c, int k, size_t n, size_t bytes, bool tpr
   if (!c || k < 0 || k >= RP_SLOTS) return nullptr;
   praos_batch* b = c->rp_keep[k];
   c->rp_keep[k] = nullptr;
-  if (b && rp_batch_fits(b, n, bytes) && b->tp_only == tpraos) return b;
+  if (b && rp_batch_fits(b, n, bytes) && b->tp_only == tpraos) {
+    batch_reuse_reset(b);
+    return b;
+  }
   rp_batch_destroy(c, b);
   return rp_batch_alloc(c, n + n / 8 + 64, bytes + bytes / 8 + 4096, tpraos);
 }
@@ -2211,6 +2171,7 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
     c->pipe_bytes[0] = bc;
   }
   praos_batch* b = c->pipe[0];
+  batch_reuse_reset(b);
   b->n = n;
   b->arena_len = bytes;
   b->body_bytes_len = (size_t)b->signed_stride * n;
@@ -2224,10 +2185,6 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
   const bool vrf = (c->kernels & 4) != 0;
-  // key prefill per landed chunk (see praos_ctx::e2e_prefill): Praos header batches with the key
-  // caches and all three crypto passes on their concurrent streams
-  const bool prefill = c->e2e_prefill > 0 && c->keycache > 0 && c->concurrent && c->kernels == 7 && n >= 2 && K >= 3;
-  int pf_chunk = 0;                               // first chunk the next prefill round covers
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
@@ -2245,25 +2202,6 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
                         b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
-    if (prefill && (k == (K - 2) / 2 || k == K - 2)) {
-      // the keys of chunks [pf_lo, k] in two rounds: a key precompute is one long chain per key
-      // whatever the number of keys, so one round per chunk would queue K chains back to back
-      // on each cache's stream.  Cache t on the stream its run uses: cold keys side[0], KES leaf
-      // keys side[1], VRF keys side[2]
-      const int sidx[3] = {0, 2, 1};
-      const size_t a = lo[pf_chunk], z = lo[k + 1], mz = z - a;
-      for (int t : {1, 0, 2}) {
-        hipStream_t st = c->side[sidx[t]];
-        HIPCHK(c, hipStreamWaitEvent(st, c->done_ev[k], 0));
-        const uint8_t* keys = t == 0 ? b->cold_vk : (t == 1 ? b->vrf_vk : b->kes_leaf);
-        if (t == 2)
-          launch_kes_leafkeys(dim3(nblocks(mz, NT)), dim3(NT), st, mz, b->kes_sig + 448 * a, b->slot + a,
-                              b->ocert_c0 + a, c->params.slots_per_kes_period, b->kes_leaf + 32 * a);
-        const int r = kc_prefill(c, b, t, keys, t == 1 ? 1 : 0, a, z, st, pf_chunk == 0 && c->pool_keys <= 0, 0);
-        if (r != PRAOS_OK) return r;
-      }
-      pf_chunk = k + 1;
-    }
     if (vrf) {
       // the chunks' stage V alternate between two streams: on one they would queue behind
       // each other (a chunk's V alone is latency-bound)
@@ -2276,11 +2214,9 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   b->decoded = true;
   b->v_done = vrf;
-  c->prefill = prefill;
   int r = praos_batch_run(c, b);
-  c->prefill = false;
-  b->decoded = false;
-  b->v_done = false;
+  b->decoded = false;                // (the downloads below still read b->n; the next call resets
+  b->v_done = false;                 // every per-run field when it takes the batch: batch_reuse_reset)
   // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
   // header) are final once the VRF stream is done: they come back while KES still runs
   if (r == PRAOS_OK && c->concurrent) {

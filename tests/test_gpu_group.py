@@ -173,9 +173,8 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
                 assert np.array_equal(o1[k], o2[k]), k
             for k in D1:
                 assert np.array_equal(D1[k], D2[k]), k
-        # the key prefill (each landed chunk's keys into the pool-key stores, PRAOS_E2E_PREFILL on by
-        # default) with the stores kept across calls (PRAOS_OPT_POOL_KEYS): the second call finds
-        # every key already stored -- the same outputs
+        # the cold / VRF pool-key stores kept across calls (PRAOS_OPT_POOL_KEYS; 2 empties them first):
+        # the second call finds every pool key already stored -- the same outputs
         ctx.set_option(abi.OPT_POOL_KEYS, 2)
         for _ in range(2):
             o3 = ctx.verify_header_bytes(arena, off, ln)

@@ -467,3 +467,48 @@ def test_fresh_context_store_on_first_call_replay(chain):
             assert stats["validated"] == len(chain["off"]) and st == chain["state"]
     finally:
         c.close()
+
+
+def test_reused_batches_alternate_replay_and_pipeline(chain):
+    """The batches a context keeps between calls (the replay's, with per-header epoch nonces; the
+    stored-bytes pipeline's, here forced to 4 chunks) are reset by one routine whenever they are
+    taken again (batch_reuse_reset).  One context alternates replay / pipeline / replay in small
+    batches / pipeline / replay under different epoch nonces: every pipeline call equals the same
+    call on a fresh context, bit for bit, and every replay ends in the generator's state."""
+    import praos_hip
+    from praos_hip import abi
+    ep = (chain["slots"] // EPOCH_LEN).astype(int)
+
+    def pipeline_call(c, e):
+        rows = np.nonzero(ep == e)[0]
+        c.set_epoch(chain["nonces"][e], chain["pools"], chain["params"])
+        o, D = c.verify_header_bytes(chain["arena"], chain["off"][rows], chain["len"][rows], decoded=True)
+        return {k: np.array(v) for k, v in o.items()}, {k: np.array(D[k]) for k in ("slot", "header_hash", "cold_vk")}
+
+    def fresh(e):
+        f = praos_hip.Context(0)
+        try:
+            f.set_option(abi.OPT_PIPELINE, 4)
+            return pipeline_call(f, e)
+        finally:
+            f.close()
+
+    want = {e: fresh(e) for e in (2, 0)}
+    c = praos_hip.Context(0)
+    try:
+        c.set_option(abi.OPT_PIPELINE, 4)
+        for step, (kind, arg) in enumerate([("replay", 1 << 16), ("pipe", 2), ("replay", 61), ("pipe", 0),
+                                            ("replay", 97)]):
+            if kind == "replay":
+                stats, v, st, env = _replay(c, chain, batch_max=arg)
+                assert stats["validated"] == len(chain["off"]) and st == chain["state"], step
+            else:
+                o, D = pipeline_call(c, arg)
+                wo, wD = want[arg]
+                for k in ("bits", "pool_idx", "beta", "leader", "nonce"):
+                    assert (o[k] == wo[k]).all(), (step, k)
+                for k in D:
+                    assert (D[k] == wD[k]).all(), (step, k)
+                assert int((o["bits"] != 0).sum()) == 0, step
+    finally:
+        c.close()
