@@ -16,6 +16,9 @@ static constexpr size_t LT_ED_B = 8 * CACHED_BYTES, LT_VRF_B = 16 * CACHED_BYTES
 static constexpr size_t VRF_MID_BYTES = 28 * 16;    // per-header records of the staged VRF (praos_core.hpp)
 static constexpr uint32_t TP_SIGNED_STRIDE = 640;   // max canonical TPraos BHBody: 598 bytes (k_decode.hip)
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -52,6 +55,17 @@ class CopyPool {
     cv_.notify_all();
     done_.wait(g, [this] { return pending_ == 0; });
     job_ = nullptr;
+  }
+  // every worker onto the given CPUs (empty: back to the process's own mask)
+  void pin(const std::vector<int>& cpus) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (cpus.empty()) {
+      if (sched_getaffinity(0, sizeof set, &set) != 0) return;
+    } else {
+      for (int c : cpus) CPU_SET(c, &set);
+    }
+    run([&](unsigned) { (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set); });
   }
   // dst[0, n) = src[0, n), split over the workers
   void copy(void* dst, const void* src, size_t n) {
@@ -320,7 +334,9 @@ static bool stage_init(praos_ctx* c) {
     if (hipEventCreateWithFlags(&c->pin_ev[k], hipEventDisableTiming) != hipSuccess) return false;
   }
   const unsigned hw = std::thread::hardware_concurrency();
-  c->pool.reset(new CopyPool(std::max(1u, std::min(16u, hw ? hw : 1u))));   // the box's CPU share per GPU
+  unsigned nt = std::max(1u, std::min(16u, hw ? hw : 1u));      // the box's CPU share per GPU
+  if (const char* e = std::getenv("PRAOS_COPY_THREADS")) nt = (unsigned)std::max(1, std::min(64, std::atoi(e)));
+  c->pool.reset(new CopyPool(nt));
   return true;
 }
 
@@ -2489,6 +2505,11 @@ static std::string issuer_hash(const praos_ctx* c, const praos_headers* h, const
 
 using praos_host::nonce_combine;
 using praos_host::nonce_eq;
+
+// the staging copy threads of a context onto the given CPUs (the replay's thread placement)
+void rp_copy_pin(praos_ctx* c, const std::vector<int>& cpus) {
+  if (c && c->device >= 0 && stage_init(c)) c->pool->pin(cpus);
+}
 
 // error text for the other host modules of the library (praos_replay.hip)
 void praos_set_error_(praos_ctx* c, const std::string& m) { if (c) c->err = m; }

@@ -37,6 +37,8 @@
 #include "replay_internal.hpp"
 
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -46,6 +48,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -55,6 +58,7 @@
 #include <vector>
 
 void praos_set_error_(praos_ctx* c, const std::string& m);   // praos_api.hip
+void rp_copy_pin(praos_ctx* c, const std::vector<int>& cpus);  // praos_api.hip
 void praos_replay_scope_(praos_ctx* c, bool on);   // replay call scope: first error kept, pool-key store on
 
 namespace {
@@ -155,6 +159,40 @@ struct ChunkReader {
 };
 
 constexpr int SLOTS = RP_SLOTS;               // batches in flight (kept by the context between calls)
+
+// Thread placement (PRAOS_REPLAY_PIN, read per call): the nonce chain -- the replay's one
+// sequential piece of work, one Blake2b compression per header in order -- on a CPU of its own,
+// the launcher, the fold and the reader on one each, and the contexts' staging copy threads on
+// the rest, so the chain is never descheduled by the copies of the next batch.  Only with at
+// least 8 CPUs in the process's mask; 0 = off.
+struct Placement {
+  bool on = false;
+  std::vector<int> cpus;                      // the process's CPUs, in order
+  cpu_set_t reader_was;
+  bool reader_saved = false;
+  static void pin_self(int cpu) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cpu, &set);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+  }
+  void init() {
+    const char* e = std::getenv("PRAOS_REPLAY_PIN");
+    if (!e || std::atoi(e) == 0) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &set)) cpus.push_back(c);
+    if (cpus.size() < 8) { cpus.clear(); return; }
+    on = true;
+  }
+  int chain() const { return cpus[0]; }
+  int launcher() const { return cpus[1]; }
+  int folder() const { return cpus[2]; }
+  int reader() const { return cpus[3]; }
+  std::vector<int> copies() const { return std::vector<int>(cpus.begin() + 4, cpus.end()); }
+};
 constexpr size_t SPAN_GAP = 4096;             // headers this close share one uploaded span
 
 }  // namespace
@@ -304,6 +342,12 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   };
   double t_io = 0, t_dev = 0, t_wait = 0, t_nonce = 0, t_fold = 0;   // per thread: reader | fold
   uint64_t epochs_seen = 0, batches = 0;
+  Placement pl;
+  pl.init();
+  if (pl.on) {
+    for (int q = 0; q < m; q++) rp_copy_pin(mem[q], pl.copies());
+    pl.reader_saved = pthread_getaffinity_np(pthread_self(), sizeof pl.reader_was, &pl.reader_was) == 0;
+  }
   // ---- nonce chain (speculative tick + reupdate as if every header were valid)
   struct Spec {
     int32_t origin;
@@ -316,6 +360,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   bool have_last = false;
   uint64_t sp_epoch = sp.origin ? 0 : epoch_of(sp.last);
   std::thread chain([&] {
+    if (pl.on) Placement::pin_self(pl.chain());
     for (uint64_t k = 0;; k++) {
       Slot& C = S[k % T];
       {
@@ -395,6 +440,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   // ---- launcher: queues each batch's crypto (~30 launches: 1-2 ms of host time per batch,
   // kept off the nonce chain's thread)
   std::thread launcher([&] {
+    if (pl.on) Placement::pin_self(pl.launcher());
     for (uint64_t k = 0;; k++) {
       Slot& C = S[k % T];
       {
@@ -433,6 +479,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   uint64_t validated = 0, headers_done = 0, stop_index = 0;
   uint8_t stop_verdict = 0;
   std::thread folder([&] {
+    if (pl.on) Placement::pin_self(pl.folder());
     for (uint64_t k = 0;; k++) {
       Slot& C = S[k % T];
       {
@@ -502,6 +549,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     }
   });
   // ---- reader (this thread): build, upload and decode batch k into slot k % T (member k % m)
+  if (pl.on) Placement::pin_self(pl.reader());
   uint64_t next_index = 0, built = 0;
   for (uint64_t k = 0;; k++) {
     Slot& C = S[k % T];
@@ -611,6 +659,10 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   chain.join();
   launcher.join();
   folder.join();
+  if (pl.on) {                                // the caller's thread and the copy threads as they were
+    if (pl.reader_saved) (void)pthread_setaffinity_np(pthread_self(), sizeof pl.reader_was, &pl.reader_was);
+    for (int q = 0; q < m; q++) rp_copy_pin(mem[q], {});
+  }
   for (int k = 0; k < T; k++) {
     Slot& C = S[k];
     // a replay that stopped early may have queued the crypto of up to two later batches:

@@ -97,7 +97,7 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
     it (the leader schedule of epoch e is searched under epoch e's stake); the result then has
     "views": [(epoch, pool list)] -- the LedgerView's PoolDistr per epoch."""
     sig0 = chains.stake(cfg["npools"], cfg["stake_offset"])
-    views = []
+    views, used = [], []
     p = chains.params(cfg)
     st = {"last_slot": None, "counters": {}, "evolving": cfg["eta0"], "candidate": cfg["eta0"],
           "epoch_nonce": cfg["eta0"], "lab": None, "leb": None}
@@ -129,6 +129,7 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
             sl = (e * epoch_length + idx).astype(np.uint64)
             pl = lead[idx].astype(np.uint32)
         n = len(sl)
+        used.append((sl, pl))
         H, keys, _ = ctx.synthesize(n, cfg["npools"], p, eta, cfg["seed"], body_len=0, schedule=(sl, pl),
                                     block_no0=block_no, link=True, prev0=prev, tpraos=tpraos)
         pool_list = [(h, v, s) for (h, v), s in zip(keys, sig) if s > 0]
@@ -168,4 +169,4 @@ def make_multi_epoch_chain(ctx, cfg, epochs, epoch_length, stability_window, tpr
     return {"arena": np.concatenate(arenas), "off": np.concatenate(offs), "len": np.concatenate(lens),
             "slots": np.concatenate(slots_all), "header_hash": np.concatenate(hh_all), "pools": pool_list,
             "params": p, "nonces": nonces, "state": st,
-            "epoch_info": ei, "views": views}
+            "epoch_info": ei, "views": views, "schedules": used}

@@ -44,6 +44,16 @@ def main():
     ap.add_argument("--members", default="1",
                     help="comma list: 1 = one context, m > 1 = a praos_group of m contexts on device 0 "
                          "(praos_group_replay_immutable: batches dealt to the members in turn, one fold)")
+    ap.add_argument("--schedule-out", default=None,
+                    help="directory: save each searched epoch's first-leader-wins schedule (e >= 1) as "
+                         "<chain>_epoch<e>_schedule.npz, so a later run can skip the search")
+    ap.add_argument("--schedule-in", default=None,
+                    help="comma list of epoch=file.npz schedules to use instead of searching (e.g. the c5 chain's "
+                         "epoch 1: 1=ouroboros-consensus_amd/praos_hip/data/c5_epoch1_schedule.npz)")
+    ap.add_argument("--env-variants", default="",
+                    help="';'-separated host settings to time, each a comma list of VAR=VALUE set before a fresh "
+                         "context is opened (e.g. 'PRAOS_REPLAY_PIN=0;PRAOS_REPLAY_PIN=1,PRAOS_COPY_THREADS=8'); "
+                         "empty: the environment as it is")
     ap.add_argument("--tpraos", action="store_true",
                     help="a Shelley..Alonzo (TPraos) chain replayed by praos_replay_immutable_tpraos (TICKN with extra entropy)")
     args = ap.parse_args()
@@ -63,6 +73,13 @@ def main():
         assert args.epoch_length == cfg["epoch_length"] and args.pools == cfg["npools"]
         f = cfg["f"]
         schedules = {0: chains.load_schedule(args.chain)}
+    if args.schedule_in:
+        import numpy as np
+        schedules = dict(schedules or {})
+        for item in args.schedule_in.split(","):
+            e, fn = item.split("=")
+            z = np.load(fn)
+            schedules[int(e)] = (z["slots"], z["pools"])
     window = args.window or int(4 * 2160 / f)   # 4k/f with k = 2160: the Babbage stability window
     t0 = time.perf_counter()
     # heartbeat while the chain is generated (the linked re-signing is sequential: minutes
@@ -82,6 +99,15 @@ def main():
         schedules=schedules)
     gen_done.set()
     t_gen = time.perf_counter() - t0
+    if args.schedule_out:
+        import numpy as np
+        os.makedirs(args.schedule_out, exist_ok=True)
+        for e in range(1, args.epochs):
+            if schedules and e in schedules:
+                continue
+            sl, pl = data["schedules"][e]
+            np.savez_compressed(os.path.join(args.schedule_out, f"{args.chain or 'replay'}_epoch{e}_schedule.npz"),
+                                slots=np.asarray(sl, np.uint64), pools=np.asarray(pl, np.uint32))
     n = len(data["off"])
     env_limits = {"max_major_pv": 9, "lv_prot_major": 8, "max_header_size": 1100, "max_body_size": 90_112}
     with tempfile.TemporaryDirectory() as tmp:
@@ -89,8 +115,14 @@ def main():
         nch = immutable.write_immutable(path, data["arena"], data["off"], data["len"], data["slots"],
                                         data["header_hash"], args.chunk_slots)
         from praos_hip import abi
-        for members in [int(x) for x in args.members.split(",")]:
-          runner = ctx if members == 1 else abi.Group([0] * members)
+        variants = [v for v in args.env_variants.split(";")] if args.env_variants else [""]
+        for variant in variants:
+         for item in filter(None, variant.split(",")):
+             k, v = item.split("=")
+             os.environ[k] = v
+         for members in [int(x) for x in args.members.split(",")]:
+          # a fresh context (or group) per variant: settings read when a context starts are seen
+          runner = praos_hip.Context(0) if members == 1 else abi.Group([0] * members)
           for mode in args.pool_keys.split(","):
               for batch_max in [int(x) for x in args.batch_sizes.split(",")]:
                   runs = []
@@ -116,12 +148,11 @@ def main():
                           "chain": args.chain or "replay-bench", "pool_keys": mode, "members": members,
                           "stages_ms": {k: round(best[k], 2) for k in ("ms_io", "ms_device", "ms_nonce", "ms_fold")},
                           "batch_max": batch_max, "batches": best["batches"], "epoch_nonces": best["epochs"],
-                          "generate_s": round(t_gen, 1), "reps": args.reps,
+                          "generate_s": round(t_gen, 1), "reps": args.reps, "host_settings": variant or None,
                           "data": "synthetic linked first-leader-wins chain, GPU-signed; written to a temp dir"}
                   print(json.dumps(line), flush=True)
           runner.set_option(abi.OPT_POOL_KEYS, -1)
-          if runner is not ctx:
-              runner.close()
+          runner.close()
     ctx.close()
 
 
