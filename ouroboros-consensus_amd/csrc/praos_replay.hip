@@ -160,11 +160,16 @@ struct ChunkReader {
 
 constexpr int SLOTS = RP_SLOTS;               // batches in flight (kept by the context between calls)
 
-// Thread placement (PRAOS_REPLAY_PIN, read per call): the nonce chain -- the replay's one
-// sequential piece of work, one Blake2b compression per header in order -- on a CPU of its own,
-// the launcher, the fold and the reader on one each, and the contexts' staging copy threads on
-// the rest, so the chain is never descheduled by the copies of the next batch.  Only with at
-// least 8 CPUs in the process's mask; 0 = off.
+// Thread placement (PRAOS_REPLAY_PIN, read per call: 1 on, 0 off, unset = on for batches of
+// 64k headers or more): the nonce chain -- the replay's one sequential piece of work, one
+// Blake2b compression per header in order -- on a CPU of its own, the launcher, the fold and the
+// reader on one each, and the contexts' staging copy threads on the rest, so the chain is never
+// descheduled by the copies of the next batch.  Only with at least 8 CPUs in the process's mask.
+// Measured on the C5 chain (863,780 headers, 2 epochs; profiles/r06/c_replay): the chain thread
+// 62-65 ms pinned against 62-105 ms unpinned; 96k-header batches 9.6-9.8 -> 10.0-10.1 M headers/s
+// on one context and 7.3-8.0 -> 9.0-9.3 M on a 2-member group; 48k-header batches slower pinned
+// (5.4-5.5 vs 5.9-8.7 M: the device stage of the many small batches, cause not isolated), hence
+// the size threshold.
 struct Placement {
   bool on = false;
   std::vector<int> cpus;                      // the process's CPUs, in order
@@ -176,9 +181,10 @@ struct Placement {
     CPU_SET(cpu, &set);
     (void)pthread_setaffinity_np(pthread_self(), sizeof set, &set);
   }
-  void init() {
+  void init(size_t batch_max) {
     const char* e = std::getenv("PRAOS_REPLAY_PIN");
-    if (!e || std::atoi(e) == 0) return;
+    const bool want = e ? std::atoi(e) != 0 : batch_max >= 65536;
+    if (!want) return;
     cpu_set_t set;
     CPU_ZERO(&set);
     if (sched_getaffinity(0, sizeof set, &set) != 0) return;
@@ -343,7 +349,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   double t_io = 0, t_dev = 0, t_wait = 0, t_nonce = 0, t_fold = 0;   // per thread: reader | fold
   uint64_t epochs_seen = 0, batches = 0;
   Placement pl;
-  pl.init();
+  pl.init(batch_max);
   if (pl.on) {
     for (int q = 0; q < m; q++) rp_copy_pin(mem[q], pl.copies());
     pl.reader_saved = pthread_getaffinity_np(pthread_self(), sizeof pl.reader_was, &pl.reader_was) == 0;
