@@ -33,6 +33,7 @@ struct VrfIn {
   int wave_prio;                         // stage V / join waves at s_setprio 3 (small batches)
   int tp_seed;                           // stage V alpha: 0 Praos mkInputVRF; 1 + k TPraos mkSeed
                                          // with ucNonce k (0 seedEta, 1 seedL)
+  int pre;                               // join: the pool part ran ahead (k_vrf_pool wrote bits[i])
 };
 
 // issuer pool: hashKey (Blake2b-224 of the cold vk, Praos.hs:552) -> sorted index or -1

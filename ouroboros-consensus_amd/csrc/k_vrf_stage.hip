@@ -155,12 +155,10 @@ __global__ void __launch_bounds__(NT, LB_VRF_F) k_vrf_u_nc(size_t n, const uint3
   vrf_u_core<false>(mid, n, i, pk, pr + 8, pr + 12, btab, lane_tab(tabs, i, LT_ED), nullptr, nullptr);
 }
 
-// join over every header: pool lookup and key hash (Praos.hs:533-541), the batched
-// inversion, the challenge, beta, the output check and the range extension
-__global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
+// the header-only part of the join: pool lookup and key hash (Praos.hs:533-541), the pool
+// indices and the leader / nonce values of the stated output (Praos.hs:468-502); returns the
+// key bits
+__device__ __forceinline__ uint16_t vrf_pool_item(const VrfIn& a, size_t i) {
   uint16_t b = 0;
   int32_t sidx;
   {
@@ -180,6 +178,34 @@ __global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_join(size_t n, VrfIn a, co
       if (!same) b |= PRAOS_BIT_VRF_KEY_WRONG;
     }
   }
+  uint32_t out[16], lv[8], nv[8], nn[8];
+  load_words(out, a.vrf_out + 64 * i, 16);
+  blake2b256_tag64(lv, 'L', out);
+  blake2b256_tag64(nv, 'N', out);
+  blake2b_32(nn, nv, 32);
+  store_words(a.leader_out + 32 * i, lv, 8);
+  store_words(a.nonce_out + 32 * i, nn, 8);
+  a.pool_idx[i] = sidx < 0 ? -1 : a.pool_map[sidx];
+  a.pool_sorted_idx[i] = sidx;
+  return b;
+}
+
+// ... ahead of the join (small batches, on a stream with slack): the join's lanes then end
+// after the inversion and the two SHA-512s (its dependent pool-search loads and five Blake2b
+// compressions no longer follow stage V)
+__global__ void __launch_bounds__(NT) k_vrf_pool(size_t n, VrfIn a) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  a.bits[i] = vrf_pool_item(a, i);
+}
+
+// join over every header: the pool part (vrf_pool_item, or its bits from k_vrf_pool when
+// a.pre), the batched inversion, the challenge, beta and the output check
+__global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_join(size_t n, VrfIn a, const uint4* __restrict__ mid) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (a.wave_prio) __builtin_amdgcn_s_setprio(3);
+  uint16_t b = a.pre ? 0 : vrf_pool_item(a, i);
   uint32_t c4[4];
   {
     const uint4 q = *(const uint4*)(a.vrf_proof + 80 * i + 32);
@@ -199,16 +225,8 @@ __global__ void __launch_bounds__(NT, LB_VRF_J) k_vrf_join(size_t n, VrfIn a, co
   for (int k = 0; k < 16; k++) out_eq &= out[k] == beta[k];
   if (!proof_ok) b |= PRAOS_BIT_VRF_PROOF;
   if (!out_eq && a.check_output) b |= PRAOS_BIT_VRF_OUTPUT;
-  uint32_t lv[8], nv[8], nn[8];
-  blake2b256_tag64(lv, 'L', out);
-  blake2b256_tag64(nv, 'N', out);
-  blake2b_32(nn, nv, 32);
-  store_words(a.leader_out + 32 * i, lv, 8);
-  store_words(a.nonce_out + 32 * i, nn, 8);
   store_words(a.beta_out + 64 * i, beta, 16);
-  a.pool_idx[i] = sidx < 0 ? -1 : a.pool_map[sidx];
-  a.pool_sorted_idx[i] = sidx;
-  a.bits[i] = b;
+  a.bits[i] = a.pre ? (uint16_t)(a.bits[i] | b) : b;
 }
 
 // TPraos join of certificate `cert` (0: eta / nonce cert, 1: leader cert), the staged form of
@@ -344,13 +362,23 @@ void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const
                      const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                      uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
-                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio) {
+                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio, int pre) {
   VrfIn a = vrf_in(cold_vk, vrf_vk, vrf_out, vrf_proof, nullptr, nullptr, 0, nullptr, pool_hash, pool_vrf,
                    pool_map, npools, check_output, bits, pool_idx, pool_sorted_idx, beta_out, leader_out,
                    nonce_out, nullptr);
   a.wave_prio = wave_prio;
+  a.pre = pre;
   const unsigned bs = lat_block(n);
   hipLaunchKernelGGL(k_vrf_join, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, stream, n, a, (const uint4*)mid);
+}
+void launch_vrf_pool(hipStream_t stream, size_t n, const uint8_t* cold_vk, const uint8_t* vrf_vk,
+                     const uint8_t* vrf_out, const uint32_t* pool_hash, const uint32_t* pool_vrf,
+                     const int32_t* pool_map, uint32_t npools, uint16_t* bits, int32_t* pool_idx,
+                     int32_t* pool_sorted_idx, uint8_t* leader_out, uint8_t* nonce_out) {
+  const VrfIn a = vrf_in(cold_vk, vrf_vk, vrf_out, nullptr, nullptr, nullptr, 0, nullptr, pool_hash, pool_vrf,
+                         pool_map, npools, 0, bits, pool_idx, pool_sorted_idx, nullptr, leader_out, nonce_out,
+                         nullptr);
+  hipLaunchKernelGGL(k_vrf_pool, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, n, a);
 }
 void launch_vrf_join_tp(hipStream_t stream, size_t n, int cert, const uint8_t* cold_vk, const uint8_t* vrf_vk,
                         const uint8_t* cert_out, const uint8_t* cert_proof, const uint32_t* pool_hash,

@@ -165,7 +165,13 @@ void launch_vrf_join(hipStream_t stream, size_t n, const uint8_t* cold_vk, const
                      const uint8_t* vrf_out, const uint8_t* vrf_proof, const uint32_t* pool_hash,
                      const uint32_t* pool_vrf, const int32_t* pool_map, uint32_t npools, int check_output,
                      uint16_t* bits, int32_t* pool_idx, int32_t* pool_sorted_idx, uint8_t* beta_out,
-                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio = 0);
+                     uint8_t* leader_out, uint8_t* nonce_out, const void* mid, int wave_prio = 0,
+                     int pre = 0);                         // pre: launch_vrf_pool ran before (bits, pool, leader, nonce)
+// the join's pool part ahead of it (k_vrf_stage.hip k_vrf_pool): key bits, pool indices, leader / nonce
+void launch_vrf_pool(hipStream_t stream, size_t n, const uint8_t* cold_vk, const uint8_t* vrf_vk,
+                     const uint8_t* vrf_out, const uint32_t* pool_hash, const uint32_t* pool_vrf,
+                     const int32_t* pool_map, uint32_t npools, uint16_t* bits, int32_t* pool_idx,
+                     int32_t* pool_sorted_idx, uint8_t* leader_out, uint8_t* nonce_out);
 // TPraos join of certificate cert (0: eta, 1: leader; k_vrf_stage.hip k_vrf_join_tp), after
 // stage V (tp_seed 1 + cert) and U of that certificate into `mid`
 void launch_vrf_join_tp(hipStream_t stream, size_t n, int cert, const uint8_t* cold_vk, const uint8_t* vrf_vk,

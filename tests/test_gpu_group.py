@@ -3,6 +3,8 @@ an 8-GPU node the members are devices 0..7), a batch split into contiguous shard
 concurrently, outputs gathered in place -- bit-exact against one context, and the
 shard -> gather -> fold path (updateChainDepState on member 0 over the gathered
 outputs) equal to the single-context fold."""
+import os
+
 import numpy as np
 import pytest
 
@@ -184,3 +186,40 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
         ctx.set_option(abi.OPT_PIPELINE, 0)
         ctx.set_option(abi.OPT_POOL_KEYS, -1)
     assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT
+
+
+@pytest.mark.parametrize("env", [{"PRAOS_E2E_KES": "1"}, {"PRAOS_E2E_KES": "2"}, {"PRAOS_E2E_KES": "8"},
+                                 {"PRAOS_PRE_JOIN": "0"}, {"PRAOS_PRE_JOIN": "1"}])
+def test_schedule_variants_equal_single_batch(ctx, c5_batch, env):
+    """Schedule options that move work between kernels and streams give the default context's
+    one-batch outputs bit for bit: the stored-bytes pipeline with the KES checks (leaf-key cache)
+    run in 1, 2 or 8 groups of chunks, each once its chunks have landed (PRAOS_E2E_KES), and the
+    join's pool part ahead of
+    it as k_vrf_pool (PRAOS_PRE_JOIN, default on below SMALL_BATCH headers) -- in one batch and
+    pipelined (8 chunks)."""
+    import praos_hip
+    from praos_hip import abi
+    cfg, H, pool_list, corrupted, p, arena, off, ln = c5_batch
+    ctx.set_epoch(cfg["eta0"], pool_list, p)
+    ctx.set_option(abi.OPT_PIPELINE, 1)
+    try:
+        o1, D1 = ctx.verify_header_bytes(arena, off, ln, decoded=True)
+    finally:
+        ctx.set_option(abi.OPT_PIPELINE, 0)
+    os.environ.update(env)
+    try:
+        c2 = praos_hip.Context(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+    try:
+        c2.set_epoch(cfg["eta0"], pool_list, p)
+        for chunks in (1, 8, 8):                      # the second 8-chunk call reuses the batch
+            c2.set_option(abi.OPT_PIPELINE, chunks)
+            o2, D2 = c2.verify_header_bytes(arena, off, ln, decoded=True)
+            for k in o1:
+                assert np.array_equal(o1[k], o2[k]), (chunks, k)
+            for k in D1:
+                assert np.array_equal(D1[k], D2[k]), (chunks, k)
+    finally:
+        c2.close()

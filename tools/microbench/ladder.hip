@@ -3,7 +3,7 @@
 // 4 doublings (dbl-2008-hwcd: 4 squarings + 3 products + the additions / subtractions, the
 // last one to extended coordinates) and 2 cached additions (add-2008-hwcd-3: 4 products +
 // 4 additions + 3 subtractions, each followed by its conversion) -- repeated ITERS times per
-// lane, in three representations of GF(2^255-19):
+// lane, in two representations of GF(2^255-19):
 //
 //   lib   the library's 8 x 32-bit limbs (fe25519.hpp / ge25519.hpp as compiled into k_vrf_v:
 //         generated MAC columns, carried additions with the rare-branch fold); PRAOS_ILP4=1
@@ -12,11 +12,8 @@
 //         carry pass); additions lazy (limb-wise, no carry), subtractions limb-wise with a 2p
 //         bias, and a carry pass before a product whenever an input could exceed the
 //         product's 2^30.4 limb bound
-//   f10   10 limbs of 26 / 25 bits (radix 2^25.5), signed, 64-bit column sums with the 19x
-//         wrap folded into the multiplier: additions and subtractions limb-wise with no carry
-//         and no bias (products accept the sums of two reduced values)
 //
-// Reports SIMD cycles per window at exactly 1..4 waves per SIMD and checks that the three
+// Reports SIMD cycles per window at exactly 1..4 waves per SIMD and checks that both
 // representations end on the same point (encoded).  Not used by the library.
 // Build: hipcc --offload-arch=gfx950 -O3 -I../../ouroboros-consensus_amd/csrc [-DPRAOS_ILP4=1] -o ladder ladder.hip
 #include <hip/hip_runtime.h>
@@ -76,7 +73,11 @@ FE_INLINE void f29_carry(f29& r, const uint64_t (&T)[9]) {
     r.v[k] = (uint32_t)u & M29;
     c = u >> 29;
   }
-  const uint64_t u0 = (uint64_t)r.v[0] + c * 1216u;   // 2^261 = 64 * 19 (mod p)
+  // fold everything at or above 2^255 (limb 8's bits 23.. and the carry at 2^261) with 19, so a
+  // reduced value's limb 8 stays below 2^23 and the subtraction's 2p bias covers it
+  const uint64_t top = ((uint64_t)(r.v[8] >> 23)) + (c << 6);
+  r.v[8] &= (1u << 23) - 1u;
+  const uint64_t u0 = (uint64_t)r.v[0] + top * 19u;
   r.v[0] = (uint32_t)u0 & M29;
   r.v[1] += (uint32_t)(u0 >> 29);
 }
@@ -181,132 +182,6 @@ FE_INLINE void g29_add(g29_p1p1& r, const g29_p3& p, const g29_cached& q) {
   f29_sub(r.T, t0, r.T);
 }
 
-// ------------------------------------------------------------------ 10 x 25.5 (signed)
-struct f10 { int32_t v[10]; };
-
-FE_INLINE void f10_from(f10& r, const fe& a) {
-  fe c;
-  fe_canon(c, a);
-  int bit = 0;
-#pragma unroll
-  for (int k = 0; k < 10; k++) {
-    const int nb = (k & 1) ? 25 : 26, w = bit >> 5, s = bit & 31;
-    uint64_t x = c.v[w];
-    if (w + 1 < 8) x |= (uint64_t)c.v[w + 1] << 32;
-    r.v[k] = (int32_t)((x >> s) & ((1u << nb) - 1));
-    bit += nb;
-  }
-}
-// carry (ref10's order) of 64-bit column sums h[0..9] into reduced limbs
-FE_INLINE void f10_carry(f10& r, int64_t (&h)[10]) {
-  int64_t c;
-#define C26(i) c = (h[i] + ((int64_t)1 << 25)) >> 26; h[(i) + 1] += c; h[i] -= c * ((int64_t)1 << 26);
-#define C25(i) c = (h[i] + ((int64_t)1 << 24)) >> 25; h[(i) + 1] += c; h[i] -= c * ((int64_t)1 << 25);
-  C26(0) C26(4) C25(1) C25(5) C26(2) C26(6) C25(3) C25(7) C26(4) C26(8)
-  c = (h[9] + ((int64_t)1 << 24)) >> 25; h[0] += c * 19; h[9] -= c * ((int64_t)1 << 25);
-  C26(0)
-#undef C26
-#undef C25
-#pragma unroll
-  for (int k = 0; k < 10; k++) r.v[k] = (int32_t)h[k];
-}
-FE_INLINE void f10_to(fe& r, const f10& a) {    // any carried value -> 8 x 32 mod p
-  int64_t h[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) h[k] = a.v[k];
-  f10 t;
-  f10_carry(t, h);                               // limbs now |t_k| <= 2^25 (+ a little)
-  fe_set(r, 0);
-  int bit = 0;
-#pragma unroll
-  for (int k = 0; k < 10; k++) {
-    fe x;
-    const int32_t v = t.v[k];
-    fe_term(x, (uint32_t)(v < 0 ? -v : v), bit);
-    if (v < 0) fe_sub(r, r, x);
-    else fe_add(r, r, x);
-    bit += (k & 1) ? 25 : 26;
-  }
-}
-FE_INLINE void f10_mul(f10& r, const f10& f, const f10& g) {
-  int64_t h[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) h[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-#pragma unroll
-    for (int j = 0; j < 10; j++) {
-      const int k = i + j;
-      int32_t gj = g.v[j];
-      if (k >= 10) gj *= 19;
-      int32_t fi = f.v[i];
-      if ((i & 1) && (j & 1)) fi *= 2;
-      h[k % 10] += (int64_t)fi * gj;
-    }
-  }
-  f10_carry(r, h);
-}
-FE_INLINE void f10_sq(f10& r, const f10& f) {
-  int64_t h[10];
-#pragma unroll
-  for (int k = 0; k < 10; k++) h[k] = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-#pragma unroll
-    for (int j = i; j < 10; j++) {
-      const int k = i + j;
-      int32_t gj = f.v[j];
-      if (k >= 10) gj *= 19;
-      int32_t fi = f.v[i];
-      if ((i & 1) && (j & 1)) fi *= 2;
-      if (j != i) fi *= 2;
-      h[k % 10] += (int64_t)fi * gj;
-    }
-  }
-  f10_carry(r, h);
-}
-FE_INLINE void f10_add(f10& r, const f10& a, const f10& b) {
-#pragma unroll
-  for (int k = 0; k < 10; k++) r.v[k] = a.v[k] + b.v[k];
-}
-FE_INLINE void f10_sub(f10& r, const f10& a, const f10& b) {
-#pragma unroll
-  for (int k = 0; k < 10; k++) r.v[k] = a.v[k] - b.v[k];
-}
-
-struct g10_p2 { f10 X, Y, Z; };
-struct g10_p3 { f10 X, Y, Z, T; };
-struct g10_p1p1 { f10 X, Y, Z, T; };
-struct g10_cached { f10 YpX, YmX, Z, T2d; };
-
-FE_INLINE void g10_p1p1_to_p2(g10_p2& r, const g10_p1p1& p) {
-  f10_mul(r.X, p.X, p.T); f10_mul(r.Y, p.Y, p.Z); f10_mul(r.Z, p.Z, p.T);
-}
-FE_INLINE void g10_p1p1_to_p3(g10_p3& r, const g10_p1p1& p) {
-  f10_mul(r.X, p.X, p.T); f10_mul(r.Y, p.Y, p.Z); f10_mul(r.Z, p.Z, p.T); f10_mul(r.T, p.X, p.Y);
-}
-FE_INLINE void g10_dbl(g10_p1p1& r, const g10_p2& p) {
-  f10 t0, s;
-  f10_add(s, p.X, p.Y);
-  f10_sq(r.X, p.X); f10_sq(r.Z, p.Y); f10_sq(r.T, p.Z); f10_sq(t0, s);
-  f10_add(r.T, r.T, r.T);
-  f10_add(r.Y, r.Z, r.X);
-  f10_sub(r.Z, r.Z, r.X);
-  f10_sub(r.X, t0, r.Y);
-  f10_sub(r.T, r.T, r.Z);
-}
-FE_INLINE void g10_add(g10_p1p1& r, const g10_p3& p, const g10_cached& q) {
-  f10 t0, a, b;
-  f10_add(a, p.Y, p.X);
-  f10_sub(b, p.Y, p.X);
-  f10_mul(r.Z, a, q.YpX); f10_mul(r.Y, b, q.YmX); f10_mul(r.T, q.T2d, p.T); f10_mul(r.X, p.Z, q.Z);
-  f10_add(t0, r.X, r.X);
-  f10_sub(r.X, r.Z, r.Y);
-  f10_add(r.Y, r.Z, r.Y);
-  f10_add(r.Z, t0, r.T);
-  f10_sub(r.T, t0, r.T);
-}
-
 // ------------------------------------------------------------------ kernels
 // The starting point and the two cached addends are derived from the lane id; the loop is the
 // window; the result is the affine encoding's hash (8 x 32 path for all three).
@@ -396,33 +271,6 @@ __global__ void __launch_bounds__(256) k_f29(uint32_t* out) {
   out[t] = hash_point(X, Y, Z);
 }
 
-__global__ void __launch_bounds__(256) k_f10(uint32_t* out) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  ge_p2 P0;
-  ge_cached Q1l, Q2l;
-  start_points(P0, Q1l, Q2l, t);
-  g10_p2 P;
-  g10_cached Q1, Q2;
-  f10_from(P.X, P0.X); f10_from(P.Y, P0.Y); f10_from(P.Z, P0.Z);
-  f10_from(Q1.YpX, Q1l.YpX); f10_from(Q1.YmX, Q1l.YmX); f10_from(Q1.Z, Q1l.Z); f10_from(Q1.T2d, Q1l.T2d);
-  f10_from(Q2.YpX, Q2l.YpX); f10_from(Q2.YmX, Q2l.YmX); f10_from(Q2.Z, Q2l.Z); f10_from(Q2.T2d, Q2l.T2d);
-  for (int it = 0; it < ITERS; it++) {
-    g10_p1p1 x;
-    g10_p3 P3;
-#pragma unroll 1
-    for (int d = 0; d < 3; d++) { g10_dbl(x, P); g10_p1p1_to_p2(P, x); }
-    g10_dbl(x, P);
-    g10_p1p1_to_p3(P3, x);
-    g10_add(x, P3, Q1);
-    g10_p1p1_to_p3(P3, x);
-    g10_add(x, P3, Q2);
-    g10_p1p1_to_p2(P, x);
-  }
-  fe X, Y, Z;
-  f10_to(X, P.X); f10_to(Y, P.Y); f10_to(Z, P.Z);
-  out[t] = hash_point(X, Y, Z);
-}
-
 template <int V>
 static int run(uint32_t* d, int blocks, float* ms) {
   hipEvent_t e0, e1;
@@ -431,8 +279,7 @@ static int run(uint32_t* d, int blocks, float* ms) {
   for (int rep = 0; rep < 2; rep++) {
     if (rep) CHK(hipEventRecord(e0));
     if (V == 0) hipLaunchKernelGGL(k_lib, dim3(blocks), dim3(256), 0, 0, d);
-    else if (V == 1) hipLaunchKernelGGL(k_f29, dim3(blocks), dim3(256), 0, 0, d);
-    else hipLaunchKernelGGL(k_f10, dim3(blocks), dim3(256), 0, 0, d);
+    else hipLaunchKernelGGL(k_f29, dim3(blocks), dim3(256), 0, 0, d);
     if (rep) CHK(hipEventRecord(e1));
     CHK(hipDeviceSynchronize());
   }
@@ -444,21 +291,21 @@ int main() {
   hipDeviceProp_t p;
   CHK(hipGetDeviceProperties(&p, 0));
   const int ncu = p.multiProcessorCount;
-  const char* names[3] = {"lib 8x32", "f29 9x29", "f10 10x25.5"};
+  const char* names[2] = {"lib 8x32", "f29 9x29"};
   uint32_t* d;
   CHK(hipMalloc(&d, (size_t)ncu * 4 * 256 * 4));
   const size_t maxl = (size_t)ncu * 4 * 256;
-  uint32_t* h[3];
-  for (int v = 0; v < 3; v++) h[v] = new uint32_t[maxl];
+  uint32_t* h[2];
+  for (int v = 0; v < 2; v++) h[v] = new uint32_t[maxl];
   int bad = 0;
   printf("PRAOS_ILP4=%d  one Straus window = 4 doublings + 2 cached additions (+ conversions), %d windows per lane\n",
          PRAOS_ILP4, ITERS);
   for (int W = 1; W <= 4; W++) {
     const int blocks = ncu * W;                 // 256-thread blocks: 4 waves per block, one per SIMD
     const size_t lanes = (size_t)blocks * 256;
-    for (int v = 0; v < 3; v++) {
+    for (int v = 0; v < 2; v++) {
       float ms;
-      const int rc = v == 0 ? run<0>(d, blocks, &ms) : v == 1 ? run<1>(d, blocks, &ms) : run<2>(d, blocks, &ms);
+      const int rc = v == 0 ? run<0>(d, blocks, &ms) : run<1>(d, blocks, &ms);
       if (rc) return rc;
       CHK(hipMemcpy(h[v], d, lanes * 4, hipMemcpyDeviceToHost));
       size_t diff = 0;
