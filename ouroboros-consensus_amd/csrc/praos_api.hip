@@ -246,8 +246,7 @@ struct praos_ctx {
                                                        // -1: batches below KEY_PRIO_BATCH headers)
   hipEvent_t ev[6] = {};
   hipEvent_t side_ev[4] = {};
-  hipEvent_t miss_ev[5] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done,
-                                                       // a KES group's misses done (stored-bytes pipeline)
+  hipEvent_t miss_ev[4] = {};                          // miss lists ready (OCert, KES, VRF), OCert misses done
   float kernel_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   bool last_from_bytes = false;
   bool v_timed = false;                                // the last run launched k_vrf_v
@@ -278,11 +277,10 @@ struct praos_ctx {
   // nothing runs on the GPU until it has landed and been decoded
   int pipe_head = 25;                                  // (432k headers, 8 chunks: 100 -> 16.9-17.0 ms,
                                                        // 50 -> 16.5, 25 -> 16.3-16.4, 12 -> 16.2-16.4)
-  int e2e_kes = 0;                                     // stored-bytes pipeline: the KES checks with the leaf-key
-                                                       // cache in this many groups of chunks, each queued once
-                                                       // its last chunk is decoded, beside the later chunks'
-                                                       // upload and stage V (PRAOS_E2E_KES; 0: after the upload
-                                                       // over the whole batch)
+  // (round 6 measured the KES checks queued while later chunks upload, in two forms, both slower:
+  // uncached per landed chunk, 432k e2e 15.5-16.0 -> 18.2-18.9 ms; with the leaf-key cache over 1,
+  // 2 or 4 groups of landed chunks, 15.8 / 17.0 / 18.2-18.7 ms: the GPU runs the chunks' stage V
+  // during the upload, so the KES work there only stretches V; profiles/r06/g_e2e_kes.  Removed.)
   int pipe_tail = 100;                                 // ... and the last chunk's (PRAOS_PIPE_TAIL): the run after it
                                                        // waits for its decode, but a smaller one leaves more of the
                                                        // batch's stage V after the upload (432k, 8 chunks: 100 ->
@@ -446,12 +444,6 @@ struct praos_batch {
   ge_cached *tab_ocert = nullptr, *tab_kes = nullptr, *tab_vrf = nullptr;
   ge_cached* tab_vrfu = nullptr;   // 8-entry lane tables of stage U on uncached VRF keys
   bool v_done = false;             // stage V already queued on ctx->vstream (stored-bytes pipeline)
-  bool kes_done = false;           // the KES checks already queued group by group (stored-bytes pipeline)
-  uint32_t* chunk_list = nullptr;  // ... their header lists: 0..n-1 and each group's count
-  uint32_t* chunk_cnt = nullptr;
-  size_t chunk_list_n = 0;
-  std::vector<uint32_t> h_iota;
-  uint32_t h_cnt[PIPE_MAX] = {};
   uint8_t* vrf_mid = nullptr;   // stage V -> stage F record of the two-stage VRF
   uint8_t* vrf_mid2 = nullptr;  // TPraos: the leader certificate's record (allocated on first use)
   ge_cached* tab_vrf2 = nullptr; // TPraos: the leader certificate's stage-V lane tables
@@ -613,7 +605,6 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_POOL_KEYS")) (void)praos_set_option(c, PRAOS_OPT_POOL_KEYS, std::atoi(e));
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PRE_JOIN")) c->pre_join = std::atoi(e);
-  if (const char* e = std::getenv("PRAOS_E2E_KES")) c->e2e_kes = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
@@ -650,7 +641,10 @@ static bool open_streams(praos_ctx* c) {
     const int vprio = (vp && std::atoi(vp) == 0) ? least : greatest;
     (void)hipStreamCreateWithPriority(&c->vstream, hipStreamNonBlocking, vprio);
     (void)hipStreamCreateWithPriority(&c->vstream2, hipStreamNonBlocking, vprio);
-    (void)hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking);
+    // the copy stream (uploads; the replay's decode): PRAOS_CSTREAM_PRIO=1 at the greatest priority
+    const char* cp = std::getenv("PRAOS_CSTREAM_PRIO");
+    (void)hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking,
+                                      (cp && std::atoi(cp) == 1) ? greatest : least);
     (void)hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking);
   }
   return true;
@@ -1208,10 +1202,8 @@ static bool ensure_pks(praos_ctx* c, int t, hipStream_t st) {
   praos_ctx::PoolKeyStore& s = c->pks[t];
   if (s.ktab) return true;
   praos_ctx::PoolKeyStore z;
-  // KES leaf keys: a 432k-header epoch has ~59k (one per pool and KES period): 131,072 entries
-  // (2 GB of tables), 262,144 slots
-  z.slots = t == 2 ? 1u << 18 : 1u << 15;
-  z.cap = t == 2 ? 1u << 17 : 1u << 14;
+  z.slots = 1u << 15;
+  z.cap = 1u << 14;
   bool ok = hipMalloc(&z.pkey, 32 * (size_t)z.slots) == hipSuccess;
   ok = ok && hipMalloc(&z.pentry, 4 * (size_t)z.slots) == hipSuccess;
   ok = ok && hipMalloc(&z.count, 8) == hipSuccess;
@@ -1522,9 +1514,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   if (ocert_miss) ocert_miss();
   HIPCHK(c, hipEventRecord(c->side_ev[0], so));
   if (c->kernels & 2) {
-    if (b->kes_done) {
-      // the stored-bytes pipeline queued every chunk's KES checks on sk while it uploaded
-    } else if (kc) {
+    if (kc) {
       // leaf-key cache: the Ed25519 key a Sum6KES signature ends on repeats for every
       // header a pool signs in one KES period
       praos_batch::KeyCache& k = b->kc[2];
@@ -1971,7 +1961,6 @@ static void batch_reuse_reset(praos_batch* b) {
   b->body_bytes_len = 0;
   b->decoded = false;
   b->v_done = false;
-  b->kes_done = false;
   b->kc_used = false;
   b->dd_used = false;
   for (auto& k : b->kc) {            // this run's entry space (set again by the run's key lists)
@@ -2226,62 +2215,6 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   }
   const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
   const bool vrf = (c->kernels & 4) != 0;
-  // KES in groups of chunks (PRAOS_E2E_KES): group j = chunks [gc[j], gc[j + 1])
-  const int ekes = (c->kernels & 2) && c->keycache > 0 && n >= 2 ? std::min(c->e2e_kes, K) : 0;
-  hipStream_t sk = c->concurrent ? c->side[1] : c->stream;
-  hipStream_t sm1 = c->concurrent ? c->mside[1] : c->stream;
-  std::vector<int> gc(ekes + 1);
-  for (int j = 0; j <= ekes; j++) gc[j] = ekes ? K * j / ekes : 0;
-  if (ekes) {
-    if (b->chunk_list_n < n) {
-      const size_t cap = std::max(n, b->cap_n);
-      if (dalloc(b, &b->chunk_list, 4 * cap) != hipSuccess || dalloc(b, &b->chunk_cnt, 4 * PIPE_MAX) != hipSuccess)
-        return PRAOS_E_OOM;
-      b->h_iota.resize(cap);
-      for (size_t i = 0; i < cap; i++) b->h_iota[i] = (uint32_t)i;
-      HIPCHK(c, hipMemcpyAsync(b->chunk_list, b->h_iota.data(), 4 * cap, hipMemcpyHostToDevice, c->cstream));
-      b->chunk_list_n = cap;
-    }
-    for (int j = 0; j < ekes; j++) b->h_cnt[j] = (uint32_t)(lo[gc[j + 1]] - lo[gc[j]]);
-    HIPCHK(c, hipMemcpyAsync(b->chunk_cnt, b->h_cnt, 4 * PIPE_MAX, hipMemcpyHostToDevice, c->cstream));
-  }
-  // group j's pass, as batch_run_impl's over the whole batch: leaf keys, the cache lists over the
-  // group's headers, the misses per lane on the miss stream, the hits' key tables and k_kes_ck.
-  // The groups share the batch's leaf-key cache in order on sk (the next group's lists wait for
-  // this group's misses too).
-  auto kes_group = [&](int j) -> int {
-    const praos_params& P = c->params;
-    const size_t i0 = lo[gc[j]], m = lo[gc[j + 1]] - i0;
-    HIPCHK(c, hipStreamWaitEvent(sk, c->done_ev[gc[j + 1] - 1], 0));
-    if (j > 0 && sm1 != sk) HIPCHK(c, hipStreamWaitEvent(sk, c->miss_ev[4], 0));
-    if (m == 0) return PRAOS_OK;
-    praos_batch::KeyCache& k = b->kc[2];
-    const dim3 g(nblocks(m, NT)), blk(NT);
-    launch_kes_leafkeys(g, blk, sk, m, b->kes_sig + 448 * i0, b->slot + i0, b->ocert_c0 + i0,
-                        P.slots_per_kes_period, b->kes_leaf + 32 * i0);
-    int r = kc_lists(c, k, m, b->kes_leaf, sk, b->chunk_list + i0, b->chunk_cnt + j, 2);
-    if (r != PRAOS_OK) return r;
-    if (sm1 != sk) {
-      HIPCHK(c, hipEventRecord(c->miss_ev[1], sk));
-      HIPCHK(c, hipStreamWaitEvent(sm1, c->miss_ev[1], 0));
-    }
-    if (c->use_miss4(n))
-      launch_kes4(g, blk, sm1, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
-                  b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, b->bits3 + n, b->tab_kes,
-                  c->miss_prio >= 0 ? c->miss_prio : 1);
-    else
-      launch_kes(g, blk, sm1, m, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
-                 b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, (const uint32_t*)nullptr,
-                 b->bits3 + n, (uint8_t*)nullptr, b->tab_kes);
-    if (sm1 != sk) HIPCHK(c, hipEventRecord(c->miss_ev[4], sm1));
-    kc_precompute(c, k, b->kes_leaf, 0, sk, n);
-    const dim3 gl(nblocks(m, lat_block(n))), bl(lat_block(n));
-    launch_kes_ck(gl, bl, sk, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, b->hot_vk, b->kes_sig,
-                  b->body_off, b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
-                  b->bits3 + n, c->kes_pair_min(), nullptr, nullptr, 0);
-    return hipGetLastError() == hipSuccess ? PRAOS_OK : PRAOS_E_HIP;
-  };
-  int kg = 0;                                    // the next KES group to queue
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
@@ -2309,18 +2242,12 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
                    b->vrf_mid, lo[k], lo[k + 1], 0, 0, c->v_ilp4(n));
       HIPCHK(c, hipGetLastError());
     }
-    if (kg < ekes && k + 1 == gc[kg + 1]) {
-      const int r = kes_group(kg++);
-      if (r != PRAOS_OK) return r;
-    }
   }
   b->decoded = true;
   b->v_done = vrf;
-  b->kes_done = ekes != 0;
   int r = praos_batch_run(c, b);
   b->decoded = false;                // (the downloads below still read b->n; the next call resets
   b->v_done = false;                 // every per-run field when it takes the batch: batch_reuse_reset)
-  b->kes_done = false;
   // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
   // header) are final once the VRF stream is done: they come back while KES still runs
   if (r == PRAOS_OK && c->concurrent) {

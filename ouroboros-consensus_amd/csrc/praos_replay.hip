@@ -314,7 +314,11 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   }
   struct Slot {
     praos_batch* b = nullptr;
-    int state = 0;                            // 0 free, 1 decoded, 2 nonces known, 3 crypto queued
+    int state = 0;                            // 0 free, 1 decoded
+    uint64_t batch = UINT64_MAX;              // the batch it holds (state 1)
+    bool chained = false;                     // the nonce chain has been over it (etas, eidx, evol)
+    bool launched = false;                    // its crypto is queued
+    bool early = false;                       // ... with the launcher's etas_l / eidx_l (PRAOS_REPLAY_EARLY)
     size_t n = 0;
     int view = 0;                             // its ledger view (a batch never spans two)
     uint64_t index0 = 0;
@@ -324,7 +328,8 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     std::vector<uint32_t> len, bsize;
     std::vector<uint8_t> prev, gen, cold, hh, nonce, v, eidx;
     std::vector<uint16_t> dstat, fails;
-    std::vector<praos_nonce> etas, evol;
+    std::vector<praos_nonce> etas, evol, etas_l;
+    std::vector<uint8_t> eidx_l;
     uint16_t* bits = nullptr;                 // pinned
     int32_t* pidx = nullptr;                  // pinned
     size_t pin_cap = 0;
@@ -347,6 +352,17 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     cv.notify_all();
   };
   double t_io = 0, t_dev = 0, t_wait = 0, t_nonce = 0, t_fold = 0;   // per thread: reader | fold
+  // per-batch stage timeline (PRAOS_REPLAY_TRACE=<file>: one line per stage of each batch, "batch
+  // stage start_ms end_ms headers", appended when the replay ends); one event list per thread
+  struct Ev { uint64_t k; const char* what; double t0, t1; size_t n; };
+  const char* trace_path = std::getenv("PRAOS_REPLAY_TRACE");
+  const auto t_base = std::chrono::steady_clock::now();
+  std::vector<Ev> ev_reader, ev_chain, ev_launch, ev_fold;
+  auto ev_add = [&](std::vector<Ev>& v, uint64_t k, const char* what, std::chrono::steady_clock::time_point t0,
+                    size_t n) {
+    if (trace_path)
+      v.push_back({k, what, std::chrono::duration<double, std::milli>(t0 - t_base).count(), ms_since(t_base), n});
+  };
   uint64_t epochs_seen = 0, batches = 0;
   Placement pl;
   pl.init(batch_max);
@@ -365,13 +381,25 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   praos_nonce last_eta{};
   bool have_last = false;
   uint64_t sp_epoch = sp.origin ? 0 : epoch_of(sp.last);
+  // Early launches (PRAOS_REPLAY_EARLY=1): the chain publishes each epoch nonce when it reaches the
+  // epoch's first header (the tick that fixes it), and a decoded batch whose headers all lie in
+  // epochs up to the last published one has its crypto queued at once, beside the chain's pass
+  // over it, instead of after it.  The fold checks every header's nonce against its own tick
+  // (fold_impl), so the launcher's nonces are the chain's or the replay stops.
+  // PRAOS_REPLAY_EARLY=2: only once the reader has decoded the next batch (or there is none), so
+  // the early crypto does not share the GPU with the decode the chain waits for next
+  const char* early_env = std::getenv("PRAOS_REPLAY_EARLY");
+  const int early_mode = early_env ? std::atoi(early_env) : 0;
+  const bool early_on = early_mode != 0;
+  std::vector<std::pair<uint64_t, praos_nonce>> pubs{{sp_epoch, sp.epoch_nonce}};   // (epoch, nonce), mu
+  uint64_t pub_epoch = sp_epoch;                                                      // mu
   std::thread chain([&] {
     if (pl.on) Placement::pin_self(pl.chain());
     for (uint64_t k = 0;; k++) {
       Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 1; });
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k); });
         if (stop || k >= nbatches) return;
       }
       auto t0 = std::chrono::steady_clock::now();
@@ -409,6 +437,12 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
           if (tpraos && extra_entropy) sp.epoch_nonce = praos_host::nonce_combine(sp.epoch_nonce, *extra_entropy);
           sp.leb = sp.lab;
           fresh = true;
+          if (early_on) {
+            std::lock_guard<std::mutex> g(mu);
+            pubs.push_back({e_new, sp.epoch_nonce});
+            pub_epoch = e_new;
+            cv.notify_all();
+          }
         }
         if (fresh) {                              // the epoch nonce changes only at a tick
           if (C.etas.empty() || !praos_host::nonce_eq(C.etas.back(), sp.epoch_nonce)) C.etas.push_back(sp.epoch_nonce);
@@ -433,8 +467,9 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       for (const praos_nonce& e : C.etas)
         if (!have_last || !praos_host::nonce_eq(e, last_eta)) { epochs_seen++; last_eta = e; have_last = true; }
       t_nonce += ms_since(t0);
+      ev_add(ev_chain, k, "chain", t0, n);
       std::lock_guard<std::mutex> g(mu);
-      C.state = 2;
+      C.chained = true;
       cv.notify_all();
     }
   });
@@ -451,8 +486,63 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 2; });
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k); });
         if (stop || k >= nbatches) return;
+      }
+      // the batch's last epoch (decoded slots; a header that did not decode may carry any slot:
+      // the batch then waits for the chain)
+      uint64_t e_max = 0;
+      if (early_on) {
+        uint64_t lo = 1, hi = 0;
+        for (size_t i = 0; i < C.n; i++) {
+          const uint64_t s = C.slot[i];
+          if (s < lo || s >= hi) {
+            const uint64_t e = epoch_of(s);
+            e_max = std::max(e_max, e);
+            lo = s < ei->epoch_base_slot ? 0 : ei->epoch_base_slot + (e - ei->epoch_base_no) * ei->epoch_length;
+            hi = s < ei->epoch_base_slot ? ei->epoch_base_slot : lo + ei->epoch_length;
+          }
+        }
+      }
+      std::vector<std::pair<uint64_t, praos_nonce>> pub;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        auto next_decoded = [&] {
+          if (early_mode != 2) return true;
+          if (nbatches != UINT64_MAX && k + 1 >= nbatches) return true;
+          const Slot& N = S[(k + 1) % T];
+          return T > 1 && N.state == 1 && N.batch == k + 1;
+        };
+        cv.wait(g, [&] { return stop || C.chained || (early_on && e_max <= pub_epoch && next_decoded()); });
+        if (stop) return;
+        C.early = !C.chained;
+        if (C.early) pub = pubs;
+      }
+      if (C.early) {
+        // each header's nonce: the last one published for an epoch <= its own (the nonce changes
+        // only at the tick into an epoch that has headers)
+        C.etas_l.clear();
+        C.eidx_l.resize(C.n);
+        size_t j = 0;
+        uint64_t lo = 1, hi = 0, e = 0;
+        for (size_t i = 0; i < C.n; i++) {
+          const uint64_t s = C.slot[i];
+          if (s < lo || s >= hi) {
+            e = epoch_of(s);
+            lo = s < ei->epoch_base_slot ? 0 : ei->epoch_base_slot + (e - ei->epoch_base_no) * ei->epoch_length;
+            hi = s < ei->epoch_base_slot ? ei->epoch_base_slot : lo + ei->epoch_length;
+          }
+          while (j + 1 < pub.size() && pub[j + 1].first <= e) j++;
+          while (j > 0 && pub[j].first > e) j--;
+          const praos_nonce& eta = pub[j].second;
+          if (C.etas_l.empty() || !praos_host::nonce_eq(C.etas_l.back(), eta)) C.etas_l.push_back(eta);
+          C.eidx_l[i] = (uint8_t)std::min<size_t>(C.etas_l.size() - 1, 255);
+        }
+        if (C.etas_l.size() > 256) {
+          praos_set_error_(ctx, "replay: > 256 epochs in a batch");
+          fail(PRAOS_E_STATE);
+          return;
+        }
       }
       if (views && cur_view[k % (uint64_t)m] != C.view) {
         // the member's launches from here on read this view's pool tables (queued kernels of
@@ -472,11 +562,14 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         }
         cur_view[q] = C.view;
       }
-      const int rc = rp_run(member(k), C.b, C.etas.data(), (uint32_t)C.etas.size(), C.eidx.data());
+      const auto t0 = std::chrono::steady_clock::now();
+      const std::vector<praos_nonce>& etas = C.early ? C.etas_l : C.etas;
+      const int rc = rp_run(member(k), C.b, etas.data(), (uint32_t)etas.size(), (C.early ? C.eidx_l : C.eidx).data());
+      ev_add(ev_launch, k, "launch", t0, C.n);
       if (rc != PRAOS_OK && member(k) != ctx) praos_set_error_(ctx, praos_last_error(member(k)));
       if (rc != PRAOS_OK) { fail(rc); return; }
       std::lock_guard<std::mutex> g(mu);
-      C.state = 3;
+      C.launched = true;
       batches++;
       cv.notify_all();
     }
@@ -490,7 +583,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || C.state == 3; });
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k && C.chained && C.launched); });
         if (stop || k >= nbatches) return;
       }
       auto t0 = std::chrono::steady_clock::now();
@@ -501,6 +594,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         return;
       }
       t_wait += ms_since(t0);
+      ev_add(ev_fold, k, "wait", t0, C.n);
       t0 = std::chrono::steady_clock::now();
       const size_t n = C.n;
       C.v.resize(n);
@@ -521,14 +615,16 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         env->max_header_size = V[C.view].maxh;
         env->max_body_size = V[C.view].maxb;
       }
-      rc = rp_fold(ctx, &h, C.prev.data(), C.gen.data(), &out, env, ei, st, C.etas.data(), (uint32_t)C.etas.size(),
-                   C.eidx.data(), C.evol.data(), tpraos, extra_entropy, C.v.data(), C.fails.data(), &stp, &done,
-                   views ? hv[C.view].get() : nullptr);
+      const std::vector<praos_nonce>& etas = C.early ? C.etas_l : C.etas;   // the nonces its crypto ran with
+      rc = rp_fold(ctx, &h, C.prev.data(), C.gen.data(), &out, env, ei, st, etas.data(), (uint32_t)etas.size(),
+                   (C.early ? C.eidx_l : C.eidx).data(), C.evol.data(), tpraos, extra_entropy, C.v.data(),
+                   C.fails.data(), &stp, &done, views ? hv[C.view].get() : nullptr);
       env->block_no = nullptr;
       env->header_hash = nullptr;
       env->header_size = nullptr;
       env->body_size = nullptr;
       t_fold += ms_since(t0);
+      ev_add(ev_fold, k, "fold", t0, C.n);
       if (rc != PRAOS_OK) { fail(rc); return; }
       for (size_t j = 0; j < done && C.index0 + j < verdicts_cap; j++) {
         verdicts[C.index0 + j] = C.v[j];
@@ -551,6 +647,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         headers_done = C.index0 + n;
       }
       C.state = 0;
+      C.chained = C.launched = C.early = false;
       cv.notify_all();
     }
   });
@@ -576,7 +673,9 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     size_t arena = 0;
     const Chunk* span_chunk = nullptr;
     // the first batch is a quarter of the others: the nonce chain (the replay's sequential
-    // part) starts as soon as possible
+    // part) starts as soon as possible.  (A geometric ramp from batch_max / 8 up by 1.4x per batch
+    // was measured slower, 84 -> 132 ms on the C5 chain: many small crypto steps,
+    // profiles/r06/g_replay.)
     const size_t cap = k == 0 ? std::max<size_t>(1, batch_max / 4) : batch_max;
     bool no_view = false;
     while (C.off.size() < cap && rd.peek(&p, &l, &s)) {
@@ -607,6 +706,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       rd.pop();
     }
     t_io += ms_since(t0);
+    ev_add(ev_reader, k, "read", t0, C.off.size());
     if (!rd.err.empty()) { praos_set_error_(ctx, rd.err); fail(PRAOS_E_ARG); break; }
     if (no_view && C.off.empty()) {
       praos_set_error_(ctx, "replay: no ledger view for epoch " + std::to_string(epoch_of(s)));
@@ -647,6 +747,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     dec.body_size = C.bsize.data(); dec.ocert_n = C.ocn.data(); dec.header_hash = C.hh.data();
     if (rc == PRAOS_OK) rc = rp_download_decoded(mc, C.b, &dec, C.nonce.data());
     t_dev += ms_since(t0);
+    ev_add(ev_reader, k, "decode", t0, n);
     if (rc != PRAOS_OK) {
       if (mc != ctx) praos_set_error_(ctx, praos_last_error(mc));
       fail(rc);
@@ -654,6 +755,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     }
     std::lock_guard<std::mutex> g(mu);
     C.state = 1;
+    C.batch = k;
     built = k + 1;
     cv.notify_all();
   }
@@ -683,6 +785,14 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   for (int q = 0; q < m; q++) {
     rp_tables_set(mem[q], own[q]);
     for (rp_view* t : dev_views[q]) rp_view_free(mem[q], t);
+  }
+  if (trace_path) {
+    if (FILE* f = std::fopen(trace_path, "a")) {
+      for (const auto* v : {&ev_reader, &ev_chain, &ev_launch, &ev_fold})
+        for (const Ev& e : *v) std::fprintf(f, "%llu %s %.3f %.3f %zu\n", (unsigned long long)e.k, e.what, e.t0, e.t1, e.n);
+      std::fprintf(f, "end - 0 %.3f 0\n", ms_since(t_base));
+      std::fclose(f);
+    }
   }
   stats->ms_io = t_io;
   stats->ms_device = t_dev + t_wait;

@@ -188,15 +188,11 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
     assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT
 
 
-@pytest.mark.parametrize("env", [{"PRAOS_E2E_KES": "1"}, {"PRAOS_E2E_KES": "2"}, {"PRAOS_E2E_KES": "8"},
-                                 {"PRAOS_PRE_JOIN": "0"}, {"PRAOS_PRE_JOIN": "1"}])
+@pytest.mark.parametrize("env", [{"PRAOS_PRE_JOIN": "0"}, {"PRAOS_PRE_JOIN": "1"}])
 def test_schedule_variants_equal_single_batch(ctx, c5_batch, env):
     """Schedule options that move work between kernels and streams give the default context's
-    one-batch outputs bit for bit: the stored-bytes pipeline with the KES checks (leaf-key cache)
-    run in 1, 2 or 8 groups of chunks, each once its chunks have landed (PRAOS_E2E_KES), and the
-    join's pool part ahead of
-    it as k_vrf_pool (PRAOS_PRE_JOIN, default on below SMALL_BATCH headers) -- in one batch and
-    pipelined (8 chunks)."""
+    one-batch outputs bit for bit: the join's pool part ahead of it as k_vrf_pool (PRAOS_PRE_JOIN,
+    default on below SMALL_BATCH headers) or in the join -- in one batch and pipelined (8 chunks)."""
     import praos_hip
     from praos_hip import abi
     cfg, H, pool_list, corrupted, p, arena, off, ln = c5_batch

@@ -512,3 +512,48 @@ def test_reused_batches_alternate_replay_and_pipeline(chain):
                 assert int((o["bits"] != 0).sum()) == 0, step
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("env", [{"PRAOS_REPLAY_EARLY": "1"}, {"PRAOS_REPLAY_EARLY": "2"},
+                                 {"PRAOS_REPLAY_PIN": "1"}, {"PRAOS_CSTREAM_PRIO": "1"}])
+def test_replay_schedule_options_equal_default(ctx, chain, tmp_path, monkeypatch, env):
+    """Host-schedule options of the replay give the default replay's stats, verdicts, state and tip:
+    crypto launched as soon as the batch's epoch nonces are published (PRAOS_REPLAY_EARLY 1; 2: and
+    the next batch decoded), pinned threads (PRAOS_REPLAY_PIN), the copy / decode stream at the
+    greatest priority (PRAOS_CSTREAM_PRIO, read when a context opens) -- over the
+    clean 4-epoch database (one context, 97-header batches; a 3-member group) and over one damaged
+    in epoch 2 (the stop, its verdict and the state before it)."""
+    from praos_hip import abi
+    k = int(np.nonzero(chain["slots"] >= 2 * EPOCH_LEN)[0][5])
+    db = _copy_db(chain, tmp_path, "bad")
+    fname, pos = _locate(chain, k)
+    raw = bytearray(open(os.path.join(db, fname), "rb").read())
+    raw[pos + int(chain["len"][k]) - 100] ^= 0x40                   # a KES signature byte
+    open(os.path.join(db, fname), "wb").write(bytes(raw))
+    base = [_replay(ctx, chain, batch_max=97), _replay(ctx, chain, batch_max=1 << 16), _replay(ctx, chain, path=db)]
+    with abi.Group([0] * 3) as g:
+        gbase = _group_replay(g, chain, batch_max=61)
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    import praos_hip
+    c2 = praos_hip.Context(0)                                            # (context-open settings)
+    try:
+        got = [_replay(c2, chain, batch_max=97), _replay(c2, chain, batch_max=1 << 16), _replay(c2, chain, path=db)]
+    finally:
+        c2.close()
+    with abi.Group([0] * 3) as g:
+        ggot = _group_replay(g, chain, batch_max=61)
+    for a, b in list(zip(base, got)) + [(gbase, ggot)]:
+        _same_replay(a, b)
+    assert got[2][0]["stop_index"] == k and got[2][0]["stop_verdict"] == abi.V_KES_SIG
+    assert got[0][2] == chain["state"] and ggot[2] == chain["state"]
+
+
+def test_tpraos_replay_early_launch_equals_default(ctx, tchain, monkeypatch):
+    """TPraos replay with early launches (the published epoch nonces carry TICKN's extra entropy):
+    the default replay's stats, verdicts, failure sets and state."""
+    a = _tp_replay(ctx, tchain, batch_max=61)
+    monkeypatch.setenv("PRAOS_REPLAY_EARLY", "1")
+    b = _tp_replay(ctx, tchain, batch_max=61)
+    assert {k: v for k, v in a[0].items() if k not in _TIMES} == {k: v for k, v in b[0].items() if k not in _TIMES}
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3] == tchain["state"]

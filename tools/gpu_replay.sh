@@ -10,12 +10,12 @@ mkdir -p $O
 SIN=""
 [ -f ouroboros-consensus_amd/praos_hip/data/c5_epoch1_schedule.npz ] && SIN="--schedule-in 1=ouroboros-consensus_amd/praos_hip/data/c5_epoch1_schedule.npz"
 timeout -k 10 1100 python3 -u tools/replay_bench.py --chain c5 --epochs 2 --pools 3000 --epoch-length 8640000 \
-  --batch-sizes ${BATCHES:-48000,96000} --members ${MEMBERS:-1,2} --reps 3 --schedule-out $O/sched $SIN \
+  --batch-sizes ${BATCHES:-48000,96000} --members ${MEMBERS:-1,2} --reps ${REPS:-3} --schedule-out $O/sched $SIN \
   --env-variants "${VARIANTS:-PRAOS_REPLAY_PIN=0,PRAOS_COPY_THREADS=16;PRAOS_REPLAY_PIN=1,PRAOS_COPY_THREADS=16;PRAOS_REPLAY_PIN=0,PRAOS_COPY_THREADS=8;PRAOS_REPLAY_PIN=1,PRAOS_COPY_THREADS=8;PRAOS_REPLAY_PIN=1,PRAOS_COPY_THREADS=4}" \
   > $O/replay.jsonl 2> $O/replay.err || { echo REPLAYFAIL; tail -30 $O/replay.err; exit 1; }
 cat $O/host_cpus.txt
 python3 -c "
 import json
 for l in open('$O/replay.jsonl'):
-    d = json.loads(l); print(d['host_settings'], d['members'], d['batch_max'], d['value'], d['wall_ms'], d['stages_ms'])
+    d = json.loads(l); print(d['host_settings'], d['members'], d['batch_max'], d['value'], d['wall_ms'], d.get('walls_ms'), d['stages_ms'])
 "

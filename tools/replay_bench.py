@@ -116,7 +116,10 @@ def main():
                                         data["header_hash"], args.chunk_slots)
         from praos_hip import abi
         variants = [v for v in args.env_variants.split(";")] if args.env_variants else [""]
+        env0 = dict(os.environ)
         for variant in variants:
+         os.environ.clear()                                                       # each variant on its own
+         os.environ.update(env0)
          for item in filter(None, variant.split(",")):
              k, v = item.split("=")
              os.environ[k] = v
@@ -144,6 +147,7 @@ def main():
                           "value": round(n / (best["wall_ms"] * 1e-3), 1), "unit": "headers/s", "headers": n,
                           "epochs": args.epochs, "blocks_per_epoch": round(n / args.epochs), "chunks": nch,
                           "pools": args.pools, "wall_ms": round(best["wall_ms"], 2),
+                          "walls_ms": [round(r["wall_ms"], 2) for r in runs],
                           "schedule": "round-robin, f = 1" if args.round_robin else "first-leader-wins, f = 1/20",
                           "chain": args.chain or "replay-bench", "pool_keys": mode, "members": members,
                           "stages_ms": {k: round(best[k], 2) for k in ("ms_io", "ms_device", "ms_nonce", "ms_fold")},
@@ -153,6 +157,8 @@ def main():
                   print(json.dumps(line), flush=True)
           runner.set_option(abi.OPT_POOL_KEYS, -1)
           runner.close()
+    os.environ.clear()
+    os.environ.update(env0)
     ctx.close()
 
 
