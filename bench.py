@@ -132,6 +132,54 @@ def host_cores():
     return usable, os.cpu_count() or 1, model
 
 
+def smt_topology():
+    """(physical cores, [(cpu, its SMT sibling)]) of the CPUs in this job's mask, from sysfs."""
+    try:
+        mask = sorted(os.sched_getaffinity(0))
+        cores, pairs = set(), []
+        for c in range(os.cpu_count() or 0):
+            base = f"/sys/devices/system/cpu/cpu{c}/topology"
+            cores.add((open(f"{base}/physical_package_id").read().strip(), open(f"{base}/core_id").read().strip()))
+        for c in mask:
+            sib = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+            parts = [int(x) for x in sib.replace("-", ",").split(",") if x]
+            other = [x for x in parts if x != c and x in mask]
+            if other:
+                pairs.append((c, other[0]))
+        return len(cores), pairs
+    except (OSError, ValueError):
+        return None, []
+
+
+def smt_pair_rate(kind, S, eta0, pool_list, p, spkp, cpus):
+    """Items/s of two one-thread CPU twins run at once, each thread pinned to one of `cpus` (its
+    twin opened after the pin, so the twin's threads inherit it)."""
+    import threading
+    from praos_hip import cpu as C
+    res, barrier = [None, None], threading.Barrier(2)
+
+    def run(j):
+        os.sched_setaffinity(0, {cpus[j]})
+        tw = C.CpuContext(1)
+        tw.set_epoch(eta0, pool_list, p)
+        _twin_run(tw, kind, _sample(S, np.arange(16)), eta0, pool_list, p, spkp)
+        barrier.wait()
+        t = time.perf_counter()
+        _twin_run(tw, kind, S, eta0, pool_list, p, spkp)
+        res[j] = time.perf_counter() - t
+        tw.close()
+    mask = os.sched_getaffinity(0)
+    try:
+        th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        os.sched_setaffinity(0, mask)
+    return 2 * len(S["slot"]) / max(res)
+
+
 def _hdr_dict(H, i):
     off, ln = int(H["body_off"][i]), int(H["body_len"][i])
     return {"slot": int(H["slot"][i]), "cold_vk": bytes(H["cold_vk"][i]), "vrf_vk": bytes(H["vrf_vk"][i]),
@@ -282,6 +330,23 @@ def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, sec
     _twin_run(twin, kind, _sample(H, idx[:n1]), eta0, pool_list, p, spkp)
     t1 = time.perf_counter() - t1
     twin.close()
+    # SMT: two one-thread twins on the two hardware threads of one core against two on two cores
+    # (the all-cores estimate counts physical cores x the rate of a core running both threads)
+    smt = None
+    phys, pairs = smt_topology()
+    if kind == "header" and phys and len(pairs) >= 2:
+        a, b = pairs[-1]
+        c2 = next((x for x, _ in pairs if x not in (a, b)), None)
+        if c2 is not None:
+            S2 = _sample(H, idx[: max(16, int(1.5 / per_item))])
+            pair = smt_pair_rate(kind, S2, eta0, pool_list, p, spkp, (a, b))
+            two = smt_pair_rate(kind, S2, eta0, pool_list, p, spkp, (a, c2))
+            smt = {"physical_cores": phys, "pair_cpus": [a, b], "two_core_cpus": [a, c2],
+                   "two_threads_one_core": round(pair, 1), "two_threads_two_cores": round(two, 1),
+                   "smt_gain": round(pair / (two / 2), 3),
+                   "all_cores_smt_estimate": round(phys * (n1 / t1) * pair / (two / 2), 1),
+                   "note": "two one-thread twins at once, pinned to the sibling hardware threads of one core "
+                           "vs to two cores; estimate = physical cores x single-thread rate x smt_gain"}
     # the oracle (checker) on a sub-sample, in a process pool
     sub = idx[:: max(1, n_sample // 2000)]
     items = [_hdr_dict(H, i) for i in sub]
@@ -306,6 +371,7 @@ def cpu_baseline(kind, H, gpu_bits, eta0, c_raw, p, spkp, maxevo, pool_list, sec
                       f"(C++, radix-2^51, sliding-window Straus, same ABI) on {threads} threads, {busy:.2f}s",
             "single_core": round(single, 1),
             "all_cores_linear_estimate": round(single * nproc, 1),
+            **({"smt": smt} if smt else {}),
             "host": {"cpu_model": model, "nproc": nproc, "usable_cores": usable,
                      "threads_used": threads, "note": "threads capped at the box's CPU share (16 per GPU)"},
             "parity_sample": {"n": n_sample, "bit_exact_twin_vs_gpu": agree,
@@ -716,6 +782,15 @@ def main():
                     "vs_cpu_all_cores": round(8 * proxy["n8"]["value"] / allc, 1),
                     "note": "8 x strong_proxy.n8.value (each GPU validating its contiguous 1/8 of the epoch, no "
                             "exchange) / cpu_baseline.all_cores_linear_estimate"}
+                smt = line["cpu_baseline"].get("smt")
+                if smt:
+                    # the same against the measured SMT estimate (physical cores x one core's rate with both
+                    # hardware threads busy): the linear estimate counts each hardware thread as a core
+                    line["projected_8gpu_strong"]["vs_cpu_all_cores_smt"] = round(
+                        8 * proxy["n8"]["value"] / smt["all_cores_smt_estimate"], 1)
+            smt = line["cpu_baseline"].get("smt")
+            if smt:
+                line["gpu_vs_cpu_all_cores_smt"] = round(value / smt["all_cores_smt_estimate"], 1)
     print(json.dumps(line), flush=True)
     ctx.close()
     if dist:

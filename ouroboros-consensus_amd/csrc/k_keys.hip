@@ -34,11 +34,11 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t k[8]) {
 
 // Items: i in [0, n), or list[0 .. *count) (e.g. the distinct OCerts of k_ocert_dedup).
 // pentry != null: the pool-key store (pkey: 8 words per slot, pentry: entry or -1); an item
-// whose key is stored gets item_slot = -2 - entry.
+// whose key is stored gets item_slot = -2 - entry and counts one use of that entry (scnt).
 __global__ void k_key_insert(size_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                              const uint8_t* __restrict__ keys, uint32_t mask, uint32_t* slot_rep,
                              uint32_t* slot_cnt, int32_t* __restrict__ item_slot, const int32_t* __restrict__ pentry,
-                             const uint32_t* __restrict__ pkey, uint32_t pmask) {
+                             const uint32_t* __restrict__ pkey, uint32_t pmask, uint32_t* __restrict__ scnt) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (list ? (size_t)*count : n)) return;
   const size_t i = list ? list[t] : t;
@@ -54,6 +54,7 @@ __global__ void k_key_insert(size_t n, const uint32_t* __restrict__ list, const 
       for (int q = 0; q < 8; q++) same &= pkey[8 * (size_t)g + q] == k[q];
       if (same) {
         item_slot[i] = -2 - e;
+        atomicAdd(&scnt[e], 1u);
         return;
       }
       g = (g + 1u) & pmask;
@@ -121,6 +122,28 @@ __global__ void k_key_assign(uint32_t cap, const uint32_t* __restrict__ slot_rep
   if (in) slot_entry[h] = e;
 }
 
+// The stored entries' hit-list ranges, after the new keys' (counters[3] is their end once
+// k_key_assign is done): spos[e] = the start of entry e's range (scnt[e] uses this run), so the
+// stored keys' hits are grouped by key as the new keys' are.
+__global__ void k_key_store_ranges(uint32_t entries, const uint32_t* __restrict__ scnt, uint32_t* __restrict__ spos,
+                                   uint32_t* counters) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t cnt = e < entries ? scnt[e] : 0u;   // every lane stays for the scan
+  const uint32_t lane = __lane_id();
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  const uint32_t total = __shfl(incl, 63);
+  if (total == 0) return;
+  uint32_t p_base = 0;
+  if (lane == 0) p_base = atomicAdd(&counters[3], total);
+  p_base = __shfl(p_base, 0);
+  if (cnt) spos[e] = p_base + incl - cnt;
+}
+
 // appends i to list (wave-aggregated atomic: one atomic per wave and list)
 __device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t* counter, uint32_t* list) {
   const uint64_t m = __ballot(pred);
@@ -136,13 +159,13 @@ __device__ __forceinline__ void wave_append(bool pred, uint32_t value, uint32_t*
   }
 }
 
-// Stored keys' items (item_slot <= -2) are hits too; they go after the new keys' ranges
-// (counters[3] is the end of those once k_key_assign is done).
+// Stored keys' items (item_slot <= -2) are hits too; they go to their entry's range after the
+// new keys' ranges (k_key_store_ranges).
 __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                 const int32_t* __restrict__ item_slot, const int32_t* __restrict__ slot_entry,
                                 int32_t* __restrict__ item_entry, uint32_t* __restrict__ entry_pos,
                                 uint32_t* __restrict__ hit_list, uint32_t* __restrict__ miss_list,
-                                uint32_t* counters) {
+                                uint32_t* counters, uint32_t* __restrict__ spos) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = t < (list ? (size_t)*count : n);   // every lane stays for the ballots
   const size_t i = in ? (list ? list[t] : t) : 0;
@@ -150,8 +173,7 @@ __global__ void k_key_partition(size_t n, const uint32_t* __restrict__ list, con
   const bool stored = sl <= -2;
   const int32_t e = !in ? -1 : (stored ? -2 - sl : slot_entry[sl]);
   if (in) item_entry[i] = e;
-  if (in && e >= 0 && !stored) hit_list[atomicAdd(&entry_pos[e], 1u)] = (uint32_t)i;
-  wave_append(in && stored, (uint32_t)i, &counters[3], hit_list);
+  if (in && e >= 0) hit_list[atomicAdd(stored ? &spos[e] : &entry_pos[e], 1u)] = (uint32_t)i;
   const uint64_t hits = __ballot(in && e >= 0);
   if (hits && __lane_id() == (uint32_t)(__ffsll((unsigned long long)hits) - 1))
     atomicAdd(&counters[1], (uint32_t)__popcll(hits));
@@ -297,9 +319,14 @@ __global__ void k_ocert_fanout(size_t n, const uint32_t* __restrict__ item_rep, 
 // ---- host launchers
 void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                        const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot,
-                       const int32_t* pentry, const uint32_t* pkey, uint32_t pmask) {
+                       const int32_t* pentry, const uint32_t* pkey, uint32_t pmask, uint32_t* scnt) {
   hipLaunchKernelGGL(k_key_insert, grid, block, 0, stream, n, list, count, keys, mask, slot_rep, slot_cnt, item_slot,
-                     pentry, pkey, pmask);
+                     pentry, pkey, pmask, scnt);
+}
+void launch_key_store_ranges(hipStream_t stream, uint32_t entries, const uint32_t* scnt, uint32_t* spos,
+                             uint32_t* counters) {
+  hipLaunchKernelGGL(k_key_store_ranges, dim3((entries + 255) / 256), dim3(256), 0, stream, entries, scnt, spos,
+                     counters);
 }
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
@@ -310,9 +337,9 @@ void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, 
 void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list,
                           const uint32_t* count, const int32_t* item_slot, const int32_t* slot_entry,
                           int32_t* item_entry, uint32_t* entry_pos, uint32_t* hit_list, uint32_t* miss_list,
-                          uint32_t* counters) {
+                          uint32_t* counters, uint32_t* spos) {
   hipLaunchKernelGGL(k_key_partition, grid, block, 0, stream, n, list, count, item_slot, slot_entry, item_entry,
-                     entry_pos, hit_list, miss_list, counters);
+                     entry_pos, hit_list, miss_list, counters, spos);
 }
 void launch_key_precompute(int kind, hipStream_t stream, const uint32_t* counters, uint32_t max_entries,
                            const uint32_t* entry_rep, const uint8_t* keys, ge_cached* ktab, uint32_t* kinfo,

@@ -38,14 +38,17 @@ void launch_vrf_ck(dim3 grid, dim3 block, hipStream_t stream, const uint32_t* li
 // pentry / pkey / pmask: the pool-key store probed first (null: none)
 void launch_key_insert(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list, const uint32_t* count,
                        const uint8_t* keys, uint32_t mask, uint32_t* slot_rep, uint32_t* slot_cnt, int32_t* item_slot,
-                       const int32_t* pentry, const uint32_t* pkey, uint32_t pmask);
+                       const int32_t* pentry, const uint32_t* pkey, uint32_t pmask, uint32_t* scnt);
+// stored entries' hit-list ranges (after the new keys'), from their uses this run
+void launch_key_store_ranges(hipStream_t stream, uint32_t entries, const uint32_t* scnt, uint32_t* spos,
+                             uint32_t* counters);
 void launch_key_assign(dim3 grid, dim3 block, hipStream_t stream, uint32_t cap, const uint32_t* slot_rep,
                        const uint32_t* slot_cnt, uint32_t min_count, uint32_t max_entries, int32_t* slot_entry,
                        uint32_t* entry_rep, uint32_t* entry_pos, uint32_t* counters);
 void launch_key_partition(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint32_t* list,
                           const uint32_t* count, const int32_t* item_slot, const int32_t* slot_entry,
                           int32_t* item_entry, uint32_t* entry_pos, uint32_t* hit_list, uint32_t* miss_list,
-                          uint32_t* counters);
+                          uint32_t* counters, uint32_t* spos);
 void launch_ocert_dedup(dim3 grid, dim3 block, hipStream_t stream, size_t n, const uint8_t* cold, const uint8_t* hot,
                         const uint64_t* on, const uint64_t* oc, const uint8_t* sig, uint32_t mask, uint32_t* slot_rep,
                         uint32_t* item_rep, uint32_t* reps, uint32_t* counters);

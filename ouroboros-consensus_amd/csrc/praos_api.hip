@@ -262,11 +262,17 @@ struct praos_ctx {
     uint32_t* kinfo = nullptr;
     int32_t* pentry = nullptr;
     ge_cached* ktab = nullptr;
+    uint32_t *scnt = nullptr, *spos = nullptr;           // per entry: uses this run, start of its hit range
   } pks[2];                                            // [0] cold keys, [1] VRF keys
   int pool_keys = -1;                                  // 1 on, 0 off, -1 on inside praos_replay_immutable*
   bool replaying = false;
   bool pk_on = false;                                  // this run uses the store
   bool pk_reset[2] = {false, false};                   // empty store t before the next run that uses it
+  // (round 6 measured key hints for the stored-bytes pipeline -- each header's cold, VRF and KES
+  // leaf keys read on the host while the chunks upload, the key stores filled from them on the
+  // side streams before the last chunk lands -- bit-exact and slower, 432k e2e 15.7 -> 18.4 ms:
+  // the fill shares the GPU with the chunks' stage V and the tail stays throughput-bound;
+  // profiles/r06/h_e2e_hints.  Removed.)
   // (round 5 measured a per-chunk key prefill in the stored-bytes pipeline -- the landed chunks'
   // cold, KES leaf and VRF keys stored and their tables built while later chunks upload -- in two
   // forms, both slower: the GPU is busy with the chunks' stage V during the upload, so the
@@ -719,7 +725,7 @@ void praos_close(praos_ctx* c) {
   (void)hipFree(c->bcomb16);
   for (auto& ps : c->pks) {
     for (void* q : {(void*)ps.pkey, (void*)ps.count, (void*)ps.base, (void*)ps.entry_rep, (void*)ps.entry_pos,
-                    (void*)ps.kinfo, (void*)ps.pentry, (void*)ps.ktab})
+                    (void*)ps.kinfo, (void*)ps.pentry, (void*)ps.ktab, (void*)ps.scnt, (void*)ps.spos})
       (void)hipFree(q);
   }
   free_spare(c);
@@ -1212,13 +1218,15 @@ static bool ensure_pks(praos_ctx* c, int t, hipStream_t st) {
   ok = ok && hipMalloc(&z.entry_pos, 4 * (size_t)z.cap) == hipSuccess;
   ok = ok && hipMalloc(&z.kinfo, 36 * (size_t)z.cap) == hipSuccess;
   ok = ok && hipMalloc(&z.ktab, KT_BYTES * (size_t)z.cap) == hipSuccess;
+  ok = ok && hipMalloc(&z.scnt, 4 * (size_t)z.cap) == hipSuccess;
+  ok = ok && hipMalloc(&z.spos, 4 * (size_t)z.cap) == hipSuccess;
   ok = ok && hipMemsetAsync(z.pentry, 0xff, 4 * (size_t)z.slots, st) == hipSuccess;
   ok = ok && hipMemsetAsync(z.count, 0, 8, st) == hipSuccess;
   ok = ok && hipMemsetAsync(z.base, 0, 8, st) == hipSuccess;
   if (!ok) {
     (void)hipStreamSynchronize(st);              // (the memsets queued so far) before the frees
     for (void* q : {(void*)z.pkey, (void*)z.count, (void*)z.base, (void*)z.entry_rep, (void*)z.entry_pos,
-                    (void*)z.kinfo, (void*)z.pentry, (void*)z.ktab})
+                    (void*)z.kinfo, (void*)z.pentry, (void*)z.ktab, (void*)z.scnt, (void*)z.spos})
       (void)hipFree(q);
     return false;
   }
@@ -1243,6 +1251,7 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
     ps = &c->pks[which];
     launch_pkey_reset(st, ps->count, ps->pentry, ps->slots, ps->cap / 4 * 3, c->pk_reset[which] ? 1 : 0);
     c->pk_reset[which] = false;
+    HIPCHK(c, hipMemsetAsync(ps->scnt, 0, 4 * (size_t)ps->cap, st));
     HIPCHK(c, hipMemcpyAsync(k.counters, ps->count, 4, hipMemcpyDeviceToDevice, st));
     HIPCHK(c, hipMemcpyAsync(ps->base, ps->count, 4, hipMemcpyDeviceToDevice, st));
     k.kt = ps->ktab; k.ki = ps->kinfo; k.erep = ps->entry_rep; k.epos = ps->entry_pos; k.emax = ps->cap;
@@ -1250,11 +1259,13 @@ static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint
     min_uses = 1;
   }
   launch_key_insert(g, blk, st, n, list, count, keys, k.cap - 1, k.slot_rep, k.slot_cnt, k.item_slot,
-                    ps ? ps->pentry : nullptr, ps ? ps->pkey : nullptr, ps ? ps->slots - 1 : 0u);
+                    ps ? ps->pentry : nullptr, ps ? ps->pkey : nullptr, ps ? ps->slots - 1 : 0u,
+                    ps ? ps->scnt : nullptr);
   launch_key_assign(dim3(nblocks(k.cap, NT)), blk, st, k.cap, k.slot_rep, k.slot_cnt, (uint32_t)min_uses,
                     k.emax, k.slot_entry, k.erep, k.epos, k.counters);
+  if (ps) launch_key_store_ranges(st, ps->cap, ps->scnt, ps->spos, k.counters);
   launch_key_partition(g, blk, st, n, list, count, k.item_slot, k.slot_entry, k.item_entry, k.epos, k.hit, k.miss,
-                       k.counters);
+                       k.counters, ps ? ps->spos : nullptr);
   return PRAOS_OK;
 }
 static void kc_precompute(praos_ctx* c, praos_batch::KeyCache& k, const uint8_t* keys, int kind, hipStream_t st, size_t n) {

@@ -188,11 +188,13 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
     assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT
 
 
-@pytest.mark.parametrize("env", [{"PRAOS_PRE_JOIN": "0"}, {"PRAOS_PRE_JOIN": "1"}])
-def test_schedule_variants_equal_single_batch(ctx, c5_batch, env):
+@pytest.mark.parametrize("env,concurrent", [({"PRAOS_PRE_JOIN": "0"}, 1), ({"PRAOS_PRE_JOIN": "1"}, 1),
+                                            ({"PRAOS_PRE_JOIN": "1"}, 0)])
+def test_schedule_variants_equal_single_batch(ctx, c5_batch, env, concurrent):
     """Schedule options that move work between kernels and streams give the default context's
     one-batch outputs bit for bit: the join's pool part ahead of it as k_vrf_pool (PRAOS_PRE_JOIN,
-    default on below SMALL_BATCH headers) or in the join -- in one batch and pipelined (8 chunks)."""
+    default on below SMALL_BATCH headers) or in the join, on concurrent streams and on one -- in one
+    batch and pipelined (8 chunks, twice)."""
     import praos_hip
     from praos_hip import abi
     cfg, H, pool_list, corrupted, p, arena, off, ln = c5_batch
@@ -209,6 +211,7 @@ def test_schedule_variants_equal_single_batch(ctx, c5_batch, env):
         for k in env:
             del os.environ[k]
     try:
+        c2.set_option(abi.OPT_CONCURRENT, concurrent)
         c2.set_epoch(cfg["eta0"], pool_list, p)
         for chunks in (1, 8, 8):                      # the second 8-chunk call reuses the batch
             c2.set_option(abi.OPT_PIPELINE, chunks)
