@@ -118,6 +118,13 @@ static constexpr size_t KEY_PRIO_BATCH = 400000;
 // (profiles/r04/y: 96k 4.06 -> 3.64 ms, 108k 4.25 -> 4.10, 112k 4.39 -> 4.15; equal at 120k,
 // slower at 128k)
 static constexpr size_t ILP4_BATCH = 120000;
+// below this many headers the KES leaf keys are not cached (every KES check uncached, from the
+// ILP-4 build, beside stage V): a 54k-header shard's stage V and uncached KES waves fit in one
+// round of wave slots (2 per SIMD), and the leaf-key chain -- lists, precompute, tables, k_kes_ck,
+// the step's longest after stage V + join -- is gone (54k 2.44-2.49 -> 2.29-2.37 ms; at 64k the
+// waves no longer fit and it is slower, 2.53 -> 3.05; 80k 2.97 -> 3.47; 108k 3.41 -> 4.59;
+// profiles/r06/i_kes_nocache).  PRAOS_KES_NOCACHE=<headers> overrides (0: always cached).
+static constexpr size_t KES_NOCACHE_BATCH = 58000;
 static constexpr int PIPE_AUTO = 8;                 // chunks in auto mode (round 3, equal chunks: 4 -> 21.9M,
                                                     // 6 -> 23.0M, 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt;
                                                     // round 5 with the first chunk at 1/4 of the others: 6 ->
@@ -235,6 +242,7 @@ struct praos_ctx {
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
   int keycache = 2;                                    // PRAOS_OPT_KEYCACHE (min uses; 0 = off)
+  size_t kes_nocache = KES_NOCACHE_BATCH;              // PRAOS_KES_NOCACHE (see KES_NOCACHE_BATCH)
   int kc_min[3] = {0, 0, 0};                           // per cache (cold, VRF, KES leaf) min uses overriding
                                                        // keycache when > 0 (PRAOS_KC_MIN="c,v,k")
   int dedup = 1;                                       // PRAOS_OPT_DEDUP
@@ -611,6 +619,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_POOL_KEYS")) (void)praos_set_option(c, PRAOS_OPT_POOL_KEYS, std::atoi(e));
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PRE_JOIN")) c->pre_join = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_KES_NOCACHE")) c->kes_nocache = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
   if (const char* e = std::getenv("PRAOS_KC_MIN")) (void)std::sscanf(e, "%d,%d,%d", &c->kc_min[0], &c->kc_min[1], &c->kc_min[2]);
@@ -1237,6 +1246,9 @@ static bool ensure_pks(praos_ctx* c, int t, hipStream_t st) {
 static int kc_lists(praos_ctx* c, praos_batch::KeyCache& k, size_t n, const uint8_t* keys, hipStream_t st,
                     const uint32_t* list, const uint32_t* count, int which) {
   int min_uses = c->kc_min[which] > 0 ? c->kc_min[which] : c->keycache;
+  // small batches: no KES leaf key is cached (every item a miss, KES_NOCACHE_BATCH); the batch size
+  // is the caller's n (the lists of the KES pass run over every header)
+  if (which == 2 && c->kc_min[2] <= 0 && n < c->kes_nocache) min_uses = INT32_MAX;
   const dim3 g(nblocks(n, NT)), blk(NT);
   k.kt = k.ktab; k.ki = k.kinfo; k.erep = k.entry_rep; k.epos = k.entry_pos; k.emax = k.max_entries;
   k.ebase = nullptr; k.store = -1;
