@@ -222,6 +222,12 @@ void praos_batch_free(praos_ctx* ctx, praos_batch* b);
  * byte; verdicts are identical either way.  1 = on, 0 = off, 2 = on and emptied before the
  * next run.  A store more than 3/4 full is emptied before a run. */
 #define PRAOS_OPT_POOL_KEYS 7
+/* PRAOS_OPT_KES_NOCACHE (default 58000): batches of fewer headers than this check every Sum6KES
+ * leaf signature uncached (no leaf-key cache: the per-lane chains run beside the VRF's stage V,
+ * and the key chain -- lists, precompute, tables -- is not on the step's critical path; the
+ * 1/8-epoch shard of a strong-scaling run is below it).  0 = the cache at every size.  Verdicts
+ * are identical either way. */
+#define PRAOS_OPT_KES_NOCACHE 8
 int praos_set_option(praos_ctx* ctx, int opt, int value);
 /* Key-cache statistics of the last praos_batch_run (after praos_batch_sync):
  * out[0..2] = cold keys cached, OCert items on cached keys, OCert items

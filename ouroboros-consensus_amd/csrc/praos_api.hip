@@ -123,7 +123,8 @@ static constexpr size_t ILP4_BATCH = 120000;
 // round of wave slots (2 per SIMD), and the leaf-key chain -- lists, precompute, tables, k_kes_ck,
 // the step's longest after stage V + join -- is gone (54k 2.44-2.49 -> 2.29-2.37 ms; at 64k the
 // waves no longer fit and it is slower, 2.53 -> 3.05; 80k 2.97 -> 3.47; 108k 3.41 -> 4.59;
-// profiles/r06/i_kes_nocache).  PRAOS_KES_NOCACHE=<headers> overrides (0: always cached).
+// profiles/r06/i_kes_nocache).  PRAOS_OPT_KES_NOCACHE / PRAOS_KES_NOCACHE=<headers> override it
+// (0: always cached).
 static constexpr size_t KES_NOCACHE_BATCH = 58000;
 static constexpr int PIPE_AUTO = 8;                 // chunks in auto mode (round 3, equal chunks: 4 -> 21.9M,
                                                     // 6 -> 23.0M, 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt;
@@ -1826,6 +1827,7 @@ int praos_set_option(praos_ctx* c, int opt, int value) {
   if (opt == PRAOS_OPT_DEDUP) { c->dedup = value != 0; return PRAOS_OK; }
   if (opt == PRAOS_OPT_PIPELINE) { c->pipeline = value < 0 ? 0 : std::min(value, PIPE_MAX); return PRAOS_OK; }
   if (opt == PRAOS_OPT_KES_PAIR) { c->kes_pair = value < 0 ? -1 : value; return PRAOS_OK; }
+  if (opt == PRAOS_OPT_KES_NOCACHE) { c->kes_nocache = value < 0 ? KES_NOCACHE_BATCH : (size_t)value; return PRAOS_OK; }
   if (opt == PRAOS_OPT_POOL_KEYS) {
     c->pool_keys = value < 0 ? -1 : (value != 0);
     if (value == 2) c->pk_reset[0] = c->pk_reset[1] = true;

@@ -358,6 +358,7 @@ def ptr(a, t=u8p):
 
 
 OPT_CONCURRENT, OPT_KERNELS, OPT_KEYCACHE, OPT_DEDUP, OPT_PIPELINE, OPT_KES_PAIR, OPT_POOL_KEYS = 1, 2, 3, 4, 5, 6, 7
+OPT_KES_NOCACHE = 8
 # (praos_set_option, praos_hip.h)
 
 

@@ -131,7 +131,7 @@ def test_option_ids_match_header():
                             "praos_hip.h")).read()
     ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define PRAOS_OPT_([A-Z_]+) (\d+)", hdr)}
     assert ids == {"CONCURRENT": 1, "KERNELS": 2, "KEYCACHE": 3, "DEDUP": 4, "PIPELINE": 5, "KES_PAIR": 6,
-                   "POOL_KEYS": 7}
+                   "POOL_KEYS": 7, "KES_NOCACHE": 8}
     for name, v in ids.items():
         assert getattr(abi, "OPT_" + name) == v, name
     assert "c_set_option p 7" in open(HASKELL).read()

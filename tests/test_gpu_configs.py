@@ -136,6 +136,7 @@ def test_kes_pair_equals_single(ctx):
     odd = False
     try:
         configs.options(ctx, "c4")
+        ctx.set_option(abi.OPT_KES_NOCACHE, 0)        # the leaf-key cache at this size too
         ctx.set_epoch(eta0, pool_list, p)
         for m in range(40_016, 40_000, -1):
             H, corrupted = _first(H0, m), corrupted0[:m]
@@ -160,5 +161,6 @@ def test_kes_pair_equals_single(ctx):
                 break
     finally:
         ctx.set_option(abi.OPT_KES_PAIR, -1)
+        ctx.set_option(abi.OPT_KES_NOCACHE, -1)
         configs.options(ctx, "c5")
     assert odd, "no prefix with an odd hit count"

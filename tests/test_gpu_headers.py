@@ -126,6 +126,7 @@ def test_stream_schedule_equivalence(ctx, oracle):
     outs = []
     try:
         ctx.set_option(abi.OPT_POOL_KEYS, 0)        # per-batch caches: the single-use keys are misses
+        ctx.set_option(abi.OPT_KES_NOCACHE, 0)      # the KES leaf-key cache at this size too
         for conc in (0, 1, 1):
             ctx.set_option(abi.OPT_CONCURRENT, conc)
             o, st, dd = _run_batch(ctx, H, 2, dedup=1, want_dedup_stats=True)
@@ -133,6 +134,7 @@ def test_stream_schedule_equivalence(ctx, oracle):
     finally:
         ctx.set_option(abi.OPT_CONCURRENT, 1)
         ctx.set_option(abi.OPT_POOL_KEYS, -1)
+        ctx.set_option(abi.OPT_KES_NOCACHE, -1)
     assert st["cold_misses"] > 0 and st["vrf_misses"] > 0 and st["kes_misses"] > 0, st
     assert st["cold_hits"] > 0 and st["vrf_hits"] > 0 and st["kes_hits"] > 0, st
     for o in outs[1:]:
