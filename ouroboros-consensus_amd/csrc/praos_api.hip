@@ -303,6 +303,8 @@ struct praos_ctx {
                                                        // profiles/r05/c16_pipe_tail)
   // epoch
   bool have_epoch = false;
+  std::vector<praos_pool> epoch_pools;                 // praos_set_epoch's inputs as installed (a call
+  praos_params epoch_params{};                         // with the same pools and parameters only swaps eta0)
   praos_params params{};
   uint32_t eta0[8] = {0};
   int eta0_neutral = 1;
@@ -525,6 +527,9 @@ struct praos_batch {
   hipEvent_t dec_ev = nullptr, run_ev = nullptr;
   uint32_t* eta_h = nullptr;       // pinned: 9-word entries (nonce, neutral flag)
   uint8_t* eidx_h = nullptr;       // pinned: per-header index
+  uint16_t* res_bits_h = nullptr;  // pinned: the replay's result downloads (bits, pool index), cap_n each
+  int32_t* res_pidx_h = nullptr;
+  uint8_t* dec_h = nullptr;        // pinned: the replay's decoded-field downloads (DEC_H_BYTES per header)
 };
 
 static constexpr size_t KT_BYTES = 16 * 8 * 4 * 32; // per cached key: 16 tables x 8 cached points
@@ -881,6 +886,23 @@ extern "C" {
 int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pools, uint32_t npools,
                     const praos_params* params) {
   if (!c || !params || (npools && !pools) || params->slots_per_kes_period == 0) return PRAOS_E_ARG;
+  // The installed ledger view again (a replay call per batch of epochs, db-analyser's per-epoch
+  // calls under an unchanged PoolDistr): only the epoch nonce changes
+  if (c->have_epoch && c->device >= 0 && npools == c->epoch_pools.size() &&
+      std::memcmp(params, &c->epoch_params, sizeof *params) == 0 &&
+      (npools == 0 || std::memcmp(pools, c->epoch_pools.data(), npools * sizeof *pools) == 0)) {
+    if ((eta0 == nullptr) == c->eta0_neutral && (eta0 == nullptr || std::memcmp(eta0, c->eta0, 32) == 0))
+      return PRAOS_OK;                            // the same nonce too: nothing to change
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // no run in flight reads the old nonce
+    uint32_t e0[8] = {0};
+    if (eta0) std::memcpy(e0, eta0, 32);
+    HIPCHK(c, hipMemcpy(c->d_eta0, e0, 32, hipMemcpyHostToDevice));
+    c->eta0_neutral = eta0 == nullptr;
+    std::memset(c->eta0, 0, 32);
+    if (eta0) std::memcpy(c->eta0, eta0, 32);
+    return PRAOS_OK;
+  }
   // Validate and build every table first; the context is only touched once all of it
   // succeeded (a failed call leaves NO epoch: runs return PRAOS_E_STATE until the next
   // successful praos_set_epoch).
@@ -917,6 +939,8 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
   c->npools = npools;
   c->pools.swap(v.pools);
   c->pool_by_hash.swap(v.by_hash);
+  c->epoch_pools.assign(pools, pools + npools);
+  c->epoch_params = *params;
   c->have_epoch = true;
   return PRAOS_OK;
 }
@@ -2007,8 +2031,17 @@ praos_batch* rp_batch_alloc(praos_ctx* c, size_t n_cap, size_t bytes_cap, bool t
   ok = ok && hipEventRecord(b->run_ev, c->stream) == hipSuccess;     // recorded once: waits on it are defined
   ok = ok && hipHostMalloc((void**)&b->eta_h, 9 * 4 * 256, hipHostMallocDefault) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&b->eidx_h, b->cap_n, hipHostMallocDefault) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&b->res_bits_h, 2 * b->cap_n, hipHostMallocDefault) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&b->res_pidx_h, 4 * b->cap_n, hipHostMallocDefault) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&b->dec_h, DEC_H_BYTES * b->cap_n, hipHostMallocDefault) == hipSuccess;
   if (!ok) { rp_batch_destroy(c, b); return nullptr; }
   return b;
+}
+
+// the batch's pinned result buffers (kept with it between calls: no page-locking per call)
+void rp_batch_results(praos_batch* b, uint16_t** bits, int32_t** pidx) {
+  *bits = b->res_bits_h;
+  *pidx = b->res_pidx_h;
 }
 
 void rp_batch_destroy(praos_ctx* c, praos_batch* b) {
@@ -2020,6 +2053,9 @@ void rp_batch_destroy(praos_ctx* c, praos_batch* b) {
   if (b->run_ev) (void)hipEventDestroy(b->run_ev);
   if (b->eta_h) (void)hipHostFree(b->eta_h);
   if (b->eidx_h) (void)hipHostFree(b->eidx_h);
+  if (b->res_bits_h) (void)hipHostFree(b->res_bits_h);
+  if (b->res_pidx_h) (void)hipHostFree(b->res_pidx_h);
+  if (b->dec_h) (void)hipHostFree(b->dec_h);
   for (void* p : b->owned) (void)hipFree(p);
   delete b;
 }
@@ -2112,23 +2148,40 @@ int rp_upload_decode(praos_ctx* c, praos_batch* b, size_t n, const praos_span* s
   return PRAOS_OK;
 }
 
-int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t* nonce) {
-  if (!c || !b || !d) return PRAOS_E_ARG;
+// The decoded fields into the batch's pinned area (direct DMA, one sync: ten pageable copies
+// with a sync each took ~2-3 ms of the replay's per-batch decode stage); d's pointers and
+// *nonce point into it until the batch's next download
+int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t** nonce) {
+  if (!c || !b || !d || !nonce || !b->dec_h) return PRAOS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = b->n;
-  auto dn = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-    return dst && bytes ? d2h_on(c, dst, src, bytes, c->cstream) : hipSuccess;
+  uint8_t* h = b->dec_h;                          // 8-byte fields first, then 32-byte, 4, 2, 1
+  *d = praos_decoded{};
+  d->block_no = (uint64_t*)h; h += 8 * n;
+  d->slot = (uint64_t*)h; h += 8 * n;
+  d->ocert_n = (uint64_t*)h; h += 8 * n;
+  d->prev_hash = h; h += 32 * n;
+  d->cold_vk = h; h += 32 * n;
+  d->header_hash = h; h += 32 * n;
+  *nonce = h; h += 32 * n;
+  d->body_size = (uint32_t*)h; h += 4 * n;
+  d->status = (uint16_t*)h; h += 2 * n;
+  d->prev_is_genesis = h;
+  if (n == 0) return PRAOS_OK;
+  auto dn = [&](void* dst, const void* src, size_t bytes) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->cstream);
   };
-  HIPCHK(c, dn(d->status, b->dec_status, 2 * n));
   HIPCHK(c, dn(d->block_no, b->block_no, 8 * n));
   HIPCHK(c, dn(d->slot, b->slot, 8 * n));
-  HIPCHK(c, dn(d->prev_hash, b->prev_hash, 32 * n));
-  HIPCHK(c, dn(d->prev_is_genesis, b->prev_genesis, n));
-  HIPCHK(c, dn(d->cold_vk, b->cold_vk, 32 * n));
-  HIPCHK(c, dn(d->body_size, b->body_size, 4 * n));
   HIPCHK(c, dn(d->ocert_n, b->ocert_n, 8 * n));
+  HIPCHK(c, dn(d->prev_hash, b->prev_hash, 32 * n));
+  HIPCHK(c, dn(d->cold_vk, b->cold_vk, 32 * n));
   HIPCHK(c, dn(d->header_hash, b->header_hash, 32 * n));
-  HIPCHK(c, dn(nonce, b->nonce, 32 * n));
+  HIPCHK(c, dn(*nonce, b->nonce, 32 * n));
+  HIPCHK(c, dn(d->body_size, b->body_size, 4 * n));
+  HIPCHK(c, dn(d->status, b->dec_status, 2 * n));
+  HIPCHK(c, dn(d->prev_is_genesis, b->prev_genesis, n));
+  HIPCHK(c, hipStreamSynchronize(c->cstream));
   return PRAOS_OK;
 }
 

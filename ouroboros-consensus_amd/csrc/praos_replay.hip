@@ -14,15 +14,21 @@
 // one the real fold ticks to.  One ledger view (pools, parameters) for the whole replay.
 // Like the reference, the replay ends at the first invalid header.
 //
-// Four host threads, up to three batches in flight per context:
-//   reader (this thread): chunk files are memory-mapped; a batch's header bytes go straight
-//     from the mappings into the pinned staging buffers (coalesced spans, no host copy of
-//     the chunk), H2D on the copy stream, decode + the nonce value of every certified VRF
-//     output on the device (k_vrf_nonce), and back the decoded fields the chain needs;
+// Host threads, up to RP_SLOTS (4) batches in flight per context:
+//   reader (this thread): chunk files are memory-mapped; a batch is the secondary index's spans
+//     of header bytes (coalesced, no host copy of the chunk);
+//   parser: the chain's inputs of each header -- slot, prev hash, the nonce value of its
+//     certified VRF output -- read on the host by a few workers (chain_fields), so the chain
+//     never waits for the device;
+//   uploader: the spans go from the mappings into the pinned staging buffers, H2D on the copy
+//     stream, decode on the device and the decoded fields back (the fold's; the chain's only
+//     for a batch the parser could not read);
 //   nonce chain: the evolving-nonce Blake2b chain in header order (the one sequential piece
-//     of work of the replay), the per-header epoch nonces, then the batch's crypto run;
+//     of work of the replay) and the per-header epoch nonces;
+//   launcher: the batch's crypto run once it is decoded and its nonces are known;
 //   fold: waits for the crypto bits, folds envelope + updateChainDepState reusing the nonce
-//     chain's evolving nonces (no second Blake2b chain), writes the verdicts.
+//     chain's evolving nonces (no second Blake2b chain), writes the verdicts (after checking
+//     that the host's reading of every decoded header is the device's).
 //
 // On-disk format (ImmutableDB, Storage/ImmutableDB/Impl): NNNNN.chunk holds the
 // stored blocks back to back; NNNNN.secondary one 56-byte Entry per block
@@ -160,6 +166,119 @@ struct ChunkReader {
 
 constexpr int SLOTS = RP_SLOTS;               // batches in flight (kept by the context between calls)
 
+// Batch k's size cap (PRAOS_REPLAY_RAMP): ramp 1 = batch_max / 4, / 2, then batch_max; ramp 2 =
+// batch_max / 8, / 4, / 2, 3/4, then batch_max.  (A geometric ramp from batch_max / 8 up by 1.4x
+// per batch was measured slower before the host parse and the pinned decode downloads, 84 ->
+// 132 ms on the C5 chain: many small device steps, profiles/r06/g_replay.)
+constexpr int RP_RAMP_DEFAULT = 1;
+size_t rp_ramp_cap(int ramp, uint64_t k, size_t batch_max) {
+  static const size_t r1[][2] = {{1, 4}, {1, 2}}, r2[][2] = {{1, 8}, {1, 4}, {1, 2}, {3, 4}};
+  const size_t (*r)[2] = ramp == 2 ? r2 : r1;
+  const uint64_t nr = ramp == 2 ? 4 : ramp == 1 ? 2 : 0;
+  return k < nr ? std::max<size_t>(1, batch_max * r[k][0] / r[k][1]) : batch_max;
+}
+
+// The nonce chain's inputs of a stored Praos header, read on the host (Praos/Header.hs HeaderRaw
+// [body, kesSig], the 10-field HeaderBody as k_decode_praos reads it): the slot, the prev hash
+// (or the genesis flag) and the header's nonce value, Blake2b-256(Blake2b-256("N" || certified
+// VRF output)) as k_vrf_nonce computes it.  false: the header does not start the usual way (the
+// batch's chain then waits for the device decode).  A header whose bytes go wrong further on is
+// rejected by the device decode and the fold stops at it, whatever the chain assumed after it.
+bool chain_fields(const uint8_t* h, uint32_t len, uint64_t* slot, uint8_t* prev, uint8_t* gen, uint8_t* nonce) {
+  size_t pos = 0;
+  auto head = [&](int want, uint64_t* v) -> bool {
+    if (pos >= len) return false;
+    const uint8_t ib = h[pos++];
+    if ((ib >> 5) != want) return false;
+    const int ai = ib & 31;
+    if (ai < 24) { *v = (uint64_t)ai; return true; }
+    if (ai > 27) return false;
+    const int nb = 1 << (ai - 24);
+    if (pos + (size_t)nb > len) return false;
+    uint64_t x = 0;
+    for (int k = 0; k < nb; k++) x = (x << 8) | h[pos++];
+    *v = x;
+    return true;
+  };
+  uint64_t v;
+  auto bytes = [&](uint64_t n) -> const uint8_t* {
+    if (!head(2, &v) || v != n || pos + n > len) return nullptr;
+    const uint8_t* q = h + pos;
+    pos += n;
+    return q;
+  };
+  if (!head(4, &v) || v != 2 || !head(4, &v) || v != 10 || !head(0, &v) || !head(0, slot)) return false;
+  if (pos < len && h[pos] == 0xF6) {
+    pos++;
+    *gen = 1;
+    std::memset(prev, 0, 32);
+  } else {
+    const uint8_t* q = bytes(32);
+    if (!q) return false;
+    *gen = 0;
+    std::memcpy(prev, q, 32);
+  }
+  if (!bytes(32) || !bytes(32) || !head(4, &v) || v != 2) return false;
+  const uint8_t* out = bytes(64);
+  if (!out) return false;
+  uint8_t msg[65], nv[32];
+  msg[0] = 'N';
+  std::memcpy(msg + 1, out, 64);
+  praos_host::blake2b(nv, 32, msg, 65);
+  praos_host::blake2b(nonce, 32, nv, 32);
+  return true;
+}
+
+// a few persistent workers for the host parse of a batch (run: f(t) on every worker, returns
+// when all are done)
+class ParPool {
+ public:
+  explicit ParPool(unsigned n) : nt_(n) {
+    for (unsigned t = 0; t < nt_; t++) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~ParPool() {
+    { std::lock_guard<std::mutex> g(m_); stop_ = true; }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return nt_; }
+  void run(const std::function<void(unsigned)>& f) {
+    std::unique_lock<std::mutex> g(m_);
+    job_ = &f;
+    pending_ = nt_;
+    gen_++;
+    cv_.notify_all();
+    done_.wait(g, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(unsigned t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned)>* f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(t);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  unsigned nt_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  unsigned pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // Thread placement (PRAOS_REPLAY_PIN, read per call: 1 on, 0 off, unset = on for batches of
 // 64k headers or more): the nonce chain -- the replay's one sequential piece of work, one
 // Blake2b compression per header in order -- on a CPU of its own, the launcher, the fold and the
@@ -195,9 +314,10 @@ struct Placement {
   }
   int chain() const { return cpus[0]; }
   int launcher() const { return cpus[1]; }
-  int folder() const { return cpus[2]; }
+  int folder() const { return cpus[2]; }         // (and the parse pool's coordinating thread)
   int reader() const { return cpus[3]; }
-  std::vector<int> copies() const { return std::vector<int>(cpus.begin() + 4, cpus.end()); }
+  int uploader() const { return cpus[4]; }       // its device syncs spin: a CPU of its own
+  std::vector<int> copies() const { return std::vector<int>(cpus.begin() + 5, cpus.end()); }
 };
 constexpr size_t SPAN_GAP = 4096;             // headers this close share one uploaded span
 
@@ -218,6 +338,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
               size_t batch_max, uint8_t* verdicts, uint16_t* failures, size_t verdicts_cap,
               praos_replay_stats* stats, bool tpraos, const praos_nonce* extra_entropy,
               const praos_ledger_view* views, uint32_t nviews) {
+  const auto t_base = std::chrono::steady_clock::now();   // (the stage trace's origin)
   praos_ctx* const ctx = m > 0 && mem ? mem[0] : nullptr;
   for (int q = 0; q < m; q++)
     if (!mem[q]) return PRAOS_E_ARG;
@@ -288,11 +409,13 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   // nonces travel with each batch, so a batch may span many epochs and stay large enough to fill
   // the device even when epochs are short.
   int v0 = 0;
+  std::chrono::steady_clock::time_point t_peek0 = t_base, t_epoch0 = t_base;   // (setup's parts, traced)
   {
     praos_nonce eta0{};
     uint32_t l;
     uint64_t s0 = 0;
     const uint8_t* p;
+    t_peek0 = std::chrono::steady_clock::now();
     if (rd.peek(&p, &l, &s0) && praos_ticked_epoch_nonce(st, ei, s0, &eta0) != PRAOS_OK) {
       praos_set_error_(ctx, "replay: first slot before the epoch base");
       return PRAOS_E_ARG;
@@ -305,6 +428,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       return PRAOS_E_ARG;
     }
     for (int q = 0; q < m; q++) {
+      if (q == 0) t_epoch0 = std::chrono::steady_clock::now();
       const int r = praos_set_epoch(mem[q], eta0.neutral ? nullptr : eta0.hash, V[v0].pools, V[v0].npools, params);
       if (r != PRAOS_OK) {
         if (q) praos_set_error_(ctx, std::string("member ") + std::to_string(q) + ": " + praos_last_error(mem[q]));
@@ -314,8 +438,11 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   }
   struct Slot {
     praos_batch* b = nullptr;
-    int state = 0;                            // 0 free, 1 decoded
+    int state = 0;                            // 0 free, 1 read (spans, offsets; the host parse)
     uint64_t batch = UINT64_MAX;              // the batch it holds (state 1)
+    bool parsed = false;                      // the host parse is done (host_ok: it read every header)
+    bool host_ok = false;                     // the chain's inputs read on the host (hslot, hprev, ...)
+    bool decoded = false;                     // uploaded and decoded on the device, fields downloaded
     bool chained = false;                     // the nonce chain has been over it (etas, eidx, evol)
     bool launched = false;                    // its crypto is queued
     bool early = false;                       // ... with the launcher's etas_l / eidx_l (PRAOS_REPLAY_EARLY)
@@ -324,15 +451,23 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     uint64_t index0 = 0;
     std::vector<praos_span> spans;
     std::vector<std::shared_ptr<Chunk>> chunks;
-    std::vector<uint64_t> off, slot, block_no, ocn;
-    std::vector<uint32_t> len, bsize;
-    std::vector<uint8_t> prev, gen, cold, hh, nonce, v, eidx;
-    std::vector<uint16_t> dstat, fails;
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    std::vector<uint8_t> v, eidx;
+    std::vector<uint16_t> fails;
+    // the device decode's fields (the batch's pinned area, rp_download_decoded)
+    const uint64_t *slot = nullptr, *block_no = nullptr, *ocn = nullptr;
+    const uint32_t* bsize = nullptr;
+    const uint8_t *prev = nullptr, *gen = nullptr, *cold = nullptr, *hh = nullptr;
+    uint8_t* nonce = nullptr;
+    const uint16_t* dstat = nullptr;
     std::vector<praos_nonce> etas, evol, etas_l;
     std::vector<uint8_t> eidx_l;
-    uint16_t* bits = nullptr;                 // pinned
-    int32_t* pidx = nullptr;                  // pinned
-    size_t pin_cap = 0;
+    std::vector<const uint8_t*> hptr;         // each header's bytes (the mapped chunk)
+    std::vector<uint64_t> hslot;
+    std::vector<uint8_t> hprev, hgen, hnonce;
+    uint16_t* bits = nullptr;                 // pinned (the batch's: rp_batch_results)
+    int32_t* pidx = nullptr;
   };
   // batch k: slot k mod T (T = m x SLOTS), member k mod m, that member's kept slot (k mod T) / m
   const int T = m * SLOTS;
@@ -356,7 +491,6 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   // stage start_ms end_ms headers", appended when the replay ends); one event list per thread
   struct Ev { uint64_t k; const char* what; double t0, t1; size_t n; };
   const char* trace_path = std::getenv("PRAOS_REPLAY_TRACE");
-  const auto t_base = std::chrono::steady_clock::now();
   std::vector<Ev> ev_reader, ev_chain, ev_launch, ev_fold;
   auto ev_add = [&](std::vector<Ev>& v, uint64_t k, const char* what, std::chrono::steady_clock::time_point t0,
                     size_t n) {
@@ -364,12 +498,36 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       v.push_back({k, what, std::chrono::duration<double, std::milli>(t0 - t_base).count(), ms_since(t_base), n});
   };
   uint64_t epochs_seen = 0, batches = 0;
+  if (trace_path) {
+    const auto ms = [&](std::chrono::steady_clock::time_point t) {
+      return std::chrono::duration<double, std::milli>(t - t_base).count();
+    };
+    ev_reader.push_back({0, "first_chunk", ms(t_peek0), ms(t_epoch0), 0});
+  }
+  ev_add(ev_reader, 0, "setup", t_base, 0);
   Placement pl;
   pl.init(batch_max);
+  const char* ramp_env = std::getenv("PRAOS_REPLAY_RAMP");
+  const int ramp = ramp_env ? std::atoi(ramp_env) : RP_RAMP_DEFAULT;
   if (pl.on) {
     for (int q = 0; q < m; q++) rp_copy_pin(mem[q], pl.copies());
     pl.reader_saved = pthread_getaffinity_np(pthread_self(), sizeof pl.reader_was, &pl.reader_was) == 0;
   }
+  // the host parse of the chain's inputs (Praos; PRAOS_PARSE_THREADS workers, 0 = off: the chain
+  // then waits for each batch's device decode)
+  std::unique_ptr<ParPool> parse;
+  {
+    const char* e = std::getenv("PRAOS_PARSE_THREADS");
+    const int np = e ? std::atoi(e) : 6;
+    if (!tpraos && np > 0) {
+      parse.reset(new ParPool((unsigned)std::min(np, 32)));
+      if (pl.on) {
+        const std::vector<int> cp = pl.copies();
+        parse->run([&](unsigned t) { Placement::pin_self(cp[t % cp.size()]); });
+      }
+    }
+  }
+  const bool parse_on = parse != nullptr;
   // ---- nonce chain (speculative tick + reupdate as if every header were valid)
   struct Spec {
     int32_t origin;
@@ -389,7 +547,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   // PRAOS_REPLAY_EARLY=2: only once the reader has decoded the next batch (or there is none), so
   // the early crypto does not share the GPU with the decode the chain waits for next
   const char* early_env = std::getenv("PRAOS_REPLAY_EARLY");
-  const int early_mode = early_env ? std::atoi(early_env) : 0;
+  const int early_mode = early_env ? std::atoi(early_env) : (pl.on ? 2 : 0);
   const bool early_on = early_mode != 0;
   std::vector<std::pair<uint64_t, praos_nonce>> pubs{{sp_epoch, sp.epoch_nonce}};   // (epoch, nonce), mu
   uint64_t pub_epoch = sp_epoch;                                                      // mu
@@ -399,11 +557,18 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k); });
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k && ((C.parsed && C.host_ok) || C.decoded)); });
         if (stop || k >= nbatches) return;
       }
       auto t0 = std::chrono::steady_clock::now();
       const size_t n = C.n;
+      // the chain's inputs: read on the host (no wait for the device), or the device decode's
+      const bool host = C.host_ok;
+      const uint64_t* c_slot = host ? C.hslot.data() : C.slot;
+      const uint8_t* c_prev = host ? C.hprev.data() : C.prev;
+      const uint8_t* c_gen = host ? C.hgen.data() : C.gen;
+      const uint8_t* c_nonce = host ? C.hnonce.data() : C.nonce;
+      const uint16_t* c_dstat = host ? nullptr : C.dstat;
       C.etas.clear();
       C.eidx.resize(n);
       C.evol.resize(n);
@@ -414,12 +579,12 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
                                                     // current labNonce / candidate (copied when needed)
       bool fresh = true;
       auto set_lab = [&](size_t j) {
-        sp.lab.neutral = C.gen[j] ? 1 : 0;
+        sp.lab.neutral = c_gen[j] ? 1 : 0;
         std::memset(sp.lab.hash, 0, 32);
-        if (!C.gen[j]) std::memcpy(sp.lab.hash, C.prev.data() + 32 * j, 32);
+        if (!c_gen[j]) std::memcpy(sp.lab.hash, c_prev + 32 * j, 32);
       };
       for (size_t i = 0; i < n; i++) {
-        const uint64_t slot_i = C.slot[i];
+        const uint64_t slot_i = c_slot[i];
         if (slot_i < ep_lo || slot_i >= ep_hi) {
           ep_no = epoch_of(slot_i);
           ep_lo = slot_i < ei->epoch_base_slot ? 0 : ei->epoch_base_slot + (ep_no - ei->epoch_base_no) * ei->epoch_length;
@@ -449,13 +614,13 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
           fresh = false;
         }
         C.eidx[i] = (uint8_t)std::min<size_t>(C.etas.size() - 1, 255);
-        if (sp.dead || (C.dstat[i] & PRAOS_DEC_FAILED)) { sp.dead = true; C.evol[i] = sp.evolving; continue; }
+        if (sp.dead || (c_dstat && (c_dstat[i] & PRAOS_DEC_FAILED))) { sp.dead = true; C.evol[i] = sp.evolving; continue; }
         sp.origin = 0;
         sp.last = slot_i;
         sp_epoch = e_new;
         lab_i = i;                                // labNonce: the prev hash of this header (copied when needed)
         praos_nonce eta;
-        std::memcpy(eta.hash, C.nonce.data() + 32 * i, 32);
+        std::memcpy(eta.hash, c_nonce + 32 * i, 32);
         eta.neutral = 0;
         sp.evolving = praos_host::nonce_combine(sp.evolving, eta);
         C.evol[i] = sp.evolving;
@@ -464,8 +629,6 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       if (lab_i != SIZE_MAX) set_lab(lab_i);
       if (cand_i != SIZE_MAX) sp.candidate = C.evol[cand_i];
       if (C.etas.size() > 256) { praos_set_error_(ctx, "replay: > 256 epochs in a batch"); fail(PRAOS_E_STATE); return; }
-      for (const praos_nonce& e : C.etas)
-        if (!have_last || !praos_host::nonce_eq(e, last_eta)) { epochs_seen++; last_eta = e; have_last = true; }
       t_nonce += ms_since(t0);
       ev_add(ev_chain, k, "chain", t0, n);
       std::lock_guard<std::mutex> g(mu);
@@ -486,7 +649,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k); });
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k && C.decoded); });
         if (stop || k >= nbatches) return;
       }
       // the batch's last epoch (decoded slots; a header that did not decode may carry any slot:
@@ -511,7 +674,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
           if (early_mode != 2) return true;
           if (nbatches != UINT64_MAX && k + 1 >= nbatches) return true;
           const Slot& N = S[(k + 1) % T];
-          return T > 1 && N.state == 1 && N.batch == k + 1;
+          return T > 1 && N.state == 1 && N.batch == k + 1 && N.decoded;
         };
         cv.wait(g, [&] { return stop || C.chained || (early_on && e_max <= pub_epoch && next_decoded()); });
         if (stop) return;
@@ -583,7 +746,8 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       Slot& C = S[k % T];
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k && C.chained && C.launched); });
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k && C.chained && C.launched &&
+                                                        (C.parsed || !parse_on)); });
         if (stop || k >= nbatches) return;
       }
       auto t0 = std::chrono::steady_clock::now();
@@ -597,18 +761,31 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       ev_add(ev_fold, k, "wait", t0, C.n);
       t0 = std::chrono::steady_clock::now();
       const size_t n = C.n;
+      if (C.host_ok &&
+          (std::memcmp(C.hslot.data(), C.slot, 8 * n) || std::memcmp(C.hgen.data(), C.gen, n) ||
+           std::memcmp(C.hprev.data(), C.prev, 32 * n) || std::memcmp(C.hnonce.data(), C.nonce, 32 * n))) {
+        // the chain ran on the host's reading of the headers: it must be the device decode's for
+        // every header that decodes (the fold stops at the first that does not)
+        for (size_t i = 0; i < n && !(C.dstat[i] & PRAOS_DEC_FAILED); i++)
+          if (C.hslot[i] != C.slot[i] || C.hgen[i] != C.gen[i] ||
+              std::memcmp(&C.hprev[32 * i], &C.prev[32 * i], 32) || std::memcmp(&C.hnonce[32 * i], &C.nonce[32 * i], 32)) {
+            praos_set_error_(ctx, "replay: host and device read header " + std::to_string(C.index0 + i) + " differently");
+            fail(PRAOS_E_STATE);
+            return;
+          }
+      }
       C.v.resize(n);
       C.fails.resize(n);
-      praos_out out{C.bits, C.pidx, nullptr, nullptr, C.nonce.data()};
+      praos_out out{C.bits, C.pidx, nullptr, nullptr, C.nonce};
       praos_headers h{};
       h.n = n;
-      h.slot = C.slot.data();
-      h.cold_vk = C.cold.data();
-      h.ocert_n = C.ocn.data();
-      env->block_no = C.block_no.data();
-      env->header_hash = C.hh.data();
+      h.slot = C.slot;
+      h.cold_vk = C.cold;
+      h.ocert_n = C.ocn;
+      env->block_no = C.block_no;
+      env->header_hash = C.hh;
       env->header_size = C.len.data();
-      env->body_size = C.bsize.data();
+      env->body_size = C.bsize;
       size_t stp = 0, done = 0;
       if (views) {                            // the envelope limits of the batch's ledger view
         env->lv_prot_major = V[C.view].prot;
@@ -616,7 +793,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         env->max_body_size = V[C.view].maxb;
       }
       const std::vector<praos_nonce>& etas = C.early ? C.etas_l : C.etas;   // the nonces its crypto ran with
-      rc = rp_fold(ctx, &h, C.prev.data(), C.gen.data(), &out, env, ei, st, etas.data(), (uint32_t)etas.size(),
+      rc = rp_fold(ctx, &h, C.prev, C.gen, &out, env, ei, st, etas.data(), (uint32_t)etas.size(),
                    (C.early ? C.eidx_l : C.eidx).data(), C.evol.data(), tpraos, extra_entropy, C.v.data(),
                    C.fails.data(), &stp, &done, views ? hv[C.view].get() : nullptr);
       env->block_no = nullptr;
@@ -626,6 +803,16 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       t_fold += ms_since(t0);
       ev_add(ev_fold, k, "fold", t0, C.n);
       if (rc != PRAOS_OK) { fail(rc); return; }
+      {
+        // epoch nonces the folded headers ran under (up to and including a stopping header: the
+        // count does not depend on how far the chain or the reader got before the stop)
+        const std::vector<uint8_t>& ix = C.early ? C.eidx_l : C.eidx;
+        const size_t upto = stp < done ? stp + 1 : done;
+        for (size_t j = 0; j < upto; j++) {
+          const praos_nonce& e = etas[ix[j]];
+          if (!have_last || !praos_host::nonce_eq(e, last_eta)) { epochs_seen++; last_eta = e; have_last = true; }
+        }
+      }
       for (size_t j = 0; j < done && C.index0 + j < verdicts_cap; j++) {
         verdicts[C.index0 + j] = C.v[j];
         if (failures) failures[C.index0 + j] = tpraos ? C.fails[j] : 0;
@@ -647,11 +834,81 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         headers_done = C.index0 + n;
       }
       C.state = 0;
-      C.chained = C.launched = C.early = false;
+      C.chained = C.launched = C.early = C.decoded = C.host_ok = C.parsed = false;
       cv.notify_all();
     }
   });
-  // ---- reader (this thread): build, upload and decode batch k into slot k % T (member k % m)
+  // ---- uploader: H2D + device decode of each batch the reader has built, then the decoded
+  // fields back (the launcher and the fold wait for them; the chain only when the host parse
+  // could not read the batch)
+  std::vector<Ev> ev_up;
+  std::thread uploader([&] {
+    if (pl.on) Placement::pin_self(pl.uploader());
+    for (uint64_t k = 0;; k++) {
+      Slot& C = S[k % T];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k); });
+        if (stop || k >= nbatches) return;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      praos_ctx* const mc = member(k);
+      const size_t n = C.n;
+      int rc = rp_upload_decode(mc, C.b, n, C.spans.data(), C.spans.size(), C.off.data(), C.len.data());
+      ev_add(ev_up, k, "gather", t0, n);        // the bytes staged and queued (host side)
+      praos_decoded dec{};
+      if (rc == PRAOS_OK) rc = rp_download_decoded(mc, C.b, &dec, &C.nonce);   // into the batch's pinned area
+      if (rc == PRAOS_OK) {
+        C.dstat = dec.status; C.block_no = dec.block_no; C.slot = dec.slot; C.ocn = dec.ocert_n;
+        C.bsize = dec.body_size; C.prev = dec.prev_hash; C.gen = dec.prev_is_genesis; C.cold = dec.cold_vk;
+        C.hh = dec.header_hash;
+      }
+      t_dev += ms_since(t0);
+      ev_add(ev_up, k, "decode", t0, n);
+      if (rc != PRAOS_OK) {
+        if (mc != ctx) praos_set_error_(ctx, praos_last_error(mc));
+        fail(rc);
+        return;
+      }
+      std::lock_guard<std::mutex> g(mu);
+      if (C.parsed || !parse_on) C.chunks.clear();   // the mappings have been read (the last reader drops them)
+      C.decoded = true;
+      cv.notify_all();
+    }
+  });
+  // ---- parser: the chain's inputs of each batch read on the host (the pool's workers), beside
+  // the reader's next batch and the uploader
+  std::vector<Ev> ev_parse;
+  std::thread parser([&] {
+    if (!parse_on) return;
+    if (pl.on) Placement::pin_self(pl.folder());
+    for (uint64_t k = 0;; k++) {
+      Slot& C = S[k % T];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || k >= nbatches || (C.state == 1 && C.batch == k); });
+        if (stop || k >= nbatches) return;
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      const size_t n = C.n;
+      C.hslot.resize(n); C.hprev.resize(32 * n); C.hgen.resize(n); C.hnonce.resize(32 * n);
+      std::atomic<bool> ok{true};
+      const unsigned np = parse->size();
+      parse->run([&](unsigned t) {
+        for (size_t i = n * t / np; i < n * (t + 1) / np; i++)
+          if (!chain_fields(C.hptr[i], C.len[i], &C.hslot[i], &C.hprev[32 * i], &C.hgen[i], &C.hnonce[32 * i]))
+            ok = false;
+      });
+      ev_add(ev_parse, k, "parse", t0, n);
+      std::lock_guard<std::mutex> g(mu);
+      C.host_ok = ok;
+      C.parsed = true;
+      if (C.decoded) C.chunks.clear();
+      cv.notify_all();
+    }
+  });
+  // ---- reader (this thread): build batch k into slot k % T (member k % m) and read the chain's
+  // inputs of its headers on the host
   if (pl.on) Placement::pin_self(pl.reader());
   uint64_t next_index = 0, built = 0;
   for (uint64_t k = 0;; k++) {
@@ -666,17 +923,17 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     C.chunks.clear();
     C.off.clear();
     C.len.clear();
+    C.hptr.clear();
     const uint8_t* p;
     uint32_t l;
     uint64_t s, e_prev = 0;
     uint32_t nep = 0;
     size_t arena = 0;
     const Chunk* span_chunk = nullptr;
-    // the first batch is a quarter of the others: the nonce chain (the replay's sequential
-    // part) starts as soon as possible.  (A geometric ramp from batch_max / 8 up by 1.4x per batch
-    // was measured slower, 84 -> 132 ms on the C5 chain: many small crypto steps,
-    // profiles/r06/g_replay.)
-    const size_t cap = k == 0 ? std::max<size_t>(1, batch_max / 4) : batch_max;
+    // the first batches ramp up to batch_max (rp_ramp_cap): the nonce chain (the replay's
+    // sequential part) starts as soon as possible, and each next batch is read and decoded by
+    // the time the chain has been over the one before
+    const size_t cap = rp_ramp_cap(ramp, k, batch_max);
     bool no_view = false;
     while (C.off.size() < cap && rd.peek(&p, &l, &s)) {
       const uint64_t e = epoch_of(s);
@@ -703,6 +960,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
         arena += l;
       }
       C.len.push_back(l);
+      C.hptr.push_back(p);
       rd.pop();
     }
     t_io += ms_since(t0);
@@ -724,35 +982,7 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
       C.b = rp_batch_take(mc, member_slot(k), n, arena, tpraos);
       if (!C.b) { fail(PRAOS_E_OOM); break; }
     }
-    if (C.pin_cap < n) {
-      if (C.bits) (void)hipHostFree(C.bits);
-      if (C.pidx) (void)hipHostFree(C.pidx);
-      C.pin_cap = n + n / 8 + 64;
-      if (hipHostMalloc((void**)&C.bits, 2 * C.pin_cap, hipHostMallocDefault) != hipSuccess ||
-          hipHostMalloc((void**)&C.pidx, 4 * C.pin_cap, hipHostMallocDefault) != hipSuccess) {
-        C.bits = nullptr;
-        C.pidx = nullptr;
-        C.pin_cap = 0;
-        fail(PRAOS_E_OOM);
-        break;
-      }
-    }
-    int rc = rp_upload_decode(mc, C.b, n, C.spans.data(), C.spans.size(), C.off.data(), C.len.data());
-    C.chunks.clear();                         // the mappings have been read (except the reader's current one)
-    C.dstat.resize(n); C.block_no.resize(n); C.slot.resize(n); C.ocn.resize(n); C.bsize.resize(n);
-    C.prev.resize(32 * n); C.gen.resize(n); C.cold.resize(32 * n); C.hh.resize(32 * n); C.nonce.resize(32 * n);
-    praos_decoded dec{};
-    dec.status = C.dstat.data(); dec.block_no = C.block_no.data(); dec.slot = C.slot.data();
-    dec.prev_hash = C.prev.data(); dec.prev_is_genesis = C.gen.data(); dec.cold_vk = C.cold.data();
-    dec.body_size = C.bsize.data(); dec.ocert_n = C.ocn.data(); dec.header_hash = C.hh.data();
-    if (rc == PRAOS_OK) rc = rp_download_decoded(mc, C.b, &dec, C.nonce.data());
-    t_dev += ms_since(t0);
-    ev_add(ev_reader, k, "decode", t0, n);
-    if (rc != PRAOS_OK) {
-      if (mc != ctx) praos_set_error_(ctx, praos_last_error(mc));
-      fail(rc);
-      break;
-    }
+    rp_batch_results(C.b, &C.bits, &C.pidx);          // pinned, kept with the batch
     std::lock_guard<std::mutex> g(mu);
     C.state = 1;
     C.batch = k;
@@ -767,6 +997,10 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   chain.join();
   launcher.join();
   folder.join();
+  uploader.join();
+  parser.join();
+  parse.reset();
+  const auto t_join = std::chrono::steady_clock::now();
   if (pl.on) {                                // the caller's thread and the copy threads as they were
     if (pl.reader_saved) (void)pthread_setaffinity_np(pthread_self(), sizeof pl.reader_was, &pl.reader_was);
     for (int q = 0; q < m; q++) rp_copy_pin(mem[q], {});
@@ -778,17 +1012,16 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
     // overwrites its buffers; rp_upload_decode also orders itself after run_ev)
     if (C.b) rp_batch_quiesce(C.b);
     if (C.b) rp_batch_keep(member(k), member_slot(k), C.b);
-    if (C.bits) (void)hipHostFree(C.bits);
-    if (C.pidx) (void)hipHostFree(C.pidx);
   }
   // every batch has finished: the members get their own tables back, the views' go
   for (int q = 0; q < m; q++) {
     rp_tables_set(mem[q], own[q]);
     for (rp_view* t : dev_views[q]) rp_view_free(mem[q], t);
   }
+  ev_add(ev_fold, nbatches, "teardown", t_join, 0);
   if (trace_path) {
     if (FILE* f = std::fopen(trace_path, "a")) {
-      for (const auto* v : {&ev_reader, &ev_chain, &ev_launch, &ev_fold})
+      for (const auto* v : {&ev_reader, &ev_parse, &ev_up, &ev_chain, &ev_launch, &ev_fold})
         for (const Ev& e : *v) std::fprintf(f, "%llu %s %.3f %.3f %zu\n", (unsigned long long)e.k, e.what, e.t0, e.t1, e.n);
       std::fprintf(f, "end - 0 %.3f 0\n", ms_since(t_base));
       std::fclose(f);

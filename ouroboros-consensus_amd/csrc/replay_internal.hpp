@@ -18,9 +18,11 @@ bool rp_batch_fits(const praos_batch* b, size_t n, size_t bytes);
 // The context keeps the replay's batches between calls (RP_SLOTS of them, freed by praos_close):
 // rp_batch_take returns slot k's batch when it fits n headers over `bytes` (else a new one),
 // rp_batch_keep hands it back.
-constexpr int RP_SLOTS = 3;
+constexpr int RP_SLOTS = 4;
 praos_batch* rp_batch_take(praos_ctx* c, int k, size_t n, size_t bytes, bool tpraos);
 void rp_batch_keep(praos_ctx* c, int k, praos_batch* b);
+// the batch's pinned result buffers (bits, pool index: its header capacity each)
+void rp_batch_results(praos_batch* b, uint16_t** bits, int32_t** pidx);
 // Waits for the batch's last decode and crypto run (a stopped replay leaves queued runs).
 void rp_batch_quiesce(praos_batch* b);
 // Copy stream: the spans' concatenation (the arena) and the per-header (offset, length) go
@@ -28,9 +30,11 @@ void rp_batch_quiesce(praos_batch* b);
 // certified VRF output (k_vrf_nonce).  Returns once the host side is queued.
 int rp_upload_decode(praos_ctx* c, praos_batch* b, size_t n, const praos_span* spans, size_t nspans,
                      const uint64_t* hoff, const uint32_t* hlen);
-// D2H of the decoded fields the nonce chain and the fold read, and the nonce values
-// (copy stream; returns when they are in host memory).
-int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t* nonce);
+// D2H of the decoded fields the nonce chain and the fold read, and the nonce values, into the
+// batch's pinned area (copy stream; returns when they are in host memory).  d's pointers and
+// *nonce stay valid until the batch's next download.
+constexpr size_t DEC_H_BYTES = 3 * 8 + 4 * 32 + 4 + 2 + 1;
+int rp_download_decoded(praos_ctx* c, praos_batch* b, praos_decoded* d, uint8_t** nonce);
 // The crypto run under per-header epoch nonces (etas[eta_idx[i]]), queued after the decode;
 // the host arrays are copied before return.
 int rp_run(praos_ctx* c, praos_batch* b, const praos_nonce* etas, uint32_t k, const uint8_t* eta_idx);

@@ -396,12 +396,12 @@ class Context:
     @staticmethod
     def pool_array(pools):
         """pools: list of (hash28: bytes, vrf_hash32: bytes, sigma_fp: int)."""
-        arr = (Pool * max(1, len(pools)))()
-        for i, (h, v, s) in enumerate(pools):
-            ctypes.memmove(arr[i].hash28, h, 28)
-            ctypes.memmove(arr[i].vrf_hash32, v, 32)
-            ctypes.memmove(arr[i].sigma_fp, int(s).to_bytes(16, "little"), 16)
-        return arr
+        if not pools:
+            return (Pool * 1)()
+        # one buffer of 76-byte records (the struct has no padding), copied in once
+        data = b"".join(bytes(h)[:28].ljust(28, b"\0") + bytes(v)[:32].ljust(32, b"\0") + int(s).to_bytes(16, "little")
+                        for h, v, s in pools)
+        return (Pool * len(pools)).from_buffer_copy(data)
 
     def set_epoch(self, eta0, pools, params: Params):
         """pools: list of (hash28: bytes, vrf_hash32: bytes, sigma_fp: int)."""
@@ -1243,12 +1243,13 @@ def _replay_views(fn, handle, check, path, views, params, epoch_info, state, env
 
 def _state_struct(state, cap):
     st = ChainState()
-    keys = list(state.get("counters", {}).keys())
+    counters = state.get("counters", {})
+    keys = list(counters.keys())
     hk = np.zeros(28 * max(cap, 1), np.uint8)
     cv = np.zeros(max(cap, 1), np.uint64)
-    for k, key in enumerate(keys):
-        hk[28 * k:28 * k + 28] = np.frombuffer(key, np.uint8)
-        cv[k] = state["counters"][key]
+    if keys:
+        hk[:28 * len(keys)] = np.frombuffer(b"".join(keys), np.uint8)
+        cv[:len(keys)] = np.fromiter((counters[k] for k in keys), np.uint64, count=len(keys))
     st.last_slot_origin = int(state.get("last_slot") is None)
     st.last_slot = state.get("last_slot") or 0
     st.counter_hash28, st.counter, st.m, st.cap = ptr(hk), ptr(cv, u64p), len(keys), cap
@@ -1276,8 +1277,9 @@ def state_encode(state):
 
 
 def _state_from_struct(st, hk, cv):
+    hb = hk[:28 * st.m].tobytes()
     state = {"last_slot": None if st.last_slot_origin else int(st.last_slot),
-             "counters": {bytes(hk[28 * k:28 * k + 28]): int(cv[k]) for k in range(st.m)}}
+             "counters": {hb[28 * k:28 * k + 28]: v for k, v in enumerate(cv[:st.m].tolist())}}
     for a, b in (("evolving", "evolving"), ("candidate", "candidate"), ("epoch_nonce", "epoch_nonce"),
                  ("lab", "lab"), ("last_epoch_block", "leb")):
         x = getattr(st, a)

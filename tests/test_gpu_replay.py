@@ -108,15 +108,25 @@ def test_replay_all_valid(ctx, chain, batch_max):
     assert (stats["headers"], stats["validated"], stats["stop_index"], stats["stop_verdict"]) == (n, n, n, 0)
     assert int((v != 0).sum()) == 0
     assert stats["epochs"] == EPOCHS and stats["chunks"] == chain["nchunks"]
-    # batches span epochs (per-header nonces); the first is a quarter of batch_max (the nonce
-    # chain starts sooner, praos_replay.hip)
-    first = max(1, batch_max // 4)
-    assert stats["batches"] == (1 + -(-(n - first) // batch_max) if n > first else 1)
+    # batches span epochs (per-header nonces); the first is a quarter of batch_max and the second
+    # a half (the nonce chain starts sooner, praos_replay.hip)
+    assert stats["batches"] == _expected_batches(n, batch_max)
     assert st == chain["state"]
     assert env["tip"] == (int(chain["slots"][-1]), n - 1, bytes(chain["header_hash"][-1]))
     ov, ost, otip, etas, ostop = _oracle_fold(ctx, chain, n)
     assert ostop == n and etas == chain["nonces"] and len(set(etas)) == EPOCHS
     assert st == ost and env["tip"] == otip
+
+
+def _expected_batches(n, batch_max):
+    """The replay's batch count: a quarter of batch_max first, then a half, then full batches
+    (praos_replay.hip)."""
+    left, k = n, 0
+    while left > 0:
+        cap = max(1, batch_max // 4) if k == 0 else max(1, batch_max // 2) if k == 1 else batch_max
+        left -= cap
+        k += 1
+    return k
 
 
 def _copy_db(chain, tmp_path, name):
@@ -343,8 +353,7 @@ def test_tpraos_replay_all_valid(ctx, tchain, batch_max):
     stats, v, f, st, env = _tp_replay(ctx, tchain, batch_max=batch_max)
     assert (stats["headers"], stats["validated"], stats["stop_index"], stats["stop_verdict"]) == (n, n, n, 0)
     assert int((v != 0).sum()) == 0 and int((f != 0).sum()) == 0
-    first = max(1, batch_max // 4)
-    assert stats["epochs"] == 3 and stats["batches"] == (1 + -(-(n - first) // batch_max) if n > first else 1)
+    assert stats["epochs"] == 3 and stats["batches"] == _expected_batches(n, batch_max)
     assert st == tchain["state"]
     assert env["tip"] == (int(tchain["slots"][-1]), n - 1, bytes(tchain["header_hash"][-1]))
     ov, of, ost, etas, ostop = _tp_oracle_fold(ctx, tchain, n)
@@ -377,7 +386,7 @@ def _same_replay(a, b):
     """Two replays' (stats, verdicts, state, envelope) agree except for the timings (and, for a
     replay that stopped early, the counts of batches whose crypto was already queued and of chunk
     files the reader had opened by then: they depend on how many batches the pipeline keeps in
-    flight -- 3 per context -- and on how far the reader got before the stop)."""
+    flight -- RP_SLOTS, 4 per context -- and on how far the reader got before the stop)."""
     (sa, va, sta, ea), (sb, vb, stb, eb) = a, b
     stopped = sa["stop_index"] < sa["headers"] + sa["skipped"] or sa["stop_verdict"]
     skip = _TIMES + (("batches", "chunks") if stopped else ())
@@ -517,12 +526,15 @@ def test_reused_batches_alternate_replay_and_pipeline(chain):
 
 
 @pytest.mark.parametrize("env", [{"PRAOS_REPLAY_EARLY": "1"}, {"PRAOS_REPLAY_EARLY": "2"},
-                                 {"PRAOS_REPLAY_PIN": "1"}, {"PRAOS_CSTREAM_PRIO": "1"}])
+                                 {"PRAOS_REPLAY_PIN": "1"}, {"PRAOS_CSTREAM_PRIO": "1"},
+                                 {"PRAOS_PARSE_THREADS": "0"}, {"PRAOS_PARSE_THREADS": "1"}])
 def test_replay_schedule_options_equal_default(ctx, chain, tmp_path, monkeypatch, env):
     """Host-schedule options of the replay give the default replay's stats, verdicts, state and tip:
     crypto launched as soon as the batch's epoch nonces are published (PRAOS_REPLAY_EARLY 1; 2: and
     the next batch decoded), pinned threads (PRAOS_REPLAY_PIN), the copy / decode stream at the
-    greatest priority (PRAOS_CSTREAM_PRIO, read when a context opens) -- over the
+    greatest priority (PRAOS_CSTREAM_PRIO, read when a context opens), the nonce chain on the
+    device decode's fields instead of the host's reading of the headers (PRAOS_PARSE_THREADS=0), or
+    that reading on one worker -- over the
     clean 4-epoch database (one context, 97-header batches; a 3-member group) and over one damaged
     in epoch 2 (the stop, its verdict and the state before it)."""
     from praos_hip import abi
