@@ -202,6 +202,14 @@ struct praos_ctx {
                                                        // off, measured slower (C4 10.7 -> 11.2 ms: the
                                                        // representatives' walks lengthen the KES chain more than
                                                        // the skipped walks save; C5 unchanged, profiles/r04/r)
+  int v_main = 3;                                      // stage V on the main stream (PRAOS_V_MAIN; 0 off): no
+                                                       // cross-stream wait between the previous run's end and V;
+                                                       // the join after U and V on the VRF stream (3), or on the
+                                                       // main stream after a wait for U (1; 2: U's two streams
+                                                       // waited for separately).  54k headers (C5 1/8 shard):
+                                                       // 2.354-2.380 ms off, 2.284-2.330 (1), 2.315-2.332 (2),
+                                                       // 2.267-2.297 (3); 108k: 3.418-3.443 off, 3.36-3.42 on
+                                                       // (profiles/r06/k_vmain)
   int pre_join = -1;                                   // the join's pool part (lookup, key hash, leader / nonce
                                                        // values) as k_vrf_pool on the VRF miss stream before the
                                                        // uncached U, off the chain after stage V (PRAOS_PRE_JOIN
@@ -625,6 +633,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_POOL_KEYS")) (void)praos_set_option(c, PRAOS_OPT_POOL_KEYS, std::atoi(e));
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PRE_JOIN")) c->pre_join = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_V_MAIN")) c->v_main = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_NOCACHE")) c->kes_nocache = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
@@ -1379,6 +1388,11 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   // 54k-header step, behind a dozen list kernels on the other streams)
   const bool do_vrf = (c->kernels & 4) != 0;
   const bool tp_staged = do_vrf && b->tp_only && c->tp_staged;
+  // PRAOS_V_MAIN: the three-kernel Praos VRF with stage V and the join on the main stream (the
+  // step's critical path then crosses streams once, U -> join, instead of at ev[0] -> V, V -> join
+  // and join -> leader)
+  const bool v_main = c->v_main > 0 && c->concurrent && do_vrf && !b->tp_only && !b->v_done &&
+                      (c->vrf3 > 0 || (c->vrf3 < 0 && n < 300000));
   const int wprio_v = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
   bool v_queued = false;
   if (tp_staged) {
@@ -1409,7 +1423,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       HIPCHK(c, hipEventRecord(c->v_ev, sVk[0]));
       HIPCHK(c, hipEventRecord(c->v2_ev, sVk[1]));
     } else {
-      hipStream_t sV = c->concurrent ? c->vstream : c->stream;
+      hipStream_t sV = c->concurrent && !v_main ? c->vstream : c->stream;
       if (sV != c->stream) HIPCHK(c, hipStreamWaitEvent(sV, c->ev[0], 0));
       HIPCHK(c, hipEventRecord(c->v0_ev, sV));
       launch_vrf_v(sV, n, b->vrf_vk, b->vrf_proof, b->slot, eta, c->eta0_neutral, b->eta_idx, b->tab_vrf,
@@ -1469,7 +1483,8 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     keycache_precompute(k, b->vrf_vk, 1, sv);
     launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
                  b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n), 0);
-    if (sm_[2] != sv) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
+    // (v_main 2: the main stream waits for u_ev itself, before the join)
+    if (sm_[2] != sv && !(v_main && c->v_main == 2)) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     vrf_keys_queued = true;
     return PRAOS_OK;
   };
@@ -1654,7 +1669,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
     // (stored-bytes pipeline: stage V was queued chunk by chunk on vstream while the later
     // chunks were still uploading; b->v_done)
-    hipStream_t sV = (c->concurrent || b->v_done) ? c->vstream : c->stream;
+    hipStream_t sV = v_main ? c->stream : (c->concurrent || b->v_done) ? c->vstream : c->stream;
     const int wprio = wprio_v;
     if (!b->v_done && !v_queued) {
       const int r = queue_stage_v();
@@ -1691,8 +1706,19 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       } else {
         stage_u(sv, nullptr, nullptr, nullptr);
       }
-      if ((r = after_v(sv)) != PRAOS_OK) return r;
-      join(sv);
+      if (v_main && c->v_main == 3) {  // V on the main stream, the join on the VRF stream after U
+        HIPCHK(c, hipEventRecord(c->v_ev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(sv, c->v_ev, 0));
+        join(sv);
+      } else if (v_main) {             // V is on the main stream: the join follows it there, after U
+        if (c->v_main == 2 && kc) HIPCHK(c, hipStreamWaitEvent(c->stream, c->u_ev, 0));
+        HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[2], 0));
+        join(c->stream);
+      } else {
+        if ((r = after_v(sv)) != PRAOS_OK) return r;
+        join(sv);
+      }
     } else if (kc) {
       praos_batch::KeyCache& k = b->kc[1];
       int r = keycache_lists(k, b->vrf_vk, sv);
@@ -1715,8 +1741,12 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   }
   HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
   if (c->concurrent) {
-    for (int k = 0; k < 3; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
+    // (v_main: the VRF stream and its miss stream -- u_ev -- were waited for before the join)
+    const bool sv_done = v_main && c->v_main != 3;
+    for (int k = 0; k < 3; k++)
+      if (!(sv_done && k == 2)) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
     for (int k = 0; k < 3; k++) {
+      if (sv_done && k == 2) continue;
       HIPCHK(c, hipEventRecord(c->mdone_ev[k], c->mside[k]));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->mdone_ev[k], 0));
     }
