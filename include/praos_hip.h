@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PRAOS_ABI_VERSION 14
+#define PRAOS_ABI_VERSION 15
 
 /* ---- return codes ---- */
 #define PRAOS_OK 0
@@ -314,6 +314,16 @@ int praos_decode_headers(praos_ctx* ctx, const praos_header_bytes* in, praos_dec
 /* Decode + full header validation on the device.  bits gets PRAOS_BIT_INPUT for
  * a header that does not decode; dec may be NULL. */
 int praos_verify_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, praos_out* out, praos_decoded* dec);
+/* ABI 15: the streaming form (a node or db-analyser validating batch after batch).  The call is
+ * queued and returns at once; a context keeps two calls in flight, so the next submit's upload,
+ * decode and stage V run under this call's key chains.  Its outputs (out, dec) are written by
+ * the submit after the next one, which waits for it, or by praos_verify_drain; in, the bytes it
+ * points to, out and dec must stay valid and unchanged until then.  Outputs equal the blocking
+ * call's.  Batches too small for the chunked pipeline (PRAOS_OPT_PIPELINE) run the blocking call
+ * after the calls in flight.  praos_verify_header_bytes and praos_close drain first. */
+int praos_verify_header_bytes_submit(praos_ctx* ctx, const praos_header_bytes* in, praos_out* out,
+                                     praos_decoded* dec);
+int praos_verify_drain(praos_ctx* ctx);
 /* Device-resident form: the batch keeps the arena; praos_batch_run decodes and
  * then validates (bench / streaming replay).  praos_batch_download_decoded
  * copies the decoded fields of the last run. */

@@ -40,6 +40,8 @@ module Ouroboros.Consensus.Protocol.Praos.Batch
   , praosValidateHeaderSpans
   , praosHostRegister
   , praosHostUnregister
+  , praosSubmitHeaderBytes
+  , praosDrainHeaderBytes
     -- * TPraos (Shelley..Alonzo) headers from stored bytes
   , TPraosBatchResult (..)
   , praosTickedEpochNonceTPraos
@@ -167,8 +169,13 @@ foreign import ccall safe "praos_verify_block_integrity" c_verify_block_integrit
 foreign import ccall safe "praos_group_verify_block_integrity" c_group_verify_block_integrity
   :: Ptr PraosGroup -> Ptr () -> Word64 -> Ptr Word8 -> Ptr Word8 -> IO CInt
 
+-- ABI 15: the streaming form of praos_verify_header_bytes (two calls in flight per context)
+foreign import ccall safe "praos_verify_header_bytes_submit" c_verify_header_bytes_submit
+  :: Ptr PraosCtx -> Ptr () -> Ptr () -> Ptr () -> IO CInt
+foreign import ccall safe "praos_verify_drain" c_verify_drain :: Ptr PraosCtx -> IO CInt
+
 abiVersion :: CInt
-abiVersion = 14
+abiVersion = 15
 
 -- ---------------------------------------------------------------- context
 
@@ -245,6 +252,22 @@ verifyHeaderBytes :: PraosBatchCtx -> Ptr () -> Ptr () -> Ptr () -> IO ()
 verifyHeaderBytes ctx hb out dec = check ctx $ case ctx of
   PraosBatchCtx p -> c_verify_header_bytes p hb out dec
   PraosBatchGroup g _ _ -> c_group_verify_header_bytes g hb out dec
+
+-- | The streaming form of 'verifyHeaderBytes' (praos_verify_header_bytes_submit): the call is
+-- queued and returns; its outputs are written by the submit after the next one (a context keeps
+-- two calls in flight, the next one's upload and stage V under this one's key chains) or by
+-- 'praosDrainHeaderBytes'.  The header-bytes struct, the arena and the output arrays must stay
+-- alive and unchanged until then.  A group runs the blocking call.
+praosSubmitHeaderBytes :: PraosBatchCtx -> Ptr () -> Ptr () -> Ptr () -> IO ()
+praosSubmitHeaderBytes ctx hb out dec = check ctx $ case ctx of
+  PraosBatchCtx p -> c_verify_header_bytes_submit p hb out dec
+  PraosBatchGroup g _ _ -> c_group_verify_header_bytes g hb out dec
+
+-- | Every submitted call's outputs written (praos_verify_drain).
+praosDrainHeaderBytes :: PraosBatchCtx -> IO ()
+praosDrainHeaderBytes ctx = case ctx of
+  PraosBatchCtx p -> check ctx (c_verify_drain p)
+  PraosBatchGroup {} -> pure ()
 
 verifyTPraosHeaderBytes :: PraosBatchCtx -> Ptr () -> Ptr () -> Ptr () -> IO ()
 verifyTPraosHeaderBytes ctx hb out dec = check ctx $ case ctx of

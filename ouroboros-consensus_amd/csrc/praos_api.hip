@@ -247,6 +247,15 @@ struct praos_ctx {
   praos_batch* rp_keep[RP_SLOTS] = {};                 // replay batches kept between calls
   hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
   praos_batch* pipe[PIPE_MAX] = {};
+  // praos_verify_header_bytes_submit: up to two calls in flight, on pipe[0] / pipe[1] in turn
+  struct PipeCall {
+    bool active = false;
+    praos_out out{};
+    praos_decoded* dec = nullptr;
+    hipEvent_t ev = nullptr;                           // the call's run has ended (ctx stream)
+    std::vector<uint64_t> off;                         // its rebased offsets (read by its H2D)
+  } pcall[2];
+  int pcall_next = 0;
   size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
@@ -646,6 +655,7 @@ static bool open_streams(praos_ctx* c) {
   (void)hipEventCreate(&c->kc1_ev);
   for (auto& e : c->up_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : c->done_ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& p : c->pcall) (void)hipEventCreateWithFlags(&p.ev, hipEventDisableTiming);
   // side streams: [0] OCert, [1] KES, [2] VRF.  The VRF stream (the longest chain of
   // work) gets the device's greatest priority, so its waves dispatch first and the
   // KES / OCert / miss kernels fill the remaining slots and its tail (C5: 15.8 ->
@@ -742,6 +752,7 @@ void praos_close(praos_ctx* c) {
   if (!c) return;
   if (c->device < 0) { delete c; return; }
   (void)hipSetDevice(c->device);
+  (void)praos_verify_drain(c);                 // submitted calls' outputs are written before the close
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_epoch(c);
   (void)hipFree(c->d_gen);
@@ -783,6 +794,7 @@ void praos_close(praos_ctx* c) {
     if (c->up_ev[k]) (void)hipEventDestroy(c->up_ev[k]);
     if (c->done_ev[k]) (void)hipEventDestroy(c->done_ev[k]);
   }
+  for (auto& p : c->pcall) if (p.ev) (void)hipEventDestroy(p.ev);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->dstream) (void)hipStreamDestroy(c->dstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -902,6 +914,16 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
       (npools == 0 || std::memcmp(pools, c->epoch_pools.data(), npools * sizeof *pools) == 0)) {
     if ((eta0 == nullptr) == c->eta0_neutral && (eta0 == nullptr || std::memcmp(eta0, c->eta0, 32) == 0))
       return PRAOS_OK;                            // the same nonce too: nothing to change
+  }
+  if (c->pcall[0].active || c->pcall[1].active) {
+    // submitted calls (praos_verify_header_bytes_submit) read the installed view and nonce until
+    // they end: their outputs first
+    const int r = praos_verify_drain(c);
+    if (r != PRAOS_OK) return r;
+  }
+  if (c->have_epoch && c->device >= 0 && npools == c->epoch_pools.size() &&
+      std::memcmp(params, &c->epoch_params, sizeof *params) == 0 &&
+      (npools == 0 || std::memcmp(pools, c->epoch_pools.data(), npools * sizeof *pools) == 0)) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));   // no run in flight reads the old nonce
     uint32_t e0[8] = {0};
@@ -2256,8 +2278,14 @@ extern "C" {
 // key caches, OCert, KES, U, the join, the leader test -- runs once over the whole batch, as
 // praos_batch_run does (full-batch key caches, no small-batch tails).  One batch for the whole
 // input, kept in the context (device buffers allocated once for a given size).
+//
+// async (praos_verify_header_bytes_submit): the call on pipe[slot], queued and not waited for:
+// each chunk is decoded on the copy stream right after its upload (on the ctx stream the decode
+// would queue behind the previous call's run), the run's end is recorded in pcall[slot].ev and the
+// outputs come back in pipe_finish.  The next call's uploads, decodes and stage V then overlap this
+// call's key chains, as back-to-back resident runs overlap.
 static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec,
-                                  int K) {
+                                  int K, int slot = 0, bool async = false) {
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = in->n;
   // the arena span of the in-range headers, and offsets rebased to it
@@ -2268,7 +2296,7 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
     end = std::max<uint64_t>(end, in->off[i] + in->len[i]);
   }
   if (base == UINT64_MAX) base = end = 0;
-  std::vector<uint64_t>& off = c->h_off2;
+  std::vector<uint64_t>& off = c->pcall[slot].off;
   off.resize(n);
   for (size_t i = 0; i < n; i++) {   // a span outside the caller's arena stays outside
     const bool in_range = in->off[i] <= in->bytes_len && in->len[i] <= in->bytes_len - in->off[i];
@@ -2295,20 +2323,20 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
     need[k] = hw;                                 // bytes [0, need[k]) cover chunks 0..k
   }
   const uint64_t bytes = end - base;
-  if (!c->pipe[0] || c->pipe_n[0] < n || c->pipe_bytes[0] < bytes) {
-    if (c->pipe[0]) {
+  if (!c->pipe[slot] || c->pipe_n[slot] < n || c->pipe_bytes[slot] < bytes) {
+    if (c->pipe[slot]) {
       HIPCHK(c, hipDeviceSynchronize());
-      for (void* q : c->pipe[0]->owned) (void)hipFree(q);
-      delete c->pipe[0];
-      c->pipe[0] = nullptr;
+      for (void* q : c->pipe[slot]->owned) (void)hipFree(q);
+      delete c->pipe[slot];
+      c->pipe[slot] = nullptr;
     }
     const size_t mc = n + n / 8 + 64, bc = bytes + bytes / 8 + 4096;   // headroom for the next call
-    c->pipe[0] = bytes_batch_alloc(c, mc, bc, false, nullptr);
-    if (!c->pipe[0]) return PRAOS_E_OOM;
-    c->pipe_n[0] = mc;
-    c->pipe_bytes[0] = bc;
+    c->pipe[slot] = bytes_batch_alloc(c, mc, bc, false, nullptr);
+    if (!c->pipe[slot]) return PRAOS_E_OOM;
+    c->pipe_n[slot] = mc;
+    c->pipe_bytes[slot] = bc;
   }
-  praos_batch* b = c->pipe[0];
+  praos_batch* b = c->pipe[slot];
   batch_reuse_reset(b);
   b->n = n;
   b->arena_len = bytes;
@@ -2329,18 +2357,21 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
       HIPCHK(c, h2d_on(c, b->arena + sent, in->bytes + base + sent, need[k] - sent, c->cstream));
       sent = need[k];
     }
-    HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->up_ev[k], 0));
+    hipStream_t sd = async ? c->cstream : c->stream;      // the chunk's decode
+    if (!async) {
+      HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->up_ev[k], 0));
+    }
     const size_t m = lo[k + 1] - lo[k];
     if (m) {
-      launch_decode_praos(dim3(nblocks(m, NT)), dim3(NT), c->stream, lo[k + 1], b->arena, bytes, b->hoff, b->hlen,
+      launch_decode_praos(dim3(nblocks(m, NT)), dim3(NT), sd, lo[k + 1], b->arena, bytes, b->hoff, b->hlen,
                           b->slot, b->cold_vk, b->vrf_vk, b->vrf_out, b->vrf_proof, b->hot_vk, b->ocert_sig,
                           b->kes_sig, b->ocert_n, b->ocert_c0, b->body_off, b->body_len, b->body, b->block_no,
                           b->prev_hash, b->prev_genesis, b->body_size, b->body_hash, b->prot_major, b->prot_minor,
                           b->header_hash, b->dec_status, 0, b->signed_stride, nullptr, nullptr, lo[k]);
       HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipEventRecord(c->done_ev[k], c->stream));
+    HIPCHK(c, hipEventRecord(c->done_ev[k], sd));
     if (m && vrf) {
       // the chunks' stage V alternate between two streams: on one they would queue behind
       // each other (a chunk's V alone is latency-bound)
@@ -2351,11 +2382,24 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
       HIPCHK(c, hipGetLastError());
     }
   }
+  if (async) HIPCHK(c, hipStreamWaitEvent(c->stream, c->done_ev[K - 1], 0));   // every chunk decoded
   b->decoded = true;
   b->v_done = vrf;
   int r = praos_batch_run(c, b);
   b->decoded = false;                // (the downloads below still read b->n; the next call resets
   b->v_done = false;                 // every per-run field when it takes the batch: batch_reuse_reset)
+  if (async) {
+    if (r != PRAOS_OK) {             // nothing of this call is left running when it reports an error
+      (void)hipDeviceSynchronize();
+      return r;
+    }
+    praos_ctx::PipeCall& p = c->pcall[slot];
+    HIPCHK(c, hipEventRecord(p.ev, c->stream));
+    p.out = *out;
+    p.dec = dec;
+    p.active = true;
+    return PRAOS_OK;
+  }
   // the VRF outputs (pool index, beta, leader and nonce values: 132 of the 134 bytes per
   // header) are final once the VRF stream is done: they come back while KES still runs
   if (r == PRAOS_OK && c->concurrent) {
@@ -2380,11 +2424,88 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   return r;
 }
 
+// the outputs of submitted call `slot` (waits for its run): on the download stream, which the
+// calls queued after it do not use
+static int pipe_finish(praos_ctx* c, int slot) {
+  praos_ctx::PipeCall& p = c->pcall[slot];
+  if (!p.active) return PRAOS_OK;
+  p.active = false;
+  HIPCHK(c, hipSetDevice(c->device));
+  const praos_batch* b = c->pipe[slot];
+  const size_t n = b->n;
+  HIPCHK(c, hipStreamWaitEvent(c->dstream, p.ev, 0));
+  auto dn = [&](void* dst, const void* src, size_t nb) -> hipError_t {
+    return dst && nb ? d2h_on(c, dst, src, nb, c->dstream) : hipSuccess;
+  };
+  HIPCHK(c, dn(p.out.bits, b->bits, 2 * n));
+  HIPCHK(c, dn(p.out.pool_idx, b->pool_idx, 4 * n));
+  HIPCHK(c, dn(p.out.beta, b->beta, 64 * n));
+  HIPCHK(c, dn(p.out.leader, b->leader, 32 * n));
+  HIPCHK(c, dn(p.out.nonce, b->nonce, 32 * n));
+  if (praos_decoded* d = p.dec) {
+    HIPCHK(c, dn(d->status, b->dec_status, 2 * n));
+    HIPCHK(c, dn(d->block_no, b->block_no, 8 * n));
+    HIPCHK(c, dn(d->slot, b->slot, 8 * n));
+    HIPCHK(c, dn(d->prev_hash, b->prev_hash, 32 * n));
+    HIPCHK(c, dn(d->prev_is_genesis, b->prev_genesis, n));
+    HIPCHK(c, dn(d->cold_vk, b->cold_vk, 32 * n));
+    HIPCHK(c, dn(d->vrf_vk, b->vrf_vk, 32 * n));
+    HIPCHK(c, dn(d->vrf_out, b->vrf_out, 64 * n));
+    HIPCHK(c, dn(d->vrf_proof, b->vrf_proof, 80 * n));
+    HIPCHK(c, dn(d->body_size, b->body_size, 4 * n));
+    HIPCHK(c, dn(d->body_hash, b->body_hash, 32 * n));
+    HIPCHK(c, dn(d->hot_vk, b->hot_vk, 32 * n));
+    HIPCHK(c, dn(d->ocert_n, b->ocert_n, 8 * n));
+    HIPCHK(c, dn(d->ocert_c0, b->ocert_c0, 8 * n));
+    HIPCHK(c, dn(d->ocert_sig, b->ocert_sig, 64 * n));
+    HIPCHK(c, dn(d->prot_major, b->prot_major, 8 * n));
+    HIPCHK(c, dn(d->prot_minor, b->prot_minor, 8 * n));
+    HIPCHK(c, dn(d->header_hash, b->header_hash, 32 * n));
+    HIPCHK(c, dn(d->kes_sig, b->kes_sig, 448 * n));
+    HIPCHK(c, dn(d->signed_body, b->body, (size_t)b->signed_stride * n));
+    HIPCHK(c, dn(d->signed_len, b->body_len, 4 * n));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->dstream));
+  return PRAOS_OK;
+}
+
+int praos_verify_drain(praos_ctx* c) {
+  if (!c) return PRAOS_E_ARG;
+  if (c->device < 0) return PRAOS_OK;
+  const int older = c->pcall_next;             // the slot the next submit reuses holds the older call
+  int r = pipe_finish(c, older);
+  const int r2 = pipe_finish(c, older ^ 1);
+  return r != PRAOS_OK ? r : r2;
+}
+
+int praos_verify_header_bytes_submit(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec) {
+  if (!c || !in || !out || !out->bits) return PRAOS_E_ARG;
+  if (!c->have_epoch) return PRAOS_E_STATE;
+  if (in->n && (!in->off || !in->len || (!in->bytes && in->bytes_len))) return PRAOS_E_ARG;
+  int K = c->pipeline;
+  if (K == 0) K = (int)std::min<size_t>(PIPE_AUTO, in->n / PIPE_MIN_CHUNK);
+  K = std::min<int>(K, (int)std::min<size_t>(PIPE_MAX, in->n));
+  if (in->n == 0 || K < 2 || c->device < 0) {  // too small to pipeline: the blocking call, in order
+    const int r = praos_verify_drain(c);
+    return r != PRAOS_OK ? r : praos_verify_header_bytes(c, in, out, dec);
+  }
+  const int slot = c->pcall_next;
+  int r = pipe_finish(c, slot);                // two in flight: the older one's outputs first
+  if (r != PRAOS_OK) return r;
+  r = verify_bytes_pipelined(c, in, out, dec, K, slot, true);
+  if (r == PRAOS_OK) c->pcall_next = slot ^ 1;
+  return r;
+}
+
 int praos_verify_header_bytes(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec) {
   if (!c || !in || !out || !out->bits) return PRAOS_E_ARG;
   if (!c->have_epoch) return PRAOS_E_STATE;
   if (in->n == 0) return PRAOS_OK;
   if (in->n && (!in->off || !in->len || (!in->bytes && in->bytes_len))) return PRAOS_E_ARG;
+  {
+    const int rd = praos_verify_drain(c);     // submitted calls use pipe[0] / pipe[1]: finished first
+    if (rd != PRAOS_OK) return rd;
+  }
   {
     // chunked pipeline (PRAOS_OPT_PIPELINE: chunks; 0 = auto: up to PIPE_AUTO chunks of >= PIPE_MIN_CHUNK)
     int K = c->pipeline;

@@ -301,6 +301,9 @@ SIGNATURES = {
     "praos_decode_headers": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.POINTER(Decoded)]),
     "praos_verify_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes), ctypes.POINTER(Out),
                                                  ctypes.POINTER(Decoded)]),
+    "praos_verify_header_bytes_submit": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
+                                                        ctypes.POINTER(Out), ctypes.POINTER(Decoded)]),
+    "praos_verify_drain": (ctypes.c_int, [ctypes.c_void_p]),
     "praos_verify_tpraos_header_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes),
                                                         ctypes.POINTER(TPOut), ctypes.POINTER(Decoded), u8p, u8p]),
     "praos_batch_upload_bytes": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.POINTER(HeaderBytes)]),
@@ -627,6 +630,23 @@ class Context:
         self.check(self.L.praos_verify_header_bytes(self.h, ctypes.byref(hb), ctypes.byref(os_),
                                                     ctypes.byref(d) if d is not None else None))
         return (o, D) if decoded else o
+
+    def submit_header_bytes(self, arena, off, length, out, decoded=None):
+        """Streaming form of verify_header_bytes (praos_verify_header_bytes_submit): queued, returns
+        at once; out (and decoded, an alloc_decoded pair) are written by the submit after the next
+        one or by drain().  The inputs and outputs stay referenced here until drained."""
+        arena, off, length = self._chunk(arena, off, length)
+        hb = self.header_bytes_struct(arena, off, length)
+        os_ = self.out_struct(out)
+        d = decoded[1] if decoded is not None else None
+        self.check(self.L.praos_verify_header_bytes_submit(self.h, ctypes.byref(hb), ctypes.byref(os_),
+                                                           ctypes.byref(d) if d is not None else None))
+        self._inflight = (getattr(self, "_inflight", []) + [(arena, off, length, hb, os_, out, decoded)])[-3:]
+
+    def drain(self):
+        """Every submitted call's outputs written (praos_verify_drain)."""
+        self.check(self.L.praos_verify_drain(self.h))
+        self._inflight = []
 
     def verify_tpraos_header_bytes(self, arena, off, length, decoded=False):
         """Stored TPraos headers (BHeader = [BHBody, kesSig], Shelley..Alonzo) decoded and

@@ -47,7 +47,7 @@ def test_struct_sizes_match_c_layout():
 
 def test_abi_version():
     from praos_hip import abi
-    assert abi.load().praos_abi_version() == 14
+    assert abi.load().praos_abi_version() == 15
 
 
 def test_no_silent_fallback_without_gpu():

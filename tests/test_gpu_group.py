@@ -188,6 +188,64 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
     assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT
 
 
+def test_submitted_bytes_equal_blocking(ctx, c5_batch):
+    """The streaming form (praos_verify_header_bytes_submit, two calls in flight, outputs written by
+    the submit after next or by praos_verify_drain) gives each call the blocking call's outputs and
+    decoded fields bit for bit: different inputs back to back (a damaged copy of the arena, the
+    headers in another order), a blocking call that drains the calls in flight, and a page-locked
+    arena and outputs (direct DMA from the caller's memory)."""
+    from praos_hip import abi
+    cfg, H, pool_list, corrupted, p, arena, off, ln = c5_batch
+    n = len(off)
+    rng = np.random.default_rng(7)
+    arena_b = arena.copy()
+    for i in rng.choice(n, 40, replace=False):        # damaged headers (bytes inside the header body)
+        arena_b[int(off[i]) + 40 + int(rng.integers(0, 200))] ^= 0x10
+    perm = rng.permutation(n)
+    inputs = [(arena, off, ln), (arena_b, off, ln), (arena, off[perm].copy(), ln[perm].copy())]
+    ctx.set_epoch(cfg["eta0"], pool_list, p)
+    try:
+        ctx.set_option(abi.OPT_PIPELINE, 8)
+        ref = [ctx.verify_header_bytes(a, o, l, decoded=True) for a, o, l in inputs]
+        assert not np.array_equal(ref[0][0]["bits"], ref[1][0]["bits"])
+        order = [0, 1, 2, 0, 2]
+        outs = [(ctx.alloc_out(n), ctx.alloc_decoded(n)) for _ in order]
+        for j, (o, d) in zip(order, outs):
+            ctx.submit_header_bytes(*inputs[j], out=o, decoded=d)
+        ctx.drain()
+        for j, (o, d) in zip(order, outs):
+            for k in o:
+                assert np.array_equal(o[k], ref[j][0][k]), (j, k)
+            for k in d[0]:
+                assert np.array_equal(d[0][k], ref[j][1][k]), (j, k)
+        # a blocking call with two calls in flight finishes them first
+        outs = [ctx.alloc_out(n) for _ in range(2)]
+        ctx.submit_header_bytes(*inputs[1], out=outs[0])
+        ctx.submit_header_bytes(*inputs[2], out=outs[1])
+        o4 = ctx.verify_header_bytes(*inputs[0])
+        for j, o in zip((1, 2, 0), outs + [o4]):
+            for k in o:
+                assert np.array_equal(o[k], ref[j][0][k]), (j, k)
+        # page-locked arena and outputs
+        outs = [ctx.alloc_out(n) for _ in range(3)]
+        bufs = [arena] + [v for o in outs for v in o.values() if v.nbytes >= (1 << 20)]
+        for b_ in bufs:
+            ctx.host_register(b_)
+        try:
+            for o in outs:
+                ctx.submit_header_bytes(arena, off, ln, out=o)
+            ctx.drain()
+        finally:
+            for b_ in bufs:
+                ctx.host_unregister(b_)
+        for o in outs:
+            for k in o:
+                assert np.array_equal(o[k], ref[0][0][k]), k
+    finally:
+        ctx.drain()
+        ctx.set_option(abi.OPT_PIPELINE, 0)
+
+
 @pytest.mark.parametrize("env,concurrent", [({"PRAOS_PRE_JOIN": "0"}, 1), ({"PRAOS_PRE_JOIN": "1"}, 1),
                                             ({"PRAOS_PRE_JOIN": "1"}, 0), ({"PRAOS_V_MAIN": "1"}, 1), ({"PRAOS_V_MAIN": "2"}, 1), ({"PRAOS_V_MAIN": "0"}, 1),
                                             ({"PRAOS_V_MAIN": "1", "PRAOS_PRE_JOIN": "0"}, 1)])
