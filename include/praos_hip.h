@@ -315,9 +315,9 @@ int praos_decode_headers(praos_ctx* ctx, const praos_header_bytes* in, praos_dec
  * a header that does not decode; dec may be NULL. */
 int praos_verify_header_bytes(praos_ctx* ctx, const praos_header_bytes* in, praos_out* out, praos_decoded* dec);
 /* ABI 15: the streaming form (a node or db-analyser validating batch after batch).  The call is
- * queued and returns at once; a context keeps two calls in flight, so the next submit's upload,
- * decode and stage V run under this call's key chains.  Its outputs (out, dec) are written by
- * the submit after the next one, which waits for it, or by praos_verify_drain; in, the bytes it
+ * queued and returns at once; a context keeps three calls in flight, so the next submits' uploads,
+ * decodes and stage V run under this call's key chains.  Its outputs (out, dec) are written by
+ * the third submit after it, which waits for it, or by praos_verify_drain; in, the bytes it
  * points to, out and dec must stay valid and unchanged until then.  Outputs equal the blocking
  * call's.  Batches too small for the chunked pipeline (PRAOS_OPT_PIPELINE) run the blocking call
  * after the calls in flight.  praos_verify_header_bytes and praos_close drain first. */

@@ -169,7 +169,7 @@ foreign import ccall safe "praos_verify_block_integrity" c_verify_block_integrit
 foreign import ccall safe "praos_group_verify_block_integrity" c_group_verify_block_integrity
   :: Ptr PraosGroup -> Ptr () -> Word64 -> Ptr Word8 -> Ptr Word8 -> IO CInt
 
--- ABI 15: the streaming form of praos_verify_header_bytes (two calls in flight per context)
+-- ABI 15: the streaming form of praos_verify_header_bytes (three calls in flight per context)
 foreign import ccall safe "praos_verify_header_bytes_submit" c_verify_header_bytes_submit
   :: Ptr PraosCtx -> Ptr () -> Ptr () -> Ptr () -> IO CInt
 foreign import ccall safe "praos_verify_drain" c_verify_drain :: Ptr PraosCtx -> IO CInt
@@ -254,8 +254,8 @@ verifyHeaderBytes ctx hb out dec = check ctx $ case ctx of
   PraosBatchGroup g _ _ -> c_group_verify_header_bytes g hb out dec
 
 -- | The streaming form of 'verifyHeaderBytes' (praos_verify_header_bytes_submit): the call is
--- queued and returns; its outputs are written by the submit after the next one (a context keeps
--- two calls in flight, the next one's upload and stage V under this one's key chains) or by
+-- queued and returns; its outputs are written by the third submit after it (a context keeps
+-- three calls in flight, the next ones' uploads and stage V under this one's key chains) or by
 -- 'praosDrainHeaderBytes'.  The header-bytes struct, the arena and the output arrays must stay
 -- alive and unchanged until then.  A group runs the blocking call.
 praosSubmitHeaderBytes :: PraosBatchCtx -> Ptr () -> Ptr () -> Ptr () -> IO ()

@@ -105,6 +105,7 @@ class CopyPool {
 
 static constexpr size_t STAGE_PIECE = 16u << 20;    // pinned staging buffers: 2 x 16 MB per context
 static constexpr int PIPE_MAX = 8;                  // chunks of the stored-bytes pipeline
+static constexpr int PIPE_CALLS = 3;                // submitted stored-bytes calls in flight (pipe[0 .. 3))
 static constexpr size_t PIPE_MIN_CHUNK = 49152;     // headers per chunk at least (auto mode)
 // Batches below this many headers (a strong-scaling shard of an epoch over 8 GPUs is 54k) leave
 // most wave slots empty and run latency-bound (PRAOS_VRF_PRIO = -1 raises stage V there)
@@ -244,18 +245,26 @@ struct praos_ctx {
   int pipeline = 0;                                    // PRAOS_OPT_PIPELINE (0 = auto)
   hipStream_t cstream = nullptr;
   hipStream_t dstream = nullptr;                       // replay: result downloads (rp_download_results)
+  hipStream_t decstream = nullptr;                     // submitted calls: each landed chunk's decode (off the
+                                                       // copy stream, whose next upload must not wait for it)
   praos_batch* rp_keep[RP_SLOTS] = {};                 // replay batches kept between calls
   hipEvent_t up_ev[PIPE_MAX] = {}, done_ev[PIPE_MAX] = {};
   praos_batch* pipe[PIPE_MAX] = {};
-  // praos_verify_header_bytes_submit: up to two calls in flight, on pipe[0] / pipe[1] in turn
+  // praos_verify_header_bytes_submit: up to PIPE_CALLS calls in flight, on pipe[0 .. PIPE_CALLS) in turn
   struct PipeCall {
     bool active = false;
     praos_out out{};
     praos_decoded* dec = nullptr;
     hipEvent_t ev = nullptr;                           // the call's run has ended (ctx stream)
-    std::vector<uint64_t> off;                         // its rebased offsets (read by its H2D)
-  } pcall[2];
-  int pcall_next = 0;
+    uint64_t* off_h = nullptr;                         // pinned: its rebased offsets and lengths (async H2D:
+    uint32_t* len_h = nullptr;                         // a pageable copy would wait for the copy stream)
+    size_t cap = 0;
+  } pcall[PIPE_CALLS];
+  int pcall_next = 0;                                  // the slot the next submit takes: the oldest call's
+  int stream_chunk_v = 1;                              // submitted calls: stage V per landed chunk (1) or in the
+                                                       // run over the whole batch (0); PRAOS_STREAM_CHUNK_V.  C5,
+                                                       // 432k headers, three calls in flight: 13.2-13.4 ms per
+                                                       // call (1) against 15.3-17.6 (0), profiles/r06/l_stream
   size_t pipe_n[PIPE_MAX] = {}, pipe_bytes[PIPE_MAX] = {};
   int concurrent = 1;                                  // PRAOS_OPT_CONCURRENT
   int kernels = 7;                                     // PRAOS_OPT_KERNELS
@@ -345,6 +354,9 @@ struct praos_ctx {
   std::vector<std::pair<uintptr_t, size_t>> registered;
   // host <-> device staging for large transfers from pageable caller memory
   uint8_t* pin[2] = {nullptr, nullptr};
+  uint8_t* zero_h = nullptr;                           // pinned zeros: an arena's tail padding by DMA (a fill
+                                                       // kernel on the copy stream could wait behind another
+                                                       // stream's kernels on a shared hardware queue)
   hipEvent_t pin_ev[2] = {};
   std::unique_ptr<CopyPool> pool;
   // device buffers of the last freed batch, reused by the next one in allocation
@@ -369,6 +381,15 @@ static void free_spare(praos_ctx* c) {
 // Large H2D / D2H copies through two pinned buffers: the host threads fill (drain) one
 // piece while the DMA engine moves the other, so pageable caller memory moves at PCIe
 // speed instead of through the runtime's own pageable path.  Small copies go direct.
+// the arena's zero padding after its last byte (< 64 bytes), copied from pinned zeros on st
+static hipError_t zero_pad(praos_ctx* c, uint8_t* dst, size_t pad, hipStream_t st) {
+  if (!c->zero_h) {
+    if (hipHostMalloc((void**)&c->zero_h, 64, hipHostMallocDefault) != hipSuccess) return hipErrorOutOfMemory;
+    std::memset(c->zero_h, 0, 64);
+  }
+  return hipMemcpyAsync(dst, c->zero_h, pad, hipMemcpyHostToDevice, st);
+}
+
 static bool stage_init(praos_ctx* c) {
   if (c->pin[0]) return true;
   for (int k = 0; k < 2; k++) {
@@ -643,6 +664,7 @@ static bool open_streams(praos_ctx* c) {
   if (const char* e = std::getenv("PRAOS_VRF_KEYS_FIRST")) c->vrf_keys_first = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_PRE_JOIN")) c->pre_join = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_V_MAIN")) c->v_main = std::atoi(e);
+  if (const char* e = std::getenv("PRAOS_STREAM_CHUNK_V")) c->stream_chunk_v = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_NOCACHE")) c->kes_nocache = (size_t)std::atoll(e);
   if (const char* e = std::getenv("PRAOS_MISS_PRIO")) c->miss_prio = std::atoi(e);
   if (const char* e = std::getenv("PRAOS_KES_PAIR")) c->kes_pair = std::atol(e);
@@ -683,9 +705,12 @@ static bool open_streams(praos_ctx* c) {
     (void)hipStreamCreateWithPriority(&c->vstream2, hipStreamNonBlocking, vprio);
     // the copy stream (uploads; the replay's decode): PRAOS_CSTREAM_PRIO=1 at the greatest priority
     const char* cp = std::getenv("PRAOS_CSTREAM_PRIO");
-    (void)hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking,
-                                      (cp && std::atoi(cp) == 1) ? greatest : least);
+    // (the copy / decode / download streams on hardware queues of their own -- CU-masked streams,
+    // every CU enabled -- or GPU_MAX_HW_QUEUES=16 were measured for the streaming form: no gain,
+    // 13.2-13.4 -> 13.5-13.7 ms per call, profiles/r06/l_stream)
+    (void)hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, (cp && std::atoi(cp) == 1) ? greatest : least);
     (void)hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&c->decstream, hipStreamNonBlocking);
   }
   return true;
 }
@@ -769,6 +794,7 @@ void praos_close(praos_ctx* c) {
     if (c->pin[k]) (void)hipHostFree(c->pin[k]);
     if (c->pin_ev[k]) (void)hipEventDestroy(c->pin_ev[k]);
   }
+  if (c->zero_h) (void)hipHostFree(c->zero_h);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : c->side_ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : c->miss_ev) if (e) (void)hipEventDestroy(e);
@@ -794,9 +820,14 @@ void praos_close(praos_ctx* c) {
     if (c->up_ev[k]) (void)hipEventDestroy(c->up_ev[k]);
     if (c->done_ev[k]) (void)hipEventDestroy(c->done_ev[k]);
   }
-  for (auto& p : c->pcall) if (p.ev) (void)hipEventDestroy(p.ev);
+  for (auto& p : c->pcall) {
+    if (p.ev) (void)hipEventDestroy(p.ev);
+    if (p.off_h) (void)hipHostFree(p.off_h);
+    if (p.len_h) (void)hipHostFree(p.len_h);
+  }
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->dstream) (void)hipStreamDestroy(c->dstream);
+  if (c->decstream) (void)hipStreamDestroy(c->decstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -915,7 +946,7 @@ int praos_set_epoch(praos_ctx* c, const uint8_t eta0[32], const praos_pool* pool
     if ((eta0 == nullptr) == c->eta0_neutral && (eta0 == nullptr || std::memcmp(eta0, c->eta0, 32) == 0))
       return PRAOS_OK;                            // the same nonce too: nothing to change
   }
-  if (c->pcall[0].active || c->pcall[1].active) {
+  if (std::any_of(std::begin(c->pcall), std::end(c->pcall), [](const praos_ctx::PipeCall& p) { return p.active; })) {
     // submitted calls (praos_verify_header_bytes_submit) read the installed view and nonce until
     // they end: their outputs first
     const int r = praos_verify_drain(c);
@@ -2183,7 +2214,7 @@ int rp_upload_decode(praos_ctx* c, praos_batch* b, size_t n, const praos_span* s
   b->body_bytes_len = (size_t)b->signed_stride * n;
   b->decoded = true;                               // praos_batch_run skips the decode
   const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
-  HIPCHK(c, hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream));
+  HIPCHK(c, zero_pad(c, b->arena + bytes, pad, c->cstream));
   if (bytes) HIPCHK(c, h2d_gather(c, b->arena, spans, nspans, bytes, c->cstream));
   if (n) {
     HIPCHK(c, h2d_on(c, b->hoff, hoff, 8 * n, c->cstream));
@@ -2286,6 +2317,7 @@ extern "C" {
 // call's key chains, as back-to-back resident runs overlap.
 static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec,
                                   int K, int slot = 0, bool async = false) {
+  const auto t_entry = std::chrono::steady_clock::now();
   HIPCHK(c, hipSetDevice(c->device));
   const size_t n = in->n;
   // the arena span of the in-range headers, and offsets rebased to it
@@ -2296,8 +2328,23 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
     end = std::max<uint64_t>(end, in->off[i] + in->len[i]);
   }
   if (base == UINT64_MAX) base = end = 0;
-  std::vector<uint64_t>& off = c->pcall[slot].off;
-  off.resize(n);
+  praos_ctx::PipeCall& pc = c->pcall[slot];
+  if (pc.cap < n) {                     // (the slot's previous call has finished: its H2D is done)
+    if (pc.off_h) (void)hipHostFree(pc.off_h);
+    if (pc.len_h) (void)hipHostFree(pc.len_h);
+    pc.off_h = nullptr;
+    pc.len_h = nullptr;
+    pc.cap = 0;
+    const size_t cap = n + n / 8 + 64;
+    if (hipHostMalloc((void**)&pc.off_h, 8 * cap, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&pc.len_h, 4 * cap, hipHostMallocDefault) != hipSuccess) {
+      c->err = "pinned offsets";
+      return PRAOS_E_OOM;
+    }
+    pc.cap = cap;
+  }
+  uint64_t* off = pc.off_h;
+  std::memcpy(pc.len_h, in->len, 4 * n);
   for (size_t i = 0; i < n; i++) {   // a span outside the caller's arena stays outside
     const bool in_range = in->off[i] <= in->bytes_len && in->len[i] <= in->bytes_len - in->off[i];
     off[i] = in_range ? in->off[i] - base : UINT64_MAX / 2;
@@ -2342,26 +2389,26 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
   b->arena_len = bytes;
   b->body_bytes_len = (size_t)b->signed_stride * n;
   const size_t pad = ((bytes + 7) & ~(size_t)7) + 16 - bytes;
-  HIPCHK(c, hipMemsetAsync(b->arena + bytes, 0, pad, c->cstream));
-  HIPCHK(c, hipMemcpyAsync(b->hoff, off.data(), 8 * n, hipMemcpyHostToDevice, c->cstream));
-  HIPCHK(c, hipMemcpyAsync(b->hlen, in->len, 4 * n, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(c, zero_pad(c, b->arena + bytes, pad, c->cstream));
+  HIPCHK(c, hipMemcpyAsync(b->hoff, off, 8 * n, hipMemcpyHostToDevice, c->cstream));
+  HIPCHK(c, hipMemcpyAsync(b->hlen, pc.len_h, 4 * n, hipMemcpyHostToDevice, c->cstream));
   if (c->keycache > 0 && n >= 2) {               // the comb the cached chains read (built once)
     const int rc = ensure_bcomb16(c);
     if (rc != PRAOS_OK) return rc;
   }
   const uint32_t* eta = b->eta_tab ? b->eta_tab : c->d_eta0;
-  const bool vrf = (c->kernels & 4) != 0;
+  // stage V chunk by chunk under the upload, or (submitted calls, PRAOS_STREAM_CHUNK_V=0) in the
+  // run over the whole batch
+  const bool vrf = (c->kernels & 4) != 0 && (!async || c->stream_chunk_v);
   uint64_t sent = 0;
   for (int k = 0; k < K; k++) {
     if (need[k] > sent) {
       HIPCHK(c, h2d_on(c, b->arena + sent, in->bytes + base + sent, need[k] - sent, c->cstream));
       sent = need[k];
     }
-    hipStream_t sd = async ? c->cstream : c->stream;      // the chunk's decode
-    if (!async) {
-      HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->up_ev[k], 0));
-    }
+    hipStream_t sd = async ? c->decstream : c->stream;    // the chunk's decode
+    HIPCHK(c, hipEventRecord(c->up_ev[k], c->cstream));
+    HIPCHK(c, hipStreamWaitEvent(sd, c->up_ev[k], 0));
     const size_t m = lo[k + 1] - lo[k];
     if (m) {
       launch_decode_praos(dim3(nblocks(m, NT)), dim3(NT), sd, lo[k + 1], b->arena, bytes, b->hoff, b->hlen,
@@ -2383,9 +2430,14 @@ static int verify_bytes_pipelined(praos_ctx* c, const praos_header_bytes* in, pr
     }
   }
   if (async) HIPCHK(c, hipStreamWaitEvent(c->stream, c->done_ev[K - 1], 0));   // every chunk decoded
+  const auto t_chunks = std::chrono::steady_clock::now();
   b->decoded = true;
   b->v_done = vrf;
   int r = praos_batch_run(c, b);
+  if (async && std::getenv("PRAOS_SUBMIT_TRACE"))
+    std::fprintf(stderr, "submit: chunks queued %.3f ms after entry, run queued %.3f ms\n",
+                 std::chrono::duration<double, std::milli>(t_chunks - t_entry).count(),
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_chunks).count());
   b->decoded = false;                // (the downloads below still read b->n; the next call resets
   b->v_done = false;                 // every per-run field when it takes the batch: batch_reuse_reset)
   if (async) {
@@ -2472,10 +2524,12 @@ static int pipe_finish(praos_ctx* c, int slot) {
 int praos_verify_drain(praos_ctx* c) {
   if (!c) return PRAOS_E_ARG;
   if (c->device < 0) return PRAOS_OK;
-  const int older = c->pcall_next;             // the slot the next submit reuses holds the older call
-  int r = pipe_finish(c, older);
-  const int r2 = pipe_finish(c, older ^ 1);
-  return r != PRAOS_OK ? r : r2;
+  int r = PRAOS_OK;
+  for (int j = 0; j < PIPE_CALLS; j++) {       // oldest first: the slot the next submit reuses
+    const int rj = pipe_finish(c, (c->pcall_next + j) % PIPE_CALLS);
+    if (r == PRAOS_OK) r = rj;
+  }
+  return r;
 }
 
 int praos_verify_header_bytes_submit(praos_ctx* c, const praos_header_bytes* in, praos_out* out, praos_decoded* dec) {
@@ -2490,10 +2544,14 @@ int praos_verify_header_bytes_submit(praos_ctx* c, const praos_header_bytes* in,
     return r != PRAOS_OK ? r : praos_verify_header_bytes(c, in, out, dec);
   }
   const int slot = c->pcall_next;
-  int r = pipe_finish(c, slot);                // two in flight: the older one's outputs first
+  const auto t0 = std::chrono::steady_clock::now();
+  int r = pipe_finish(c, slot);                // PIPE_CALLS in flight: the oldest one's outputs first
   if (r != PRAOS_OK) return r;
+  if (std::getenv("PRAOS_SUBMIT_TRACE"))
+    std::fprintf(stderr, "submit: finish of the oldest call %.3f ms\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   r = verify_bytes_pipelined(c, in, out, dec, K, slot, true);
-  if (r == PRAOS_OK) c->pcall_next = slot ^ 1;
+  if (r == PRAOS_OK) c->pcall_next = (slot + 1) % PIPE_CALLS;
   return r;
 }
 

@@ -633,15 +633,15 @@ class Context:
 
     def submit_header_bytes(self, arena, off, length, out, decoded=None):
         """Streaming form of verify_header_bytes (praos_verify_header_bytes_submit): queued, returns
-        at once; out (and decoded, an alloc_decoded pair) are written by the submit after the next
-        one or by drain().  The inputs and outputs stay referenced here until drained."""
+        at once; out (and decoded, an alloc_decoded pair) are written by the third submit after it
+        or by drain().  The inputs and outputs stay referenced here until drained."""
         arena, off, length = self._chunk(arena, off, length)
         hb = self.header_bytes_struct(arena, off, length)
         os_ = self.out_struct(out)
         d = decoded[1] if decoded is not None else None
         self.check(self.L.praos_verify_header_bytes_submit(self.h, ctypes.byref(hb), ctypes.byref(os_),
                                                            ctypes.byref(d) if d is not None else None))
-        self._inflight = (getattr(self, "_inflight", []) + [(arena, off, length, hb, os_, out, decoded)])[-3:]
+        self._inflight = (getattr(self, "_inflight", []) + [(arena, off, length, hb, os_, out, decoded)])[-4:]
 
     def drain(self):
         """Every submitted call's outputs written (praos_verify_drain)."""

@@ -188,14 +188,20 @@ def test_pipelined_bytes_equals_single_batch(ctx, c5_batch, chunks):
     assert D1["status"][5000] & abi.DEC_RANGE and o1["bits"][5000] & abi.BIT_INPUT
 
 
-def test_submitted_bytes_equal_blocking(ctx, c5_batch):
-    """The streaming form (praos_verify_header_bytes_submit, two calls in flight, outputs written by
-    the submit after next or by praos_verify_drain) gives each call the blocking call's outputs and
+@pytest.mark.parametrize("chunk_v", [None, "0"])
+def test_submitted_bytes_equal_blocking(ctx, c5_batch, chunk_v, monkeypatch):
+    """The streaming form (praos_verify_header_bytes_submit, three calls in flight, outputs written by
+    the third submit after or by praos_verify_drain) gives each call the blocking call's outputs and
     decoded fields bit for bit: different inputs back to back (a damaged copy of the arena, the
     headers in another order), a blocking call that drains the calls in flight, and a page-locked
-    arena and outputs (direct DMA from the caller's memory)."""
+    arena and outputs (direct DMA from the caller's memory); with stage V chunk by chunk under the
+    upload (default) and in the run (PRAOS_STREAM_CHUNK_V=0, a context of its own)."""
+    import praos_hip
     from praos_hip import abi
     cfg, H, pool_list, corrupted, p, arena, off, ln = c5_batch
+    if chunk_v is not None:
+        monkeypatch.setenv("PRAOS_STREAM_CHUNK_V", chunk_v)
+        ctx = praos_hip.Context(0)
     n = len(off)
     rng = np.random.default_rng(7)
     arena_b = arena.copy()
@@ -244,6 +250,8 @@ def test_submitted_bytes_equal_blocking(ctx, c5_batch):
     finally:
         ctx.drain()
         ctx.set_option(abi.OPT_PIPELINE, 0)
+        if chunk_v is not None:
+            ctx.close()
 
 
 @pytest.mark.parametrize("env,concurrent", [({"PRAOS_PRE_JOIN": "0"}, 1), ({"PRAOS_PRE_JOIN": "1"}, 1),
