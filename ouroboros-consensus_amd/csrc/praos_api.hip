@@ -367,7 +367,7 @@ struct praos_ctx {
   // allocation per 432k batch cost its page faults and its unmapping on every call)
   std::unique_ptr<uint8_t[]> h_arena;
   size_t h_arena_cap = 0;
-  std::vector<uint64_t> h_off, h_off2;
+  std::vector<uint64_t> h_off;
   std::vector<uint32_t> h_len;
 };
 
