@@ -417,8 +417,55 @@ static void phase_binding(const chain_t* ch, int members) {
   else praos_close(ctx);
 }
 
-/* ---- phase 1b: Batch/Validate.hs validateEpochHeaders (Storable vectors, registered arena) ---- */
-static void phase_typed(const chain_t* ch, int members) {
+/* ---- phase 1b: Batch/Validate.hs validateEpochHeaders (Storable vectors, registered arena) ----
+ * sub > 0 (one context): each epoch's headers as `sub` consecutive batches through the streaming
+ * form (Batch.hs praosSubmitHeaderBytes / praosDrainHeaderBytes: praos_verify_header_bytes_submit
+ * with the chunked pipeline forced on, then praos_verify_drain), folded in order afterwards. */
+typedef struct {
+  size_t i0, n, alen;
+  uint8_t *arena, *verdict, *decbuf;
+  uint64_t* off;
+  uint16_t* bits;
+  int32_t* pidx;
+  praos_header_bytes hb;
+  praos_out out;
+  praos_decoded dec;
+} part_t;
+
+static void part_init(part_t* p, const chain_t* ch, size_t i0, size_t n) {
+  memset(p, 0, sizeof *p);
+  p->i0 = i0;
+  p->n = n;
+  for (size_t k = 0; k < n; k++) p->alen += ch->hlen[i0 + k];
+  p->arena = malloc(p->alen ? p->alen : 1);
+  p->off = malloc(8 * (n ? n : 1));
+  for (size_t k = 0, o = 0; k < n; o += ch->hlen[i0 + k], k++) {   /* the spans back to back */
+    memcpy(p->arena + o, ch->bytes + ch->off[i0 + k], ch->hlen[i0 + k]);
+    p->off[k] = o;
+  }
+  p->verdict = calloc(n ? n : 1, 1);
+  p->bits = calloc(n ? n : 1, 2);
+  p->pidx = calloc(n ? n : 1, 4);
+  p->decbuf = calloc(n ? n : 1, 157);  /* slot, block no, ocert n | prev, cold, hash | body size | gen | nonce */
+  praos_header_bytes hb = {n, p->arena, p->alen, p->off, ch->hlen + i0};
+  p->hb = hb;
+  praos_out out = {p->bits, p->pidx, NULL, NULL, p->decbuf + 125 * n};   /* nonce values: the fold evolves them */
+  p->out = out;
+  p->dec.slot = (uint64_t*)p->decbuf;
+  p->dec.block_no = (uint64_t*)(p->decbuf + 8 * n);
+  p->dec.ocert_n = (uint64_t*)(p->decbuf + 16 * n);
+  p->dec.prev_hash = p->decbuf + 24 * n;
+  p->dec.cold_vk = p->decbuf + 56 * n;
+  p->dec.header_hash = p->decbuf + 88 * n;
+  p->dec.body_size = (uint32_t*)(p->decbuf + 120 * n);
+  p->dec.prev_is_genesis = p->decbuf + 124 * n;
+}
+
+static void part_free(part_t* p) {
+  free(p->arena); free(p->off); free(p->verdict); free(p->bits); free(p->pidx); free(p->decbuf);
+}
+
+static void phase_typed(const chain_t* ch, int members, int sub) {
   praos_group* g = NULL;
   praos_ctx* ctx;
   if (members > 0) {
@@ -430,6 +477,7 @@ static void phase_typed(const chain_t* ch, int members) {
     ctx = praos_open(0);
   }
   if (!ctx) DIE("praos_open(0)");
+  if (sub > 0) CK(ctx, praos_set_option(ctx, PRAOS_OPT_PIPELINE, 2));
   static state_buf S;
   genesis_state(&S);
   praos_envelope env = g_env0;
@@ -437,11 +485,11 @@ static void phase_typed(const chain_t* ch, int members) {
   int stop_verdict = 0;
   unsigned stop_bits = 0;
   size_t i = 0;
-  while (i < ch->n) {
+  int stopped = 0;
+  while (i < ch->n && !stopped) {
     const uint64_t e = (ch->slot[i] - g_ei.epoch_base_slot) / g_ei.epoch_length;
     size_t j = i;
     while (j < ch->n && (ch->slot[j] - g_ei.epoch_base_slot) / g_ei.epoch_length == e) j++;
-    const size_t n = j - i;
     praos_nonce eta;
     CK(ctx, praos_ticked_epoch_nonce(&S.st, &g_ei, ch->slot[i], &eta));
     if (g) {
@@ -451,57 +499,56 @@ static void phase_typed(const chain_t* ch, int members) {
       CK(ctx, praos_set_epoch(ctx, eta.neutral ? NULL : eta.hash, g_pools, g_npools, &g_params));
     }
     epochs++;
-    /* the epoch's arena: its header spans back to back (what the binding concatenates) */
-    size_t alen = 0;
-    for (size_t k = 0; k < n; k++) alen += ch->hlen[i + k];
-    uint8_t* arena = malloc(alen ? alen : 1);
-    uint64_t* off = malloc(8 * n);
-    for (size_t k = 0, o = 0; k < n; o += ch->hlen[i + k], k++) {
-      memcpy(arena + o, ch->bytes + ch->off[i + k], ch->hlen[i + k]);
-      off[k] = o;
+    const int np = sub > 0 ? sub : 1;
+    part_t parts[8];
+    for (int q = 0; q < np; q++) {
+      const size_t a = i + (j - i) * (size_t)q / (size_t)np, b = i + (j - i) * (size_t)(q + 1) / (size_t)np;
+      part_init(&parts[q], ch, a, b - a);
     }
-    uint8_t* verdict = calloc(n, 1);
-    uint16_t* bits = calloc(n, 2);
-    int32_t* pidx = calloc(n, 4);
-    uint8_t* decbuf = calloc(n, 157);      /* slot, block no, ocert n | prev, cold, hash | body size | gen | nonce */
-    uint64_t *slot = (uint64_t*)decbuf, *bno = (uint64_t*)(decbuf + 8 * n), *ocn = (uint64_t*)(decbuf + 16 * n);
-    uint8_t *prev = decbuf + 24 * n, *cold = decbuf + 56 * n, *hh = decbuf + 88 * n, *gen = decbuf + 124 * n;
-    uint32_t* bsz = (uint32_t*)(decbuf + 120 * n);
-    uint8_t* nonce = decbuf + 125 * n;     /* the certified VRF outputs' nonce values (the fold evolves them) */
-    praos_header_bytes hb = {n, arena, alen, off, ch->hlen + i};
-    praos_out out = {bits, pidx, NULL, NULL, nonce};
-    praos_decoded dec;
-    memset(&dec, 0, sizeof dec);
-    dec.slot = slot; dec.block_no = bno; dec.ocert_n = ocn; dec.prev_hash = prev; dec.prev_is_genesis = gen;
-    dec.cold_vk = cold; dec.header_hash = hh; dec.body_size = bsz;
-    if (g) {
-      if (praos_group_host_register(g, arena, alen ? alen : 1) != PRAOS_OK ||
-          praos_group_verify_header_bytes(g, &hb, &out, &dec) != PRAOS_OK ||
-          praos_group_host_unregister(g, arena) != PRAOS_OK)
-        DIE("%s", praos_group_last_error(g));
-    } else {
-      CK(ctx, praos_host_register(ctx, arena, alen ? alen : 1));
-      CK(ctx, praos_verify_header_bytes(ctx, &hb, &out, &dec));
-      CK(ctx, praos_host_unregister(ctx, arena));
+    for (int q = 0; q < np; q++) {
+      part_t* p = &parts[q];
+      if (g) {
+        if (praos_group_host_register(g, p->arena, p->alen ? p->alen : 1) != PRAOS_OK ||
+            praos_group_verify_header_bytes(g, &p->hb, &p->out, &p->dec) != PRAOS_OK ||
+            praos_group_host_unregister(g, p->arena) != PRAOS_OK)
+          DIE("%s", praos_group_last_error(g));
+      } else if (sub > 0) {
+        CK(ctx, praos_host_register(ctx, p->arena, p->alen ? p->alen : 1));
+        CK(ctx, praos_verify_header_bytes_submit(ctx, &p->hb, &p->out, &p->dec));
+      } else {
+        CK(ctx, praos_host_register(ctx, p->arena, p->alen ? p->alen : 1));
+        CK(ctx, praos_verify_header_bytes(ctx, &p->hb, &p->out, &p->dec));
+        CK(ctx, praos_host_unregister(ctx, p->arena));
+      }
     }
-    praos_headers h;
-    memset(&h, 0, sizeof h);
-    h.n = n; h.slot = slot; h.cold_vk = cold; h.ocert_n = ocn;
-    env.block_no = bno; env.header_hash = hh; env.header_size = ch->hlen + i; env.body_size = bsz;
-    size_t stop = 0, done = 0;
-    CK(ctx, praos_validate_headers(ctx, &h, prev, gen, &out, &env, &g_ei, &S.st, verdict, &stop, &done));
-    if (done != n) DIE("an epoch batch did not fold through (%zu of %zu)", done, n);
-    const int stopped = stop < n;
-    if (stopped) {
-      stop_index = i + stop; stop_verdict = verdict[stop]; stop_bits = bits[stop]; validated += stop;
-    } else {
-      validated += n;
+    if (sub > 0) {
+      CK(ctx, praos_verify_drain(ctx));
+      for (int q = 0; q < np; q++) CK(ctx, praos_host_unregister(ctx, parts[q].arena));
     }
-    free(arena); free(off); free(verdict); free(bits); free(pidx); free(decbuf);
-    if (stopped) break;
+    for (int q = 0; q < np && !stopped; q++) {
+      part_t* p = &parts[q];
+      const size_t n = p->n;
+      praos_headers h;
+      memset(&h, 0, sizeof h);
+      h.n = n; h.slot = p->dec.slot; h.cold_vk = p->dec.cold_vk; h.ocert_n = p->dec.ocert_n;
+      env.block_no = p->dec.block_no; env.header_hash = p->dec.header_hash; env.header_size = ch->hlen + p->i0;
+      env.body_size = p->dec.body_size;
+      size_t stop = 0, done = 0;
+      CK(ctx, praos_validate_headers(ctx, &h, p->dec.prev_hash, p->dec.prev_is_genesis, &p->out, &env, &g_ei, &S.st,
+                                     p->verdict, &stop, &done));
+      if (done != n) DIE("an epoch batch did not fold through (%zu of %zu)", done, n);
+      if (stop < n) {
+        stopped = 1;
+        stop_index = p->i0 + stop; stop_verdict = p->verdict[stop]; stop_bits = p->bits[stop]; validated += stop;
+      } else {
+        validated += n;
+      }
+    }
+    for (int q = 0; q < np; q++) part_free(&parts[q]);
     i = j;
   }
-  print_state(g ? "typed_group" : "typed", &S, &env, validated, stop_index, stop_verdict, epochs, (long)stop_bits);
+  print_state(g ? "typed_group" : sub > 0 ? "typed_stream" : "typed", &S, &env, validated, stop_index, stop_verdict,
+              epochs, (long)stop_bits);
   if (g) praos_group_close(g);
   else praos_close(ctx);
 }
@@ -900,8 +947,9 @@ int main(int argc, char** argv) {
   if (T < 1 || T > 64) DIE("threads: 1..64");
   phase_binding(&ch, 0);
   if (g_tpraos) phase_binding(&ch, T);
-  if (!g_tpraos) phase_typed(&ch, 0);
-  if (!g_tpraos) phase_typed(&ch, T);
+  if (!g_tpraos) phase_typed(&ch, 0, 0);
+  if (!g_tpraos) phase_typed(&ch, T, 0);
+  if (!g_tpraos) phase_typed(&ch, 0, 3);
   phase_replay(argv[1], 0);
   phase_replay(argv[1], T);
   if (!g_tpraos) {

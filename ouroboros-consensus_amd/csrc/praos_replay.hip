@@ -342,6 +342,10 @@ int rp_replay(praos_ctx* const* mem, int m, const char* dir, const praos_pool* p
   praos_ctx* const ctx = m > 0 && mem ? mem[0] : nullptr;
   for (int q = 0; q < m; q++)
     if (!mem[q]) return PRAOS_E_ARG;
+  for (int q = 0; q < m; q++) {     // submitted stored-bytes calls read the tables the replay swaps
+    const int rd = praos_verify_drain(mem[q]);
+    if (rd != PRAOS_OK) return rd;
+  }
   if (!ctx || !dir || !params || (npools && !pools) || !ei || !env || !st || !stats || batch_max == 0 ||
       ei->epoch_length == 0 || (verdicts_cap && !verdicts) || (views && (nviews == 0 || tpraos)))
     return PRAOS_E_ARG;

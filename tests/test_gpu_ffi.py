@@ -53,7 +53,7 @@ def _python_replay(ctx, chain, db):
 
 
 def _agree(out, stats, cbor, tip):
-    for phase in ("binding", "binding_group", "typed", "typed_group", "replay", "replay_group"):
+    for phase in ("binding", "binding_group", "typed", "typed_group", "typed_stream", "replay", "replay_group"):
         if phase not in out:                 # (no typed phases for TPraos databases, no binding_group for Praos)
             continue
         o = out[phase]
@@ -74,6 +74,8 @@ def test_ffi_sequence_matches_replay(ctx, chain, tmp_path):  # noqa: F811
     # the group sequences (validateEpochHeaders on withPraosBatchDevices [0,0,0,0]; the replay dealt
     # over 4 members in 97-header batches) end in the same state
     assert {"typed_group", "replay_group"} <= set(out) and out["typed_group"]["stop_bits"] == 0
+    # the streaming form (praosSubmitHeaderBytes: each epoch as 3 batches in flight, then the drain)
+    assert out["typed_stream"]["epochs"] == 4 and out["typed_stream"]["stop_bits"] == 0
     _agree(out, stats, cbor, tip)
     t = out["threads"]
     assert t["threads_equal"] and t["group_equal"] and t["group_size"] == 4
@@ -98,7 +100,7 @@ def test_ffi_sequence_stops_with_replay(ctx, chain, tmp_path):  # noqa: F811
     # the typed path (Batch/Validate.hs) gets the stopping header's bits: a KES failure in
     # the leaf signature, which Batch.Errors turns into InvalidKesSignatureOCERT
     assert out["typed"]["stop_bits"] & (abi.BIT_KES_MERKLE | abi.BIT_KES_LEAF)
-    assert out["typed_group"]["stop_bits"] == out["typed"]["stop_bits"]
+    assert out["typed_group"]["stop_bits"] == out["typed"]["stop_bits"] == out["typed_stream"]["stop_bits"]
 
 
 def test_ffi_tpraos_sequence_matches_replay(ctx, tchain, tmp_path):  # noqa: F811
