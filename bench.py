@@ -627,10 +627,11 @@ def main():
                    "pageable": {"value": round(n / te_pageable, 1), "ms": round(te_pageable * 1e3, 2),
                                 "note": "the same calls with the arena and outputs in pageable memory: "
                                         "uploads staged through the library's pinned buffers by 16 host threads"},
-                   "path": "praos_verify_header_bytes: stored header bytes (host arena page-locked once with "
-                           "praos_host_register) -> H2D in 8 chunks on a copy stream, each landed chunk decoded "
+                   "path": "praos_verify_header_bytes[_submit]: stored header bytes (host arena page-locked once "
+                           "with praos_host_register) -> H2D in 8 chunks on a copy stream, each landed chunk decoded "
                            "and its VRF stage V run while later chunks upload -> the rest of the batch once -> "
-                           "VRF outputs D2H while the KES checks finish (best of 3 calls)"}
+                           "outputs D2H; streaming: the next calls' uploads, decodes and stage V under this call's "
+                           "key chains"}
         # the host-SoA entry point (every decoded field from the host, 1,236 B per header)
         oe = ctx.verify_headers(H)
         te = time.perf_counter()

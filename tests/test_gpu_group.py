@@ -247,8 +247,25 @@ def test_submitted_bytes_equal_blocking(ctx, c5_batch, chunk_v, monkeypatch):
         for o in outs:
             for k in o:
                 assert np.array_equal(o[k], ref[0][0][k]), k
+        # a new epoch nonce while calls are in flight: praos_set_epoch finishes them first (under the
+        # nonce they were queued with); a call after it runs under the new one
+        eta1 = bytes(32 - len(b"other")) + b"other"
+        ctx.set_epoch(eta1, pool_list, p)
+        ref1 = ctx.verify_header_bytes(arena, off, ln)
+        assert not np.array_equal(ref1["bits"], ref[0][0]["bits"])
+        ctx.set_epoch(cfg["eta0"], pool_list, p)
+        outs = [ctx.alloc_out(n) for _ in range(3)]
+        ctx.submit_header_bytes(arena, off, ln, out=outs[0])
+        ctx.submit_header_bytes(arena, off, ln, out=outs[1])
+        ctx.set_epoch(eta1, pool_list, p)
+        ctx.submit_header_bytes(arena, off, ln, out=outs[2])
+        ctx.drain()
+        for o, want in zip(outs, (ref[0][0], ref[0][0], ref1)):
+            for k in o:
+                assert np.array_equal(o[k], want[k]), k
     finally:
         ctx.drain()
+        ctx.set_epoch(cfg["eta0"], pool_list, p)
         ctx.set_option(abi.OPT_PIPELINE, 0)
         if chunk_v is not None:
             ctx.close()
