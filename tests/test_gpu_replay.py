@@ -382,14 +382,14 @@ def test_tpraos_replay_stops_at_corruption(ctx, tchain, tmp_path):
 _TIMES = ("ms_io", "ms_device", "ms_fold", "ms_nonce")
 
 
-def _same_replay(a, b):
+def _same_replay(a, b, ignore=()):
     """Two replays' (stats, verdicts, state, envelope) agree except for the timings (and, for a
     replay that stopped early, the counts of batches whose crypto was already queued and of chunk
     files the reader had opened by then: they depend on how many batches the pipeline keeps in
     flight -- RP_SLOTS, 4 per context -- and on how far the reader got before the stop)."""
     (sa, va, sta, ea), (sb, vb, stb, eb) = a, b
     stopped = sa["stop_index"] < sa["headers"] + sa["skipped"] or sa["stop_verdict"]
-    skip = _TIMES + (("batches", "chunks") if stopped else ())
+    skip = _TIMES + (("batches", "chunks") if stopped else ()) + tuple(ignore)
     assert {k: v for k, v in sa.items() if k not in skip} == {k: v for k, v in sb.items() if k not in skip}
     assert np.array_equal(va, vb) and sta == stb and ea["tip"] == eb["tip"]
 
@@ -527,14 +527,16 @@ def test_reused_batches_alternate_replay_and_pipeline(chain):
 
 @pytest.mark.parametrize("env", [{"PRAOS_REPLAY_EARLY": "1"}, {"PRAOS_REPLAY_EARLY": "2"},
                                  {"PRAOS_REPLAY_PIN": "1"}, {"PRAOS_CSTREAM_PRIO": "1"},
-                                 {"PRAOS_PARSE_THREADS": "0"}, {"PRAOS_PARSE_THREADS": "1"}])
+                                 {"PRAOS_PARSE_THREADS": "0"}, {"PRAOS_PARSE_THREADS": "1"},
+                                 {"PRAOS_REPLAY_RAMP": "0"}, {"PRAOS_REPLAY_RAMP": "2"}])
 def test_replay_schedule_options_equal_default(ctx, chain, tmp_path, monkeypatch, env):
     """Host-schedule options of the replay give the default replay's stats, verdicts, state and tip:
     crypto launched as soon as the batch's epoch nonces are published (PRAOS_REPLAY_EARLY 1; 2: and
     the next batch decoded), pinned threads (PRAOS_REPLAY_PIN), the copy / decode stream at the
     greatest priority (PRAOS_CSTREAM_PRIO, read when a context opens), the nonce chain on the
     device decode's fields instead of the host's reading of the headers (PRAOS_PARSE_THREADS=0), or
-    that reading on one worker -- over the
+    that reading on one worker, other batch-size ramps (PRAOS_REPLAY_RAMP 0 / 2: the batch count
+    differs) -- over the
     clean 4-epoch database (one context, 97-header batches; a 3-member group) and over one damaged
     in epoch 2 (the stop, its verdict and the state before it)."""
     from praos_hip import abi
@@ -558,7 +560,7 @@ def test_replay_schedule_options_equal_default(ctx, chain, tmp_path, monkeypatch
     with abi.Group([0] * 3) as g:
         ggot = _group_replay(g, chain, batch_max=61)
     for a, b in list(zip(base, got)) + [(gbase, ggot)]:
-        _same_replay(a, b)
+        _same_replay(a, b, ("batches",) if "PRAOS_REPLAY_RAMP" in env else ())
     assert got[2][0]["stop_index"] == k and got[2][0]["stop_verdict"] == abi.V_KES_SIG
     assert got[0][2] == chain["state"] and ggot[2] == chain["state"]
 
