@@ -164,6 +164,8 @@ __global__ void k_debug_fe(int op, size_t n, const uint8_t* a, const uint8_t* b,
     case 3: fe_sub(z, x, y); break;
     case 4: fe_invert(z, x); break;
     case 5: fe_pow22523(z, x); break;
+    case 7: z = fe_invert_v(x); break;         // Fermat's chain (the PRAOS_INV_GCD=0 inversion)
+    case 8: z = fe_invert_gcd_v(x); break;     // the binary GCD (fe_inv_gcd.hpp)
     default: fe_canon(z, x); break;
   }
   store_words(r + 32 * i, z.v, 8);

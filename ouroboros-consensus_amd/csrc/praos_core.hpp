@@ -677,7 +677,7 @@ FE_INLINE bool vrf_join_core(uint32_t beta[16], bool& gamma_ok, const uint4* __r
     fe_mul(z12, UZ, VZ);
     fe_mul(z123, z12, G8Z);
     fe_mul(z1234, z123, HZ);
-    fe_invert_inl(inv, z1234);       // inline: no caller-saved registers around a call
+    fe_invert_sel_inl(inv, z1234);   // inline: no caller-saved registers around a call
     fe_mul(zi, inv, z123);            // 1/H.Z
     fe_mul(inv, inv, HZ);             // 1/(U.Z V.Z G8.Z)
     fe X, Y;

@@ -77,6 +77,21 @@ def test_fe_invert_pow_canon(ctx):
         assert c == x % P
 
 
+def test_fe_invert_gcd_vs_fermat(ctx):
+    """The binary-GCD inversion (fe_inv_gcd.hpp, op 8) and Fermat's chain (op 7) give the same
+    field element on edge, structured and random inputs, weakly reduced (< 2^256)."""
+    xs, _ = _fe_inputs(5, 3000)
+    xs += [2 ** k for k in range(256)] + [P - 2 ** k for k in range(255)] + [2 ** k - 1 for k in range(1, 257)]
+    a, b = 1, 1
+    while b < 2 ** 256:
+        xs.append(b)
+        a, b = b, a + b
+    g = _from(ctx.debug_fe(8, _to(xs)))
+    f = _from(ctx.debug_fe(7, _to(xs)))
+    for x, u, v in zip(xs, g, f):
+        assert u % P == v % P == pow(x % P, P - 2, P), hex(x)
+
+
 def test_sha512_stream(ctx):
     r = rng(3)
     lens = list(range(0, 140)) + [300, 397, 461, 511, 512, 1000]
