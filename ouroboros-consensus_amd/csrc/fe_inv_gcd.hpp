@@ -67,9 +67,13 @@
 #endif
 // iterations before the first exit test: random inputs end within 13 (99.9 %) or 14
 // (tests/test_inv_gcd.py measures it), the bound is 17
-// FEG_INNER32=1: the inner steps on 32-bit halves (A/B against the 64-bit compare and shift)
+// FEG_INNER32=1: the inner steps on 32-bit halves (A/B against the 64-bit compare and shift);
+// FEG_INNER_MASK=1: the conditions as VGPR masks (A/B against compares into SGPR masks)
 #ifndef FEG_INNER32
 #define FEG_INNER32 0
+#endif
+#ifndef FEG_INNER_MASK
+#define FEG_INNER_MASK 0
 #endif
 #ifndef FEG_EXIT_FROM
 #define FEG_EXIT_FROM 12
@@ -223,6 +227,29 @@ FEG_INLINE bool feg_core(uint32_t vout[8], const uint32_t y[8], int* iters) {
       const int32_t nf0 = sw ? f1 : f0, ng0 = sw ? g1 : g0, nf1 = sw ? f0 : f1, ng1 = sw ? g0 : g1;
       f0 = odd ? nf0 - nf1 : nf0;
       g0 = odd ? ng0 - ng1 : ng0;
+      f1 = nf1 * 2;
+      g1 = ng1 * 2;
+    }
+#elif FEG_INNER_MASK
+    // the same steps with the conditions as all-ones VGPR masks and bit selects: no compare into
+    // an SGPR mask and no scalar AND between the vector instructions of a step (ah, bh < 2^62, so
+    // the sign of ah - bh is ah < bh)
+#pragma unroll
+    for (int j = 0; j < 30; j++) {
+      const uint64_t d = ah - bh;
+      const uint32_t oddm = 0u - ((uint32_t)ah & 1u);
+      const uint32_t ltm = (uint32_t)((int64_t)d >> 63);
+      const uint32_t swm = oddm & ltm;
+      const uint64_t sw64 = ((uint64_t)swm << 32) | swm, odd64 = ((uint64_t)oddm << 32) | oddm;
+      const uint64_t lt64 = ((uint64_t)ltm << 32) | ltm;
+      const uint64_t ad = (d ^ lt64) - lt64;                   // |ah - bh|
+      bh = (ah & sw64) | (bh & ~sw64);
+      ah = ((ad & odd64) | (ah & ~odd64)) >> 1;
+      const int32_t sf = (int32_t)swm, so = (int32_t)oddm;
+      const int32_t nf0 = (f1 & sf) | (f0 & ~sf), ng0 = (g1 & sf) | (g0 & ~sf);
+      const int32_t nf1 = (f0 & sf) | (f1 & ~sf), ng1 = (g0 & sf) | (g1 & ~sf);
+      f0 = nf0 - (nf1 & so);
+      g0 = ng0 - (ng1 & so);
       f1 = nf1 * 2;
       g1 = ng1 * 2;
     }

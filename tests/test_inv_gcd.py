@@ -19,9 +19,6 @@ HDR = os.path.join(os.path.dirname(__file__), "..", "ouroboros-consensus_amd", "
 SHIM = r"""
 #define FEG_INLINE static inline
 #define FEG_ALL(x) (x)
-#ifndef FEG_INNER32
-#define FEG_INNER32 0
-#endif
 #include "fe_inv_gcd.hpp"
 extern "C" void feg_batch(long n, const uint32_t* in, uint32_t* out, uint8_t* ok, int32_t* iters) {
   for (long i = 0; i < n; i++) ok[i] = feg_core(out + 8 * i, in + 8 * i, iters + i) ? 1 : 0;
@@ -29,13 +26,14 @@ extern "C" void feg_batch(long n, const uint32_t* in, uint32_t* out, uint8_t* ok
 """
 
 
-@pytest.fixture(scope="module", params=[0, 1], ids=["inner64", "inner32"])
+@pytest.fixture(scope="module", params=["-DFEG_INNER32=0", "-DFEG_INNER32=1", "-DFEG_INNER_MASK=1"],
+                ids=["inner64", "inner32", "inner_mask"])
 def lib(tmp_path_factory, request):
-    d = tmp_path_factory.mktemp("feg%d" % request.param)
+    d = tmp_path_factory.mktemp("feg")
     src = d / "shim.cpp"
     src.write_text(SHIM)
     so = d / "libfeg.so"
-    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-DFEG_INNER32=%d" % request.param, "-I", os.path.abspath(HDR),
+    subprocess.run(["g++", "-O2", "-shared", "-fPIC", request.param, "-I", os.path.abspath(HDR),
                     str(src), "-o", str(so)],
                    check=True)
     L = ctypes.CDLL(str(so))
