@@ -51,7 +51,7 @@ PEAK_INT32 = 256 * 128 * 2.4e9
 MASK = {"ocert": 1, "kes": 2, "vrf": 4}
 # committed rocprofv3 summaries (tools/profile.sh <tag>): <tag>_traffic.json names its workload;
 # the first tag whose workload is the bench's supplies traffic and PMC for the roofline kernel
-PROFILE_TAGS = ("r06c6", "r06c5", "r05c5", "r05c4", "r05c3", "r05c2", "r05tp", "r04c5", "r04c4b", "r04c3", "r04c2", "r04tp", "r04c4", "r03e")
+PROFILE_TAGS = ("r06c7", "r06c6", "r06c5", "r05c5", "r05c4", "r05c3", "r05c2", "r05tp", "r04c5", "r04c4b", "r04c3", "r04c2", "r04tp", "r04c4", "r03e")
 
 
 def profile_tag(workload):
