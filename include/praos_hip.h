@@ -820,7 +820,8 @@ int praos_synthesize_tpraos(praos_ctx* ctx, const praos_synth_params* sp, const 
                             uint8_t* corrupted);
 
 /* ---- self-test entry points (unit tests of the device arithmetic) ---- */
-/* op: 0 mul, 1 sq, 2 add, 3 sub, 4 invert, 5 pow22523, 6 canon; inputs/outputs n*32 bytes LE */
+/* op: 0 mul, 1 sq, 2 add, 3 sub, 4 invert (the build's: binary GCD unless PRAOS_INV_GCD=0), 5 pow22523,
+   6 canon, 7 invert by Fermat's z^(p-2), 8 invert by the binary GCD; inputs/outputs n*32 bytes LE */
 int praos_debug_fe(praos_ctx* ctx, int op, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* r);
 /* SHA-512 of (64-byte prefix || msg) per item; out n*64 */
 int praos_debug_sha512(praos_ctx* ctx, size_t n, const uint8_t* prefix, const uint64_t* msg_off,
