@@ -127,6 +127,9 @@ static constexpr size_t ILP4_BATCH = 120000;
 // profiles/r06/i_kes_nocache).  PRAOS_OPT_KES_NOCACHE / PRAOS_KES_NOCACHE=<headers> override it
 // (0: always cached).
 static constexpr size_t KES_NOCACHE_BATCH = 58000;
+// below this many headers (the 1/8-epoch shard of a 432k epoch is 54k) stage V's join runs on the
+// main stream after U (PRAOS_V_MAIN 1) and the uncached verifies keep normal wave priority
+static constexpr size_t SHARD_SMALL = 60000;
 static constexpr int PIPE_AUTO = 8;                 // chunks in auto mode (round 3, equal chunks: 4 -> 21.9M,
                                                     // 6 -> 23.0M, 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt;
                                                     // round 5 with the first chunk at 1/4 of the others: 6 ->
@@ -191,6 +194,10 @@ struct praos_ctx {
                                                        // (k_miss4.hip): PRAOS_MISS4 1 / 0, -1 below ILP4_BATCH
                                                        // (54k: 3.33 -> 3.09 ms; 108k: 4.26 -> 4.66, so not there)
   int miss_prio = -1;                                  // ... at s_setprio 3: PRAOS_MISS_PRIO 1 / 0, -1 with miss4
+                                                       // from SHARD_SMALL headers on (below it, beside the GCD
+                                                       // inversion's shorter join, normal priority with
+                                                       // v_main 1 was faster: profiles/r06/s_retune)
+  int miss_prio_for(size_t n) const { return miss_prio >= 0 ? miss_prio : (n < SHARD_SMALL ? 0 : 1); }
   long kes_pair = -1;                                  // k_kes_ck two headers per lane from this many hits on
                                                        // (PRAOS_KES_PAIR, 0 = never; -1: from 196,608 when the
                                                        // KES pass runs alone -- beside the OCert / VRF passes
@@ -203,14 +210,19 @@ struct praos_ctx {
                                                        // off, measured slower (C4 10.7 -> 11.2 ms: the
                                                        // representatives' walks lengthen the KES chain more than
                                                        // the skipped walks save; C5 unchanged, profiles/r04/r)
-  int v_main = 3;                                      // stage V on the main stream (PRAOS_V_MAIN; 0 off): no
+  int v_main = -1;                                     // stage V on the main stream (PRAOS_V_MAIN; 0 off): no
                                                        // cross-stream wait between the previous run's end and V;
                                                        // the join after U and V on the VRF stream (3), or on the
                                                        // main stream after a wait for U (1; 2: U's two streams
                                                        // waited for separately).  54k headers (C5 1/8 shard):
                                                        // 2.354-2.380 ms off, 2.284-2.330 (1), 2.315-2.332 (2),
                                                        // 2.267-2.297 (3); 108k: 3.418-3.443 off, 3.36-3.42 on
-                                                       // (profiles/r06/k_vmain)
+                                                       // (profiles/r06/k_vmain); -1: 1 below SHARD_SMALL
+                                                       // headers, 3 from it (with the GCD inversion, mode 1 +
+                                                       // normal-priority misses: 54k 2.18-2.22 -> 2.17-2.19 ms,
+                                                       // 40k 2.19-2.21 -> 2.08; 64k-80k equal or slower,
+                                                       // profiles/r06/s_retune)
+  int vmain_mode(size_t n) const { return v_main >= 0 ? v_main : (n < SHARD_SMALL ? 1 : 3); }
   int pre_join = -1;                                   // the join's pool part (lookup, key hash, leader / nonce
                                                        // values) as k_vrf_pool on the VRF miss stream before the
                                                        // uncached U, off the chain after stage V (PRAOS_PRE_JOIN
@@ -1444,7 +1456,8 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   // PRAOS_V_MAIN: the three-kernel Praos VRF with stage V and the join on the main stream (the
   // step's critical path then crosses streams once, U -> join, instead of at ev[0] -> V, V -> join
   // and join -> leader)
-  const bool v_main = c->v_main > 0 && c->concurrent && do_vrf && !b->tp_only && !b->v_done &&
+  const int vm_mode = c->vmain_mode(n);
+  const bool v_main = vm_mode > 0 && c->concurrent && do_vrf && !b->tp_only && !b->v_done &&
                       (c->vrf3 > 0 || (c->vrf3 < 0 && n < 300000));
   const int wprio_v = c->vrf_prio > 0 || (c->vrf_prio < 0 && n < SMALL_BATCH);
   bool v_queued = false;
@@ -1537,7 +1550,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
     launch_vrf_u(sv, n, k.hit, k.counters + 1, k.item_entry, k.kt, k.ki, c->bcomb16, c->btab, b->vrf_vk,
                  b->vrf_proof, b->tab_vrfu, b->vrf_mid, c->use_u4(n), 0);
     // (v_main 2: the main stream waits for u_ev itself, before the join)
-    if (sm_[2] != sv && !(v_main && c->v_main == 2)) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
+    if (sm_[2] != sv && !(v_main && vm_mode == 2)) HIPCHK(c, hipStreamWaitEvent(sv, c->u_ev, 0));
     vrf_keys_queued = true;
     return PRAOS_OK;
   };
@@ -1563,7 +1576,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         if (c->use_miss4(n))
           launch_ocert4(g, blk, sm_[0], k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                         b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
-                        b->tab_ocert, c->miss_prio >= 0 ? c->miss_prio : 1);
+                        b->tab_ocert, c->miss_prio_for(n));
         else
           launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                        b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo, b->dd_ok,
@@ -1604,7 +1617,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
         if (c->use_miss4(n))
           launch_ocert4(g, blk, sm_[0], k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                         b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
-                        (uint8_t*)nullptr, b->tab_ocert, c->miss_prio >= 0 ? c->miss_prio : 1);
+                        (uint8_t*)nullptr, b->tab_ocert, c->miss_prio_for(n));
         else
           launch_ocert(g, blk, sm_[0], n, k.miss, k.counters + 2, c->btab, b->cold_vk, b->hot_vk, b->ocert_n,
                        b->ocert_c0, b->ocert_sig, b->slot, P.slots_per_kes_period, P.max_kes_evo, bo,
@@ -1641,7 +1654,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       if (c->use_miss4(n))
         launch_kes4(g, blk, sm_[1], k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off, b->body_len,
                     b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period, bk, b->tab_kes,
-                    c->miss_prio >= 0 ? c->miss_prio : 1);
+                    c->miss_prio_for(n));
       else
         launch_kes(g, blk, sm_[1], n, k.miss, k.counters + 2, c->btab, b->hot_vk, b->kes_sig, b->body_off,
                    b->body_len, b->body, b->body_bytes_len, b->slot, b->ocert_c0, P.slots_per_kes_period,
@@ -1759,12 +1772,12 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
       } else {
         stage_u(sv, nullptr, nullptr, nullptr);
       }
-      if (v_main && c->v_main == 3) {  // V on the main stream, the join on the VRF stream after U
+      if (v_main && vm_mode == 3) {  // V on the main stream, the join on the VRF stream after U
         HIPCHK(c, hipEventRecord(c->v_ev, c->stream));
         HIPCHK(c, hipStreamWaitEvent(sv, c->v_ev, 0));
         join(sv);
       } else if (v_main) {             // V is on the main stream: the join follows it there, after U
-        if (c->v_main == 2 && kc) HIPCHK(c, hipStreamWaitEvent(c->stream, c->u_ev, 0));
+        if (vm_mode == 2 && kc) HIPCHK(c, hipStreamWaitEvent(c->stream, c->u_ev, 0));
         HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[2], 0));
         join(c->stream);
@@ -1795,7 +1808,7 @@ static int batch_run_impl(praos_ctx* c, praos_batch* b) {
   HIPCHK(c, hipEventRecord(c->side_ev[2], sv));
   if (c->concurrent) {
     // (v_main: the VRF stream and its miss stream -- u_ev -- were waited for before the join)
-    const bool sv_done = v_main && c->v_main != 3;
+    const bool sv_done = v_main && vm_mode != 3;
     for (int k = 0; k < 3; k++)
       if (!(sv_done && k == 2)) HIPCHK(c, hipStreamWaitEvent(c->stream, c->side_ev[k], 0));
     for (int k = 0; k < 3; k++) {

@@ -1,7 +1,8 @@
-# re-tune after the GCD inversion: the KES leaf-key cache cut (KES_NOCACHE_BATCH) at 54k / 64k
+# after making the small-shard schedule the default below SHARD_SMALL: GPU suite, smoke, bench, and
+# the A/B against the previous default (PRAOS_V_MAIN=3 PRAOS_MISS_PRIO=1) at 54k
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/retune
-bash tools/ab.sh rt54 54000 "-" "PRAOS_KES_NOCACHE=0" 2>&1 | tee gpurun_out/retune/ab54.txt
-bash tools/ab.sh rt64 64000 "-" "PRAOS_KES_NOCACHE=70000" 2>&1 | tee gpurun_out/retune/ab64.txt
-bash tools/ab.sh rt40 40000 "-" "PRAOS_KES_NOCACHE=0" 2>&1 | tee gpurun_out/retune/ab40.txt
+mkdir -p gpurun_out/retune5
+export STEPS=40
+bash tools/ab.sh rt5_54 54000 "-" "PRAOS_V_MAIN=3 PRAOS_MISS_PRIO=1" 2>&1 | tee gpurun_out/retune5/ab54.txt || exit 1
+bash tools/gpu_full.sh
