@@ -10,7 +10,9 @@ each operation in the radix-2^32 implementation (fe25519.hpp):
     A   add / sub / neg  8 + 8 carry-propagating adds + fold                =  17
     SHA-512 compression  80 rounds on 64-bit words in VGPR pairs            = 5000
     BLAKE2b compression  12 rounds                                          = 2700
-    X   exponentiation   (p-2, (p-5)/8, (p-1)/2): 254 S + 11 M (+ canon)
+    X   exponentiation   ((p-5)/8, (p-1)/2): 254 S + 11 M (+ canon)
+    INV inversion        binary GCD (fe_inv_gcd.hpp): ~13.5 outer iterations x ~1,300 VALU
+                         (30 steps x ~24 + the matrix applied to a, b, u, v) + the 2^(-30k) product
 
 Everything else (digit extraction, table selection, sign handling, loads,
 loop control) is overhead and not counted: `frac` therefore reports how much
@@ -22,6 +24,7 @@ M, S, A = 154, 130, 17
 SHA, B2B = 5000, 2700
 CANON = 30
 X = 254 * S + 11 * M + CANON            # one exponentiation chain
+INV = 27 * 1300 // 2 + M + CANON          # one inversion (binary GCD; Fermat's z^(p-2) was X)
 
 # group operations (ge25519.hpp)
 DBL = 4 * S + 6 * A                     # ge_p2_dbl -> p1p1
@@ -31,7 +34,7 @@ TO_P2, TO_P3 = 3 * M, 4 * M
 CNEG = A                                # negation of the selected entry
 TABLE8 = 8 * (M + 2 * A) + (DBL + TO_P3) + 6 * (ADD + TO_P3)   # {1..8}P cached
 DECODE = X + 2 * S + 10 * M + 3 * A + 3 * CANON                # ge_frombytes (sqrt ratio)
-ENCODE = X + 2 * M + CANON                                     # ge_tobytes (one inversion)
+ENCODE = INV + 2 * M + CANON                                   # ge_tobytes (one inversion)
 SC_REDUCE = 600
 
 
@@ -59,7 +62,7 @@ def vrf_verify():
     w += TABLE8 + straus(33, 33, 0, 32) + TO_P2      # U = [s]B - [c]Y (B, 2^128 B)
     w += 2 * TABLE8 + straus(64, 64, 33, 0) + TO_P2  # V = [s]H - [c]Gamma
     w += 3 * (DBL + TO_P3)                           # 8 Gamma
-    w += X + 10 * M + 4 * (2 * M + CANON)            # batched inversion + 4 encodings
+    w += INV + 10 * M + 4 * (2 * M + CANON)          # batched inversion + 4 encodings
     w += 3 * SHA + SC_REDUCE                         # c' (2 blocks), beta (1 block)
     return w
 
@@ -91,7 +94,7 @@ W_VRF_V = (B2B                                        # alpha = mkInputVRF(slot,
            + CANON + ELLIGATOR                        # canonical Y (no decode), H = hash_to_curve
            + DECODE + 3 * (DBL + TO_P3)               # Gamma, 8 Gamma
            + 2 * TABLE8 + SC_REDUCE + straus(64, 64, 33, 0) + TO_P2)   # V = [s]H - [c]Gamma
-_FIN = SC_REDUCE + TO_P2 + X + 10 * M + 4 * (2 * M + CANON) + 3 * SHA + 5 * B2B + 1000
+_FIN = SC_REDUCE + TO_P2 + INV + 10 * M + 4 * (2 * M + CANON) + 3 * SHA + 5 * B2B + 1000
 W_VRF_F_CK = _FIN + straus_comb(8, True)             # U from the cached key + comb; inversion, c', beta, L/N
 W_VRF_F = _FIN + DECODE + TABLE8 + straus(33, 33, 0, 32)
 # TPraos header (TPraos.hs:361-387, k_vrf_tp): two certificates (eta, L) per header, each a full
