@@ -128,7 +128,8 @@ static constexpr size_t ILP4_BATCH = 120000;
 // (0: always cached).
 static constexpr size_t KES_NOCACHE_BATCH = 58000;
 // below this many headers (the 1/8-epoch shard of a 432k epoch is 54k) stage V's join runs on the
-// main stream after U (PRAOS_V_MAIN 1) and the uncached verifies keep normal wave priority
+// main stream after it waits for U itself (PRAOS_V_MAIN 2) and the uncached verifies keep normal
+// wave priority
 static constexpr size_t SHARD_SMALL = 60000;
 static constexpr int PIPE_AUTO = 8;                 // chunks in auto mode (round 3, equal chunks: 4 -> 21.9M,
                                                     // 6 -> 23.0M, 8 -> 22.1M headers/s, profiles/r03/e2e_chunks.txt;
@@ -217,12 +218,13 @@ struct praos_ctx {
                                                        // waited for separately).  54k headers (C5 1/8 shard):
                                                        // 2.354-2.380 ms off, 2.284-2.330 (1), 2.315-2.332 (2),
                                                        // 2.267-2.297 (3); 108k: 3.418-3.443 off, 3.36-3.42 on
-                                                       // (profiles/r06/k_vmain); -1: 1 below SHARD_SMALL
+                                                       // (profiles/r06/k_vmain); -1: 2 below SHARD_SMALL
                                                        // headers, 3 from it (with the GCD inversion, mode 1 +
                                                        // normal-priority misses: 54k 2.18-2.22 -> 2.17-2.19 ms,
-                                                       // 40k 2.19-2.21 -> 2.08; 64k-80k equal or slower,
-                                                       // profiles/r06/s_retune)
-  int vmain_mode(size_t n) const { return v_main >= 0 ? v_main : (n < SHARD_SMALL ? 1 : 3); }
+                                                       // 40k 2.19-2.21 -> 2.08; 64k-80k equal or slower; then
+                                                       // mode 2 over mode 1 at 54k 2.16-2.19 -> 2.15, 40k equal
+                                                       // or 2 % faster, profiles/r06/s_retune)
+  int vmain_mode(size_t n) const { return v_main >= 0 ? v_main : (n < SHARD_SMALL ? 2 : 3); }
   int pre_join = -1;                                   // the join's pool part (lookup, key hash, leader / nonce
                                                        // values) as k_vrf_pool on the VRF miss stream before the
                                                        // uncached U, off the chain after stage V (PRAOS_PRE_JOIN

@@ -279,7 +279,7 @@ def test_schedule_variants_equal_single_batch(ctx, c5_batch, env, concurrent):
     """Schedule options that move work between kernels and streams give the default context's
     one-batch outputs bit for bit: the join's pool part ahead of it as k_vrf_pool (PRAOS_PRE_JOIN,
     default on below SMALL_BATCH headers) or in the join, stage V and the join on the main stream
-    (PRAOS_V_MAIN; at this batch size the default is mode 1, so mode 3 with the uncached verifies
+    (PRAOS_V_MAIN; at this batch size the default is mode 2, so mode 3 with the uncached verifies
     at raised priority, the default from SHARD_SMALL headers, is a variant here), on concurrent
     streams and on one -- in one
     batch and pipelined (8 chunks, twice)."""

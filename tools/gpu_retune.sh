@@ -1,8 +1,8 @@
-# after making the small-shard schedule the default below SHARD_SMALL: GPU suite, smoke, bench, and
-# the A/B against the previous default (PRAOS_V_MAIN=3 PRAOS_MISS_PRIO=1) at 54k
+# join placement below SHARD_SMALL with the uncached verifies at normal priority (the default there)
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/retune5
+mkdir -p gpurun_out/retune7
 export STEPS=40
-bash tools/ab.sh rt5_54 54000 "-" "PRAOS_V_MAIN=3 PRAOS_MISS_PRIO=1" 2>&1 | tee gpurun_out/retune5/ab54.txt || exit 1
-bash tools/gpu_full.sh
+bash tools/ab.sh rt7_54 54000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune7/ab54.txt
+bash tools/ab.sh rt7_40 40000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune7/ab40.txt
+bash tools/ab.sh rt7_20 20000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune7/ab20.txt
