@@ -218,13 +218,15 @@ struct praos_ctx {
                                                        // waited for separately).  54k headers (C5 1/8 shard):
                                                        // 2.354-2.380 ms off, 2.284-2.330 (1), 2.315-2.332 (2),
                                                        // 2.267-2.297 (3); 108k: 3.418-3.443 off, 3.36-3.42 on
-                                                       // (profiles/r06/k_vmain); -1: 2 below SHARD_SMALL
+                                                       // (profiles/r06/k_vmain); -1: 2 below ILP4_BATCH
                                                        // headers, 3 from it (with the GCD inversion, mode 1 +
-                                                       // normal-priority misses: 54k 2.18-2.22 -> 2.17-2.19 ms,
-                                                       // 40k 2.19-2.21 -> 2.08; 64k-80k equal or slower; then
+                                                       // normal-priority misses below SHARD_SMALL: 54k
+                                                       // 2.18-2.22 -> 2.17-2.19 ms, 40k 2.19-2.21 -> 2.08; then
                                                        // mode 2 over mode 1 at 54k 2.16-2.19 -> 2.15, 40k equal
-                                                       // or 2 % faster, profiles/r06/s_retune)
-  int vmain_mode(size_t n) const { return v_main >= 0 ? v_main : (n < SHARD_SMALL ? 2 : 3); }
+                                                       // or 2 % faster; over mode 3 at 80k 2.78-2.80 -> 2.76,
+                                                       // 108k 3.24-3.26 -> 3.21-3.22, 216k 5.63-5.70 -> 5.70-5.71;
+                                                       // profiles/r06/s_retune)
+  int vmain_mode(size_t n) const { return v_main >= 0 ? v_main : (n < ILP4_BATCH ? 2 : 3); }
   int pre_join = -1;                                   // the join's pool part (lookup, key hash, leader / nonce
                                                        // values) as k_vrf_pool on the VRF miss stream before the
                                                        // uncached U, off the chain after stage V (PRAOS_PRE_JOIN

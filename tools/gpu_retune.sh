@@ -1,8 +1,6 @@
-# join placement below SHARD_SMALL with the uncached verifies at normal priority (the default there)
+# join placement A/Bs (PRAOS_V_MAIN) at the shard sizes; see DESIGN §15 "Small-shard schedule"
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/retune7
-export STEPS=40
-bash tools/ab.sh rt7_54 54000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune7/ab54.txt
-bash tools/ab.sh rt7_40 40000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune7/ab40.txt
-bash tools/ab.sh rt7_20 20000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune7/ab20.txt
+mkdir -p gpurun_out/retune9
+export STEPS=30
+bash tools/ab.sh rt9_216 216000 "-" "PRAOS_V_MAIN=2" 2>&1 | tee gpurun_out/retune9/ab216.txt
